@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Benchmark: novel views/s at 256x256 with 2 context views on MI355X (BASELINE.json metric).
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1 launched by
+torch.distributed.run, one rank per GPU. W untimed warm-up steps, then exactly K steps between a
+barrier + device synchronise on both sides; the slowest rank's time is used; rank 0 prints ONE
+JSON line.
+
+Workloads (a "step" = one pass of the hot path over one batch of synthetic scenes):
+  e2e    : encoder (backbone + DA-V2 + depth predictor + adapter) -> decoder for B scenes of
+           2 context views, rendering 3 target views each (reference test_step,
+           src/model/model_wrapper.py:185-323, metrics excluded)
+  raster : the decoder alone on precomputed synthetic Gaussians (G = 131,072 per scene)
+Scenes shard embarrassingly across ranks (rank r renders its own B scenes; no data-path
+collective); one all-reduce of the timing and a gather of per-rank counts close the run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import time
+
+import torch
+import torch.distributed as dist
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+RASTER_BYTES_PER_VIEW = None  # computed: G*(12+24+4*d_sh*3+4) + H*W*12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", choices=["e2e", "raster"], default="raster")
+    ap.add_argument("--batch", type=int, default=1, help="scenes per step per GPU")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def init_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    return world, rank, local
+
+
+def raster_bytes_per_view(g: int, d_sh: int, h: int, w: int) -> int:
+    # means 12 + cov 24 (upper triangle of the 3x3) + SH 3*d_sh*4 + opacity 4, image 3*4 per pixel
+    return g * (12 + 24 + 3 * d_sh * 4 + 4) + h * w * 12
+
+
+def build_raster_workload(batch: int, device, scene_offset: int):
+    from transplat_amd import synthetic as S
+    from transplat_amd.model.decoder.hip_splatting import prepare_cameras, rasterize
+
+    hw = (256, 256)
+    g = S.make_gaussians(batch, image_shape=hw, scene_offset=scene_offset, device=device)
+    tb = S.make_batch(batch, image_shape=hw, scene_offset=scene_offset, device=device)["target"]
+    b, v = tb["near"].shape
+    cams = prepare_cameras(tb["extrinsics"].reshape(b * v, 4, 4), tb["intrinsics"].reshape(b * v, 3, 3),
+                           tb["near"].reshape(-1), tb["far"].reshape(-1), torch.zeros(b * v, 3, device=device))
+
+    def step():
+        return rasterize(g["means"], g["covariances"], g["harmonics"], g["opacities"], cams, hw, v,
+                         check=False)
+
+    g_per_scene = g["means"].shape[1]
+    info = {
+        "views_per_step": b * v,
+        "dominant": "raster",
+        "alg_bytes_per_launch": raster_bytes_per_view(g_per_scene, g["harmonics"].shape[-1], *hw) * b * v,
+        "workload": "raster-only: decoder on synthetic Gaussians (G=131072/scene, 3 target views)",
+    }
+    cpu_inputs = ({k: t.cpu() for k, t in g.items()}, cams.to("cpu"), hw, v)
+    return step, info, cpu_inputs
+
+
+def cpu_baseline_raster(cpu_inputs, seconds: float):
+    """Oracle C rasterizer (scalar, 1 thread) on as many views as fit `seconds` (>= 1)."""
+    from oracle import raster as oracle_raster
+
+    g, cams, hw, vps = cpu_inputs
+    one = {k: t[:1] for k, t in g.items()}
+    n_views, t0 = 0, time.perf_counter()
+    while True:
+        i = n_views % vps
+        sub = type(cams)(*(getattr(cams, f)[i : i + 1] for f in cams.__dataclass_fields__))
+        oracle_raster.render(one["means"], one["covariances"], one["harmonics"], one["opacities"], sub, hw, 1,
+                             min(3, int(round(one["harmonics"].shape[-1] ** 0.5)) - 1))
+        n_views += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {
+        "value": n_views / el,
+        "unit": "views/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"{n_views} views of one synthetic 256x256 scene (G=131072) through oracle/raster_ref.c, "
+                  f"{el:.1f} s, host {platform.processor() or platform.machine()}, nproc={os.cpu_count()}",
+    }
+
+
+def main():
+    args = parse()
+    world, rank, local = init_dist()
+    device = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(device)
+    from transplat_amd import _lib
+
+    _lib.load()
+
+    if args.workload == "raster":
+        step, info, cpu_inputs = build_raster_workload(args.batch, device, scene_offset=rank * args.batch)
+    else:
+        from transplat_amd.e2e import build_e2e_workload
+
+        step, info, cpu_inputs = build_e2e_workload(args.batch, device, scene_offset=rank * args.batch)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    from transplat_amd.model.decoder.hip_splatting import check_status
+
+    check_status(device)  # any capacity overflow during the timed steps invalidates the run
+
+    # dominant-kernel timing (HIP events on the launch stream), separate from the timed region
+    _lib.prof_enable(info["dominant"])
+    n_prof = max(3, min(args.steps, 20))
+    for _ in range(n_prof):
+        step()
+    ms, launches = _lib.prof_read()
+    _lib.prof_enable(None)
+    avg_ms = ms / max(launches, 1)
+    achieved = info["alg_bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
+
+    views = world * info["views_per_step"] * args.steps
+    result = {
+        "metric": "novel views/sec at 256x256, 2 ctx views; PSNR parity vs reference",
+        "value": views / elapsed,
+        "unit": "views/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic",
+        "config": {
+            "workload": info["workload"],
+            "scenes_per_gpu_per_step": args.batch,
+            "views_per_scene": 3,
+            "image": [256, 256],
+            "parallelism": f"scene-shard x{world}",
+        },
+        "roofline": {
+            "kernel": info["dominant"],
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "avg_launch_ms": avg_ms,
+            "launches": launches,
+        },
+    }
+    if rank == 0 and not args.no_cpu_baseline and cpu_inputs is not None:
+        result["cpu_baseline"] = cpu_baseline_raster(cpu_inputs, args.cpu_baseline_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,103 @@
+/*
+ * transplat_hip.h — C-ABI of the MI355X (gfx950) TranSplat inference hot path.
+ *
+ * Every entry point is `extern "C"`, takes plain device pointers + sizes and an explicit
+ * hipStream_t (passed as void*), allocates nothing, and returns an int status:
+ *   0 = OK, TSPLAT_EINVAL = bad argument, TSPLAT_EHIP = HIP launch error.
+ * All pointers are device-resident and owned by the caller (the PyTorch caching allocator on
+ * the Python side). Calls are thread-compatible (one stream per thread), never thread-safe
+ * on a shared workspace. No entry point synchronises the stream.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   - rasterizer: `GaussianRasterizer(GaussianRasterizationSettings(...))(means3D, means2D,
+ *     shs, colors_precomp, opacities, cov3D_precomp)` called once per view inside the Python
+ *     loop of `render_cuda` (src/model/decoder/cuda_splatting.py:100-135), i.e. the
+ *     third-party `diff_gaussian_rasterization._C.rasterize_gaussians` forward.
+ *   - depth-candidate correlation: `UVCoarseAttention.forward` / `UVCrossAttention.forward`
+ *     (src/model/utils/attention.py:468-551 / :329-416) together with `calculate_grid`
+ *     (src/model/encoder/matching/depth_predictor_trans.py:11-57) and mmcv's
+ *     `ext_module.ms_deform_attn_forward`
+ *     (src/model/utils/multi_scale_deformable_attn_function.py:111-117).
+ *   - window attention: `single_head_split_window_attention`
+ *     (src/model/encoder/backbone/multiview_transformer.py:57-206) with the shifted-window
+ *     mask of `generate_shift_window_attn_mask` (:17-54).
+ */
+#ifndef TRANSPLAT_HIP_H
+#define TRANSPLAT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TSPLAT_OK 0
+#define TSPLAT_EINVAL (-1)
+#define TSPLAT_EHIP (-2)
+
+/* Library version / build identification (for the smoke check and the loader). */
+int tsplat_version(void);
+
+/* Per-kernel timing with HIP events recorded on the launch stream around every launch of ONE
+ * kernel (ids: 1 raster preprocess, 2 raster scan, 3 raster scatter, 4 raster render,
+ * 5 uv coarse correlation, 6 uv cross correlation, 7 msda, 8 window attention, 9 the whole
+ * rasterizer launch sequence; 0 = off).
+ * tsplat_prof_read waits for the recorded events, returns the summed duration and the number of
+ * launches timed since the last enable/read, and resets the record. Used by bench.py only. */
+int tsplat_prof_enable(int32_t kernel_id);
+int tsplat_prof_read(double* total_ms, int32_t* launches);
+
+/* ------------------------------------------------------------------------------------------
+ * Gaussian-splat forward rasterizer (graphdeco forward algorithm: preprocess, per-tile binning,
+ * depth sort, front-to-back alpha blending), all views of all scenes in ONE set of launches.
+ *
+ * View v renders the Gaussians of scene (v / views_per_scene); Gaussian arrays are
+ * [num_scenes, G, ...] with num_scenes = num_views / views_per_scene.
+ * Layouts (fp32, contiguous):
+ *   means      [S, G, 3]
+ *   cov        [S, G, 3, 3]     full symmetric 3x3 (upper triangle read, as the reference's
+ *                               cov3D_precomp = cov[:, row, col] with triu_indices(3,3))
+ *   shs        [S, G, 3, M]     colour-major SH (the Gaussians.harmonics layout; the reference
+ *                               transposes it to [G, M, 3] before the call)
+ *   opacity    [S, G]
+ *   viewmat    [V, 16]          view matrix, column-major (= inverse(c2w)^T row-major)
+ *   projmat    [V, 16]          full projection, column-major (viewmat @ P^T)
+ *   campos     [V, 3]           camera centre (scaled c2w[:3, 3])
+ *   tanfov     [V, 2]           tan(fov_x/2), tan(fov_y/2)
+ *   bg         [V, 3]           background colour
+ *   scene_scale[V, 2]           (s, s*s) scale-invariance factors applied to means / cov
+ * Outputs:
+ *   out_color  [V, 3, H, W]
+ *   out_radii  [V, G] int32     (0 = culled), the rasterizer's `radii`
+ * Workspace: tsplat_raster_workspace_bytes(G, V, H, W, capacity) bytes, 256-byte aligned.
+ * `capacity` bounds the number of (Gaussian, tile) instances; if a call needs more, the sticky
+ * int at `status` gets bit 0 set and the image is incomplete (the Python side checks it).
+ * ---------------------------------------------------------------------------------------- */
+typedef struct tsplat_raster_desc {
+    int32_t num_gaussians;    /* G per scene */
+    int32_t num_views;        /* V total views = num_scenes * views_per_scene */
+    int32_t views_per_scene;
+    int32_t height;
+    int32_t width;
+    int32_t sh_coeffs;        /* M = coefficients stored per colour channel ((deg+1)^2) */
+    int32_t sh_degree;        /* degree evaluated; 3 = upstream graphdeco, 4 = full degree-4 */
+    int32_t capacity;         /* instance capacity of the workspace */
+} tsplat_raster_desc;
+
+size_t tsplat_raster_workspace_bytes(int32_t num_gaussians, int32_t num_views, int32_t height,
+                                     int32_t width, int32_t capacity);
+
+int tsplat_raster_fwd(const tsplat_raster_desc* desc,
+                      const float* means, const float* cov, const float* shs,
+                      const float* opacity, const float* viewmat, const float* projmat,
+                      const float* campos, const float* tanfov, const float* bg,
+                      const float* scene_scale,
+                      float* out_color, int32_t* out_radii,
+                      void* workspace, int32_t* status, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRANSPLAT_HIP_H */

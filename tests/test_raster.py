@@ -1,0 +1,219 @@
+"""Rasterizer parity: gfx950 kernel (tsplat_raster_fwd) vs the scalar C restatement (oracle/).
+
+CPU tests check the oracle itself (single-Gaussian closed form in float64, culling rules);
+GPU tests compare the HIP path through the C-ABI with the oracle on identical inputs.
+Tolerance (BASELINE.json north_star): L-inf <= 1e-4 on fp32 images, radii identical.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import raster as oracle_raster
+from transplat_amd import synthetic as S
+from transplat_amd.model.decoder.hip_splatting import RasterCameras, prepare_cameras, rasterize
+
+ATOL = 1e-4
+
+
+def _cams(ext, K, near, far, bg):
+    return prepare_cameras(ext, K, near, far, bg)
+
+
+def single_gaussian_scene(pos, cov_scale, opacity, rgb_dc, bg, hw=(64, 64)):
+    """One Gaussian (isotropic covariance, DC colour only) seen by an identity camera."""
+    means = torch.tensor([[pos]], dtype=torch.float32)
+    cov = (torch.eye(3) * cov_scale)[None, None].float()
+    sh = torch.zeros((1, 1, 3, 1))
+    sh[0, 0, :, 0] = torch.tensor(rgb_dc)
+    op = torch.tensor([[opacity]], dtype=torch.float32)
+    ext = torch.eye(4)[None]
+    K = S.intrinsics(1)
+    cams = _cams(ext, K, torch.ones(1), torch.full((1,), 100.0), torch.tensor([bg], dtype=torch.float32))
+    return means, cov, sh, op, cams
+
+
+def closed_form_single(pos, cov_scale, opacity, rgb_dc, bg, hw):
+    """float64 restatement of preprocess + render for one Gaussian, identity camera, fx=fy=1."""
+    h, w = hw
+    x, y, z = pos
+    fx, fy = float(w), float(h)  # W / (2 tan(fov/2)) with tan(fov/2) = 0.5 for normalised fx = 1
+    tx = max(-0.65, min(0.65, x / z)) * z
+    ty = max(-0.65, min(0.65, y / z)) * z
+    J = np.array([[fx / z, 0, -fx * tx / z**2], [0, fy / z, -fy * ty / z**2]])
+    c2 = J @ (np.eye(3) * cov_scale) @ J.T + np.eye(2) * 0.3
+    a, b, c = c2[0, 0], c2[0, 1], c2[1, 1]
+    det = a * c - b * b
+    conic = (c / det, -b / det, a / det)
+    mid = 0.5 * (a + c)
+    lam = mid + math.sqrt(max(0.1, mid * mid - det))
+    r = math.ceil(3 * math.sqrt(lam))
+    # ndc from the projection matrix: x_ndc = 2 n / (r - l) * x / z = x / (z * tan) with tan = 0.5
+    px = ((x / (z * 0.5) + 1) * w - 1) * 0.5
+    py = ((y / (z * 0.5) + 1) * h - 1) * 0.5
+    rgb = np.maximum(0.28209479177387814 * np.array(rgb_dc) + 0.5, 0)
+    tiles_x, tiles_y = (w + 15) // 16, (h + 15) // 16
+    x0 = min(tiles_x, max(0, int((px - r) / 16))); x1 = min(tiles_x, max(0, int((px + r + 15) / 16)))
+    y0 = min(tiles_y, max(0, int((py - r) / 16))); y1 = min(tiles_y, max(0, int((py + r + 15) / 16)))
+    img = np.zeros((3, h, w))
+    img[:] = np.array(bg)[:, None, None]
+    for yy in range(y0 * 16, min(h, y1 * 16)):
+        for xx in range(x0 * 16, min(w, x1 * 16)):
+            dx, dy = px - xx, py - yy
+            power = -0.5 * (conic[0] * dx * dx + conic[2] * dy * dy) - conic[1] * dx * dy
+            if power > 0:
+                continue
+            alpha = min(0.99, opacity * math.exp(power))
+            if alpha < 1 / 255:
+                continue
+            img[:, yy, xx] = rgb * alpha + (1 - alpha) * np.array(bg)
+    return img, r
+
+
+@pytest.mark.parametrize(
+    "pos,cov_scale,opacity,bg",
+    [((0.1, -0.05, 4.0), 0.01, 0.8, (0.0, 0.0, 0.0)),
+     ((-0.3, 0.2, 2.5), 0.002, 0.5, (0.2, 0.5, 1.0)),
+     ((0.9, 0.0, 3.0), 0.02, 0.99, (0.0, 0.0, 0.0))],  # mean outside the 1.3 tan clamp region
+)
+def test_oracle_single_gaussian_closed_form(pos, cov_scale, opacity, bg):
+    hw = (64, 64)
+    rgb = (0.4, -0.3, 1.2)
+    means, cov, sh, op, cams = single_gaussian_scene(pos, cov_scale, opacity, rgb, bg, hw)
+    img, radii, _ = oracle_raster.render(means, cov, sh, op, cams, hw, 1, 0)
+    ref, r = closed_form_single(pos, cov_scale, opacity, rgb, bg, hw)
+    assert radii[0, 0] == r
+    np.testing.assert_allclose(img[0], ref, atol=2e-5)
+
+
+def test_oracle_culls_near_plane():
+    hw = (32, 32)
+    means, cov, sh, op, cams = single_gaussian_scene((0.0, 0.0, 0.15), 0.01, 0.9, (1, 1, 1), (0.1, 0.2, 0.3), hw)
+    img, radii, n = oracle_raster.render(means, cov, sh, op, cams, hw, 1, 0)
+    assert radii[0, 0] == 0 and n == [0]
+    np.testing.assert_allclose(img[0], np.array([0.1, 0.2, 0.3])[:, None, None].repeat(32, 1).repeat(32, 2))
+
+
+def test_oracle_depth_order_front_to_back():
+    """Two overlapping opaque Gaussians: the nearer one dominates whichever id it has."""
+    hw = (32, 32)
+    means = torch.tensor([[[0, 0, 5.0], [0, 0, 3.0]]])
+    cov = (torch.eye(3) * 0.05).expand(1, 2, 3, 3).clone()
+    sh = torch.full((1, 2, 3, 1), -2.0)  # DC -2 -> colour clamps to 0
+    sh[0, 0, 0, 0] = 2.0  # far one red
+    sh[0, 1, 2, 0] = 2.0  # near one blue
+    op = torch.full((1, 2), 0.99)
+    cams = _cams(torch.eye(4)[None], S.intrinsics(1), torch.ones(1), torch.full((1,), 100.0), torch.zeros(1, 3))
+    img, _, _ = oracle_raster.render(means, cov, sh, op, cams, hw, 1, 0)
+    c = img[0, :, 16, 16]
+    assert c[2] > c[0] * 10
+
+
+# ----------------------------------------------------------------------------- GPU parity
+
+
+def _run_both(g, cams_cpu, hw, vps, deg, device, capacity=None):
+    color_ref, radii_ref, counts = oracle_raster.render(
+        g["means"], g["covariances"], g["harmonics"], g["opacities"], cams_cpu, hw, vps, deg)
+    gd = {k: v.to(device) for k, v in g.items()}
+    color, radii = rasterize(gd["means"], gd["covariances"], gd["harmonics"], gd["opacities"],
+                             cams_cpu.to(device), hw, vps, sh_degree=deg, capacity=capacity)
+    torch.cuda.synchronize()
+    return color.cpu().numpy(), radii.cpu().numpy(), color_ref, radii_ref, counts
+
+
+def _assert_parity(color, radii, color_ref, radii_ref):
+    np.testing.assert_array_equal(radii, radii_ref)
+    err = np.abs(color - color_ref).max()
+    assert err <= ATOL, f"L-inf {err:.3e} > {ATOL}"
+
+
+def _target_cams(batch, hw, bg=None):
+    t = batch["target"]
+    b, v = t["near"].shape
+    ext = t["extrinsics"].reshape(b * v, 4, 4)
+    K = t["intrinsics"].reshape(b * v, 3, 3)
+    bgv = torch.zeros(b * v, 3) if bg is None else torch.tensor(bg, dtype=torch.float32).expand(b * v, 3)
+    return prepare_cameras(ext, K, t["near"].reshape(-1), t["far"].reshape(-1), bgv)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("deg", [3, 4, 0])
+def test_raster_small_scene_parity(device, deg):
+    hw = (64, 64)
+    g = S.make_gaussians(1, image_shape=hw)
+    cams = _target_cams(S.make_batch(1, image_shape=hw), hw)
+    _assert_parity(*_run_both(g, cams, hw, 3, deg, device)[:4])
+
+
+@pytest.mark.gpu
+def test_raster_multi_scene_batch_nonzero_bg(device):
+    hw = (48, 80)  # not a multiple of 16 in one axis, non-square
+    g = S.make_gaussians(3, image_shape=hw)
+    cams = _target_cams(S.make_batch(3, image_shape=hw), hw, bg=(0.3, 0.6, 0.9))
+    _assert_parity(*_run_both(g, cams, hw, 3, 3, device)[:4])
+
+
+@pytest.mark.gpu
+def test_raster_full_size_scene_parity(device):
+    hw = (256, 256)
+    g = S.make_gaussians(1, image_shape=hw)
+    cams = _target_cams(S.make_batch(1, image_shape=hw), hw)
+    color, radii, cref, rref, counts = _run_both(g, cams, hw, 3, 3, device)
+    _assert_parity(color, radii, cref, rref)
+    assert min(counts) > 100_000
+
+
+@pytest.mark.gpu
+def test_raster_near_plane_and_behind_camera(device):
+    hw = (64, 64)
+    g = S.make_gaussians(1, image_shape=hw, depth_range=(0.05, 3.0))  # many below z = 0.2
+    cams = _target_cams(S.make_batch(1, image_shape=hw), hw)
+    color, radii, cref, rref, _ = _run_both(g, cams, hw, 3, 3, device)
+    _assert_parity(color, radii, cref, rref)
+    assert (rref == 0).sum() > 0
+
+
+@pytest.mark.gpu
+def test_raster_long_tile_lists_global_sort_path(device):
+    """> 4096 instances in one tile exercises the in-global-memory bitonic path."""
+    n = 9000
+    gen = torch.Generator().manual_seed(5)
+    means = torch.zeros((1, n, 3))
+    means[0, :, 0] = (torch.rand(n, generator=gen) - 0.5) * 0.05
+    means[0, :, 1] = (torch.rand(n, generator=gen) - 0.5) * 0.05
+    means[0, :, 2] = 4.0 + torch.rand(n, generator=gen)
+    cov = (torch.eye(3) * 1e-4).expand(1, n, 3, 3).clone()
+    sh = torch.randn((1, n, 3, 16), generator=gen) * S.sh_mask(3)
+    op = torch.rand((1, n), generator=gen) * 0.3
+    g = {"means": means, "covariances": cov, "harmonics": sh, "opacities": op}
+    cams = _cams(torch.eye(4)[None], S.intrinsics(1), torch.ones(1), torch.full((1,), 100.0), torch.zeros(1, 3))
+    color, radii, cref, rref, counts = _run_both(g, cams, (64, 64), 1, 3, device)
+    assert max(counts) > 4096
+    _assert_parity(color, radii, cref, rref)
+
+
+@pytest.mark.gpu
+def test_raster_saturation_and_early_stop(device):
+    """Opaque stacks: alpha clamps at 0.99 and pixels stop at T < 1e-4."""
+    n = 64
+    means = torch.zeros((1, n, 3))
+    means[0, :, 2] = torch.linspace(2, 6, n)
+    cov = (torch.eye(3) * 0.5).expand(1, n, 3, 3).clone()
+    sh = torch.rand((1, n, 3, 1)) * 2
+    op = torch.ones((1, n))
+    g = {"means": means, "covariances": cov, "harmonics": sh, "opacities": op}
+    cams = _cams(torch.eye(4)[None], S.intrinsics(1), torch.ones(1), torch.full((1,), 100.0), torch.full((1, 3), 0.5))
+    _assert_parity(*_run_both(g, cams, (32, 32), 1, 0, device)[:4])
+
+
+@pytest.mark.gpu
+def test_raster_capacity_overflow_is_reported(device):
+    hw = (64, 64)
+    g = S.make_gaussians(1, image_shape=hw)
+    cams = _target_cams(S.make_batch(1, image_shape=hw), hw).to(device)
+    gd = {k: v.to(device) for k, v in g.items()}
+    with pytest.raises(RuntimeError, match="capacity"):
+        rasterize(gd["means"], gd["covariances"], gd["harmonics"], gd["opacities"], cams, hw, 3,
+                  capacity=1000)

@@ -1,0 +1,107 @@
+"""ctypes binding of the C-ABI in include/transplat_hip.h.
+
+The product path has exactly one implementation: the gfx950 HIP library built in-tree
+(`transplat_amd/libtransplat_hip.so`). There is no CPU or PyTorch fallback; if the library is
+missing or a tensor is not on a HIP device, the call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+_LIB_PATH = Path(__file__).resolve().parent / "libtransplat_hip.so"
+_lib = None
+
+
+class RasterDesc(ctypes.Structure):
+    _fields_ = [
+        ("num_gaussians", ctypes.c_int32),
+        ("num_views", ctypes.c_int32),
+        ("views_per_scene", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("sh_coeffs", ctypes.c_int32),
+        ("sh_degree", ctypes.c_int32),
+        ("capacity", ctypes.c_int32),
+    ]
+
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+
+# name -> (restype, argtypes); must match include/transplat_hip.h exactly
+SIGNATURES = {
+    "tsplat_version": (ctypes.c_int, []),
+    "tsplat_prof_enable": (ctypes.c_int, [_I32]),
+    "tsplat_prof_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I32)]),
+    "tsplat_raster_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, _I32, _I32, _I32]),
+    "tsplat_raster_fwd": (
+        ctypes.c_int,
+        [ctypes.POINTER(RasterDesc)] + [_P] * 15,
+    ),
+}
+
+ERRORS = {-1: "invalid argument", -2: "HIP launch error"}
+
+
+def lib_path() -> Path:
+    return _LIB_PATH
+
+
+def load(build_if_missing: bool = False):
+    """Load the HIP library (torch must already be imported so its HIP runtime is the one used)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not _LIB_PATH.exists():
+        if build_if_missing:
+            from .build import build
+
+            build()
+        else:
+            raise RuntimeError(
+                f"transplat HIP library not built ({_LIB_PATH}); run `python -m transplat_amd.build`"
+            )
+    lib = ctypes.CDLL(str(_LIB_PATH), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        raise RuntimeError(f"{what} failed: {ERRORS.get(status, status)}")
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("transplat HIP ops need device tensors (no CPU path)")
+    return t.data_ptr()
+
+
+def stream_ptr(device: torch.device | None = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+PROF_IDS = {"raster_preprocess": 1, "raster_scan": 2, "raster_scatter": 3, "raster_render": 4,
+            "uv_coarse": 5, "uv_cross": 6, "msda": 7, "win_attn": 8, "raster": 9}
+
+
+def prof_enable(name: str | None) -> None:
+    check(load().tsplat_prof_enable(PROF_IDS[name] if name else 0), "tsplat_prof_enable")
+
+
+def prof_read() -> tuple[float, int]:
+    """(total ms, launches) of the kernel being timed since the last enable/read."""
+    ms = ctypes.c_double(0.0)
+    n = _I32(0)
+    check(load().tsplat_prof_read(ctypes.byref(ms), ctypes.byref(n)), "tsplat_prof_read")
+    return ms.value, n.value

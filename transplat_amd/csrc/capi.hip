@@ -1,0 +1,72 @@
+// Library identification + the kernel-timing facility of the C-ABI (include/transplat_hip.h).
+#include <vector>
+
+#include "prof.h"
+
+namespace tsplat {
+namespace prof {
+
+static int g_active = kNone;
+static std::vector<hipEvent_t> g_ev;  // begin/end pairs
+static size_t g_used = 0;             // events recorded
+static bool g_open = false;
+
+int active() { return g_active; }
+
+static hipEvent_t next_event() {
+    if (g_used >= g_ev.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        g_ev.push_back(e);
+    }
+    return g_ev[g_used++];
+}
+
+void begin(int, hipStream_t s) {
+    if (g_open) return;
+    hipEvent_t e = next_event();
+    if (e) {
+        hipEventRecord(e, s);
+        g_open = true;
+    }
+}
+
+void end(int, hipStream_t s) {
+    if (!g_open) return;
+    hipEvent_t e = next_event();
+    if (e) hipEventRecord(e, s);
+    g_open = false;
+}
+
+}  // namespace prof
+}  // namespace tsplat
+
+extern "C" int tsplat_version(void) { return 1; }
+
+extern "C" int tsplat_prof_enable(int32_t kernel_id) {
+    using namespace tsplat::prof;
+    if (kernel_id < 0 || kernel_id >= kNumKernels) return TSPLAT_EINVAL;
+    g_active = kernel_id;
+    g_used = 0;
+    g_open = false;
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_prof_read(double* total_ms, int32_t* launches) {
+    using namespace tsplat::prof;
+    if (!total_ms || !launches) return TSPLAT_EINVAL;
+    double tot = 0.0;
+    int n = 0;
+    for (size_t i = 0; i + 1 < g_used; i += 2) {
+        if (hipEventSynchronize(g_ev[i + 1]) != hipSuccess) return TSPLAT_EHIP;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, g_ev[i], g_ev[i + 1]) != hipSuccess) return TSPLAT_EHIP;
+        tot += ms;
+        ++n;
+    }
+    *total_ms = tot;
+    *launches = n;
+    g_used = 0;
+    g_open = false;
+    return TSPLAT_OK;
+}

@@ -1,0 +1,34 @@
+// Optional per-kernel HIP-event timing (used by bench.py to measure one kernel's average launch
+// duration on the stream it is launched on). Disabled by default: one branch per launch.
+#pragma once
+
+#include "common.h"
+
+namespace tsplat {
+namespace prof {
+
+enum KernelId : int {
+    kNone = 0,
+    kRasterPreprocess = 1,
+    kRasterScan = 2,
+    kRasterScatter = 3,
+    kRasterRender = 4,
+    kUvCoarse = 5,
+    kUvCross = 6,
+    kMsda = 7,
+    kWinAttn = 8,
+    kRasterAll = 9,   // the whole tsplat_raster_fwd launch sequence
+    kNumKernels = 10,
+};
+
+int active();                 // kernel id being timed (0 = off)
+void begin(int kid, hipStream_t s);
+void end(int kid, hipStream_t s);
+
+}  // namespace prof
+}  // namespace tsplat
+
+#define TSPLAT_PROF_BEGIN(kid, s) \
+    if (::tsplat::prof::active() == (kid)) ::tsplat::prof::begin((kid), (s))
+#define TSPLAT_PROF_END(kid, s) \
+    if (::tsplat::prof::active() == (kid)) ::tsplat::prof::end((kid), (s))

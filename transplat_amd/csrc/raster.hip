@@ -1,0 +1,573 @@
+// Gaussian-splat forward rasterizer for gfx950 (MI355X).
+//
+// Algorithm = the graphdeco forward rasterizer behind `GaussianRasterizer` as called by
+// `render_cuda` (reference src/model/decoder/cuda_splatting.py:56-136): preprocess (cull at
+// z_view <= 0.2, EWA 2-D covariance with the 1.3*tan(fov) clamp and +0.3 low-pass, conic, 3-sigma
+// radius, 16x16 tile rect, SH -> RGB), binning of (Gaussian, tile) instances, front-to-back depth
+// order per tile, alpha blending with the 1/255 skip, 0.99 cap and T < 1e-4 stop.
+//
+// MI355X-first structure (not a translation of the CUDA one):
+//   * every view of every scene is rendered by ONE set of launches (blockIdx.y = view); the
+//     reference loops views in Python with two host syncs per view;
+//   * no global radix sort: tiles are binned by a block-aggregated counting pass (LDS histogram,
+//     one global atomic per (block, tile)), and each tile's list is ordered by a bitonic sort in
+//     LDS inside the render kernel, keyed (depth bits << 32 | gaussian id) -- exactly the
+//     (depth, id) order of the reference's stable sort over id-ordered duplicates;
+//   * per-(view, Gaussian) records are packed float2/float4 SoA so the render kernel's staging
+//     reads are 8/16-byte vector loads.
+//
+// Floating point: contraction is OFF in this file so that the preprocess / alpha arithmetic is
+// reproducible bit for bit by the CPU restatement in oracle/raster_ref.c (same op order, same
+// exp polynomial). Threshold tests (alpha < 1/255, radius ceil, depth order) are discontinuous,
+// so bitwise agreement is what makes an L-inf 1e-4 image check meaningful.
+#pragma clang fp contract(off)
+
+#include "common.h"
+#include "prof.h"
+
+namespace tsplat {
+namespace raster {
+
+constexpr int kTile = 16;                 // BLOCK_X = BLOCK_Y of the reference rasterizer
+constexpr int kTileThreads = kTile * kTile;
+constexpr int kSortCap = 4096;            // tile lists up to this length are sorted in LDS
+constexpr int kPreThreads = 256;
+
+__constant__ float kSH_C0 = 0.28209479177387814f;
+__constant__ float kSH_C1 = 0.4886025119029199f;
+__constant__ float kSH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                                -1.0925484305920792f, 0.5462742152960396f};
+__constant__ float kSH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                                0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                                -0.5900435899266435f};
+// Degree-4 real SH constants (same sign convention as the lower degrees).
+__constant__ float kSH_C4[9] = {2.5033429417967046f, -1.7701307697799304f, 0.9461746957575601f,
+                                -0.6690465435572892f, 0.10578554691520431f, -0.6690465435572892f,
+                                0.47308734787878004f, -1.7701307697799304f, 0.6258357354491761f};
+
+// exp(x) for x <= 0 (Cephes range reduction + degree-5 polynomial). Identical op sequence in
+// oracle/raster_ref.c so both sides produce the same float.
+__device__ __forceinline__ float exp_neg(float x) {
+    if (x < -87.0f) return 0.0f;
+    float kf = rintf(x * 1.44269504088896341f);
+    float r = x - kf * 0.693359375f;
+    r = r - kf * -2.12194440e-4f;
+    float z = r * r;
+    float p = 1.9875691500e-4f;
+    p = p * r + 1.3981999507e-3f;
+    p = p * r + 8.3334519073e-3f;
+    p = p * r + 4.1665795894e-2f;
+    p = p * r + 1.6666665459e-1f;
+    p = p * r + 5.0000001201e-1f;
+    p = p * z + r + 1.0f;
+    int k = (int)kf;
+    return p * __int_as_float((k + 127) << 23);
+}
+
+struct Workspace {
+    float4* xy;          // [V*G] pixel-space mean + half-extents of the alpha >= 1/255 ellipse
+    float4* conic_o;     // [V*G] conic (a, b, c) + opacity
+    float4* rgbd;        // [V*G] rgb + view-space depth
+    uint32_t* counts;    // [V*T]
+    uint32_t* offsets;   // [V*T + 1]
+    uint32_t* cursor;    // [V*T]
+    uint64_t* keys;      // [capacity]
+};
+
+__host__ __device__ inline Workspace carve(void* base, int G, int V, int T, int capacity,
+                                           size_t* total) {
+    Workspace w;
+    size_t off = 0;
+    char* p = (char*)base;
+    auto take = [&](size_t bytes) {
+        char* r = p ? p + off : nullptr;
+        off = align_up(off + bytes, 256);
+        return r;
+    };
+    size_t n = (size_t)V * G;
+    w.xy = (float4*)take(n * sizeof(float4));
+    w.conic_o = (float4*)take(n * sizeof(float4));
+    w.rgbd = (float4*)take(n * sizeof(float4));
+    // counts + cursor contiguous so one memset clears both
+    w.counts = (uint32_t*)take((size_t)2 * V * T * sizeof(uint32_t));
+    w.cursor = w.counts ? w.counts + (size_t)V * T : nullptr;
+    w.offsets = (uint32_t*)take(((size_t)V * T + 1) * sizeof(uint32_t));
+    w.keys = (uint64_t*)take((size_t)capacity * sizeof(uint64_t));
+    if (total) *total = off;
+    return w;
+}
+
+struct Params {
+    int G, V, vps, H, W, M, deg, tiles_x, tiles_y, T, capacity;
+};
+
+__device__ __forceinline__ void get_rect(float px, float py, int r, int tx, int ty, int& x0,
+                                         int& y0, int& x1, int& y1) {
+    // (int) truncation and clamps exactly as the reference getRect (auxiliary.h)
+    x0 = min(tx, max(0, (int)((px - (float)r) / (float)kTile)));
+    y0 = min(ty, max(0, (int)((py - (float)r) / (float)kTile)));
+    x1 = min(tx, max(0, (int)((px + (float)r + (float)(kTile - 1)) / (float)kTile)));
+    y1 = min(ty, max(0, (int)((py + (float)r + (float)(kTile - 1)) / (float)kTile)));
+}
+
+__device__ __forceinline__ void sh_to_rgb(const float* __restrict__ sh, int M, int deg, float dx,
+                                          float dy, float dz, float out[3]) {
+    // sh is colour-major [3][M]; coefficient k of channel c is sh[c*M + k]
+    float len = sqrtf(dx * dx + dy * dy + dz * dz);
+    float x = dx / len, y = dy / len, z = dz / len;
+    float xx = x * x, yy = y * y, zz = z * z;
+    float xy = x * y, yz = y * z, xz = x * z;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float* s = sh + c * M;
+        float r = kSH_C0 * s[0];
+        if (deg > 0) {
+            r = r - kSH_C1 * y * s[1] + kSH_C1 * z * s[2] - kSH_C1 * x * s[3];
+            if (deg > 1) {
+                r = r + kSH_C2[0] * xy * s[4] + kSH_C2[1] * yz * s[5] +
+                    kSH_C2[2] * (2.0f * zz - xx - yy) * s[6] + kSH_C2[3] * xz * s[7] +
+                    kSH_C2[4] * (xx - yy) * s[8];
+                if (deg > 2) {
+                    r = r + kSH_C3[0] * y * (3.0f * xx - yy) * s[9] + kSH_C3[1] * xy * z * s[10] +
+                        kSH_C3[2] * y * (4.0f * zz - xx - yy) * s[11] +
+                        kSH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * s[12] +
+                        kSH_C3[4] * x * (4.0f * zz - xx - yy) * s[13] +
+                        kSH_C3[5] * z * (xx - yy) * s[14] + kSH_C3[6] * x * (xx - 3.0f * yy) * s[15];
+                    if (deg > 3) {
+                        r = r + kSH_C4[0] * xy * (xx - yy) * s[16] +
+                            kSH_C4[1] * yz * (3.0f * xx - yy) * s[17] +
+                            kSH_C4[2] * xy * (7.0f * zz - 1.0f) * s[18] +
+                            kSH_C4[3] * yz * (7.0f * zz - 3.0f) * s[19] +
+                            kSH_C4[4] * (zz * (35.0f * zz - 30.0f) + 3.0f) * s[20] +
+                            kSH_C4[5] * xz * (7.0f * zz - 3.0f) * s[21] +
+                            kSH_C4[6] * (xx - yy) * (7.0f * zz - 1.0f) * s[22] +
+                            kSH_C4[7] * xz * (xx - 3.0f * yy) * s[23] +
+                            kSH_C4[8] * (xx * (xx - 3.0f * yy) - yy * (3.0f * xx - yy)) * s[24];
+                    }
+                }
+            }
+        }
+        r = r + 0.5f;
+        out[c] = fmaxf(r, 0.0f);
+    }
+}
+
+// --- K1: preprocess + per-tile instance counts ----------------------------------------------
+__global__ void __launch_bounds__(kPreThreads)
+preprocess_kernel(Params p, const float* __restrict__ means, const float* __restrict__ cov,
+                  const float* __restrict__ shs, const float* __restrict__ opacity,
+                  const float* __restrict__ viewmat, const float* __restrict__ projmat,
+                  const float* __restrict__ campos, const float* __restrict__ tanfov,
+                  const float* __restrict__ scene_scale, int32_t* __restrict__ out_radii,
+                  Workspace ws) {
+    extern __shared__ uint32_t hist[];  // [T]
+    const int v = blockIdx.y;
+    const int g = blockIdx.x * kPreThreads + threadIdx.x;
+    for (int i = threadIdx.x; i < p.T; i += kPreThreads) hist[i] = 0;
+    __syncthreads();
+
+    if (g < p.G) {
+        const size_t vg = (size_t)v * p.G + g;
+        const int scene = v / p.vps;
+        const size_t sg = (size_t)scene * p.G + g;
+        const float* vm = viewmat + 16 * v;
+        const float* pm = projmat + 16 * v;
+        const float s = scene_scale[2 * v], s2 = scene_scale[2 * v + 1];
+        int radius = 0;
+        // scale-invariant rendering: means * s, cov * s^2 (cuda_splatting.py:73-80)
+        const float mx = means[3 * sg] * s, my = means[3 * sg + 1] * s, mz = means[3 * sg + 2] * s;
+        // in_frustum: view-space depth test (auxiliary.h in_frustum)
+        const float vx = vm[0] * mx + vm[4] * my + vm[8] * mz + vm[12];
+        const float vy = vm[1] * mx + vm[5] * my + vm[9] * mz + vm[13];
+        const float vz = vm[2] * mx + vm[6] * my + vm[10] * mz + vm[14];
+        bool ok = vz > 0.2f;
+        float px = 0.f, py = 0.f, conic_a = 0.f, conic_b = 0.f, conic_c = 0.f;
+        float cov_a = 0.f, cov_c = 0.f;
+        int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+        if (ok) {
+            const float hx = pm[0] * mx + pm[4] * my + pm[8] * mz + pm[12];
+            const float hy = pm[1] * mx + pm[5] * my + pm[9] * mz + pm[13];
+            const float hw = pm[3] * mx + pm[7] * my + pm[11] * mz + pm[15];
+            const float pw = 1.0f / (hw + 0.0000001f);
+            const float ndc_x = hx * pw, ndc_y = hy * pw;
+            const float* C = cov + 9 * sg;
+            const float c00 = C[0] * s2, c01 = C[1] * s2, c02 = C[2] * s2;
+            const float c11 = C[4] * s2, c12 = C[5] * s2, c22 = C[8] * s2;
+            // EWA splatting (computeCov2D)
+            const float tfx = tanfov[2 * v], tfy = tanfov[2 * v + 1];
+            const float fx = (float)p.W / (2.0f * tfx), fy = (float)p.H / (2.0f * tfy);
+            const float limx = 1.3f * tfx, limy = 1.3f * tfy;
+            const float tz = vz;
+            const float tx = fminf(limx, fmaxf(-limx, vx / tz)) * tz;
+            const float ty = fminf(limy, fmaxf(-limy, vy / tz)) * tz;
+            const float j00 = fx / tz, j02 = -(fx * tx) / (tz * tz);
+            const float j11 = fy / tz, j12 = -(fy * ty) / (tz * tz);
+            // M = J * R_w2c, R[r][c] = vm[c*4 + r]
+            const float m00 = j00 * vm[0] + j02 * vm[2];
+            const float m01 = j00 * vm[4] + j02 * vm[6];
+            const float m02 = j00 * vm[8] + j02 * vm[10];
+            const float m10 = j11 * vm[1] + j12 * vm[2];
+            const float m11 = j11 * vm[5] + j12 * vm[6];
+            const float m12 = j11 * vm[9] + j12 * vm[10];
+            const float u00 = m00 * c00 + m01 * c01 + m02 * c02;
+            const float u01 = m00 * c01 + m01 * c11 + m02 * c12;
+            const float u02 = m00 * c02 + m01 * c12 + m02 * c22;
+            const float u10 = m10 * c00 + m11 * c01 + m12 * c02;
+            const float u11 = m10 * c01 + m11 * c11 + m12 * c12;
+            const float u12 = m10 * c02 + m11 * c12 + m12 * c22;
+            const float a = u00 * m00 + u01 * m01 + u02 * m02 + 0.3f;
+            const float b = u00 * m10 + u01 * m11 + u02 * m12;
+            const float c = u10 * m10 + u11 * m11 + u12 * m12 + 0.3f;
+            const float det = a * c - b * b;
+            cov_a = a;
+            cov_c = c;
+            ok = det != 0.0f;
+            if (ok) {
+                const float det_inv = 1.0f / det;
+                conic_a = c * det_inv;
+                conic_b = -b * det_inv;
+                conic_c = a * det_inv;
+                const float mid = 0.5f * (a + c);
+                const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+                const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+                radius = (int)ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
+                px = ((ndc_x + 1.0f) * (float)p.W - 1.0f) * 0.5f;
+                py = ((ndc_y + 1.0f) * (float)p.H - 1.0f) * 0.5f;
+                get_rect(px, py, radius, p.tiles_x, p.tiles_y, x0, y0, x1, y1);
+                ok = (x1 - x0) * (y1 - y0) != 0;
+            }
+        }
+        if (ok) {
+            float rgb[3];
+            const float* cp = campos + 3 * v;
+            sh_to_rgb(shs + (size_t)3 * p.M * sg, p.M, p.deg, mx - cp[0], my - cp[1], mz - cp[2],
+                      rgb);
+            // Conservative half-extents of the region where o * exp(power) >= 1/255 (power =
+            // -Q/2, Q <= 2 ln(255 o)); lets a wave skip Gaussians that miss its 8x8 pixels.
+            // Pure culling: pixels inside keep the exact reference arithmetic.
+            const float o = opacity[sg];
+            float ex = INFINITY, ey = INFINITY;
+            if (o == o) {
+                const float q = 2.0f * logf(255.0f * o);
+                if (q < 0.0f) {
+                    ex = ey = -1.0f;  // alpha < 1/255 everywhere
+                } else if (cov_a > 0.0f && cov_c > 0.0f && q < INFINITY) {
+                    ex = sqrtf(q * cov_a) * 1.001f + 0.01f;
+                    ey = sqrtf(q * cov_c) * 1.001f + 0.01f;
+                }
+            }
+            ws.xy[vg] = make_float4(px, py, ex, ey);
+            ws.conic_o[vg] = make_float4(conic_a, conic_b, conic_c, o);
+            ws.rgbd[vg] = make_float4(rgb[0], rgb[1], rgb[2], vz);
+            for (int ty = y0; ty < y1; ++ty)
+                for (int tx = x0; tx < x1; ++tx) atomicAdd(&hist[ty * p.tiles_x + tx], 1u);
+        } else {
+            radius = 0;
+        }
+        out_radii[vg] = radius;
+    }
+    __syncthreads();
+    uint32_t* gcount = ws.counts + (size_t)v * p.T;
+    for (int i = threadIdx.x; i < p.T; i += kPreThreads)
+        if (hist[i]) atomicAdd(&gcount[i], hist[i]);
+}
+
+// --- K2: exclusive scan of the V*T tile counts (single workgroup) ----------------------------
+constexpr int kScanThreads = 1024;
+__global__ void __launch_bounds__(kScanThreads)
+scan_kernel(int n, int capacity, const uint32_t* __restrict__ counts,
+            uint32_t* __restrict__ offsets, int32_t* __restrict__ status) {
+    __shared__ uint32_t wsum[kScanThreads / kWave];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
+    for (int base = 0; base < n; base += kScanThreads) {
+        const int i = base + threadIdx.x;
+        uint32_t x = i < n ? counts[i] : 0u;
+        uint32_t incl = x;
+#pragma unroll
+        for (int d = 1; d < kWave; d <<= 1) {
+            uint32_t y = __shfl_up(incl, d, kWave);
+            if (lane >= d) incl += y;
+        }
+        if (lane == kWave - 1) wsum[wid] = incl;
+        __syncthreads();
+        if (wid == 0) {
+            uint32_t w = lane < kScanThreads / kWave ? wsum[lane] : 0u;
+            uint32_t wi = w;
+#pragma unroll
+            for (int d = 1; d < kScanThreads / kWave; d <<= 1) {
+                uint32_t y = __shfl_up(wi, d, kWave);
+                if (lane >= d) wi += y;
+            }
+            if (lane < kScanThreads / kWave) wsum[lane] = wi - w;  // exclusive wave prefix
+        }
+        __syncthreads();
+        const uint32_t c0 = carry;
+        if (i < n) offsets[i] = c0 + wsum[wid] + incl - x;
+        __syncthreads();
+        if (threadIdx.x == kScanThreads - 1) carry = c0 + wsum[wid] + incl;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        offsets[n] = carry;
+        if (carry > (uint32_t)capacity) atomicOr(status, 1);
+    }
+}
+
+// --- K3: scatter (gaussian, tile) instances into per-tile ranges ------------------------------
+__global__ void __launch_bounds__(kPreThreads)
+scatter_kernel(Params p, const int32_t* __restrict__ radii, Workspace ws) {
+    extern __shared__ uint32_t lds[];  // hist[T] then base[T]
+    uint32_t* hist = lds;
+    uint32_t* base = lds + p.T;
+    const int v = blockIdx.y;
+    const int g = blockIdx.x * kPreThreads + threadIdx.x;
+    for (int i = threadIdx.x; i < p.T; i += kPreThreads) hist[i] = 0;
+    __syncthreads();
+    int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    uint64_t key_lo = 0, depth_bits = 0;
+    const size_t vg = (size_t)v * p.G + g;
+    if (g < p.G) {
+        r = radii[vg];
+        if (r > 0) {
+            float4 xy = ws.xy[vg];
+            get_rect(xy.x, xy.y, r, p.tiles_x, p.tiles_y, x0, y0, x1, y1);
+            depth_bits = (uint64_t)__float_as_uint(ws.rgbd[vg].w);
+            key_lo = (uint64_t)(uint32_t)g;
+            for (int ty = y0; ty < y1; ++ty)
+                for (int tx = x0; tx < x1; ++tx) atomicAdd(&hist[ty * p.tiles_x + tx], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t* gcur = ws.cursor + (size_t)v * p.T;
+    const uint32_t* goff = ws.offsets + (size_t)v * p.T;
+    for (int i = threadIdx.x; i < p.T; i += kPreThreads) {
+        uint32_t h = hist[i];
+        base[i] = h ? goff[i] + atomicAdd(&gcur[i], h) : 0u;
+        hist[i] = 0;
+    }
+    __syncthreads();
+    if (r > 0) {
+        const uint64_t key = (depth_bits << 32) | key_lo;
+        for (int ty = y0; ty < y1; ++ty)
+            for (int tx = x0; tx < x1; ++tx) {
+                const int t = ty * p.tiles_x + tx;
+                const uint32_t pos = base[t] + atomicAdd(&hist[t], 1u);
+                if (pos < (uint32_t)p.capacity) ws.keys[pos] = key;
+            }
+    }
+}
+
+// Bitonic sort (all-ascending "mirror" network) of n keys held in `buf`, virtual length
+// next_pow2(n); positions >= n behave as +inf and never move, so no padding is written.
+template <typename Ptr>
+__device__ __forceinline__ void bitonic_sort(Ptr buf, int n) {
+    int logP = 0;
+    while ((1 << logP) < n) ++logP;
+    const int half = (1 << logP) >> 1;
+    for (int lk = 1; lk <= logP; ++lk) {
+        for (int lj = lk - 1; lj >= 0; --lj) {
+            const int j = 1 << lj;
+            for (int i = threadIdx.x; i < half; i += kTileThreads) {
+                const int blk = i >> lj, q = i & (j - 1);
+                int a, b;
+                if (lj == lk - 1) {  // first step of a merge: compare mirrored pairs
+                    a = (blk << (lj + 1)) + q;
+                    b = (blk << (lj + 1)) + (2 * j - 1 - q);
+                } else {
+                    a = (blk << (lj + 1)) + q;
+                    b = a + j;
+                }
+                if (b < n) {
+                    const uint64_t ka = buf[a], kb = buf[b];
+                    if (ka > kb) {
+                        buf[a] = kb;
+                        buf[b] = ka;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// --- K4: per-tile depth sort + front-to-back alpha blending ---------------------------------
+// One workgroup per (tile, view); each wave owns an 8x8 pixel block. Gaussians are staged in
+// batches of 256 in LDS; every wave then compacts, in depth order, the entries whose
+// alpha >= 1/255 ellipse can touch its block (conservative, so exact) and blends only those
+// with branch-free selects (no exec-mask flow per Gaussian), leaving as soon as all its 64
+// pixels are saturated.
+__global__ void __launch_bounds__(kTileThreads)
+render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_color,
+              Workspace ws) {
+    __shared__ uint64_t skeys[kSortCap];
+    __shared__ float4 s_xy[kTileThreads];
+    __shared__ float4 s_co[kTileThreads];
+    __shared__ float4 s_rgb[kTileThreads];
+    __shared__ uint16_t s_list[kTileThreads / kWave][kTileThreads];
+
+    const int v = blockIdx.y;
+    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const int tx = tile % p.tiles_x, ty = tile / p.tiles_x;
+    const int t_idx = v * p.T + tile;
+    uint32_t start = ws.offsets[t_idx];
+    uint32_t end = ws.offsets[t_idx + 1];
+    if (end > (uint32_t)p.capacity) end = (uint32_t)p.capacity;
+    if (start > end) start = end;
+    const int n = (int)(end - start);
+
+    uint64_t* gkeys = ws.keys + start;
+    const bool in_lds = n <= kSortCap;
+    if (in_lds) {
+        for (int i = threadIdx.x; i < n; i += kTileThreads) skeys[i] = gkeys[i];
+        __syncthreads();
+        bitonic_sort(skeys, n);
+    } else {
+        bitonic_sort(gkeys, n);  // rare: very long tile list, sorted in place in global memory
+    }
+
+    const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    const int lx = (wid & 1) * 8 + (lane & 7), ly = (wid >> 1) * 8 + (lane >> 3);
+    const int pxi = tx * kTile + lx, pyi = ty * kTile + ly;
+    const float wx0 = (float)(tx * kTile + (wid & 1) * 8), wx1 = wx0 + 7.0f;
+    const float wy0 = (float)(ty * kTile + (wid >> 1) * 8), wy1 = wy0 + 7.0f;
+    const bool inside = pxi < p.W && pyi < p.H;
+    bool done = !inside;
+    const float pfx = (float)pxi, pfy = (float)pyi;
+    float T = 1.0f;
+    float C0 = 0.f, C1 = 0.f, C2 = 0.f;
+    const size_t vbase = (size_t)v * p.G;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+
+    for (int b0 = 0; b0 < n; b0 += kTileThreads) {
+        if (__syncthreads_count(done) == kTileThreads) break;
+        const int k = b0 + threadIdx.x;
+        if (k < n) {
+            const uint64_t key = in_lds ? skeys[k] : gkeys[k];
+            const size_t id = vbase + (uint32_t)(key & 0xffffffffu);
+            s_xy[threadIdx.x] = ws.xy[id];
+            s_co[threadIdx.x] = ws.conic_o[id];
+            s_rgb[threadIdx.x] = ws.rgbd[id];
+        }
+        __syncthreads();
+        const int cnt = min(kTileThreads, n - b0);
+        // order-preserving compaction of this wave's candidates
+        int m = 0;
+#pragma unroll
+        for (int c = 0; c < kTileThreads / kWave; ++c) {
+            const int e = c * kWave + lane;
+            bool hit = false;
+            if (e < cnt) {
+                const float4 xy = s_xy[e];
+                hit = !(xy.x + xy.z < wx0 || xy.x - xy.z > wx1 || xy.y + xy.w < wy0 ||
+                        xy.y - xy.w > wy1);
+            }
+            const uint64_t mask = __ballot(hit);
+            if (hit) s_list[wid][m + __popcll(mask & lt_mask)] = (uint16_t)e;
+            m += __popcll(mask);
+        }
+        __syncthreads();
+        for (int i = 0; i < m; ++i) {
+            if (__all(done)) break;
+            const int e = s_list[wid][i];
+            const float4 xy = s_xy[e];
+            const float4 co = s_co[e];
+            const float4 c = s_rgb[e];
+            const float dx = xy.x - pfx, dy = xy.y - pfy;
+            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            const float alpha = fminf(0.99f, co.w * exp_neg(power));
+            const float test_T = T * (1.0f - alpha);
+            // reference order: skip power > 0, skip alpha < 1/255, stop if test_T < 1e-4
+            const bool contrib = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const bool stop = contrib && (test_T < 0.0001f);
+            const bool acc = contrib && !stop;
+            C0 = acc ? C0 + c.x * alpha * T : C0;
+            C1 = acc ? C1 + c.y * alpha * T : C1;
+            C2 = acc ? C2 + c.z * alpha * T : C2;
+            T = acc ? test_T : T;
+            done = done || stop;
+        }
+    }
+    if (inside) {
+        const size_t hw = (size_t)p.H * p.W;
+        float* o = out_color + (size_t)v * 3 * hw + (size_t)pyi * p.W + pxi;
+        const float* bgv = bg + 3 * v;
+        o[0] = C0 + T * bgv[0];
+        o[hw] = C1 + T * bgv[1];
+        o[2 * hw] = C2 + T * bgv[2];
+    }
+}
+
+}  // namespace raster
+}  // namespace tsplat
+
+using namespace tsplat;
+using namespace tsplat::raster;
+
+extern "C" size_t tsplat_raster_workspace_bytes(int32_t G, int32_t V, int32_t H, int32_t W,
+                                                int32_t capacity) {
+    const int T = ceil_div(W, kTile) * ceil_div(H, kTile);
+    size_t total = 0;
+    carve(nullptr, G, V, T, capacity, &total);
+    return total;
+}
+
+extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means, const float* cov,
+                                 const float* shs, const float* opacity, const float* viewmat,
+                                 const float* projmat, const float* campos, const float* tanfov,
+                                 const float* bg, const float* scene_scale, float* out_color,
+                                 int32_t* out_radii, void* workspace, int32_t* status,
+                                 void* stream_) {
+    if (!d || !means || !cov || !shs || !opacity || !viewmat || !projmat || !campos || !tanfov ||
+        !bg || !scene_scale || !out_color || !out_radii || !workspace || !status)
+        return TSPLAT_EINVAL;
+    if (d->num_gaussians <= 0 || d->num_views <= 0 || d->views_per_scene <= 0 ||
+        d->num_views % d->views_per_scene != 0 || d->height <= 0 || d->width <= 0 ||
+        d->sh_coeffs <= 0 || d->sh_degree < 0 || d->sh_degree > 4 ||
+        (d->sh_degree + 1) * (d->sh_degree + 1) > d->sh_coeffs || d->capacity <= 0)
+        return TSPLAT_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    Params p;
+    p.G = d->num_gaussians;
+    p.V = d->num_views;
+    p.vps = d->views_per_scene;
+    p.H = d->height;
+    p.W = d->width;
+    p.M = d->sh_coeffs;
+    p.deg = d->sh_degree;
+    p.tiles_x = ceil_div(p.W, kTile);
+    p.tiles_y = ceil_div(p.H, kTile);
+    p.T = p.tiles_x * p.tiles_y;
+    p.capacity = d->capacity;
+    if ((size_t)p.T * 2 * sizeof(uint32_t) > 64 * 1024) return TSPLAT_EINVAL;  // LDS histogram
+    Workspace ws = carve(workspace, p.G, p.V, p.T, p.capacity, nullptr);
+
+    TSPLAT_PROF_BEGIN(prof::kRasterAll, stream);
+    TSPLAT_CHECK(hipMemsetAsync(ws.counts, 0, (size_t)2 * p.V * p.T * sizeof(uint32_t), stream));
+    dim3 pre_grid(ceil_div(p.G, kPreThreads), p.V);
+    TSPLAT_PROF_BEGIN(prof::kRasterPreprocess, stream);
+    hipLaunchKernelGGL(preprocess_kernel, pre_grid, dim3(kPreThreads), p.T * sizeof(uint32_t),
+                       stream, p, means, cov, shs, opacity, viewmat, projmat, campos, tanfov,
+                       scene_scale, out_radii, ws);
+    TSPLAT_PROF_END(prof::kRasterPreprocess, stream);
+    TSPLAT_CHECK_LAUNCH();
+    TSPLAT_PROF_BEGIN(prof::kRasterScan, stream);
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, p.V * p.T,
+                       p.capacity, (const uint32_t*)ws.counts, ws.offsets, status);
+    TSPLAT_PROF_END(prof::kRasterScan, stream);
+    TSPLAT_CHECK_LAUNCH();
+    TSPLAT_PROF_BEGIN(prof::kRasterScatter, stream);
+    hipLaunchKernelGGL(scatter_kernel, pre_grid, dim3(kPreThreads), 2 * p.T * sizeof(uint32_t),
+                       stream, p, (const int32_t*)out_radii, ws);
+    TSPLAT_PROF_END(prof::kRasterScatter, stream);
+    TSPLAT_CHECK_LAUNCH();
+    TSPLAT_PROF_BEGIN(prof::kRasterRender, stream);
+    hipLaunchKernelGGL(render_kernel, dim3(p.T, p.V), dim3(kTileThreads), 0, stream, p, bg,
+                       out_color, ws);
+    TSPLAT_PROF_END(prof::kRasterRender, stream);
+    TSPLAT_PROF_END(prof::kRasterAll, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

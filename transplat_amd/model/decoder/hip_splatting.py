@@ -1,0 +1,184 @@
+"""Camera setup + call of the gfx950 Gaussian rasterizer (replaces reference `render_cuda`).
+
+Reference: src/model/decoder/cuda_splatting.py:26-136. The reference repeats the Gaussians
+over every target view, then loops the views in Python (two `.item()` host syncs per view) and
+calls the third-party CUDA rasterizer once per view. Here the per-view camera constants are
+computed once on the device (same torch expressions as the reference) and every view of every
+scene is rasterized by one `tsplat_raster_fwd` call that reads the un-repeated Gaussian buffers.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from math import isqrt
+
+import torch
+from torch import Tensor
+
+from ... import _lib
+from ...geometry.projection import get_fov
+
+
+def get_projection_matrix(near: Tensor, far: Tensor, fov_x: Tensor, fov_y: Tensor) -> Tensor:
+    """(reference cuda_splatting.py:26-53) x/y -> (-1, 1), z -> (0, 1)."""
+    tan_fov_x = (0.5 * fov_x).tan()
+    tan_fov_y = (0.5 * fov_y).tan()
+    top = tan_fov_y * near
+    bottom = -top
+    right = tan_fov_x * near
+    left = -right
+    (b,) = near.shape
+    result = torch.zeros((b, 4, 4), dtype=torch.float32, device=near.device)
+    result[:, 0, 0] = 2 * near / (right - left)
+    result[:, 1, 1] = 2 * near / (top - bottom)
+    result[:, 0, 2] = (right + left) / (right - left)
+    result[:, 1, 2] = (top + bottom) / (top - bottom)
+    result[:, 3, 2] = 1
+    result[:, 2, 2] = far / (far - near)
+    result[:, 2, 3] = -(far * near) / (far - near)
+    return result
+
+
+@dataclass
+class RasterCameras:
+    """Per-view constants in the layouts of `tsplat_raster_fwd` (all fp32, contiguous)."""
+
+    viewmat: Tensor  # [V, 16] column-major view matrix (= inverse(c2w)^T row-major)
+    projmat: Tensor  # [V, 16] column-major full projection
+    campos: Tensor  # [V, 3]
+    tanfov: Tensor  # [V, 2]
+    bg: Tensor  # [V, 3]
+    scale: Tensor  # [V, 2] (s, s^2), s = 1/near when scale-invariant, else 1
+
+    def to(self, device) -> "RasterCameras":
+        return RasterCameras(*(getattr(self, f).to(device) for f in self.__dataclass_fields__))
+
+
+def prepare_cameras(
+    extrinsics: Tensor,
+    intrinsics: Tensor,
+    near: Tensor,
+    far: Tensor,
+    background_color: Tensor,
+    scale_invariant: bool = True,
+) -> RasterCameras:
+    """Camera math of render_cuda (cuda_splatting.py:73-96) for V = (b v) flattened views."""
+    extrinsics = extrinsics.float()
+    if scale_invariant:
+        scale = 1 / near
+        extrinsics = extrinsics.clone()
+        extrinsics[..., :3, 3] = extrinsics[..., :3, 3] * scale[:, None]
+        near = near * scale
+        far = far * scale
+    else:
+        scale = torch.ones_like(near)
+    fov_x, fov_y = get_fov(intrinsics).unbind(dim=-1)
+    tan_fov_x = (0.5 * fov_x).tan()
+    tan_fov_y = (0.5 * fov_y).tan()
+    projection_matrix = get_projection_matrix(near, far, fov_x, fov_y).transpose(1, 2)
+    view_matrix = extrinsics.inverse().transpose(1, 2)
+    full_projection = view_matrix @ projection_matrix
+    v = extrinsics.shape[0]
+    return RasterCameras(
+        viewmat=view_matrix.contiguous().view(v, 16),
+        projmat=full_projection.contiguous().view(v, 16),
+        campos=extrinsics[:, :3, 3].contiguous(),
+        tanfov=torch.stack((tan_fov_x, tan_fov_y), dim=-1).contiguous(),
+        bg=background_color.float().contiguous(),
+        scale=torch.stack((scale, scale * scale), dim=-1).float().contiguous(),
+    )
+
+
+class _RasterState:
+    """Per-device workspace + sticky overflow status (grown on demand, never freed mid-run)."""
+
+    def __init__(self):
+        self.workspace: dict = {}
+        self.status: dict = {}
+
+    def get(self, device, nbytes: int):
+        key = (device.type, device.index)
+        ws = self.workspace.get(key)
+        if ws is None or ws.numel() < nbytes:
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+            self.workspace[key] = ws
+        st = self.status.get(key)
+        if st is None:
+            st = torch.zeros(1, dtype=torch.int32, device=device)
+            self.status[key] = st
+        return ws, st
+
+
+_STATE = _RasterState()
+
+
+def default_capacity(num_gaussians: int, num_views: int) -> int:
+    return max(1 << 20, 24 * num_gaussians * num_views)
+
+
+def rasterize(
+    means: Tensor,
+    covariances: Tensor,
+    harmonics: Tensor,
+    opacities: Tensor,
+    cameras: RasterCameras,
+    image_shape: tuple[int, int],
+    views_per_scene: int,
+    sh_degree: int | None = None,
+    capacity: int | None = None,
+    check: bool = True,
+) -> tuple[Tensor, Tensor]:
+    """Render V = scenes * views_per_scene views.
+
+    means [S, G, 3], covariances [S, G, 3, 3], harmonics [S, G, 3, M], opacities [S, G]
+    -> color [V, 3, H, W], radii [V, G] int32.
+    `sh_degree` defaults to isqrt(M) - 1 (the degree render_cuda passes) capped at the
+    evaluated degree of the upstream rasterizer (3); pass 4 to evaluate degree-4 terms.
+    """
+    lib = _lib.load()
+    s, g, _ = means.shape
+    m = harmonics.shape[-1]
+    v = cameras.viewmat.shape[0]
+    if v != s * views_per_scene:
+        raise ValueError(f"{v} views for {s} scenes x {views_per_scene} views per scene")
+    if covariances.shape != (s, g, 3, 3) or harmonics.shape[:3] != (s, g, 3) or opacities.shape != (s, g):
+        raise ValueError("Gaussian tensor shapes disagree")
+    if sh_degree is None:
+        sh_degree = min(isqrt(m) - 1, 3)
+    h, w = image_shape
+    dev = means.device
+    f32 = lambda t: t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
+    means, covariances, harmonics, opacities = map(f32, (means, covariances, harmonics, opacities))
+    if capacity is None:
+        capacity = default_capacity(g, v)
+    nbytes = int(lib.tsplat_raster_workspace_bytes(g, v, h, w, capacity))
+    ws, status = _STATE.get(dev, nbytes)
+    color = torch.empty((v, 3, h, w), dtype=torch.float32, device=dev)
+    radii = torch.empty((v, g), dtype=torch.int32, device=dev)
+    desc = _lib.RasterDesc(g, v, views_per_scene, h, w, m, sh_degree, capacity)
+    cams = [f32(cameras.viewmat), f32(cameras.projmat), f32(cameras.campos), f32(cameras.tanfov),
+            f32(cameras.bg), f32(cameras.scale)]
+    for t in cams:
+        if t.device != dev:
+            raise ValueError("camera tensors must be on the Gaussians' device")
+    rc = lib.tsplat_raster_fwd(
+        desc,
+        *(_lib.ptr(t) for t in (means, covariances, harmonics, opacities)),
+        *(_lib.ptr(t) for t in cams),
+        _lib.ptr(color),
+        _lib.ptr(radii),
+        _lib.ptr(ws),
+        _lib.ptr(status),
+        _lib.stream_ptr(dev),
+    )
+    _lib.check(rc, "tsplat_raster_fwd")
+    if check:
+        check_status(dev)
+    return color, radii
+
+
+def check_status(device) -> None:
+    """Raise if any rasterizer call on `device` overflowed its instance capacity (syncs)."""
+    st = _STATE.status.get((device.type, device.index))
+    if st is not None and int(st.item()) != 0:
+        st.zero_()
+        raise RuntimeError("tsplat_raster_fwd: instance capacity exceeded; pass a larger capacity")
