@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
+FP32_MFMA_PEAK_TFS = 157.3  # v_mfma_f32_16x16x4_f32 dense peak (= FP32 vector peak)
 RASTER_BYTES_PER_VIEW = None  # computed: G*(12+24+4*d_sh*3+4) + H*W*12
 
 
@@ -34,7 +35,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["e2e", "raster"], default="raster")
+    ap.add_argument("--workload", choices=["e2e", "raster"], default="e2e")
+    ap.add_argument("--dense-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--dominant", default=None, help="kernel timed for the roofline object")
     ap.add_argument("--batch", type=int, default=1, help="scenes per step per GPU")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -83,6 +86,68 @@ def build_raster_workload(batch: int, device, scene_offset: int):
     return step, info, cpu_inputs
 
 
+def e2e_roofline_info(kernel: str, batch: int) -> dict:
+    """Algorithmic HBM bytes (or FLOPs) per launch of the hand-written encoder kernels at 256x256,
+    2 views, D = 128, C = 128, per SURVEY §8d (units per launch = `batch` scenes)."""
+    hw, c, d, p = 64 * 64, 128, 128, 4
+    n = 2 * batch  # (b v) query maps per launch
+    if kernel == "uv_cross":
+        # value (other view) + key + offsets + logits + output, fp32, each read once
+        per = n * hw * (c * 4 + c * 4 + d * p * 2 * 4 + d * p * 4 + d * 4)
+        return {"dominant": kernel, "alg_bytes_per_launch": per, "bound": "hbm"}
+    if kernel == "uv_coarse":
+        per = n * hw * (c * 4 + d * 4) + n * hw * c * 4  # own + other features, output
+        return {"dominant": kernel, "alg_bytes_per_launch": per, "bound": "hbm"}
+    if kernel == "win_attn":
+        # 4 L S d FLOPs per window, 8 windows per scene-call (v = 2), fp32 MFMA
+        return {"dominant": kernel, "alg_flops_per_launch": 4 * 1024 * 1024 * 128 * 8 * batch, "bound": "mfma"}
+    if kernel == "raster":
+        return {"dominant": kernel, "alg_bytes_per_launch": raster_bytes_per_view(131072, 25, 256, 256) * 3 * batch,
+                "bound": "hbm"}
+    raise ValueError(kernel)
+
+
+def cpu_baseline_e2e(model, seconds: float):
+    """The same test_step on the host: the build's modules with the oracle's CPU restatements in
+    place of the HIP kernels and the C oracle rasterizer (kind 'port'), on >= 1 scene."""
+    import copy
+
+    from oracle import encoder_ops as E
+    from oracle import raster as oracle_raster
+    from transplat_amd import kernels
+    from transplat_amd import synthetic as S
+    from transplat_amd.model.decoder.hip_splatting import prepare_cameras
+
+    saved = {n: getattr(kernels, n) for n in ("window_attention", "uv_coarse", "uv_cross", "msda")}
+    for n in saved:
+        setattr(kernels, n, getattr(E, n))
+    threads = torch.get_num_threads()
+    try:
+        enc = copy.deepcopy(model.encoder).float().cpu()
+        enc.cfg.dense_dtype = "fp32"
+        n_views, t0 = 0, time.perf_counter()
+        while True:
+            batch = S.make_batch(1, image_shape=(256, 256))
+            with torch.no_grad():
+                g = enc(batch["context"], 0, deterministic=True)
+            t = batch["target"]
+            cams = prepare_cameras(t["extrinsics"][0], t["intrinsics"][0], t["near"][0], t["far"][0], torch.zeros(3, 3))
+            oracle_raster.render(g.means, g.covariances, g.harmonics, g.opacities, cams, (256, 256), 3, 3)
+            n_views += 3
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    finally:
+        for n, f in saved.items():
+            setattr(kernels, n, f)
+    return {
+        "value": n_views / el, "unit": "views/s", "cores": threads, "kind": "port",
+        "sample": f"{n_views // 3} scene(s) x 3 views, 256x256: the build's encoder modules on CPU (torch, "
+                  f"{threads} threads) with oracle/encoder_ops.py restatements for the HIP kernels + "
+                  f"oracle/raster_ref.c (1 thread), {el:.1f} s, nproc={os.cpu_count()}",
+    }
+
+
 def cpu_baseline_raster(cpu_inputs, seconds: float):
     """Oracle C rasterizer (scalar, 1 thread) on as many views as fit `seconds` (>= 1)."""
     from oracle import raster as oracle_raster
@@ -123,7 +188,12 @@ def main():
     else:
         from transplat_amd.e2e import build_e2e_workload
 
-        step, info, cpu_inputs = build_e2e_workload(args.batch, device, scene_offset=rank * args.batch)
+        step, info, model = build_e2e_workload(args.batch, device, scene_offset=rank * args.batch,
+                                               dense_dtype=args.dense_dtype)
+        info.update(e2e_roofline_info(args.dominant or "uv_cross", args.batch))
+        cpu_inputs = ("e2e", model)
+    if args.dominant and args.workload == "raster":
+        info["dominant"] = args.dominant
 
     for _ in range(args.warmup):
         step()
@@ -154,7 +224,12 @@ def main():
     ms, launches = _lib.prof_read()
     _lib.prof_enable(None)
     avg_ms = ms / max(launches, 1)
-    achieved = info["alg_bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
+    if info.get("bound", "hbm") == "mfma":
+        achieved = info["alg_flops_per_launch"] / (avg_ms * 1e-3) / 1e12
+        peak, unit = FP32_MFMA_PEAK_TFS, "TFLOP/s"
+    else:
+        achieved = info["alg_bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
+        peak, unit = HBM_PEAK_GBS, "GB/s"
 
     views = world * info["views_per_step"] * args.steps
     result = {
@@ -168,7 +243,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": "fp32" if args.workload == "raster" or args.dense_dtype == "fp32" else "bf16+fp32",
         "data": "synthetic",
         "config": {
             "workload": info["workload"],
@@ -179,18 +254,21 @@ def main():
         },
         "roofline": {
             "kernel": info["dominant"],
-            "bound": "hbm",
+            "bound": info.get("bound", "hbm"),
             "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "peak": peak,
+            "unit": unit,
+            "frac": achieved / peak,
             "traffic": None,
             "avg_launch_ms": avg_ms,
             "launches": launches,
         },
     }
     if rank == 0 and not args.no_cpu_baseline and cpu_inputs is not None:
-        result["cpu_baseline"] = cpu_baseline_raster(cpu_inputs, args.cpu_baseline_seconds)
+        if isinstance(cpu_inputs, tuple) and cpu_inputs[0] == "e2e":
+            result["cpu_baseline"] = cpu_baseline_e2e(cpu_inputs[1], args.cpu_baseline_seconds)
+        else:
+            result["cpu_baseline"] = cpu_baseline_raster(cpu_inputs, args.cpu_baseline_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

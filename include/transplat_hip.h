@@ -96,6 +96,51 @@ int tsplat_raster_fwd(const tsplat_raster_desc* desc,
                       float* out_color, int32_t* out_radii,
                       void* workspace, int32_t* status, void* stream);
 
+
+/* ------------------------------------------------------------------------------------------
+ * Depth-candidate correlation (cost volume), all fp32, channel-last features.
+ * Queries are (b v)-ordered: n = 2*b + v (the UVTransformerEncoder layout, utils/encoder.py:44);
+ * cameras and disparities are (v b)-ordered: index v*batch + b (prepare_feat_proj_data_lists).
+ *   cams [2*batch, 30] = K^-1 (9, row-major), K (9), R (9) = pose[:3,:3], t (3) = pose[:3,3] of
+ *                        the relative pose own -> other camera, pixel-unit intrinsics
+ *   disp [2*batch, depths] inverse-depth candidates
+ * Only two views are supported (the reference's match_two pairs views for V > 2).
+ * ---------------------------------------------------------------------------------------- */
+
+/* UVCoarseAttention + calculate_grid: out[n, p, d] = <bilinear(feat[n^1], ref_3d(p, d)),
+ * feat[n, p]> / sqrt(C). feat [2*batch, H*W, C]; out [2*batch, H*W, depths]; C must be 128. */
+int tsplat_uv_coarse_fwd(const float* feat, const float* cams, const float* disp, float* out,
+                         int32_t batch, int32_t height, int32_t width, int32_t channels,
+                         int32_t depths, void* stream);
+
+/* UVCrossAttention core: out[n, p, d] = mean_c key[n, p, c] * sum_pt softmax(logits[n, p, d, :])_pt
+ * * bilinear(value[n^1], ref_3d(p, d) + offsets[n, p, d, pt, :] / (W, H))_c.
+ * value = value_proj output per view (un-flipped), key = raw own feature, both [2*batch, H*W, C];
+ * offsets [2*batch, H*W, depths*points*2]; logits [2*batch, H*W, depths*points];
+ * out [2*batch, H*W, depths]; points <= 8. */
+int tsplat_uv_cross_fwd(const float* value, const float* key, const float* cams,
+                        const float* disp, const float* offsets, const float* logits, float* out,
+                        int32_t batch, int32_t height, int32_t width, int32_t channels,
+                        int32_t depths, int32_t points, void* stream);
+
+/* Single-level single-head multi-scale deformable attention (mmcv ms_deform_attn_forward with
+ * num_levels = num_heads = 1): out[i, q] = sum_pt weights[i, q, pt] * bilinear(value[i],
+ * loc[i, q, pt] * (W, H) - 0.5). value [n, H*W, C], loc [n, queries, points, 2] in [0, 1],
+ * weights [n, queries, points] (already softmax-normalised), out [n, queries, C]. */
+int tsplat_msda_fwd(const float* value, const float* loc, const float* weights, float* out,
+                    int32_t n, int32_t height, int32_t width, int32_t channels, int32_t queries,
+                    int32_t points, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Shifted-window attention of the multi-view transformer (exact fp32 MFMA):
+ *   q [batch, H*W, C]; k, v [batch, key_views, H*W, C] (key_views = 1 for two views);
+ *   out [batch, H*W, C]; C must be 128; window pixels and window pixels * key_views must be
+ *   multiples of 64. with_shift rolls by half a window and applies the -100 region mask.
+ * ---------------------------------------------------------------------------------------- */
+int tsplat_win_attn_fwd(const float* q, const float* k, const float* v, float* out,
+                        int32_t batch, int32_t height, int32_t width, int32_t channels,
+                        int32_t key_views, int32_t splits, int32_t with_shift, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

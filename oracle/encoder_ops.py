@@ -1,0 +1,188 @@
+"""TEST INFRASTRUCTURE ONLY — CPU restatements of the encoder hot-path ops (torch fp32, CPU).
+
+Each function has the exact signature of its gfx950 counterpart in transplat_amd/kernels.py so a
+test can run the surrounding module code on the CPU with these in place (monkeypatched), and the
+GPU tests compare the HIP ops with these on identical inputs. Pinned by tests/golden/*.npz
+(generated from the reference modules, see tests/golden/gen_golden.py).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+# --------------------------------------------------------------------- window attention (T2, T3)
+def _window_pixel_index(h: int, w: int, splits: int, shift: int) -> torch.Tensor:
+    """[K*K, L] original pixel of every (window, in-window position) after a roll by -shift.
+
+    Restates split_feature (reference unimatch/utils.py:34-59: windows ordered (row-split,
+    col-split), positions row-major) applied to torch.roll(x, (-shift, -shift)) (reference
+    multiview_transformer.py:91-98): rolled[y, x] = x_orig[(y + shift) % h, (x + shift) % w].
+    """
+    wh, ww = h // splits, w // splits
+    idx = []
+    for sy in range(splits):
+        for sx in range(splits):
+            yy = (torch.arange(wh) + sy * wh + shift) % h
+            xx = (torch.arange(ww) + sx * ww + shift) % w
+            idx.append((yy[:, None] * w + xx[None, :]).reshape(-1))
+    return torch.stack(idx)
+
+
+def _region_ids(h: int, w: int, splits: int) -> torch.Tensor:
+    """[K*K, L] Swin region id of each in-window position (generate_shift_window_attn_mask,
+    reference multiview_transformer.py:17-54): slices (0:-wsize), (-wsize:-shift), (-shift:)."""
+    wh, ww = h // splits, w // splits
+    sh, sw = wh // 2, ww // 2
+
+    def band(coord, size, win, sft):
+        return torch.where(coord < size - win, 0, torch.where(coord < size - sft, 1, 2))
+
+    ids = []
+    for sy in range(splits):
+        for sx in range(splits):
+            yy = torch.arange(wh) + sy * wh
+            xx = torch.arange(ww) + sx * ww
+            r = band(yy, h, wh, sh)[:, None] * 3 + band(xx, w, ww, sw)[None, :]
+            ids.append(r.reshape(-1))
+    return torch.stack(ids)
+
+
+def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool):
+    """softmax(Q K^T / sqrt(C) + mask) V over split windows (reference
+    single_head_split_window_attention, multiview_transformer.py:57-206).
+
+    q [B, L, C]; k, v [B, L, C] (two views) or [B, m, L, C] (m = V - 1 key views).
+    Multi-view keys are ordered pixel-major / view-minor within a window and the shift mask is
+    tiled view-major (`attn_mask.repeat(b, 1, m)`, :130), so key j takes mask column j mod L.
+    """
+    q = q.float()
+    b, _, c = q.shape
+    if k.dim() == 3:
+        k = k[:, None]
+        v = v[:, None]
+    m = k.shape[1]
+    wh = h // num_splits
+    shift = wh // 2 if with_shift else 0
+    pix = _window_pixel_index(h, w, num_splits, shift)  # [K2, L]
+    k2, L = pix.shape
+    out = torch.empty_like(q)
+    if with_shift:
+        reg = _region_ids(h, w, num_splits)  # [K2, L]
+        kcol = torch.arange(L * m) % L
+    for bi in range(b):
+        for wi in range(k2):
+            qi = q[bi, pix[wi]]  # [L, C]
+            # keys: pixel-major, view-minor
+            kw = k[bi][:, pix[wi]].permute(1, 0, 2).reshape(L * m, c).float()
+            vw = v[bi][:, pix[wi]].permute(1, 0, 2).reshape(L * m, c).float()
+            s = qi @ kw.T / math.sqrt(c)
+            if with_shift:
+                r = reg[wi]
+                s = s + torch.where(r[:, None] == r[kcol][None, :], 0.0, -100.0)
+            out[bi, pix[wi]] = torch.softmax(s, dim=-1) @ vw
+    return out
+
+
+# --------------------------------------------------------------------- correlation (C2-C9)
+def calculate_grid(intr, pose, disp, h: int, w: int):
+    """Projection grid (reference depth_predictor_trans.py:11-57): pixel (x, y) at depth 1/disp
+    of camera n lands at uv in the other camera; normalised 2u/(W-1) - 1. -> [N, D, HW, 2]."""
+    n, d = disp.shape
+    ys, xs = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+    pts = torch.stack([xs, ys, torch.ones_like(xs)], 0).float().reshape(3, -1)  # [3, HW]
+    depth = 1.0 / disp  # [N, D]
+    cam = torch.inverse(intr) @ pts  # [N, 3, HW]
+    rot = pose[:, :3, :3] @ cam  # [N, 3, HW]
+    p = rot[:, :, None, :] * depth[:, None, :, None] + pose[:, :3, 3][:, :, None, None]
+    p = (intr @ p.reshape(n, 3, -1)).reshape(n, 3, d, h * w)
+    uv = p[:, :2] / p[:, 2:].clamp(min=1e-3)
+    gx = 2 * uv[:, 0] / (w - 1) - 1
+    gy = 2 * uv[:, 1] / (h - 1) - 1
+    return torch.stack([gx, gy], -1)
+
+
+def bilinear_zero(img, x, y):
+    """Sample img [HW... as H, W, C] at pixel coords (x, y) with zero padding (mmcv MSDA /
+    grid_sample(align_corners=False) after loc * size - 0.5). x, y: [...] -> [..., C]."""
+    hh, ww, c = img.shape
+    x0 = torch.floor(x)
+    y0 = torch.floor(y)
+    out = torch.zeros((*x.shape, c))
+    for dy in (0, 1):
+        for dx in (0, 1):
+            xi = x0 + dx
+            yi = y0 + dy
+            wgt = (1 - (x - xi).abs()) * (1 - (y - yi).abs())
+            ok = (xi >= 0) & (xi <= ww - 1) & (yi >= 0) & (yi <= hh - 1)
+            xc = xi.clamp(0, ww - 1).long()
+            yc = yi.clamp(0, hh - 1).long()
+            val = img[yc, xc]
+            out = out + torch.where(ok[..., None], wgt[..., None] * val, torch.zeros(()))
+    return out
+
+
+def _ref3d(intr, pose, disp, h, w, b):
+    """ref_3d of UVTransformerEncoder (reference utils/encoder.py:57-59) in (b v) order,
+    normalised to [0, 1] as grid / 2 + 0.5 -> [B*2, HW, D, 2]."""
+    grid = calculate_grid(intr, pose, disp, h, w)  # [(v b), D, HW, 2]
+    d = disp.shape[1]
+    r = grid.reshape(2, b, d, h * w, 2).permute(1, 0, 3, 2, 4).reshape(b * 2, h * w, d, 2)
+    return r / 2 + 0.5
+
+
+def uv_coarse(feat, intr, pose, disp, h: int, w: int):
+    """UVCoarseAttention core (reference attention.py:468-551 with calculate_grid): for query
+    (b, v) pixel p and depth d, sample the OTHER view's feature at ref_3d and dot with the own
+    feature, / sqrt(C).  feat [B, 2, HW, C] -> [B*2, HW, D]."""
+    b, _, hw, c = feat.shape
+    ref = _ref3d(intr, pose, disp, h, w, b)
+    d = disp.shape[1]
+    out = torch.empty((b * 2, hw, d))
+    for bi in range(b):
+        for vi in range(2):
+            other = feat[bi, 1 - vi].reshape(h, w, c)
+            r = ref[bi * 2 + vi]
+            for q0 in range(0, hw, 512):
+                sl = slice(q0, q0 + 512)
+                s = bilinear_zero(other, r[sl, :, 0] * w - 0.5, r[sl, :, 1] * h - 0.5)  # [q, D, C]
+                out[bi * 2 + vi, sl] = (s * feat[bi, vi][sl, None, :]).sum(-1) / math.sqrt(c)
+    return out
+
+
+def uv_cross(value, key, intr, pose, disp, offsets, logits, h: int, w: int):
+    """UVCrossAttention core (reference attention.py:329-416): per (query, depth) 4 points at
+    ref_3d + offset / (W, H), softmax weights over the points, sampled from the OTHER view's
+    value_proj output, then mean over channels of (sample * own key).
+    value, key [B, 2, HW, C]; offsets [B*2, HW, D*P*2]; logits [B*2, HW, D*P] -> [B*2, HW, D]."""
+    b, _, hw, c = value.shape
+    d = disp.shape[1]
+    p = logits.shape[-1] // d
+    ref = _ref3d(intr, pose, disp, h, w, b)
+    off = offsets.reshape(b * 2, hw, d, p, 2)
+    wts = torch.softmax(logits.reshape(b * 2, hw, d, p), -1)
+    out = torch.empty((b * 2, hw, d))
+    for bi in range(b):
+        for vi in range(2):
+            n = bi * 2 + vi
+            other = value[bi, 1 - vi].reshape(h, w, c)
+            for q0 in range(0, hw, 256):  # chunked: [256, D, P, C] samples at a time
+                sl = slice(q0, q0 + 256)
+                loc = ref[n][sl, :, None, :] + off[n][sl] / torch.tensor([w, h], dtype=torch.float32)
+                s = bilinear_zero(other, loc[..., 0] * w - 0.5, loc[..., 1] * h - 0.5)  # [q, D, P, C]
+                s = (s * wts[n][sl][..., None]).sum(2)
+                out[n, sl] = (s * key[bi, vi][sl, None, :]).mean(-1)
+    return out
+
+
+def msda(value, loc, weights, h: int, w: int):
+    """Single-level single-head MSDA (mmcv ms_deform_attn_forward semantics): value [N, HW, C],
+    loc [N, Q, P, 2] in [0, 1], weights [N, Q, P] -> [N, Q, C]."""
+    n, hw, c = value.shape
+    out = []
+    for i in range(n):
+        img = value[i].reshape(h, w, c)
+        s = bilinear_zero(img, loc[i, ..., 0] * w - 0.5, loc[i, ..., 1] * h - 0.5)  # [Q, P, C]
+        out.append((s * weights[i][..., None]).sum(1))
+    return torch.stack(out)

@@ -1,0 +1,332 @@
+#!/usr/bin/env python3
+"""Generate golden vectors by running the REFERENCE modules (in this container only).
+
+Usage: python tests/golden/gen_golden.py [--ref /root/reference] [--only name ...]
+
+Only harness code lives here: namespace-package registration (so the reference's side-effectful
+package __init__ files are not executed) and import shims for packages absent from the image:
+  * `mmcv`: `ext_loader.load_ext` returns dummies (never called: the CUDA branch is gated by
+    torch.cuda.is_available(), reference attention.py:259,393,529) and
+    `mmcv.ops.multi_scale_deform_attn.multi_scale_deformable_attn_pytorch` is restated from
+    mmcv 2.1.0 (grid_sample bilinear, zeros padding, align_corners=False);
+  * `jaxtyping`: annotation-only stub;  `cv2`, `torchvision.transforms`: import-only stubs
+    (used by DepthAnythingV2.image2tensor, never on the forward path);
+  * `torch.cuda.synchronize` = no-op (called unconditionally by the reference).
+Reference modules are imported by path from --ref and the script refuses to run without it, so
+no reference source or bytecode is written into the repo: only inputs' seeds and the outputs
+(as .npz data) are committed next to this script.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import sys
+import types
+from pathlib import Path
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(HERE))
+
+from canonical import canonical_init, seeded  # noqa: E402
+
+
+# ----------------------------------------------------------------------------- harness shims
+def msda_pytorch(value, value_spatial_shapes, sampling_locations, attention_weights):
+    """mmcv 2.1.0 multi_scale_deformable_attn_pytorch (restated for the harness)."""
+    bs, _, num_heads, embed_dims = value.shape
+    _, num_queries, num_heads, num_levels, num_points, _ = sampling_locations.shape
+    value_list = value.split([int(h) * int(w) for h, w in value_spatial_shapes], dim=1)
+    sampling_grids = 2 * sampling_locations - 1
+    sampling_value_list = []
+    for level, (h, w) in enumerate(value_spatial_shapes):
+        h, w = int(h), int(w)
+        value_l = value_list[level].flatten(2).transpose(1, 2).reshape(bs * num_heads, embed_dims, h, w)
+        grid_l = sampling_grids[:, :, :, level].transpose(1, 2).flatten(0, 1)
+        sampling_value_list.append(
+            F.grid_sample(value_l, grid_l, mode="bilinear", padding_mode="zeros", align_corners=False))
+    attention_weights = attention_weights.transpose(1, 2).reshape(
+        bs * num_heads, 1, num_queries, num_levels * num_points)
+    output = (torch.stack(sampling_value_list, dim=-2).flatten(-2) * attention_weights).sum(-1).view(
+        bs, num_heads * embed_dims, num_queries)
+    return output.transpose(1, 2).contiguous()
+
+
+def install_shims(ref: Path):
+    class _Ann:
+        def __class_getitem__(cls, item):
+            return cls
+
+    jt = types.ModuleType("jaxtyping")
+    for n in ("Float", "Bool", "Int64", "Int", "Shaped", "Integer", "UInt8", "Float32"):
+        setattr(jt, n, _Ann)
+    sys.modules["jaxtyping"] = jt
+
+    mmcv = types.ModuleType("mmcv")
+    utils = types.ModuleType("mmcv.utils")
+    ext_loader = types.ModuleType("mmcv.utils.ext_loader")
+    ext_loader.load_ext = lambda name, funcs: types.SimpleNamespace(**{f: None for f in funcs})
+    utils.ext_loader = ext_loader
+    ops = types.ModuleType("mmcv.ops")
+    msda = types.ModuleType("mmcv.ops.multi_scale_deform_attn")
+    msda.multi_scale_deformable_attn_pytorch = msda_pytorch
+    ops.multi_scale_deform_attn = msda
+    mmcv.utils, mmcv.ops = utils, ops
+    sys.modules.update({"mmcv": mmcv, "mmcv.utils": utils, "mmcv.utils.ext_loader": ext_loader,
+                        "mmcv.ops": ops, "mmcv.ops.multi_scale_deform_attn": msda})
+
+    class _Cv2(types.ModuleType):
+        def __getattr__(self, name):  # only interpolation-flag constants are read at import
+            return 0
+
+    sys.modules["cv2"] = _Cv2("cv2")
+    if "torchvision" not in sys.modules:
+        tv = types.ModuleType("torchvision")
+        tvt = types.ModuleType("torchvision.transforms")
+        tvt.Compose = lambda x: x
+        tv.transforms = tvt
+        sys.modules.update({"torchvision": tv, "torchvision.transforms": tvt})
+
+    torch.cuda.synchronize = lambda *a, **k: None
+
+    sys.path.insert(0, str(ref))
+    for name in ("src", "src.model", "src.model.encoder", "src.model.encoder.backbone",
+                 "src.depth_anything_v2"):
+        m = types.ModuleType(name)
+        m.__path__ = [str(ref / name.replace(".", "/"))]
+        sys.modules[name] = m
+
+
+def imp(name):
+    return importlib.import_module(name)
+
+
+def save(name, **arrays):
+    out = {k: (v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)) for k, v in arrays.items()}
+    np.savez_compressed(HERE / f"{name}.npz", **out)
+    print(f"wrote {name}.npz: " + ", ".join(f"{k}{tuple(v.shape)}" for k, v in out.items()))
+
+
+def subset_rows(x: torch.Tensor, n: int, seed: int):
+    """Deterministic row subset of a [N, ...] tensor (large outputs are pinned by a sample)."""
+    g = torch.Generator().manual_seed(seed)
+    idx = torch.randperm(x.shape[0], generator=g)[:n].sort().values
+    return idx, x[idx]
+
+
+# ----------------------------------------------------------------------------- fixtures
+def gen_window_attention():
+    mvt = imp("src.model.encoder.backbone.multiview_transformer")
+    h = w = 16
+    c = 128
+    out = {}
+    for shift in (False, True):
+        q = seeded((2, h * w, c), 101)
+        k = seeded((2, h * w, c), 102)
+        v = seeded((2, h * w, c), 103)
+        mask = mvt.generate_shift_window_attn_mask((h, w), h // 2, w // 2, h // 4, w // 4, device="cpu")
+        o = mvt.single_head_split_window_attention(q, k, v, num_splits=2, with_shift=shift, h=h, w=w,
+                                                   attn_mask=mask)
+        out[f"o2_shift{int(shift)}"] = o
+        # multi-view branch (V = 3 -> 2 key views): keys pixel-major / view-minor
+        k4 = seeded((2, 2, h * w, c), 104)
+        v4 = seeded((2, 2, h * w, c), 105)
+        o3 = mvt.single_head_split_window_attention(q, k4, v4, num_splits=2, with_shift=shift, h=h, w=w,
+                                                    attn_mask=mask)
+        out[f"o3_shift{int(shift)}"] = o3
+    out["mask"] = mask
+    save("win_attn", **out)
+
+
+def gen_mvt():
+    mvt = imp("src.model.encoder.backbone.multiview_transformer")
+    for nv in (2, 3):
+        t = canonical_init(mvt.MultiViewFeatureTransformer(num_layers=6, d_model=128, nhead=1,
+                                                           ffn_dim_expansion=4), seed=11).eval()
+        feats = [seeded((1, 128, 16, 16), 200 + i) for i in range(nv)]
+        with torch.no_grad():
+            o = t(feats, attn_num_splits=2)
+        save(f"mvt_v{nv}", out=torch.stack(o, 1))
+
+
+def gen_backbone():
+    bb = imp("src.model.encoder.backbone.backbone_multiview")
+    from transplat_amd import synthetic as S
+
+    m = canonical_init(bb.BackboneMultiview(feature_channels=128, downscale_factor=4), seed=12).eval()
+    batch = S.make_batch(1, image_shape=(64, 64))
+    ctx = batch["context"]
+    images = ctx["image"]
+    b, v, _, h, w = images.shape
+    intr = ctx["intrinsics"].clone()
+    intr[:, :, 0, :] *= float(w)
+    intr[:, :, 1, :] *= float(h)
+    camk = torch.eye(4).view(1, 1, 4, 4).repeat(b, v, 1, 1)
+    camk[:, :, :3, :3] = intr
+    img2world = ctx["extrinsics"] @ torch.inverse(camk)
+    with torch.no_grad():
+        trans, cnn = m(images, attn_splits=2, return_cnn_features=True, img2world=img2world)
+    save("backbone_64", trans=trans, cnn=cnn)
+
+
+def gen_calculate_grid():
+    dp = imp("src.model.encoder.matching.depth_predictor_trans")
+    from transplat_amd import synthetic as S
+
+    batch = S.make_batch(1, image_shape=(16, 16))
+    ctx = batch["context"]
+    feats = seeded((1, 2, 128, 16, 16), 301)
+    _, intr_curr, pose_curr_lists, disp = dp.prepare_feat_proj_data_lists(
+        feats, ctx["intrinsics"], ctx["extrinsics"], ctx["near"], ctx["far"], num_samples=128)
+    grid, _ = dp.calculate_grid(intr_curr, pose_curr_lists[0], 1.0 / disp.repeat([1, 1, 16, 16]))
+    save("calc_grid", intr=intr_curr, pose=pose_curr_lists[0], disp=disp.flatten(1), grid=grid)
+
+
+def _uv_inputs(hw=16, b=1):
+    """Features + coarse grid for a UV transformer at an hw x hw feature map (D = 128)."""
+    dp = imp("src.model.encoder.matching.depth_predictor_trans")
+    from transplat_amd import synthetic as S
+
+    batch = S.make_batch(b, image_shape=(hw, hw))
+    ctx = batch["context"]
+    feats = seeded((b, 2, 128, hw, hw), 401)
+    _, intr_curr, pose_curr_lists, disp = dp.prepare_feat_proj_data_lists(
+        feats, ctx["intrinsics"], ctx["extrinsics"], ctx["near"], ctx["far"], num_samples=128)
+    grid, _ = dp.calculate_grid(intr_curr, pose_curr_lists[0], 1.0 / disp.repeat([1, 1, hw, hw]))
+    return feats, grid, intr_curr, pose_curr_lists[0], disp
+
+
+def gen_uv():
+    tr = imp("src.model.utils.transformer")
+    hw = 16
+    feats, grid, intr, pose, disp = _uv_inputs(hw)
+    b = feats.shape[0]
+    coarse = canonical_init(tr.UVTransformer(embed_dims=128, mode="coarse", num_layers=1), seed=21).eval()
+    fine = canonical_init(tr.UVTransformer(embed_dims=128, mode="fine", num_layers=2), seed=22).eval()
+    bev_pos = seeded((2 * hw * hw, b, 128), 402, 0.5)
+    q0 = torch.zeros((2 * hw * hw, b, 128))
+    with torch.no_grad():
+        c = coarse([feats], q0, hw, hw, grid=grid)
+        f = fine([feats], c, hw, hw, bev_pos=bev_pos, grid=grid)
+    save("uv_16", intr=intr, pose=pose, disp=disp.flatten(1), coarse=c, fine=f)
+
+
+def gen_depth_predictor():
+    dp = imp("src.model.encoder.matching.depth_predictor_trans")
+    from transplat_amd import synthetic as S
+
+    m = dp.DepthPredictorTrans(
+        feature_channels=128, upscale_factor=4, num_depth_candidates=128,
+        costvolume_unet_feat_dim=128, costvolume_unet_channel_mult=(1, 1, 1),
+        costvolume_unet_attn_res=(4,), gaussian_raw_channels=84, gaussians_per_pixel=1,
+        num_views=2, depth_unet_feat_dim=32, depth_unet_attn_res=[16],
+        depth_unet_channel_mult=[1, 1, 1, 1, 1], DA_size=64)
+    m = canonical_init(m, seed=31).eval()
+    batch = S.make_batch(1, image_shape=(256, 256))
+    ctx = batch["context"]
+    feats = seeded((1, 2, 128, 64, 64), 501, 0.5)
+    cnn = seeded((1, 2, 128, 64, 64), 502, 0.5)
+    da_depth = seeded((1, 2, 1, 256, 256), 503, 1.0, kind="rand")
+    dino = seeded((1, 2, 64, 144, 144), 504, 0.5)
+    images = ctx["image"]
+    extra = {"images": images.permute(1, 0, 2, 3, 4).reshape(2, 3, 256, 256), "scene_names": None}
+    with torch.no_grad():
+        depths, dens, raw = m(feats, ctx["intrinsics"], ctx["extrinsics"], ctx["near"], ctx["far"],
+                              gaussians_per_pixel=1, deterministic=True, extra_info=extra,
+                              cnn_features=cnn, da_depth=da_depth, dino_feature=dino)
+    idx, raw_s = subset_rows(raw.reshape(-1, raw.shape[-1]), 4096, 7)
+    didx, d_s = subset_rows(depths.flatten(), 16384, 8)
+    save("depth_predictor", depth_idx=didx, depths=d_s, densities=dens.flatten()[didx], raw_idx=idx,
+         raw_rows=raw_s)
+
+
+def gen_unet():
+    un = imp("src.model.encoder.matching.ldm_unet.unet")
+    for tag, ch, mult, attn, hw in (("cv", 128, (1, 1, 1), (4,), 16), ("depth", 32, (1, 1, 1, 1, 1), (16,), 32)):
+        m = un.UNetModel(image_size=None, in_channels=ch, model_channels=ch, out_channels=ch,
+                         num_res_blocks=1, attention_resolutions=attn, channel_mult=mult,
+                         num_head_channels=32, dims=2, postnorm=True, num_frames=2,
+                         use_cross_view_self_attn=True)
+        m = canonical_init(m, seed=41).eval()
+        x = seeded((2, ch, hw, hw), 601)
+        with torch.no_grad():
+            y = m(x)
+        save(f"unet_{tag}", out=y)
+
+
+def gen_depth_anything():
+    dpt = imp("src.depth_anything_v2.dpt")
+    m = dpt.DepthAnythingV2(encoder="vitb", features=128, out_channels=[96, 192, 384, 768])
+    m = canonical_init(m, seed=51).eval()
+    x = seeded((1, 3, 252, 252), 701)
+    with torch.no_grad():
+        depth, feat = m(x)
+    idx, feat_s = subset_rows(feat.reshape(-1), 8192, 9)
+    save("depth_anything", depth=depth, feat_idx=idx, feat_vals=feat_s, feat_shape=np.array(feat.shape))
+
+
+def gen_covariance():
+    gs = imp("src.model.encoder.common.gaussians")
+    s = seeded((64, 3), 801, kind="rand") + 0.1
+    q = seeded((64, 4), 802)
+    q = q / q.norm(dim=-1, keepdim=True)
+    save("covariance", cov=gs.build_covariance(s, q))
+
+
+def gen_state_dict_keys():
+    """Parameter names + shapes of the reference submodules an `encoder.*` checkpoint holds."""
+    import json
+
+    bb = imp("src.model.encoder.backbone.backbone_multiview")
+    dp = imp("src.model.encoder.matching.depth_predictor_trans")
+    dpt = imp("src.depth_anything_v2.dpt")
+    mods = {
+        "backbone": bb.BackboneMultiview(feature_channels=128, downscale_factor=4),
+        "depth_predictor": dp.DepthPredictorTrans(
+            feature_channels=128, upscale_factor=4, num_depth_candidates=128, costvolume_unet_feat_dim=128,
+            costvolume_unet_channel_mult=(1, 1, 1), costvolume_unet_attn_res=(4,), gaussian_raw_channels=84,
+            gaussians_per_pixel=1, num_views=2, depth_unet_feat_dim=32, depth_unet_attn_res=[16],
+            depth_unet_channel_mult=[1, 1, 1, 1, 1], DA_size=64),
+        "da_model": dpt.DepthAnythingV2(encoder="vitb", features=128, out_channels=[96, 192, 384, 768]),
+    }
+    keys = {f"{p}.{k}": list(v.shape) for p, m in mods.items() for k, v in m.state_dict().items()}
+    (HERE / "state_dict_keys.json").write_text(json.dumps(keys, indent=0, sort_keys=True))
+    print(f"wrote state_dict_keys.json: {len(keys)} tensors")
+
+
+ALL = {
+    "state_dict_keys": gen_state_dict_keys,
+    "win_attn": gen_window_attention,
+    "mvt": gen_mvt,
+    "backbone": gen_backbone,
+    "calc_grid": gen_calculate_grid,
+    "uv": gen_uv,
+    "unet": gen_unet,
+    "depth_predictor": gen_depth_predictor,
+    "depth_anything": gen_depth_anything,
+    "covariance": gen_covariance,
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", nargs="*")
+    a = ap.parse_args()
+    ref = Path(a.ref)
+    if not (ref / "src" / "model").is_dir():
+        raise SystemExit(f"reference not found at {ref}: golden vectors can only be generated there")
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    install_shims(ref)
+    for name in a.only or ALL:
+        ALL[name]()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,133 @@
+"""Encoder hot-path ops: oracle pinned to the reference's golden vectors (CPU), and the gfx950
+kernels (transplat_amd.kernels, called through the C-ABI) against the oracle (GPU).
+
+Tolerances: the window attention runs exact-fp32 MFMA but with a different summation order and
+exp2-based softmax than torch: 2e-4 absolute on O(1) outputs. The correlation kernels sum 128
+products in a different order than MSDA+mean: 1e-4 absolute (outputs are O(1)).
+"""
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
+from canonical import seeded  # noqa: E402
+
+from oracle import encoder_ops as E  # noqa: E402
+from transplat_amd import synthetic as S  # noqa: E402
+
+GOLD = Path(__file__).resolve().parent / "golden"
+
+
+def _cams(b, hw):
+    """(v b)-ordered pixel intrinsics, relative poses and 128 disparities as the reference's
+    prepare_feat_proj_data_lists builds them for the synthetic context views."""
+    from transplat_amd.model.encoder.matching.depth_predictor_trans import prepare_feat_proj_data_lists
+
+    ctx = S.make_batch(b, image_shape=(hw, hw))["context"]
+    feats = torch.zeros((b, 2, 1, hw, hw))
+    _, intr, poses, disp = prepare_feat_proj_data_lists(feats, ctx["intrinsics"], ctx["extrinsics"], ctx["near"],
+                                                        ctx["far"], 128)
+    return intr, poses[0], disp.flatten(1)
+
+
+# ------------------------------------------------------------------ oracle vs reference golden
+@pytest.mark.parametrize("shift", [0, 1])
+def test_oracle_window_attention_matches_reference(shift):
+    g = np.load(GOLD / "win_attn.npz")
+    h = w = 16
+    q, k, v = seeded((2, h * w, 128), 101), seeded((2, h * w, 128), 102), seeded((2, h * w, 128), 103)
+    np.testing.assert_allclose(E.window_attention(q, k, v, h, w, 2, bool(shift)).numpy(), g[f"o2_shift{shift}"],
+                               atol=1e-5)
+    k4, v4 = seeded((2, 2, h * w, 128), 104), seeded((2, 2, h * w, 128), 105)
+    np.testing.assert_allclose(E.window_attention(q, k4, v4, h, w, 2, bool(shift)).numpy(), g[f"o3_shift{shift}"],
+                               atol=1e-5)
+
+
+def test_oracle_calculate_grid_matches_reference():
+    g = np.load(GOLD / "calc_grid.npz")
+    grid = E.calculate_grid(torch.tensor(g["intr"]), torch.tensor(g["pose"]), torch.tensor(g["disp"]), 16, 16)
+    np.testing.assert_allclose(grid.numpy(), g["grid"], atol=1e-5)
+
+
+def test_camera_prep_matches_reference_golden():
+    """prepare_feat_proj_data_lists restatement == the reference's (intr, pose, disp)."""
+    g = np.load(GOLD / "calc_grid.npz")
+    intr, pose, disp = _cams(1, 16)
+    np.testing.assert_allclose(intr.numpy(), g["intr"], rtol=1e-6)
+    np.testing.assert_allclose(pose.numpy(), g["pose"], atol=1e-6)
+    np.testing.assert_allclose(disp.numpy(), g["disp"], rtol=1e-6)
+
+
+# ------------------------------------------------------------------ HIP kernels vs oracle
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,m,shift", [(16, 1, False), (16, 1, True), (16, 2, True), (64, 1, False),
+                                        (64, 1, True), (64, 2, True), (32, 2, False)])
+def test_window_attention_kernel(device, hw, m, shift):
+    from transplat_amd import kernels as K
+
+    b = 2
+    q = seeded((b, hw * hw, 128), 11)
+    k = seeded((b, m, hw * hw, 128), 12) if m > 1 else seeded((b, hw * hw, 128), 12)
+    v = seeded(k.shape, 13)
+    ref = E.window_attention(q, k, v, hw, hw, 2, shift)
+    out = K.window_attention(q.to(device), k.to(device), v.to(device), hw, hw, 2, shift).cpu()
+    err = (out - ref).abs().max().item()
+    assert err < 2e-4, err
+
+
+@pytest.mark.gpu
+def test_window_attention_kernel_large_logits(device):
+    """Scores far from 0 (online-softmax rescaling path exercised: later key tiles raise the max)."""
+    from transplat_amd import kernels as K
+
+    hw = 32
+    q = seeded((1, hw * hw, 128), 21) * 3
+    k = seeded((1, hw * hw, 128), 22) * 3
+    k[:, -64:] *= 4  # the last key tile of every window holds the largest scores
+    v = seeded((1, hw * hw, 128), 23)
+    ref = E.window_attention(q, k, v, hw, hw, 2, True)
+    out = K.window_attention(q.to(device), k.to(device), v.to(device), hw, hw, 2, True).cpu()
+    assert (out - ref).abs().max().item() < 2e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,b", [(16, 1), (32, 2)])
+def test_uv_coarse_kernel(device, hw, b):
+    from transplat_amd import kernels as K
+
+    intr, pose, disp = _cams(b, hw)
+    feat = seeded((b, 2, hw * hw, 128), 31)
+    ref = E.uv_coarse(feat, intr, pose, disp, hw, hw)
+    out = K.uv_coarse(feat.to(device), intr.to(device), pose.to(device), disp.to(device), hw, hw).cpu()
+    assert (out - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,b", [(16, 1), (24, 2)])
+def test_uv_cross_kernel(device, hw, b):
+    from transplat_amd import kernels as K
+
+    intr, pose, disp = _cams(b, hw)
+    value = seeded((b, 2, hw * hw, 128), 41)
+    key = seeded((b, 2, hw * hw, 128), 42)
+    offsets = seeded((b * 2, hw * hw, 128 * 4 * 2), 43, 2.0)
+    logits = seeded((b * 2, hw * hw, 128 * 4), 44)
+    ref = E.uv_cross(value, key, intr, pose, disp, offsets, logits, hw, hw)
+    out = K.uv_cross(*(t.to(device) for t in (value, key, intr, pose, disp, offsets, logits)), hw, hw).cpu()
+    assert (out - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.gpu
+def test_msda_kernel(device):
+    from transplat_amd import kernels as K
+
+    hw = 16
+    value = seeded((2, hw * hw, 128), 51)
+    loc = seeded((2, hw * hw, 4, 2), 52, kind="rand") * 1.2 - 0.1  # some samples off-image
+    wts = torch.softmax(seeded((2, hw * hw, 4), 53), -1)
+    ref = E.msda(value, loc, wts, hw, hw)
+    out = K.msda(value.to(device), loc.to(device), wts.to(device), hw, hw).cpu()
+    assert (out - ref).abs().max().item() < 1e-5

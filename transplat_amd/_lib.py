@@ -42,6 +42,10 @@ SIGNATURES = {
         ctypes.c_int,
         [ctypes.POINTER(RasterDesc)] + [_P] * 15,
     ),
+    "tsplat_uv_coarse_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 5 + [_P]),
+    "tsplat_uv_cross_fwd": (ctypes.c_int, [_P] * 7 + [_I32] * 6 + [_P]),
+    "tsplat_msda_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 6 + [_P]),
+    "tsplat_win_attn_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 7 + [_P]),
 }
 
 ERRORS = {-1: "invalid argument", -2: "HIP launch error"}

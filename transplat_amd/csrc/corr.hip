@@ -1,0 +1,297 @@
+// Depth-candidate correlation of the TranSplat cost volume on gfx950.
+//
+// Fuses, per (query pixel, depth candidate), what the reference does in four materialising steps:
+//   calculate_grid (src/model/encoder/matching/depth_predictor_trans.py:11-57): back-project the
+//     integer pixel with K^-1, rotate/translate into the other camera at depth 1/disp, project with
+//     K, divide by max(z, 1e-3), normalise 2u/(W-1) - 1            -> grid [(v b), D, HW, 2], 8 MB
+//   UVTransformerEncoder ref_3d = grid / 2 + 0.5 in (b v) order (utils/encoder.py:57-59)
+//   mmcv ms_deform_attn bilinear sampling of the OTHER view's features at loc * size - 0.5 with
+//     zero padding (attention.py:359 view flip; MSDA im2col)           -> [2, HW*D, C], 537 MB
+//   correlation with the own feature: coarse sum_c / sqrt(C) (attention.py:542-547),
+//     cross mean_c over softmax-weighted 4-point samples (attention.py:365-410)
+// The grid is recomputed in registers from 2 x (K, K^-1, R, t) + D disparities, the sampled
+// features never leave registers, and the only HBM traffic is the two channel-last feature maps
+// (L2-resident), the per-(query, depth) offsets/weights of the cross layer, and the [.., D] output.
+//
+// Mapping: one workgroup per query pixel, 16 lanes per (query, depth) (8 channels per lane, so a
+// 16-lane group reads one 512-B feature row as 16 x 32 B), 16 depths in flight per workgroup.
+#include "common.h"
+#include "prof.h"
+
+namespace tsplat {
+namespace corr {
+
+constexpr int kC = 128;        // feature channels (= embed_dims)
+constexpr int kThreads = 256;  // 16 groups of 16 lanes
+constexpr int kGroups = kThreads / 16;
+constexpr int kMaxPoints = 8;
+
+struct Cam {
+    float kinv[9], k[9], r[9], t[3];
+};
+
+struct Geo {
+    int B, H, W, D;
+};
+
+// (b v)-ordered query n = 2b + v uses camera (v b) index v*B + b
+__device__ __forceinline__ const float* cam_ptr(const float* cams, const Geo& g, int n) {
+    const int b = n >> 1, v = n & 1;
+    return cams + (size_t)(v * g.B + b) * 30;
+}
+
+// ray of integer pixel (x, y) in the own camera, rotated into the other: R K^-1 [x, y, 1]
+__device__ __forceinline__ void pixel_ray(const float* c, float x, float y, float ray[3]) {
+    const float* ki = c;
+    const float* R = c + 18;
+    const float p0 = ki[0] * x + ki[1] * y + ki[2];
+    const float p1 = ki[3] * x + ki[4] * y + ki[5];
+    const float p2 = ki[6] * x + ki[7] * y + ki[8];
+    ray[0] = R[0] * p0 + R[1] * p1 + R[2] * p2;
+    ray[1] = R[3] * p0 + R[4] * p1 + R[5] * p2;
+    ray[2] = R[6] * p0 + R[7] * p1 + R[8] * p2;
+}
+
+// ref_3d of the ray at depth 1/disp: normalised grid coordinate / 2 + 0.5, in [0, 1] on-image
+__device__ __forceinline__ void sample_ref(const float* c, const Geo& g, const float ray[3],
+                                           float disp, float& rx, float& ry) {
+    const float* K = c + 9;
+    const float* t = c + 27;
+    const float depth = 1.0f / disp;
+    const float P0 = ray[0] * depth + t[0];
+    const float P1 = ray[1] * depth + t[1];
+    const float P2 = ray[2] * depth + t[2];
+    const float u = K[0] * P0 + K[1] * P1 + K[2] * P2;
+    const float v = K[3] * P0 + K[4] * P1 + K[5] * P2;
+    const float w = fmaxf(K[6] * P0 + K[7] * P1 + K[8] * P2, 1e-3f);
+    const float gx = 2.0f * (u / w) / (float)(g.W - 1) - 1.0f;
+    const float gy = 2.0f * (v / w) / (float)(g.H - 1) - 1.0f;
+    rx = gx / 2.0f + 0.5f;
+    ry = gy / 2.0f + 0.5f;
+}
+
+// bilinear sample (zero padding, mmcv ms_deform_attn_im2col_bilinear) of 8 channels [c0, c0+8)
+// of a channel-last [H*W, C] map; accumulates w * value into acc
+__device__ __forceinline__ void bilinear_acc8(const float* __restrict__ img, const Geo& g, float xim,
+                                              float yim, float w, int c0, float acc[8]) {
+    if (!(yim > -1.0f && xim > -1.0f && yim < (float)g.H && xim < (float)g.W)) return;
+    const float fy = floorf(yim), fx = floorf(xim);
+    const int y0 = (int)fy, x0 = (int)fx, y1 = y0 + 1, x1 = x0 + 1;
+    const float ly = yim - fy, lx = xim - fx, hy = 1.0f - ly, hx = 1.0f - lx;
+    const float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+    auto corner = [&](int yy, int xx, float cw) {
+        const float4* s = reinterpret_cast<const float4*>(img + ((size_t)yy * g.W + xx) * kC + c0);
+        const float4 a = s[0], b = s[1];
+        v[0] += cw * a.x; v[1] += cw * a.y; v[2] += cw * a.z; v[3] += cw * a.w;
+        v[4] += cw * b.x; v[5] += cw * b.y; v[6] += cw * b.z; v[7] += cw * b.w;
+    };
+    if (y0 >= 0 && x0 >= 0) corner(y0, x0, w1);
+    if (y0 >= 0 && x1 <= g.W - 1) corner(y0, x1, w2);
+    if (y1 <= g.H - 1 && x0 >= 0) corner(y1, x0, w3);
+    if (y1 <= g.H - 1 && x1 <= g.W - 1) corner(y1, x1, w4);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += w * v[i];
+}
+
+__device__ __forceinline__ float group_sum16(float x) {
+    x += __shfl_xor(x, 1, 16);
+    x += __shfl_xor(x, 2, 16);
+    x += __shfl_xor(x, 4, 16);
+    x += __shfl_xor(x, 8, 16);
+    return x;
+}
+
+// ---- coarse: corr[n][p][d] = <sample(feat_other, loc(p, d)), feat_own[p]> / sqrt(C)
+__global__ void __launch_bounds__(kThreads)
+uv_coarse_kernel(Geo g, const float* __restrict__ feat, const float* __restrict__ cams,
+                 const float* __restrict__ disp, float* __restrict__ out) {
+    __shared__ float s_out[256];
+    const int p = blockIdx.x, n = blockIdx.y;
+    const int grp = threadIdx.x >> 4, gl = threadIdx.x & 15, c0 = gl * 8;
+    const size_t HW = (size_t)g.H * g.W;
+    const float* own = feat + (size_t)n * HW * kC;
+    const float* other = feat + (size_t)(n ^ 1) * HW * kC;
+    const float* c = cam_ptr(cams, g, n);
+    const int b = n >> 1, v = n & 1;
+    const float* dsp = disp + (size_t)(v * g.B + b) * g.D;
+    float key[8];
+    {
+        const float4* s = reinterpret_cast<const float4*>(own + (size_t)p * kC + c0);
+        const float4 a = s[0], bb = s[1];
+        key[0] = a.x; key[1] = a.y; key[2] = a.z; key[3] = a.w;
+        key[4] = bb.x; key[5] = bb.y; key[6] = bb.z; key[7] = bb.w;
+    }
+    float ray[3];
+    pixel_ray(c, (float)(p % g.W), (float)(p / g.W), ray);
+    const float inv_sqrt_c = 1.0f / sqrtf((float)kC);
+    for (int d0 = 0; d0 < g.D; d0 += kGroups) {
+        const int d = d0 + grp;
+        float acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+        if (d < g.D) {
+            float rx, ry;
+            sample_ref(c, g, ray, dsp[d], rx, ry);
+            bilinear_acc8(other, g, rx * (float)g.W - 0.5f, ry * (float)g.H - 0.5f, 1.0f, c0, acc);
+        }
+        float part = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) part += acc[i] * key[i];
+        part = group_sum16(part);
+        if (gl == 0 && d < g.D) s_out[d & 255] = part * inv_sqrt_c;
+        if (((d0 + kGroups) & 255) == 0 || d0 + kGroups >= g.D) {
+            __syncthreads();
+            const int base = d0 & ~255;
+            const int cnt = min(256, g.D - base);
+            if ((int)threadIdx.x < cnt) out[((size_t)n * HW + p) * g.D + base + threadIdx.x] = s_out[threadIdx.x];
+            __syncthreads();
+        }
+    }
+}
+
+// ---- cross: out[n][p][d] = mean_c key[p]_c * sum_pt softmax(logit)_pt sample(value_other, loc + off)
+__global__ void __launch_bounds__(kThreads)
+uv_cross_kernel(Geo g, int P, const float* __restrict__ value, const float* __restrict__ key,
+                const float* __restrict__ cams, const float* __restrict__ disp,
+                const float* __restrict__ offsets, const float* __restrict__ logits,
+                float* __restrict__ out) {
+    __shared__ float s_out[256];
+    const int p = blockIdx.x, n = blockIdx.y;
+    const int grp = threadIdx.x >> 4, gl = threadIdx.x & 15, c0 = gl * 8;
+    const size_t HW = (size_t)g.H * g.W;
+    const float* other = value + (size_t)(n ^ 1) * HW * kC;
+    const float* c = cam_ptr(cams, g, n);
+    const int b = n >> 1, v = n & 1;
+    const float* dsp = disp + (size_t)(v * g.B + b) * g.D;
+    const float* off = offsets + ((size_t)n * HW + p) * g.D * P * 2;
+    const float* lg = logits + ((size_t)n * HW + p) * g.D * P;
+    float kv[8];
+    {
+        const float4* s = reinterpret_cast<const float4*>(key + ((size_t)n * HW + p) * kC + c0);
+        const float4 a = s[0], bb = s[1];
+        kv[0] = a.x; kv[1] = a.y; kv[2] = a.z; kv[3] = a.w;
+        kv[4] = bb.x; kv[5] = bb.y; kv[6] = bb.z; kv[7] = bb.w;
+    }
+    float ray[3];
+    pixel_ray(c, (float)(p % g.W), (float)(p / g.W), ray);
+    const float fw = (float)g.W, fh = (float)g.H;
+    for (int d0 = 0; d0 < g.D; d0 += kGroups) {
+        const int d = d0 + grp;
+        float acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+        if (d < g.D) {
+            float rx, ry;
+            sample_ref(c, g, ray, dsp[d], rx, ry);
+            float e[kMaxPoints];
+            float mx = -INFINITY;
+            for (int pt = 0; pt < P; ++pt) mx = fmaxf(mx, lg[d * P + pt]);
+            float ssum = 0.f;
+            for (int pt = 0; pt < P; ++pt) {
+                e[pt] = __expf(lg[d * P + pt] - mx);
+                ssum += e[pt];
+            }
+            for (int pt = 0; pt < P; ++pt) {
+                const float wgt = e[pt] / ssum;  // torch softmax over the points
+                const float lx = rx + off[(d * P + pt) * 2] / fw;
+                const float ly = ry + off[(d * P + pt) * 2 + 1] / fh;
+                bilinear_acc8(other, g, lx * fw - 0.5f, ly * fh - 0.5f, wgt, c0, acc);
+            }
+        }
+        float part = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) part += acc[i] * kv[i];
+        part = group_sum16(part);
+        if (gl == 0 && d < g.D) s_out[d & 255] = part * (1.0f / (float)kC);
+        if (((d0 + kGroups) & 255) == 0 || d0 + kGroups >= g.D) {
+            __syncthreads();
+            const int base = d0 & ~255;
+            const int cnt = min(256, g.D - base);
+            if ((int)threadIdx.x < cnt) out[((size_t)n * HW + p) * g.D + base + threadIdx.x] = s_out[threadIdx.x];
+            __syncthreads();
+        }
+    }
+}
+
+// ---- single-level single-head MSDA: out[n][q] = sum_pt w_pt sample(value[n], loc_pt)
+__global__ void __launch_bounds__(kThreads)
+msda_kernel(Geo g, int Q, int P, const float* __restrict__ value, const float* __restrict__ loc,
+            const float* __restrict__ weights, float* __restrict__ out) {
+    const int n = blockIdx.y;
+    const int q = blockIdx.x * kGroups + (threadIdx.x >> 4);
+    const int gl = threadIdx.x & 15, c0 = gl * 8;
+    if (q >= Q) return;
+    const size_t HW = (size_t)g.H * g.W;
+    const float* img = value + (size_t)n * HW * kC;
+    const float* lc = loc + ((size_t)n * Q + q) * P * 2;
+    const float* wt = weights + ((size_t)n * Q + q) * P;
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    for (int pt = 0; pt < P; ++pt)
+        bilinear_acc8(img, g, lc[2 * pt] * (float)g.W - 0.5f, lc[2 * pt + 1] * (float)g.H - 0.5f, wt[pt],
+                      c0, acc);
+    float4* o = reinterpret_cast<float4*>(out + ((size_t)n * Q + q) * kC + c0);
+    o[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+
+}  // namespace corr
+}  // namespace tsplat
+
+using namespace tsplat;
+
+extern "C" int tsplat_uv_coarse_fwd(const float* feat, const float* cams, const float* disp,
+                                    float* out, int32_t batch, int32_t height, int32_t width,
+                                    int32_t channels, int32_t depths, void* stream_) {
+    using namespace tsplat::corr;
+    if (!feat || !cams || !disp || !out || channels != kC || batch <= 0 || height <= 1 ||
+        width <= 1 || depths <= 0)
+        return TSPLAT_EINVAL;
+    Geo g{batch, height, width, depths};
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(prof::kUvCoarse, stream);
+    hipLaunchKernelGGL(uv_coarse_kernel, dim3(height * width, 2 * batch), dim3(kThreads), 0, stream,
+                       g, feat, cams, disp, out);
+    TSPLAT_PROF_END(prof::kUvCoarse, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_uv_cross_fwd(const float* value, const float* key, const float* cams,
+                                   const float* disp, const float* offsets, const float* logits,
+                                   float* out, int32_t batch, int32_t height, int32_t width,
+                                   int32_t channels, int32_t depths, int32_t points, void* stream_) {
+    using namespace tsplat::corr;
+    if (!value || !key || !cams || !disp || !offsets || !logits || !out || channels != kC ||
+        batch <= 0 || height <= 1 || width <= 1 || depths <= 0 || points <= 0 || points > kMaxPoints)
+        return TSPLAT_EINVAL;
+    Geo g{batch, height, width, depths};
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(prof::kUvCross, stream);
+    hipLaunchKernelGGL(uv_cross_kernel, dim3(height * width, 2 * batch), dim3(kThreads), 0, stream,
+                       g, points, value, key, cams, disp, offsets, logits, out);
+    TSPLAT_PROF_END(prof::kUvCross, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_msda_fwd(const float* value, const float* loc, const float* weights,
+                               float* out, int32_t n, int32_t height, int32_t width,
+                               int32_t channels, int32_t queries, int32_t points, void* stream_) {
+    using namespace tsplat::corr;
+    if (!value || !loc || !weights || !out || channels != kC || n <= 0 || height <= 0 ||
+        width <= 0 || queries <= 0 || points <= 0)
+        return TSPLAT_EINVAL;
+    Geo g{1, height, width, 1};
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(prof::kMsda, stream);
+    hipLaunchKernelGGL(msda_kernel, dim3(ceil_div(queries, kGroups), n), dim3(kThreads), 0, stream, g,
+                       queries, points, value, loc, weights, out);
+    TSPLAT_PROF_END(prof::kMsda, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

@@ -1,0 +1,68 @@
+"""End-to-end inference step (reference ModelWrapper.test_step, src/model/model_wrapper.py:185-323):
+data shim -> EncoderTrans -> DecoderSplattingHIP for every target view, on synthetic scenes.
+
+Weights are seeded random (no checkpoint is reachable offline); the work per step does not depend
+on their values. `build_e2e_workload` is the bench.py workload: one step = B scenes of 2 context
+views -> 3 rendered 256x256 target views each.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import synthetic as S
+from .model.decoder import DatasetCfgLite, DecoderSplattingHIP, DecoderSplattingHIPCfg
+from .model.encoder import EncoderTrans, EncoderTransCfg
+
+
+class TransplatModel(torch.nn.Module):
+    """encoder + decoder pair with the reference ModelWrapper's `encoder.` / `decoder.` names."""
+
+    def __init__(self, encoder_cfg: EncoderTransCfg | None = None, decoder_cfg: DecoderSplattingHIPCfg | None = None,
+                 background=(0.0, 0.0, 0.0)):
+        super().__init__()
+        self.encoder = EncoderTrans(encoder_cfg or EncoderTransCfg())
+        self.decoder = DecoderSplattingHIP(decoder_cfg or DecoderSplattingHIPCfg(), DatasetCfgLite(background))
+        self.data_shim = self.encoder.get_data_shim()
+
+    @torch.no_grad()
+    def test_step(self, batch: dict, global_step: int = 0):
+        batch = self.data_shim(batch)
+        _, _, _, h, w = batch["target"]["image"].shape
+        gaussians = self.encoder(batch["context"], global_step, deterministic=True)
+        t = batch["target"]
+        return self.decoder(gaussians, t["extrinsics"], t["intrinsics"], t["near"], t["far"], (h, w))
+
+    def load_checkpoint(self, path: str, strict: bool = True):
+        """Lightning checkpoint of the reference (`state_dict` with `encoder.` / `decoder.` keys);
+        loaded with weights_only=True (nothing in the file is executed)."""
+        ckpt = torch.load(path, map_location="cpu", weights_only=True)
+        sd = ckpt.get("state_dict", ckpt)
+        sd = {k: v for k, v in sd.items() if k.startswith("encoder.")}
+        missing, unexpected = self.load_state_dict(sd, strict=False)
+        missing = [k for k in missing if k.startswith("encoder.")]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"checkpoint mismatch: missing {missing[:5]}..., unexpected {unexpected[:5]}...")
+        return missing, unexpected
+
+
+def build_model(device, dense_dtype: str = "fp32", seed: int = 0) -> TransplatModel:
+    torch.manual_seed(seed)
+    cfg = EncoderTransCfg(dense_dtype=dense_dtype)
+    model = TransplatModel(cfg, DecoderSplattingHIPCfg(check_overflow=False))
+    S.init_synthetic_weights(model.encoder, seed)
+    return model.eval().to(device)
+
+
+def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: str = "fp32"):
+    model = build_model(device, dense_dtype)
+    data = S.make_batch(batch, image_shape=(256, 256), scene_offset=scene_offset, device=device)
+
+    def step():
+        return model.test_step(data)
+
+    info = {
+        "views_per_step": batch * data["target"]["near"].shape[1],
+        "workload": f"e2e TranSplat test_step: {batch} scene(s) x (2 ctx -> 3 tgt) 256x256, "
+                    f"dense layers {dense_dtype}, correlation/attention/raster fp32",
+    }
+    return step, info, model

@@ -1,0 +1,85 @@
+"""Python face of the encoder-side gfx950 kernels (C-ABI in include/transplat_hip.h).
+
+Signatures match the CPU restatements in oracle/encoder_ops.py one for one. Every function
+requires device tensors and the in-tree HIP library; there is no fallback path.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    if t.dtype != torch.float32:
+        t = t.float()
+    return t.contiguous()
+
+
+def pack_cameras(intr: torch.Tensor, pose: torch.Tensor) -> torch.Tensor:
+    """[N, 30] = K^-1, K, R, t per (v b) camera (the inputs of calculate_grid,
+    reference depth_predictor_trans.py:36-49, with K^-1 taken by torch.inverse as there)."""
+    intr = intr.float()
+    return torch.cat(
+        [torch.inverse(intr).reshape(-1, 9), intr.reshape(-1, 9), pose[:, :3, :3].reshape(-1, 9).float(),
+         pose[:, :3, 3].float()], dim=1).contiguous()
+
+
+def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool):
+    """Shifted-window attention (reference single_head_split_window_attention).
+    q [B, L, C]; k, v [B, L, C] or [B, m, L, C] -> [B, L, C] fp32."""
+    lib = _lib.load()
+    b, l, c = q.shape
+    m = 1 if k.dim() == 3 else k.shape[1]
+    q, k, v = _f32(q), _f32(k), _f32(v)
+    out = torch.empty((b, l, c), dtype=torch.float32, device=q.device)
+    rc = lib.tsplat_win_attn_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(out), b, h, w, c, m,
+                                 num_splits, int(with_shift), _lib.stream_ptr(q.device))
+    _lib.check(rc, "tsplat_win_attn_fwd")
+    return out
+
+
+def uv_coarse(feat, intr, pose, disp, h: int, w: int):
+    """Coarse correlation volume. feat [B, 2, HW, C] -> [B*2, HW, D] (see oracle.uv_coarse)."""
+    lib = _lib.load()
+    b, _, hw, c = feat.shape
+    d = disp.shape[1]
+    feat = _f32(feat)
+    cams = pack_cameras(intr, pose)
+    disp = _f32(disp)
+    out = torch.empty((b * 2, hw, d), dtype=torch.float32, device=feat.device)
+    rc = lib.tsplat_uv_coarse_fwd(_lib.ptr(feat), _lib.ptr(cams), _lib.ptr(disp), _lib.ptr(out), b, h, w,
+                                  c, d, _lib.stream_ptr(feat.device))
+    _lib.check(rc, "tsplat_uv_coarse_fwd")
+    return out
+
+
+def uv_cross(value, key, intr, pose, disp, offsets, logits, h: int, w: int):
+    """Fine cross correlation. value, key [B, 2, HW, C]; offsets [B*2, HW, D*P*2];
+    logits [B*2, HW, D*P] -> [B*2, HW, D] (see oracle.uv_cross)."""
+    lib = _lib.load()
+    b, _, hw, c = value.shape
+    d = disp.shape[1]
+    p = logits.shape[-1] // d
+    value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
+    cams = pack_cameras(intr, pose)
+    out = torch.empty((b * 2, hw, d), dtype=torch.float32, device=value.device)
+    rc = lib.tsplat_uv_cross_fwd(_lib.ptr(value), _lib.ptr(key), _lib.ptr(cams), _lib.ptr(disp),
+                                 _lib.ptr(offsets), _lib.ptr(logits), _lib.ptr(out), b, h, w, c, d, p,
+                                 _lib.stream_ptr(value.device))
+    _lib.check(rc, "tsplat_uv_cross_fwd")
+    return out
+
+
+def msda(value, loc, weights, h: int, w: int):
+    """Single-level single-head deformable sampling. value [N, HW, C], loc [N, Q, P, 2],
+    weights [N, Q, P] -> [N, Q, C] (see oracle.msda)."""
+    lib = _lib.load()
+    n, hw, c = value.shape
+    _, q, p, _ = loc.shape
+    value, loc, weights = _f32(value), _f32(loc), _f32(weights)
+    out = torch.empty((n, q, c), dtype=torch.float32, device=value.device)
+    rc = lib.tsplat_msda_fwd(_lib.ptr(value), _lib.ptr(loc), _lib.ptr(weights), _lib.ptr(out), n, h, w, c,
+                             q, p, _lib.stream_ptr(value.device))
+    _lib.check(rc, "tsplat_msda_fwd")
+    return out

@@ -1,0 +1,130 @@
+"""Depth-Anything-V2 DPT head + model (reference src/depth_anything_v2/dpt.py:38-184,
+util/blocks.py). Returns (relative depth [B, H, W], the 64-channel output_conv1 feature) exactly
+as the reference forward does; parameter names match (`depth_head.{projects,resize_layers,
+scratch.{layer*_rn,refinenet*,output_conv*}}`)."""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .dinov2 import DINOv2
+
+
+class ResidualConvUnit(nn.Module):
+    def __init__(self, features, activation, bn):
+        super().__init__()
+        self.bn = bn
+        self.conv1 = nn.Conv2d(features, features, kernel_size=3, stride=1, padding=1, bias=True)
+        self.conv2 = nn.Conv2d(features, features, kernel_size=3, stride=1, padding=1, bias=True)
+        if bn:
+            self.bn1 = nn.BatchNorm2d(features)
+            self.bn2 = nn.BatchNorm2d(features)
+        self.activation = activation
+
+    def forward(self, x):
+        out = self.conv1(self.activation(x))
+        if self.bn:
+            out = self.bn1(out)
+        out = self.conv2(self.activation(out))
+        if self.bn:
+            out = self.bn2(out)
+        return out + x
+
+
+class FeatureFusionBlock(nn.Module):
+    def __init__(self, features, activation, bn=False, align_corners=True, size=None):
+        super().__init__()
+        self.align_corners = align_corners
+        self.out_conv = nn.Conv2d(features, features, kernel_size=1, stride=1, padding=0, bias=True)
+        self.resConfUnit1 = ResidualConvUnit(features, activation, bn)
+        self.resConfUnit2 = ResidualConvUnit(features, activation, bn)
+        self.size = size
+
+    def forward(self, *xs, size=None):
+        output = xs[0]
+        if len(xs) == 2:
+            output = output + self.resConfUnit1(xs[1])
+        output = self.resConfUnit2(output)
+        if size is None and self.size is None:
+            modifier = {"scale_factor": 2}
+        elif size is None:
+            modifier = {"size": self.size}
+        else:
+            modifier = {"size": size}
+        output = F.interpolate(output, **modifier, mode="bilinear", align_corners=self.align_corners)
+        return self.out_conv(output)
+
+
+class _Scratch(nn.Module):
+    pass
+
+
+class DPTHead(nn.Module):
+    def __init__(self, in_channels, features=256, use_bn=False, out_channels=(256, 512, 1024, 1024),
+                 use_clstoken=False):
+        super().__init__()
+        if use_clstoken:
+            raise NotImplementedError("Depth-Anything-V2 ViT-B runs without the class-token readout")
+        self.use_clstoken = use_clstoken
+        self.projects = nn.ModuleList([nn.Conv2d(in_channels, oc, kernel_size=1, stride=1, padding=0)
+                                       for oc in out_channels])
+        self.resize_layers = nn.ModuleList([
+            nn.ConvTranspose2d(out_channels[0], out_channels[0], kernel_size=4, stride=4, padding=0),
+            nn.ConvTranspose2d(out_channels[1], out_channels[1], kernel_size=2, stride=2, padding=0),
+            nn.Identity(),
+            nn.Conv2d(out_channels[3], out_channels[3], kernel_size=3, stride=2, padding=1)])
+        s = _Scratch()
+        s.layer1_rn = nn.Conv2d(out_channels[0], features, 3, 1, 1, bias=False)
+        s.layer2_rn = nn.Conv2d(out_channels[1], features, 3, 1, 1, bias=False)
+        s.layer3_rn = nn.Conv2d(out_channels[2], features, 3, 1, 1, bias=False)
+        s.layer4_rn = nn.Conv2d(out_channels[3], features, 3, 1, 1, bias=False)
+        s.stem_transpose = None
+        act = nn.ReLU(False)
+        s.refinenet1 = FeatureFusionBlock(features, act, bn=use_bn)
+        s.refinenet2 = FeatureFusionBlock(features, act, bn=use_bn)
+        s.refinenet3 = FeatureFusionBlock(features, act, bn=use_bn)
+        s.refinenet4 = FeatureFusionBlock(features, act, bn=use_bn)
+        s.output_conv1 = nn.Conv2d(features, features // 2, kernel_size=3, stride=1, padding=1)
+        s.output_conv2 = nn.Sequential(
+            nn.Conv2d(features // 2, 32, kernel_size=3, stride=1, padding=1), nn.ReLU(True),
+            nn.Conv2d(32, 1, kernel_size=1, stride=1, padding=0), nn.ReLU(True), nn.Identity())
+        self.scratch = s
+
+    def forward(self, out_features, patch_h, patch_w):
+        out = []
+        for i, x in enumerate(out_features):
+            x = x[0]
+            x = x.permute(0, 2, 1).reshape((x.shape[0], x.shape[-1], patch_h, patch_w))
+            out.append(self.resize_layers[i](self.projects[i](x)))
+        layer_1, layer_2, layer_3, layer_4 = out
+        s = self.scratch
+        layer_1_rn, layer_2_rn = s.layer1_rn(layer_1), s.layer2_rn(layer_2)
+        layer_3_rn, layer_4_rn = s.layer3_rn(layer_3), s.layer4_rn(layer_4)
+        path_4 = s.refinenet4(layer_4_rn, size=layer_3_rn.shape[2:])
+        path_3 = s.refinenet3(path_4, layer_3_rn, size=layer_2_rn.shape[2:])
+        path_2 = s.refinenet2(path_3, layer_2_rn, size=layer_1_rn.shape[2:])
+        path_1 = s.refinenet1(path_2, layer_1_rn)
+        final_out = s.output_conv1(path_1)
+        out_feature = final_out.clone().detach()
+        final_out = F.interpolate(final_out, (int(patch_h * 14), int(patch_w * 14)), mode="bilinear",
+                                  align_corners=True)
+        return s.output_conv2(final_out), out_feature
+
+
+class DepthAnythingV2(nn.Module):
+    def __init__(self, encoder="vitl", features=256, out_channels=(256, 512, 1024, 1024), use_bn=False,
+                 use_clstoken=False):
+        super().__init__()
+        self.intermediate_layer_idx = {"vits": [2, 5, 8, 11], "vitb": [2, 5, 8, 11], "vitl": [4, 11, 17, 23]}
+        self.encoder = encoder
+        self.pretrained = DINOv2(model_name=encoder)
+        self.depth_head = DPTHead(self.pretrained.embed_dim, features, use_bn, out_channels=out_channels,
+                                  use_clstoken=use_clstoken)
+
+    def forward(self, x):
+        patch_h, patch_w = x.shape[-2] // 14, x.shape[-1] // 14
+        features = self.pretrained.get_intermediate_layers(x, self.intermediate_layer_idx[self.encoder],
+                                                           return_class_token=True)
+        depth, out_features = self.depth_head(features, patch_h, patch_w)
+        return F.relu(depth).squeeze(1), out_features

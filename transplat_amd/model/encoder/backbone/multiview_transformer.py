@@ -1,0 +1,118 @@
+"""Multi-view swin transformer (reference src/model/encoder/backbone/multiview_transformer.py).
+
+Same module tree and parameter names as the reference (`layers.{i}.self_attn.{q_proj,k_proj,
+v_proj,merge,norm1}`, `layers.{i}.cross_attn_ffn.{...,mlp.{0,2},norm2}`) so checkpoints load;
+the split-window attention (T2/T3 of SURVEY §8a: roll, partition, shifted mask, QK^T, softmax,
+AV, merge, roll back) is ONE gfx950 kernel call (transplat_amd.kernels.window_attention).
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from .... import kernels
+
+
+class TransformerLayer(nn.Module):
+    """reference multiview_transformer.py:285-407 (swin, single head)."""
+
+    def __init__(self, d_model=256, nhead=1, attention_type="swin", no_ffn=False, ffn_dim_expansion=4,
+                 with_shift=False, add_per_view_attn=False, **kwargs):
+        super().__init__()
+        if nhead != 1 or attention_type != "swin" or add_per_view_attn:
+            raise NotImplementedError("TranSplat uses single-head swin attention")
+        self.dim = d_model
+        self.nhead = nhead
+        self.attention_type = attention_type
+        self.no_ffn = no_ffn
+        self.with_shift = with_shift
+        self.q_proj = nn.Linear(d_model, d_model, bias=False)
+        self.k_proj = nn.Linear(d_model, d_model, bias=False)
+        self.v_proj = nn.Linear(d_model, d_model, bias=False)
+        self.merge = nn.Linear(d_model, d_model, bias=False)
+        self.norm1 = nn.LayerNorm(d_model)
+        if not self.no_ffn:
+            in_channels = d_model * 2
+            self.mlp = nn.Sequential(
+                nn.Linear(in_channels, in_channels * ffn_dim_expansion, bias=False),
+                nn.GELU(),
+                nn.Linear(in_channels * ffn_dim_expansion, d_model, bias=False),
+            )
+            self.norm2 = nn.LayerNorm(d_model)
+
+    def forward(self, source, target, height=None, width=None, attn_num_splits=None, **kwargs):
+        # source [B, L, C]; target [B, L, C] (self) or [B, V-1, L, C] (cross)
+        query = self.q_proj(source)
+        key = self.k_proj(target)
+        value = self.v_proj(target)
+        message = kernels.window_attention(query, key, value, height, width, attn_num_splits, self.with_shift)
+        message = self.norm1(self.merge(message))
+        if not self.no_ffn:
+            message = self.norm2(self.mlp(torch.cat([source, message], dim=-1)))
+        return source + message
+
+
+class TransformerBlock(nn.Module):
+    """self attention + cross attention + FFN (reference :410-492)."""
+
+    def __init__(self, d_model=256, nhead=1, attention_type="swin", ffn_dim_expansion=4, with_shift=False,
+                 add_per_view_attn=False, no_cross_attn=False, **kwargs):
+        super().__init__()
+        if no_cross_attn:
+            raise NotImplementedError("TranSplat always uses cross-view attention")
+        self.no_cross_attn = no_cross_attn
+        self.self_attn = TransformerLayer(d_model=d_model, nhead=nhead, attention_type=attention_type,
+                                          no_ffn=True, ffn_dim_expansion=ffn_dim_expansion, with_shift=with_shift)
+        self.cross_attn_ffn = TransformerLayer(d_model=d_model, nhead=nhead, attention_type=attention_type,
+                                               ffn_dim_expansion=ffn_dim_expansion, with_shift=with_shift,
+                                               add_per_view_attn=add_per_view_attn)
+
+    def forward(self, source, target, height=None, width=None, attn_num_splits=None, **kwargs):
+        source = self.self_attn(source, source, height=height, width=width, attn_num_splits=attn_num_splits)
+        return self.cross_attn_ffn(source, target, height=height, width=width, attn_num_splits=attn_num_splits)
+
+
+def batch_features(features):
+    """(reference :495-515) queries [N*B, ...] and the other N-1 views [N*B, N-1, ...]."""
+    q, kv = [], []
+    for i in range(len(features)):
+        x = list(features)
+        q.append(x.pop(i))
+        kv.append(torch.stack(x, dim=1))
+    return torch.cat(q, dim=0), torch.cat(kv, dim=0)
+
+
+class MultiViewFeatureTransformer(nn.Module):
+    """6 blocks of self + cross window attention (reference :518-630); odd blocks shifted."""
+
+    def __init__(self, num_layers=6, d_model=128, nhead=1, attention_type="swin", ffn_dim_expansion=4,
+                 add_per_view_attn=False, no_cross_attn=False, **kwargs):
+        super().__init__()
+        self.attention_type = attention_type
+        self.d_model = d_model
+        self.nhead = nhead
+        self.layers = nn.ModuleList([
+            TransformerBlock(d_model=d_model, nhead=nhead, attention_type=attention_type,
+                             ffn_dim_expansion=ffn_dim_expansion, with_shift=(attention_type == "swin" and i % 2 == 1),
+                             add_per_view_attn=add_per_view_attn, no_cross_attn=no_cross_attn)
+            for i in range(num_layers)
+        ])
+        for p in self.parameters():
+            if p.dim() > 1:
+                nn.init.xavier_uniform_(p)
+
+    def forward(self, multi_view_features, attn_num_splits=None, **kwargs):
+        b, c, h, w = multi_view_features[0].shape
+        assert self.d_model == c
+        num_views = len(multi_view_features)
+        if not attn_num_splits or attn_num_splits <= 1:
+            raise NotImplementedError("TranSplat runs split-window attention (multiview_trans_attn_split=2)")
+        concat0, concat1 = batch_features(multi_view_features)
+        concat0 = concat0.reshape(num_views * b, c, -1).permute(0, 2, 1)  # [N*B, HW, C]
+        concat1 = concat1.reshape(num_views * b, num_views - 1, c, -1).permute(0, 1, 3, 2)  # [N*B, N-1, HW, C]
+        for i, layer in enumerate(self.layers):
+            concat0 = layer(concat0, concat1, height=h, width=w, attn_num_splits=attn_num_splits)
+            if i < len(self.layers) - 1:
+                concat0, concat1 = batch_features(list(concat0.chunk(chunks=num_views, dim=0)))
+        features = concat0.chunk(chunks=num_views, dim=0)
+        return [f.view(b, h, w, c).permute(0, 3, 1, 2).contiguous() for f in features]

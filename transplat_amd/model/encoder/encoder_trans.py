@@ -1,0 +1,191 @@
+"""TranSplat encoder: context views -> per-pixel 3-D Gaussians
+(reference src/model/encoder/encoder_trans.py:40-376, same constructor config and forward
+signature, same module names -> `encoder.*` checkpoint keys load).
+
+Stages (reference bench tags encoder_1..5): intrinsics prep, multi-view backbone (gfx950 window
+attention), Depth-Anything-V2 (no_grad), cost-volume depth predictor (gfx950 correlation
+kernels), Gaussian adapter (e3nn-free SH rotation). No host synchronisation between stages
+(the reference forces torch.cuda.synchronize() around each).
+"""
+from __future__ import annotations
+
+from contextlib import nullcontext
+from dataclasses import dataclass, field
+from typing import List, Literal, Optional
+
+import torch
+import torch.nn.functional as F
+from einops import rearrange
+from torch import nn
+
+from ...geometry.projection import sample_image_grid
+from ..depth_anything.dpt import DepthAnythingV2
+from ..types import Gaussians
+from .backbone.backbone_multiview import BackboneMultiview
+from .common.gaussian_adapter import GaussianAdapter, GaussianAdapterCfg
+from .encoder import Encoder
+from .matching.depth_predictor_trans import DepthPredictorTrans
+
+_DA_CONFIGS = {
+    "vits": {"encoder": "vits", "features": 64, "out_channels": [48, 96, 192, 384]},
+    "vitb": {"encoder": "vitb", "features": 128, "out_channels": [96, 192, 384, 768]},
+    "vitl": {"encoder": "vitl", "features": 256, "out_channels": [256, 512, 1024, 1024]},
+}
+
+
+@dataclass
+class OpacityMappingCfg:
+    initial: float = 0.0
+    final: float = 0.0
+    warm_up: int = 1
+
+
+@dataclass
+class EncoderTransCfg:
+    """Defaults = config/model/encoder/trans.yaml overridden by config/experiment/re10k.yaml."""
+
+    name: Literal["trans"] = "trans"
+    d_feature: int = 128
+    num_depth_candidates: int = 128
+    num_surfaces: int = 1
+    gaussian_adapter: GaussianAdapterCfg = field(default_factory=GaussianAdapterCfg)
+    opacity_mapping: OpacityMappingCfg = field(default_factory=OpacityMappingCfg)
+    gaussians_per_pixel: int = 1
+    unimatch_weights_path: Optional[str] = None
+    downscale_factor: int = 4
+    shim_patch_size: int = 4
+    multiview_trans_attn_split: int = 2
+    costvolume_unet_feat_dim: int = 128
+    costvolume_unet_channel_mult: List[int] = field(default_factory=lambda: [1, 1, 1])
+    costvolume_unet_attn_res: List[int] = field(default_factory=lambda: [4])
+    depth_unet_feat_dim: int = 32
+    depth_unet_attn_res: List[int] = field(default_factory=lambda: [16])
+    depth_unet_channel_mult: List[int] = field(default_factory=lambda: [1, 1, 1, 1, 1])
+    wo_depth_refine: bool = False
+    wo_cost_volume: bool = False
+    wo_cost_volume_refine: bool = False
+    num_context_views: int = 2  # the reference reads it from the global dataset config
+    da_encoder: str = "vitb"
+    # Arithmetic of the conv / GEMM layers around the hand-written kernels (CNN, cam encoders,
+    # DA-V2, U-Nets, heads): "fp32" (parity mode) or "bf16" (autocast). Correlation and the
+    # rasterizer always run fp32.
+    dense_dtype: str = "fp32"
+
+
+class EncoderTrans(Encoder[EncoderTransCfg]):
+    def __init__(self, cfg: EncoderTransCfg) -> None:
+        super().__init__(cfg)
+        self.backbone = BackboneMultiview(feature_channels=cfg.d_feature, downscale_factor=cfg.downscale_factor)
+        self.gaussian_adapter = GaussianAdapter(cfg.gaussian_adapter)
+        da = _DA_CONFIGS[cfg.da_encoder]
+        self.da_model = DepthAnythingV2(**da).eval()
+        for p in self.da_model.parameters():
+            p.requires_grad = False
+        self.depth_predictor = DepthPredictorTrans(
+            feature_channels=cfg.d_feature, upscale_factor=cfg.downscale_factor,
+            num_depth_candidates=cfg.num_depth_candidates, costvolume_unet_feat_dim=cfg.costvolume_unet_feat_dim,
+            costvolume_unet_channel_mult=tuple(cfg.costvolume_unet_channel_mult),
+            costvolume_unet_attn_res=tuple(cfg.costvolume_unet_attn_res),
+            gaussian_raw_channels=cfg.num_surfaces * (self.gaussian_adapter.d_in + 2),
+            gaussians_per_pixel=cfg.gaussians_per_pixel, num_views=cfg.num_context_views,
+            depth_unet_feat_dim=cfg.depth_unet_feat_dim, depth_unet_attn_res=cfg.depth_unet_attn_res,
+            depth_unet_channel_mult=cfg.depth_unet_channel_mult, DA_size=da["features"] // 2)
+
+    def map_pdf_to_opacity(self, pdf, global_step: int):
+        """(reference :139-152)"""
+        cfg = self.cfg.opacity_mapping
+        x = cfg.initial + min(global_step / cfg.warm_up, 1) * (cfg.final - cfg.initial)
+        exponent = 2**x
+        return 0.5 * (1 - (1 - pdf) ** exponent + pdf ** (1 / exponent))
+
+    @staticmethod
+    def normalize_images(images):
+        shape = [*[1] * (images.dim() - 3), 3, 1, 1]
+        mean = torch.tensor([0.485, 0.456, 0.406]).reshape(*shape).to(images.device)
+        std = torch.tensor([0.229, 0.224, 0.225]).reshape(*shape).to(images.device)
+        return (images - mean) / std
+
+    def _dense(self):
+        if self.cfg.dense_dtype == "bf16":
+            return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
+        return nullcontext()
+
+    def forward(self, context: dict, global_step: int = 0, deterministic: bool = False,
+                visualization_dump: Optional[dict] = None, scene_names=None, benchmarker=None,
+                analyze_feature_depth: bool = False, enable_saes: bool = False, saes_config=None) -> Gaussians:
+        device = context["image"].device
+        b, v, _, h, w = context["image"].shape
+
+        def bench(tag):
+            return benchmarker.time(tag) if benchmarker is not None else nullcontext()
+
+        with bench("encoder_1_prep_intrinsics"):
+            intr_curr = context["intrinsics"][:, :, :3, :3].clone().detach()
+            intr_curr[:, :, 0, :] *= float(w)
+            intr_curr[:, :, 1, :] *= float(h)
+            camk = torch.eye(4, device=device).view(1, 1, 4, 4).repeat(b, v, 1, 1).float()
+            camk[:, :, :3, :3] = intr_curr
+            img2world = torch.matmul(context["extrinsics"].clone().detach(), torch.inverse(camk))
+
+        with bench("encoder_2_backbone"), self._dense():
+            trans_features, cnn_features = self.backbone(context["image"], attn_splits=self.cfg.multiview_trans_attn_split,
+                                                         return_cnn_features=True, img2world=img2world)
+        trans_features = trans_features.float()
+        cnn_features = cnn_features.float()
+
+        with bench("encoder_3_depth_anything"), torch.no_grad(), self._dense():
+            da_images = self.normalize_images(context["image"])[:, :, [2, 0, 1]]
+            da_images = da_images.reshape(b * v, 3, h, w)
+            da_images = F.interpolate(da_images, (252, 252), mode="bilinear", align_corners=True)
+            da_depth, out_feature = self.da_model(da_images)
+            da_depth = F.interpolate(da_depth[None].float(), (h, w), mode="bilinear", align_corners=True)
+            da_depth = da_depth.view(b, v, 1, h, w).flatten(2)
+            da_max = torch.max(da_depth, dim=-1, keepdim=True)[0]
+            da_min = torch.min(da_depth, dim=-1, keepdim=True)[0]
+            da_depth = ((da_depth - da_min) / (da_max - da_min)).reshape(b, v, 1, h, w)
+        dino_feature = out_feature.float().view(b, v, *out_feature.shape[1:])
+
+        extra_info = {"images": rearrange(context["image"], "b v c h w -> (v b) c h w"), "scene_names": scene_names}
+        gpp = self.cfg.gaussians_per_pixel
+        with bench("encoder_4_depth_predictor"), self._dense():
+            depths, densities, raw_gaussians = self.depth_predictor(
+                trans_features, context["intrinsics"], context["extrinsics"], context["near"], context["far"],
+                gaussians_per_pixel=gpp, deterministic=deterministic, extra_info=extra_info,
+                cnn_features=cnn_features, da_depth=da_depth, dino_feature=dino_feature, benchmarker=benchmarker)
+        depths, densities, raw_gaussians = depths.float(), densities.float(), raw_gaussians.float()
+
+        with bench("encoder_5_gaussian_adapter"):
+            xy_ray, _ = sample_image_grid((h, w), device)
+            xy_ray = rearrange(xy_ray, "h w xy -> (h w) () xy")
+            gaussians = rearrange(raw_gaussians, "... (srf c) -> ... srf c", srf=self.cfg.num_surfaces)
+            offset_xy = gaussians[..., :2].sigmoid()
+            pixel_size = 1 / torch.tensor((w, h), dtype=torch.float32, device=device)
+            xy_ray = xy_ray + (offset_xy - 0.5) * pixel_size
+            gaussians = self.gaussian_adapter.forward(
+                rearrange(context["extrinsics"], "b v i j -> b v () () () i j"),
+                rearrange(context["intrinsics"], "b v i j -> b v () () () i j"),
+                rearrange(xy_ray, "b v r srf xy -> b v r srf () xy"),
+                depths,
+                self.map_pdf_to_opacity(densities, global_step) / gpp,
+                rearrange(gaussians[..., 2:], "b v r srf c -> b v r srf () c"),
+                (h, w),
+            )
+        if visualization_dump is not None:
+            visualization_dump["depth"] = rearrange(depths, "b v (h w) srf s -> b v h w srf s", h=h, w=w)
+        return Gaussians(
+            rearrange(gaussians.means, "b v r srf spp xyz -> b (v r srf spp) xyz"),
+            rearrange(gaussians.covariances, "b v r srf spp i j -> b (v r srf spp) i j"),
+            rearrange(gaussians.harmonics, "b v r srf spp c d_sh -> b (v r srf spp) c d_sh"),
+            rearrange(gaussians.opacities, "b v r srf spp -> b (v r srf spp)"),
+        )
+
+    def get_data_shim(self):
+        """(reference :355-371) crop to a multiple of shim_patch_size * downscale_factor."""
+        patch = self.cfg.shim_patch_size * self.cfg.downscale_factor
+
+        def data_shim(batch):
+            from ...dataset_shims import apply_patch_shim
+
+            return apply_patch_shim(batch, patch_size=patch)
+
+        return data_shim

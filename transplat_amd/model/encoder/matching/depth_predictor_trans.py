@@ -1,0 +1,156 @@
+"""Cost-volume depth predictor (reference src/model/encoder/matching/depth_predictor_trans.py).
+
+IMPORTANT (as in the reference): tensors here are (v b)-ordered, not (b v).
+Stages: camera prep -> coarse + fine UV correlation (gfx950 kernels, grid
+computed in-kernel) -> cost-volume U-Net -> softmax depth -> refine U-Net -> Gaussian heads.
+Parameter names match the reference for checkpoint loading.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+from einops import rearrange, repeat
+from torch import nn
+
+from ...utils.cam_param_encoder import cam_param_encoder
+from ...utils.uv_transformer import UVTransformer
+from .ldm_unet import UNetModel
+
+
+def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, num_samples):
+    """(reference :59-109) per-view features, pixel intrinsics, relative poses and disparity
+    candidates 1/far + linspace(0, 1, D) (1/near - 1/far), all in (v b) order."""
+    b, v, _, h, w = features.shape
+    feat_lists = [rearrange(features, "b v ... -> (v b) ...")]
+    pose_curr_lists = []
+    init_view_order = list(range(v))
+    for idx in range(1, v):
+        cur_view_order = init_view_order[idx:] + init_view_order[:idx]
+        feat_lists.append(rearrange(features[:, cur_view_order], "b v ... -> (v b) ..."))
+        if v > 2:
+            cur = [extrinsics[:, v1].clone().detach().inverse() @ extrinsics[:, v0].clone().detach()
+                   for v0, v1 in zip(init_view_order, cur_view_order)]
+            pose_curr_lists.append(torch.cat(cur, dim=0))
+    if v == 2:
+        pose_ref = extrinsics[:, 0].clone().detach()
+        pose_tgt = extrinsics[:, 1].clone().detach()
+        pose = pose_tgt.inverse() @ pose_ref
+        pose_curr_lists = [torch.cat((pose, pose.inverse()), dim=0)]
+    intr_curr = intrinsics[:, :, :3, :3].clone().detach()
+    intr_curr[:, :, 0, :] *= float(w)
+    intr_curr[:, :, 1, :] *= float(h)
+    intr_curr = rearrange(intr_curr, "b v ... -> (v b) ...", b=b, v=v)
+    min_depth = rearrange(1.0 / far.clone().detach(), "b v -> (v b) 1")
+    max_depth = rearrange(1.0 / near.clone().detach(), "b v -> (v b) 1")
+    depth_candi_curr = (min_depth + torch.linspace(0.0, 1.0, num_samples).unsqueeze(0).to(min_depth.device)
+                        * (max_depth - min_depth)).type_as(features)
+    depth_candi_curr = repeat(depth_candi_curr, "vb d -> vb d () ()")
+    return feat_lists, intr_curr, pose_curr_lists, depth_candi_curr
+
+
+class DepthPredictorTrans(nn.Module):
+    def __init__(self, feature_channels=128, upscale_factor=4, num_depth_candidates=32, costvolume_unet_feat_dim=128,
+                 costvolume_unet_channel_mult=(1, 1, 1), costvolume_unet_attn_res=(), gaussian_raw_channels=-1,
+                 gaussians_per_pixel=1, num_views=2, depth_unet_feat_dim=64, depth_unet_attn_res=(),
+                 depth_unet_channel_mult=(1, 1, 1), DA_size=128, **kwargs):
+        super().__init__()
+        self.num_depth_candidates = num_depth_candidates
+        self.regressor_feat_dim = costvolume_unet_feat_dim
+        self.upscale_factor = upscale_factor
+        input_channels = num_depth_candidates + feature_channels
+        channels = self.regressor_feat_dim
+        self.corr_refine_net = nn.Sequential(
+            nn.Conv2d(input_channels, channels, 3, 1, 1), nn.GroupNorm(8, channels), nn.GELU(),
+            UNetModel(image_size=None, in_channels=channels, model_channels=channels, out_channels=channels,
+                      num_res_blocks=1, attention_resolutions=costvolume_unet_attn_res,
+                      channel_mult=costvolume_unet_channel_mult, num_head_channels=32, dims=2, postnorm=True,
+                      num_frames=num_views, use_cross_view_self_attn=True),
+            nn.Conv2d(channels, num_depth_candidates, 3, 1, 1))
+        self.regressor_residual = nn.Conv2d(input_channels, num_depth_candidates, 1, 1, 0)
+        self.depth_head_lowres = nn.Sequential(
+            nn.Conv2d(num_depth_candidates, num_depth_candidates * 2, 3, 1, 1), nn.GELU(),
+            nn.Conv2d(num_depth_candidates * 2, num_depth_candidates, 3, 1, 1))
+        proj_in_channels = feature_channels + feature_channels
+        upsample_out_channels = feature_channels
+        self.upsampler = nn.Sequential(
+            nn.Conv2d(proj_in_channels, upsample_out_channels, 3, 1, 1),
+            nn.Upsample(scale_factor=upscale_factor, mode="bilinear", align_corners=True), nn.GELU())
+        self.proj_feature = nn.Conv2d(upsample_out_channels, depth_unet_feat_dim, 3, 1, 1)
+        input_channels = 3 + 1 + depth_unet_feat_dim + 1 + 1
+        channels = depth_unet_feat_dim
+        self.refine_unet = nn.Sequential(
+            nn.Conv2d(input_channels, channels, 3, 1, 1), nn.GroupNorm(4, channels), nn.GELU(),
+            UNetModel(image_size=None, in_channels=channels, model_channels=channels, out_channels=channels,
+                      num_res_blocks=1, attention_resolutions=depth_unet_attn_res,
+                      channel_mult=depth_unet_channel_mult, num_head_channels=32, dims=2, postnorm=True,
+                      num_frames=num_views, use_cross_view_self_attn=True))
+        gau_in = depth_unet_feat_dim + 3 + feature_channels
+        self.to_gaussians = nn.Sequential(
+            nn.Conv2d(gau_in, gaussian_raw_channels * 2, 3, 1, 1), nn.GELU(),
+            nn.Conv2d(gaussian_raw_channels * 2, gaussian_raw_channels, 3, 1, 1))
+        channels = depth_unet_feat_dim
+        self.to_disparity = nn.Sequential(
+            nn.Conv2d(channels, channels * 2, 3, 1, 1), nn.GELU(),
+            nn.Conv2d(channels * 2, gaussians_per_pixel * 2, 3, 1, 1))
+        self.embed_dims = 128
+        self.coarse_transformer = UVTransformer(embed_dims=self.embed_dims, mode="coarse", num_layers=1)
+        self.fine_transformer = UVTransformer(embed_dims=self.embed_dims, mode="fine", num_layers=2)
+        self.cam_param_encoder = cam_param_encoder(in_channels=DA_size, mid_channels=128, embed_dims=128)
+
+    def match_two(self, intr_curr, pose_curr, extrinsics, disp_candi_curr, dino_feature, features):
+        """(reference :236-290) coarse then fine correlation for a pair of views -> [(v b), D, h, w]."""
+        b, v, c, h, w = features.shape
+        cameras = (intr_curr, pose_curr, disp_candi_curr.flatten(1))
+        camk = torch.eye(4, device=intr_curr.device).view(1, 4, 4).repeat(intr_curr.shape[0], 1, 1).float()
+        camk[:, :3, :3] = intr_curr
+        c2w = rearrange(extrinsics.clone().detach(), "b v ... -> (v b) ...", b=b, v=v)
+        img2world = torch.matmul(c2w, torch.inverse(camk)).reshape(-1, 16)
+        pos_feature = self.cam_param_encoder(dino_feature, img2world)  # [(v b), C, h, w]
+        # (b v)-ordered channel-last query positions: the reference's bev_pos after its permutes
+        bev_pos = rearrange(pos_feature, "(v b) c h w -> (b v) (h w) c", v=v, b=b)
+        feat_cl = features.flatten(3).transpose(2, 3).contiguous()  # [b, v, HW, C]
+        query = torch.zeros((b * v, h * w, self.embed_dims), device=features.device, dtype=features.dtype)
+        corr = self.coarse_transformer([features], query, w, h, cameras=cameras, channel_last=feat_cl)
+        corr = self.fine_transformer([features], corr, w, h, bev_pos=bev_pos, cameras=cameras, channel_last=feat_cl)
+        return rearrange(corr, "(b v) (h w) c -> (v b) c h w", b=b, v=v, h=h, w=w)
+
+    def forward(self, features, intrinsics, extrinsics, near, far, gaussians_per_pixel=1, deterministic=True,
+                extra_info=None, cnn_features=None, da_depth=None, dino_feature=None, benchmarker=None):
+        b, v, c, h, w = features.shape
+        if da_depth is not None:
+            da_depth = rearrange(da_depth, "b v ... -> (v b) ...")
+        if cnn_features is not None:
+            cnn_features = rearrange(cnn_features, "b v ... -> (v b) ...")
+        if dino_feature is not None:
+            dino_feature = rearrange(dino_feature, "b v ... -> (v b) ...")
+            dino_feature = F.interpolate(dino_feature, size=(h, w), mode="bilinear", align_corners=True)
+        feat_comb_lists, intr_curr, pose_curr_lists, disp_candi_curr = prepare_feat_proj_data_lists(
+            features, intrinsics, extrinsics, near, far, num_samples=self.num_depth_candidates)
+        feat01 = feat_comb_lists[0]
+        if v != 2:
+            raise NotImplementedError("V > 2 context views: pairwise match_two averaging not built yet")
+        raw_correlation_in = self.match_two(intr_curr, pose_curr_lists[0], extrinsics, disp_candi_curr, dino_feature,
+                                            features)
+        raw_correlation_in = torch.cat((raw_correlation_in, feat01), dim=1)
+
+        raw_correlation = self.corr_refine_net(raw_correlation_in) + self.regressor_residual(raw_correlation_in)
+        pdf = F.softmax(self.depth_head_lowres(raw_correlation), dim=1)
+        coarse_disps = (disp_candi_curr * pdf).sum(dim=1, keepdim=True)
+        pdf_max = torch.max(pdf, dim=1, keepdim=True)[0]
+        pdf_max = F.interpolate(pdf_max, scale_factor=self.upscale_factor)
+        fullres_disps = F.interpolate(coarse_disps, scale_factor=self.upscale_factor, mode="bilinear",
+                                      align_corners=True)
+
+        proj_feat_in_fullres = self.upsampler(torch.cat((feat01, cnn_features), dim=1))
+        proj_feature = self.proj_feature(proj_feat_in_fullres)
+        refine_out = self.refine_unet(torch.cat((extra_info["images"], da_depth, proj_feature, fullres_disps,
+                                                 pdf_max), dim=1))
+
+        raw_gaussians = self.to_gaussians(torch.cat([refine_out, extra_info["images"], proj_feat_in_fullres], dim=1))
+        raw_gaussians = rearrange(raw_gaussians, "(v b) c h w -> b v (h w) c", v=v, b=b)
+        delta_disps, raw_densities = self.to_disparity(refine_out).split(gaussians_per_pixel, dim=1)
+        densities = repeat(F.sigmoid(raw_densities), "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
+        fine_disps = (fullres_disps + delta_disps).clamp(1.0 / rearrange(far, "b v -> (v b) () () ()"),
+                                                         1.0 / rearrange(near, "b v -> (v b) () () ()"))
+        depths = repeat(1.0 / fine_disps, "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
+        return depths, densities, raw_gaussians

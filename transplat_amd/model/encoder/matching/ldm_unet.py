@@ -1,0 +1,169 @@
+"""LDM-style 2-D U-Net with cross-view self-attention, as configured by DepthPredictorTrans
+(reference src/model/encoder/matching/ldm_unet/{unet.py:589-1144, util.py}).
+
+Only the configuration the depth predictor instantiates is built: postnorm ResBlocks, conv
+down/up-sampling, legacy QKV attention at the requested resolutions with views folded into the
+token axis, middle block = ResBlock, Identity, ResBlock. Module indices and parameter names
+follow the reference (`input_blocks.{i}.{j}`, `middle_block.{0,2}`, `output_blocks.{i}.{j}`,
+`out.{0,1}`) so checkpoint keys load. Convolutions and GEMMs run on MIOpen / hipBLASLt.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from einops import rearrange
+from torch import nn
+
+
+class GroupNorm32(nn.GroupNorm):
+    def forward(self, x):
+        return super().forward(x.float()).type(x.dtype)
+
+
+def normalization(channels):
+    """GroupNorm8 when channels % 8 == 0 else GroupNorm4 (reference util.py:189-208)."""
+    return GroupNorm32(8 if channels % 8 == 0 else 4, channels)
+
+
+class ResBlock(nn.Module):
+    """postnorm residual block (reference unet.py:177-300): conv-GN-SiLU, conv-GN-SiLU, skip."""
+
+    def __init__(self, channels, out_channels=None, kernel_size=3):
+        super().__init__()
+        self.channels = channels
+        self.out_channels = out_channels or channels
+        pad = (kernel_size - 1) // 2
+        self.in_layers = nn.Sequential(
+            nn.Conv2d(channels, self.out_channels, kernel_size, padding=pad), normalization(self.out_channels),
+            nn.SiLU())
+        self.out_layers = nn.Sequential(
+            nn.Conv2d(self.out_channels, self.out_channels, kernel_size, padding=pad),
+            normalization(self.out_channels), nn.SiLU())
+        self.skip_connection = (nn.Identity() if self.out_channels == channels
+                                else nn.Conv2d(channels, self.out_channels, 1))
+
+    def forward(self, x):
+        return self.skip_connection(x) + self.out_layers(self.in_layers(x))
+
+
+class QKVAttentionLegacy(nn.Module):
+    """heads split before q/k/v; views folded into tokens ((v b) n t -> b n (v t))
+    (reference unet.py:510-552)."""
+
+    def __init__(self, n_heads, n_frames=2, use_cross_view_self_attn=False):
+        super().__init__()
+        self.n_heads = n_heads
+        self.n_frames = n_frames
+        self.use_cross_view_self_attn = use_cross_view_self_attn
+
+    def forward(self, qkv):
+        if self.use_cross_view_self_attn:
+            qkv = rearrange(qkv, "(v b) n t -> b n (v t)", v=self.n_frames)
+        bs, width, length = qkv.shape
+        ch = width // (3 * self.n_heads)
+        q, k, v = qkv.reshape(bs * self.n_heads, ch * 3, length).split(ch, dim=1)
+        scale = 1 / math.sqrt(math.sqrt(ch))
+        weight = torch.einsum("bct,bcs->bts", q * scale, k * scale)
+        weight = torch.softmax(weight.float(), dim=-1).type(weight.dtype)
+        a = torch.einsum("bts,bcs->bct", weight, v).reshape(bs, -1, length)
+        if self.use_cross_view_self_attn:
+            a = rearrange(a, "b n (v t) -> (v b) n t", v=self.n_frames)
+        return a
+
+
+class AttentionBlock(nn.Module):
+    """postnorm self-attention block (reference unet.py:306-370)."""
+
+    def __init__(self, channels, num_head_channels=32, num_frames=2, use_cross_view_self_attn=False):
+        super().__init__()
+        self.channels = channels
+        self.num_heads = channels // num_head_channels
+        self.qkv = nn.Conv1d(channels, channels * 3, 1)
+        self.attention = QKVAttentionLegacy(self.num_heads, n_frames=num_frames,
+                                            use_cross_view_self_attn=use_cross_view_self_attn)
+        self.proj_out = nn.Conv1d(channels, channels, 1)
+        self.norm = normalization(channels)
+
+    def forward(self, x):
+        b, c, *spatial = x.shape
+        x = x.reshape(b, c, -1)
+        h = self.norm(self.proj_out(self.attention(self.qkv(x))))
+        return (x + h).reshape(b, c, *spatial)
+
+
+class Downsample(nn.Module):
+    def __init__(self, channels, out_channels=None):
+        super().__init__()
+        self.channels = channels
+        self.op = nn.Conv2d(channels, out_channels or channels, 3, stride=2, padding=1)
+
+    def forward(self, x):
+        return self.op(x)
+
+
+class Upsample(nn.Module):
+    def __init__(self, channels, out_channels=None):
+        super().__init__()
+        self.channels = channels
+        self.conv = nn.Conv2d(channels, out_channels or channels, 3, padding=1)
+
+    def forward(self, x):
+        return self.conv(F.interpolate(x, scale_factor=2, mode="nearest"))
+
+
+class UNetModel(nn.Module):
+    def __init__(self, image_size, in_channels, model_channels, out_channels, num_res_blocks, attention_resolutions,
+                 dropout=0, channel_mult=(1, 2, 4, 8), conv_resample=True, dims=2, postnorm=False,
+                 num_head_channels=-1, num_frames=2, use_cross_view_self_attn=False, **kwargs):
+        super().__init__()
+        if dims != 2 or not postnorm or not conv_resample or num_head_channels <= 0:
+            raise NotImplementedError("only the DepthPredictorTrans configuration is built")
+        self.in_channels = in_channels
+        self.model_channels = model_channels
+        self.out_channels = out_channels
+        attn = lambda ch: AttentionBlock(ch, num_head_channels=num_head_channels, num_frames=num_frames,
+                                         use_cross_view_self_attn=use_cross_view_self_attn)
+        self.input_blocks = nn.ModuleList([nn.Sequential(nn.Conv2d(in_channels, model_channels, 3, padding=1))])
+        input_block_chans = [model_channels]
+        ch = model_channels
+        ds = 1
+        for level, mult in enumerate(channel_mult):
+            for _ in range(num_res_blocks):
+                layers = [ResBlock(ch, out_channels=mult * model_channels)]
+                ch = mult * model_channels
+                if ds in attention_resolutions:
+                    layers.append(attn(ch))
+                self.input_blocks.append(nn.Sequential(*layers))
+                input_block_chans.append(ch)
+            if level != len(channel_mult) - 1:
+                self.input_blocks.append(nn.Sequential(Downsample(ch, out_channels=ch)))
+                input_block_chans.append(ch)
+                ds *= 2
+        self.middle_block = nn.Sequential(ResBlock(ch), nn.Identity(), ResBlock(ch))
+        self.output_blocks = nn.ModuleList([])
+        for level, mult in list(enumerate(channel_mult))[::-1]:
+            for i in range(num_res_blocks + 1):
+                ich = input_block_chans.pop()
+                layers = [ResBlock(ch + ich, out_channels=model_channels * mult)]
+                ch = model_channels * mult
+                if ds in attention_resolutions:
+                    layers.append(attn(ch))
+                if level and i == num_res_blocks:
+                    layers.append(Upsample(ch, out_channels=ch))
+                    ds //= 2
+                self.output_blocks.append(nn.Sequential(*layers))
+        self.out = nn.Sequential(nn.Conv2d(model_channels, out_channels, 3, padding=1), normalization(out_channels),
+                                 nn.SiLU())
+
+    def forward(self, x, timesteps=None, context=None, y=None, **kwargs):
+        hs = []
+        h = x
+        for module in self.input_blocks:
+            h = module(h)
+            hs.append(h)
+        h = self.middle_block(h)
+        for module in self.output_blocks:
+            h = module(torch.cat([h, hs.pop()], dim=1))
+        return self.out(h)
