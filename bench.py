@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--workload", choices=["e2e", "raster"], default="e2e")
     ap.add_argument("--dense-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--dominant", default=None, help="kernel timed for the roofline object")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
     ap.add_argument("--batch", type=int, default=1, help="scenes per step per GPU")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -118,7 +119,8 @@ def cpu_baseline_e2e(model, seconds: float):
     from transplat_amd import synthetic as S
     from transplat_amd.model.decoder.hip_splatting import prepare_cameras
 
-    saved = {n: getattr(kernels, n) for n in ("window_attention", "uv_coarse", "uv_cross", "msda")}
+    saved = {n: getattr(kernels, n) for n in ("window_attention", "uv_coarse", "uv_cross", "msda",
+                                              "gaussian_adapter")}
     for n in saved:
         setattr(kernels, n, getattr(E, n))
     threads = torch.get_num_threads()
@@ -189,7 +191,7 @@ def main():
         from transplat_amd.e2e import build_e2e_workload
 
         step, info, model = build_e2e_workload(args.batch, device, scene_offset=rank * args.batch,
-                                               dense_dtype=args.dense_dtype)
+                                               dense_dtype=args.dense_dtype, graph=not args.no_graph)
         info.update(e2e_roofline_info(args.dominant or "uv_cross", args.batch))
         cpu_inputs = ("e2e", model)
     if args.dominant and args.workload == "raster":

@@ -132,6 +132,24 @@ int tsplat_msda_fwd(const float* value, const float* loc, const float* weights, 
                     int32_t points, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Gaussian adapter (encoder stage 5 + GaussianAdapter.forward, reference
+ * src/model/encoder/encoder_trans.py:294-353, common/gaussian_adapter.py:48-96), one pass:
+ *   raw [batch, views, H*W, raw_ch] head output (2 offset + 3 scale + 4 xyzw quaternion +
+ *       3*d_sh SH, raw_ch = 9 + 3*d_sh); depths, densities [batch, views, H*W];
+ *   cams [batch*views, 22] = c2w R (9, row-major), c2w t (3), K^-1 of the normalised
+ *       intrinsics (9), scale multiplier 0.1 * sum(K[:2,:2]^-1 (1/W, 1/H)) (1);
+ *   sh_rot [batch*views, d_sh, d_sh] block-diagonal real-SH rotation of c2w R (e3nn wigner_D);
+ *   outputs means [batch, views*H*W, 3], cov [.., 3, 3], harmonics [.., 3, d_sh], opacities [..];
+ *   opacity = 0.5 (1 - (1 - pdf)^e + pdf^(1/e)) / gaussians_per_pixel (map_pdf_to_opacity).
+ * ---------------------------------------------------------------------------------------- */
+int tsplat_gaussian_adapter_fwd(const float* raw, const float* depths, const float* densities,
+                                const float* cams, const float* sh_rot, float* means, float* cov,
+                                float* harmonics, float* opacities, int32_t batch, int32_t views,
+                                int32_t height, int32_t width, int32_t raw_ch, int32_t d_sh,
+                                float scale_min, float scale_max, float opacity_exponent,
+                                int32_t gaussians_per_pixel, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Shifted-window attention of the multi-view transformer (exact fp32 MFMA):
  *   q [batch, H*W, C]; k, v [batch, key_views, H*W, C] (key_views = 1 for two views);
  *   out [batch, H*W, C]; C must be 128; window pixels and window pixels * key_views must be

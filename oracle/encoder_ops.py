@@ -186,3 +186,51 @@ def msda(value, loc, weights, h: int, w: int):
         s = bilinear_zero(img, loc[i, ..., 0] * w - 0.5, loc[i, ..., 1] * h - 0.5)  # [Q, P, C]
         out.append((s * weights[i][..., None]).sum(1))
     return torch.stack(out)
+
+
+# --------------------------------------------------------------------- Gaussian adapter (A1-A4)
+def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape, scale_min: float,
+                     scale_max: float, opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1):
+    """Encoder stage 5 (reference encoder_trans.py:294-353) + GaussianAdapter.forward
+    (reference gaussian_adapter.py:48-96), restated with the reference's torch expressions.
+    The SH rotation uses the e3nn construction restated in transplat_amd.misc.sh_rotation."""
+    from transplat_amd.misc.sh_rotation import rotate_sh
+
+    b, v, hw, r = raw.shape
+    h, w = image_shape
+    d_sh = (r - 9) // 3
+    ys, xs = torch.meshgrid(torch.arange(h), torch.arange(w), indexing="ij")
+    xy_ray = torch.stack([(xs + 0.5) / w, (ys + 0.5) / h], -1).reshape(hw, 2).float()
+    pixel_size = 1 / torch.tensor((w, h), dtype=torch.float32)
+    xy_ray = xy_ray + (raw[..., :2].sigmoid() - 0.5) * pixel_size  # [b, v, hw, 2]
+    scales = scale_min + (scale_max - scale_min) * raw[..., 2:5].sigmoid()
+    k = intrinsics[:, :, None]  # [b, v, 1, 3, 3]
+    mult = 0.1 * (torch.inverse(k[..., :2, :2]) @ pixel_size[:, None])[..., 0].sum(-1)
+    scales = scales * depths[..., None] * mult[..., None]
+    rot = raw[..., 5:9]
+    rot = rot / (rot.norm(dim=-1, keepdim=True) + 1e-8)
+    i, j, kk, rr = rot.unbind(-1)
+    two_s = 2 / ((rot * rot).sum(-1) + 1e-8)
+    q = torch.stack((1 - two_s * (j * j + kk * kk), two_s * (i * j - kk * rr), two_s * (i * kk + j * rr),
+                     two_s * (i * j + kk * rr), 1 - two_s * (i * i + kk * kk), two_s * (j * kk - i * rr),
+                     two_s * (i * kk - j * rr), two_s * (j * kk + i * rr), 1 - two_s * (i * i + j * j)), -1)
+    q = q.reshape(*q.shape[:-1], 3, 3)
+    s = scales.diag_embed()
+    cov = q @ s @ s.transpose(-1, -2) @ q.transpose(-1, -2)
+    c2w = extrinsics[:, :, None, :3, :3]
+    cov = c2w @ cov @ c2w.transpose(-1, -2)
+    dirs = torch.cat([xy_ray, torch.ones_like(xy_ray[..., :1])], -1)
+    dirs = (torch.inverse(k) @ dirs[..., None])[..., 0]
+    dirs = dirs / dirs.norm(dim=-1, keepdim=True)
+    dirs = (c2w @ dirs[..., None])[..., 0]
+    means = extrinsics[:, :, None, :3, 3] + dirs * depths[..., None]
+    mask = torch.ones(d_sh)
+    deg = int(round(d_sh**0.5)) - 1
+    for l in range(1, deg + 1):
+        mask[l * l:(l + 1) ** 2] = 0.1 * 0.25**l
+    sh = raw[..., 9:].reshape(b, v, hw, 3, d_sh) * mask
+    harm = rotate_sh(sh, extrinsics[:, :, None, None, :3, :3])
+    e = float(opacity_exponent)
+    opac = 0.5 * (1 - (1 - densities) ** e + densities ** (1 / e)) / gaussians_per_pixel
+    flat = lambda t: t.reshape(b, v * hw, *t.shape[3:])
+    return flat(means), flat(cov), flat(harm), flat(opac)

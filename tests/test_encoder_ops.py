@@ -131,3 +131,35 @@ def test_msda_kernel(device):
     ref = E.msda(value, loc, wts, hw, hw)
     out = K.msda(value.to(device), loc.to(device), wts.to(device), hw, hw).cpu()
     assert (out - ref).abs().max().item() < 1e-5
+
+
+def _adapter_inputs(b=2, v=2, h=24, w=32, d_sh=25):
+    raw = seeded((b, v, h * w, 9 + 3 * d_sh), 61)
+    depths = 1.0 + 20 * seeded((b, v, h * w), 62, kind="rand")
+    dens = seeded((b, v, h * w), 63, kind="rand")
+    ctx = S.make_batch(b, image_shape=(h, w))["context"]
+    ext = ctx["extrinsics"].clone()
+    ext[:, 1, :3, :3] = torch.tensor([[0.36, 0.48, -0.8], [-0.8, 0.6, 0.0], [0.48, 0.64, 0.6]])  # non-trivial rotation
+    return raw, depths, dens, ext, ctx["intrinsics"]
+
+
+def test_oracle_adapter_shapes_and_identity_rotation():
+    raw, depths, dens, ext, K = _adapter_inputs(b=1, v=1)
+    ext = torch.eye(4)[None, None]
+    m, c, hsh, o = E.gaussian_adapter(raw, depths, dens, ext, K[:, :1], (24, 32), 0.5, 15.0)
+    assert m.shape == (1, 768, 3) and c.shape == (1, 768, 3, 3) and hsh.shape == (1, 768, 3, 25)
+    assert torch.allclose(o, dens.reshape(1, -1))  # map_pdf_to_opacity is the identity at exponent 1
+    assert torch.allclose(c, c.transpose(-1, -2), atol=1e-7)
+
+
+@pytest.mark.gpu
+def test_gaussian_adapter_kernel(device):
+    from transplat_amd import kernels as K
+
+    raw, depths, dens, ext, intr = _adapter_inputs()
+    ref = E.gaussian_adapter(raw, depths, dens, ext, intr, (24, 32), 0.5, 15.0, 2.0)
+    out = K.gaussian_adapter(*(t.to(device) for t in (raw, depths, dens, ext, intr)), (24, 32), 0.5, 15.0, 2.0)
+    for name, r, o in zip(("means", "cov", "harmonics", "opacity"), ref, out):
+        o = o.cpu()
+        err = ((o - r).abs() / (r.abs() + 1e-3)).max().item()
+        assert err < 1e-4, (name, err)

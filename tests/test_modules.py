@@ -27,7 +27,7 @@ from transplat_amd import synthetic as S  # noqa: E402
 def cpu_ops(monkeypatch):
     from transplat_amd import kernels
 
-    for name in ("window_attention", "uv_coarse", "uv_cross", "msda"):
+    for name in ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter"):
         monkeypatch.setattr(kernels, name, getattr(E, name))
     return torch.device("cpu")
 

@@ -46,6 +46,7 @@ SIGNATURES = {
     "tsplat_uv_cross_fwd": (ctypes.c_int, [_P] * 7 + [_I32] * 6 + [_P]),
     "tsplat_msda_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 6 + [_P]),
     "tsplat_win_attn_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 7 + [_P]),
+    "tsplat_gaussian_adapter_fwd": (ctypes.c_int, [_P] * 9 + [_I32] * 6 + [ctypes.c_float] * 3 + [_I32, _P]),
 }
 
 ERRORS = {-1: "invalid argument", -2: "HIP launch error"}

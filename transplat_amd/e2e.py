@@ -53,12 +53,57 @@ def build_model(device, dense_dtype: str = "fp32", seed: int = 0) -> TransplatMo
     return model.eval().to(device)
 
 
-def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: str = "fp32"):
+class GraphedStep:
+    """The whole test_step captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed:
+    at batch 1 the ~2,500 kernel launches of a step otherwise leave ~30 % of the GPU time idle.
+    Inputs live in static buffers: `run(batch)` copies a new batch in (device-to-device) and
+    replays; outputs are the graph's static output tensors (valid until the next replay)."""
+
+    def __init__(self, model: TransplatModel, example: dict, warmup: int = 2):
+        self.model = model
+        self.static = _clone_batch(example)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                model.test_step(self.static)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = model.test_step(self.static)
+
+    def run(self, batch: dict | None = None):
+        if batch is not None:
+            _copy_batch(self.static, batch)
+        self.graph.replay()
+        return self.out
+
+
+def _clone_batch(b):
+    if isinstance(b, dict):
+        return {k: _clone_batch(v) for k, v in b.items()}
+    return b.clone() if torch.is_tensor(b) else b
+
+
+def _copy_batch(dst, src):
+    for k, v in src.items():
+        if isinstance(v, dict):
+            _copy_batch(dst[k], v)
+        elif torch.is_tensor(v):
+            dst[k].copy_(v, non_blocking=True)
+
+
+def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: str = "fp32", graph: bool = True):
     model = build_model(device, dense_dtype)
     data = S.make_batch(batch, image_shape=(256, 256), scene_offset=scene_offset, device=device)
+    if graph:
+        graphed = GraphedStep(model, data)
 
-    def step():
-        return model.test_step(data)
+        def step():
+            return graphed.run()
+    else:
+        def step():
+            return model.test_step(data)
 
     info = {
         "views_per_step": batch * data["target"]["near"].shape[1],

@@ -52,19 +52,32 @@ def sample_image_grid(shape: tuple[int, ...], device: torch.device = torch.devic
     return coordinates, stacked_indices
 
 
+_EDGE_MIDPOINTS: dict = {}
+
+
+def _edge_midpoints(device) -> Tensor:
+    """left, right, top, bottom image-edge midpoints, cached per device so no host->device copy
+    happens after the first call (graph-capture safe)."""
+    key = (device.type, device.index)
+    if key not in _EDGE_MIDPOINTS:
+        _EDGE_MIDPOINTS[key] = torch.tensor([[0, 0.5, 1], [1, 0.5, 1], [0.5, 0, 1], [0.5, 1, 1]],
+                                            dtype=torch.float32).to(device)
+    return _EDGE_MIDPOINTS[key]
+
+
 def get_fov(intrinsics: Tensor) -> Tensor:
     """(reference projection.py:233-247) fov from K^-1 applied to the edge midpoints."""
-    intrinsics_inv = intrinsics.inverse()
+    intrinsics_inv = torch.linalg.inv_ex(intrinsics)[0]
+    mids = _edge_midpoints(intrinsics.device)
 
-    def process_vector(vector):
-        vector = torch.tensor(vector, dtype=torch.float32, device=intrinsics.device)
-        vector = einsum(intrinsics_inv, vector, "b i j, j -> b i")
+    def process_vector(i):
+        vector = einsum(intrinsics_inv, mids[i], "b i j, j -> b i")
         return vector / vector.norm(dim=-1, keepdim=True)
 
-    left = process_vector([0, 0.5, 1])
-    right = process_vector([1, 0.5, 1])
-    top = process_vector([0.5, 0, 1])
-    bottom = process_vector([0.5, 1, 1])
+    left = process_vector(0)
+    right = process_vector(1)
+    top = process_vector(2)
+    bottom = process_vector(3)
     fov_x = (left * right).sum(dim=-1).acos()
     fov_y = (top * bottom).sum(dim=-1).acos()
     return torch.stack((fov_x, fov_y), dim=-1)

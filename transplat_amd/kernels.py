@@ -21,7 +21,7 @@ def pack_cameras(intr: torch.Tensor, pose: torch.Tensor) -> torch.Tensor:
     reference depth_predictor_trans.py:36-49, with K^-1 taken by torch.inverse as there)."""
     intr = intr.float()
     return torch.cat(
-        [torch.inverse(intr).reshape(-1, 9), intr.reshape(-1, 9), pose[:, :3, :3].reshape(-1, 9).float(),
+        [torch.linalg.inv_ex(intr)[0].reshape(-1, 9), intr.reshape(-1, 9), pose[:, :3, :3].reshape(-1, 9).float(),
          pose[:, :3, 3].float()], dim=1).contiguous()
 
 
@@ -83,3 +83,45 @@ def msda(value, loc, weights, h: int, w: int):
                              q, p, _lib.stream_ptr(value.device))
     _lib.check(rc, "tsplat_msda_fwd")
     return out
+
+
+def adapter_cameras(extrinsics: torch.Tensor, intrinsics: torch.Tensor, image_shape) -> torch.Tensor:
+    """[N, 22] per-camera constants of tsplat_gaussian_adapter_fwd: c2w R, c2w t, K^-1 of the
+    normalised intrinsics, and the scale multiplier of GaussianAdapter.get_scale_multiplier
+    (reference gaussian_adapter.py:98-109). Inverses via inv_ex (no host sync)."""
+    h, w = image_shape
+    ext = extrinsics.reshape(-1, 4, 4).float()
+    k = intrinsics.reshape(-1, 3, 3).float()
+    kinv = torch.linalg.inv_ex(k)[0]
+    k2inv = torch.linalg.inv_ex(k[:, :2, :2])[0]
+    pix = torch.stack([torch.full_like(k[:, 0, 0], 1.0 / w), torch.full_like(k[:, 0, 0], 1.0 / h)], -1)
+    mult = 0.1 * (k2inv @ pix[..., None])[..., 0].sum(-1)
+    return torch.cat([ext[:, :3, :3].reshape(-1, 9), ext[:, :3, 3], kinv.reshape(-1, 9), mult[:, None]], 1).contiguous()
+
+
+def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape, scale_min: float,
+                     scale_max: float, opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1):
+    """Raw head output -> Gaussians (see oracle.gaussian_adapter). raw [B, V, HW, 9 + 3 d_sh];
+    depths, densities [B, V, HW]; extrinsics [B, V, 4, 4]; intrinsics [B, V, 3, 3]
+    -> means [B, V*HW, 3], covariances [B, V*HW, 3, 3], harmonics [B, V*HW, 3, d_sh], opacities [B, V*HW]."""
+    from .misc.sh_rotation import sh_rotation_matrix
+
+    lib = _lib.load()
+    b, v, hw, r = raw.shape
+    d_sh = (r - 9) // 3
+    h, w = image_shape
+    raw, depths, densities = _f32(raw), _f32(depths), _f32(densities)
+    cams = adapter_cameras(extrinsics, intrinsics, image_shape)
+    shrot = sh_rotation_matrix(extrinsics.reshape(-1, 4, 4)[:, :3, :3], d_sh).float().contiguous()
+    dev = raw.device
+    g = v * hw
+    means = torch.empty((b, g, 3), device=dev)
+    cov = torch.empty((b, g, 3, 3), device=dev)
+    harm = torch.empty((b, g, 3, d_sh), device=dev)
+    opac = torch.empty((b, g), device=dev)
+    rc = lib.tsplat_gaussian_adapter_fwd(
+        _lib.ptr(raw), _lib.ptr(depths), _lib.ptr(densities), _lib.ptr(cams), _lib.ptr(shrot), _lib.ptr(means),
+        _lib.ptr(cov), _lib.ptr(harm), _lib.ptr(opac), b, v, h, w, r, d_sh, float(scale_min), float(scale_max),
+        float(opacity_exponent), int(gaussians_per_pixel), _lib.stream_ptr(dev))
+    _lib.check(rc, "tsplat_gaussian_adapter_fwd")
+    return means, cov, harm, opac

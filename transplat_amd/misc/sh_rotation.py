@@ -61,7 +61,7 @@ def _matrix_y(a):
 
 def matrix_to_angles(r: torch.Tensor):
     """e3nn.o3.matrix_to_angles: R = Y(alpha) X(beta) Y(gamma)."""
-    x = r @ r.new_tensor([0.0, 1.0, 0.0])
+    x = r[..., :, 1]  # R e_y
     x = torch.nn.functional.normalize(x, p=2, dim=-1).clamp(-1, 1)
     b = torch.acos(x[..., 1])
     a = torch.atan2(x[..., 0], x[..., 2])
@@ -70,13 +70,28 @@ def matrix_to_angles(r: torch.Tensor):
     return a, b, c
 
 
+def _expm(a: torch.Tensor, squarings: int = 6, terms: int = 16) -> torch.Tensor:
+    """exp of [..., n, n] float64 matrices by fixed scaling-and-squaring + Taylor. The generators
+    are skew-symmetric with |eigenvalue| <= l <= 4 and angles < 2 pi, so ||a|| / 2^6 < 0.4 and 16
+    terms are exact to float64 rounding; no data-dependent control flow (torch.matrix_exp reads
+    norms back to the host), so it is safe inside a captured graph."""
+    a = a / (2.0**squarings)
+    eye = torch.eye(a.shape[-1], dtype=a.dtype, device=a.device).expand_as(a)
+    out = eye.clone()
+    for k in range(terms, 0, -1):  # Horner: I + a/1 (I + a/2 (I + ...))
+        out = eye + (a @ out) / k
+    for _ in range(squarings):
+        out = out @ out
+    return out
+
+
 def wigner_d(l: int, alpha, beta, gamma) -> torch.Tensor:
     """e3nn.o3.wigner_D(l, alpha, beta, gamma) -> [..., 2l+1, 2l+1] (float64)."""
     gen = _so3_generators(l).to(alpha.device)
     a = (alpha.double() % (2 * math.pi))[..., None, None]
     b = (beta.double() % (2 * math.pi))[..., None, None]
     c = (gamma.double() % (2 * math.pi))[..., None, None]
-    return torch.matrix_exp(a * gen[1]) @ torch.matrix_exp(b * gen[0]) @ torch.matrix_exp(c * gen[1])
+    return _expm(a * gen[1]) @ _expm(b * gen[0]) @ _expm(c * gen[1])
 
 
 def sh_rotation_matrix(rotations: torch.Tensor, d_sh: int) -> torch.Tensor:

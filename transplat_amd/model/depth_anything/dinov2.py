@@ -110,7 +110,19 @@ class DinoVisionTransformer(nn.Module):
         nn.init.normal_(self.cls_token, std=1e-6)
 
     def interpolate_pos_encoding(self, x, w, h):
-        """(reference dinov2.py:185-217) bicubic resample of the 37x37 grid with the 0.1 offset."""
+        """(reference dinov2.py:185-217) bicubic resample of the 37x37 grid with the 0.1 offset.
+        The result depends only on the weights and the input size, so it is cached (the bicubic
+        kernel alone cost 2.3 ms per forward on MI355X); the key includes the parameter's version
+        counter so a checkpoint load or in-place update invalidates it."""
+        key = (w, h, x.dtype, x.device, self.pos_embed.data_ptr(), self.pos_embed._version)
+        cached = getattr(self, "_pos_cache", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        out = self._interpolate_pos_encoding(x, w, h)
+        self._pos_cache = (key, out)
+        return out
+
+    def _interpolate_pos_encoding(self, x, w, h):
         previous_dtype = x.dtype
         npatch = x.shape[1] - 1
         n = self.pos_embed.shape[1] - 1

@@ -13,12 +13,25 @@ _IMAGENET_MEAN = (0.485, 0.456, 0.406)
 _IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
+_POSITION_CACHE: dict = {}
+
+
+def _window_position(x, feature_channels):
+    """Sine embedding of one window (constant per shape/device; cached)."""
+    key = (tuple(x.shape), x.dtype, x.device, feature_channels)
+    pos = _POSITION_CACHE.get(key)
+    if pos is None:
+        pos = PositionEmbeddingSine(num_pos_feats=feature_channels // 2)(x).to(x.dtype)
+        _POSITION_CACHE[key] = pos
+    return pos
+
+
 def feature_add_position_list(features_list, attn_splits, feature_channels):
     """(reference :14-34) add the sine embedding of one window to every window."""
     pos_enc = PositionEmbeddingSine(num_pos_feats=feature_channels // 2)
     if attn_splits > 1:
         features_splits = [split_feature(x, num_splits=attn_splits) for x in features_list]
-        position = pos_enc(features_splits[0])
+        position = _window_position(features_splits[0], feature_channels)
         features_splits = [x + position for x in features_splits]
         return [merge_splits(x, num_splits=attn_splits) for x in features_splits]
     position = pos_enc(features_list[0])
@@ -34,13 +47,12 @@ class BackboneMultiview(torch.nn.Module):
         self.transformer = MultiViewFeatureTransformer(num_layers=num_transformer_layers, d_model=feature_channels,
                                                        nhead=num_head, ffn_dim_expansion=ffn_dim_expansion)
         self.cam_param_encoder = cam_param_encoder(in_channels=128, mid_channels=128, embed_dims=128)
+        self.register_buffer("img_mean", torch.tensor(_IMAGENET_MEAN), persistent=False)
+        self.register_buffer("img_std", torch.tensor(_IMAGENET_STD), persistent=False)
 
-    @staticmethod
-    def normalize_images(images):
+    def normalize_images(self, images):
         shape = [*[1] * (images.dim() - 3), 3, 1, 1]
-        mean = torch.tensor(_IMAGENET_MEAN).reshape(*shape).to(images.device)
-        std = torch.tensor(_IMAGENET_STD).reshape(*shape).to(images.device)
-        return (images - mean) / std
+        return (images - self.img_mean.reshape(*shape)) / self.img_std.reshape(*shape)
 
     def extract_feature(self, images):
         b, v = images.shape[:2]

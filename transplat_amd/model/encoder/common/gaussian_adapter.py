@@ -1,5 +1,6 @@
 """Raw per-pixel head output -> world-space Gaussians (reference
-src/model/encoder/common/gaussian_adapter.py:30-117)."""
+src/model/encoder/common/gaussian_adapter.py:30-117), as one fused gfx950 kernel
+(tsplat_gaussian_adapter_fwd); the torch expressions of the reference live in the oracle."""
 from __future__ import annotations
 
 from dataclasses import dataclass
@@ -8,9 +9,7 @@ import torch
 from einops import einsum, rearrange
 from torch import Tensor, nn
 
-from ....geometry.projection import get_world_rays
-from ....misc.sh_rotation import rotate_sh, sh_rotation_matrix
-from .gaussians import build_covariance
+from .... import kernels
 
 
 @dataclass
@@ -38,42 +37,14 @@ class GaussianAdapter(nn.Module):
         for degree in range(1, self.cfg.sh_degree + 1):
             self.sh_mask[degree**2:(degree + 1) ** 2] = 0.1 * 0.25**degree
 
-    def forward(self, extrinsics, intrinsics, coordinates, depths, opacities, raw_gaussians, image_shape,
-                eps: float = 1e-8) -> Gaussians:
-        device = extrinsics.device
-        scales, rotations, sh = raw_gaussians.split((3, 4, 3 * self.d_sh), dim=-1)
-        scales = self.cfg.gaussian_scale_min + (self.cfg.gaussian_scale_max - self.cfg.gaussian_scale_min) * scales.sigmoid()
-        h, w = image_shape
-        pixel_size = 1 / torch.tensor((w, h), dtype=torch.float32, device=device)
-        multiplier = self.get_scale_multiplier(intrinsics, pixel_size)
-        scales = scales * depths[..., None] * multiplier[..., None]
-        rotations = rotations / (rotations.norm(dim=-1, keepdim=True) + eps)
-        sh = rearrange(sh, "... (xyz d_sh) -> ... xyz d_sh", xyz=3)
-        sh = sh.broadcast_to((*opacities.shape, 3, self.d_sh)) * self.sh_mask
-        covariances = build_covariance(scales, rotations)
-        c2w_rotations = extrinsics[..., :3, :3]
-        covariances = c2w_rotations @ covariances @ c2w_rotations.transpose(-1, -2)
-        origins, directions = get_world_rays(coordinates, extrinsics, intrinsics)
-        means = origins + directions * depths[..., None]
-        return Gaussians(
-            means=means,
-            covariances=covariances,
-            harmonics=self.rotate_harmonics(sh, c2w_rotations),
-            opacities=opacities,
-            scales=scales,
-            rotations=rotations.broadcast_to((*scales.shape[:-1], 4)),
-        )
-
-    @staticmethod
-    def rotate_harmonics(sh, c2w_rotations):
-        """rotate_sh(sh, R[..., None, :, :]) with one D matrix per camera applied as a batched
-        GEMM over the pixels (no per-pixel broadcast of D)."""
-        b, v = sh.shape[:2]
-        if c2w_rotations.shape[:2] == (b, v) and all(s == 1 for s in c2w_rotations.shape[2:-2]):
-            d = sh_rotation_matrix(c2w_rotations.reshape(b, v, 3, 3), sh.shape[-1]).to(sh.dtype)
-            flat = sh.reshape(b, v, -1, sh.shape[-1])
-            return torch.einsum("bvij,bvnj->bvni", d, flat).reshape(sh.shape)
-        return rotate_sh(sh, c2w_rotations[..., None, :, :])
+    def forward(self, extrinsics, intrinsics, raw_gaussians, depths, densities, image_shape,
+                opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1):
+        """Fused stage 5 + adapter on the GPU (kernels.gaussian_adapter):
+        raw [b, v, HW, 2 + d_in] head output, depths / densities [b, v, HW], cameras [b, v, ...]
+        -> (means, covariances, harmonics, opacities) flattened to [b, v*HW, ...]."""
+        return kernels.gaussian_adapter(raw_gaussians, depths, densities, extrinsics, intrinsics, image_shape,
+                                        self.cfg.gaussian_scale_min, self.cfg.gaussian_scale_max,
+                                        opacity_exponent, gaussians_per_pixel)
 
     def get_scale_multiplier(self, intrinsics, pixel_size, multiplier: float = 0.1):
         xy_multipliers = multiplier * einsum(intrinsics[..., :2, :2].inverse(), pixel_size, "... i j, j -> ... i")

@@ -18,7 +18,6 @@ import torch.nn.functional as F
 from einops import rearrange
 from torch import nn
 
-from ...geometry.projection import sample_image_grid
 from ..depth_anything.dpt import DepthAnythingV2
 from ..types import Gaussians
 from .backbone.backbone_multiview import BackboneMultiview
@@ -90,6 +89,9 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
             gaussians_per_pixel=cfg.gaussians_per_pixel, num_views=cfg.num_context_views,
             depth_unet_feat_dim=cfg.depth_unet_feat_dim, depth_unet_attn_res=cfg.depth_unet_attn_res,
             depth_unet_channel_mult=cfg.depth_unet_channel_mult, DA_size=da["features"] // 2)
+        # constants as non-persistent buffers: no host->device copy inside forward (graph capture)
+        self.register_buffer("img_mean", torch.tensor([0.485, 0.456, 0.406]), persistent=False)
+        self.register_buffer("img_std", torch.tensor([0.229, 0.224, 0.225]), persistent=False)
 
     def map_pdf_to_opacity(self, pdf, global_step: int):
         """(reference :139-152)"""
@@ -98,12 +100,9 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         exponent = 2**x
         return 0.5 * (1 - (1 - pdf) ** exponent + pdf ** (1 / exponent))
 
-    @staticmethod
-    def normalize_images(images):
+    def normalize_images(self, images):
         shape = [*[1] * (images.dim() - 3), 3, 1, 1]
-        mean = torch.tensor([0.485, 0.456, 0.406]).reshape(*shape).to(images.device)
-        std = torch.tensor([0.229, 0.224, 0.225]).reshape(*shape).to(images.device)
-        return (images - mean) / std
+        return (images - self.img_mean.reshape(*shape)) / self.img_std.reshape(*shape)
 
     def _dense(self):
         if self.cfg.dense_dtype == "bf16":
@@ -125,7 +124,7 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
             intr_curr[:, :, 1, :] *= float(h)
             camk = torch.eye(4, device=device).view(1, 1, 4, 4).repeat(b, v, 1, 1).float()
             camk[:, :, :3, :3] = intr_curr
-            img2world = torch.matmul(context["extrinsics"].clone().detach(), torch.inverse(camk))
+            img2world = torch.matmul(context["extrinsics"].clone().detach(), torch.linalg.inv_ex(camk)[0])
 
         with bench("encoder_2_backbone"), self._dense():
             trans_features, cnn_features = self.backbone(context["image"], attn_splits=self.cfg.multiview_trans_attn_split,
@@ -155,29 +154,18 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         depths, densities, raw_gaussians = depths.float(), densities.float(), raw_gaussians.float()
 
         with bench("encoder_5_gaussian_adapter"):
-            xy_ray, _ = sample_image_grid((h, w), device)
-            xy_ray = rearrange(xy_ray, "h w xy -> (h w) () xy")
-            gaussians = rearrange(raw_gaussians, "... (srf c) -> ... srf c", srf=self.cfg.num_surfaces)
-            offset_xy = gaussians[..., :2].sigmoid()
-            pixel_size = 1 / torch.tensor((w, h), dtype=torch.float32, device=device)
-            xy_ray = xy_ray + (offset_xy - 0.5) * pixel_size
-            gaussians = self.gaussian_adapter.forward(
-                rearrange(context["extrinsics"], "b v i j -> b v () () () i j"),
-                rearrange(context["intrinsics"], "b v i j -> b v () () () i j"),
-                rearrange(xy_ray, "b v r srf xy -> b v r srf () xy"),
-                depths,
-                self.map_pdf_to_opacity(densities, global_step) / gpp,
-                rearrange(gaussians[..., 2:], "b v r srf c -> b v r srf () c"),
-                (h, w),
-            )
+            # fused: sub-pixel offsets, rays, means, covariances, SH mask + rotation, opacity
+            srf = self.cfg.num_surfaces
+            if srf != 1 or gpp != 1:
+                raise NotImplementedError("TranSplat runs 1 surface and 1 Gaussian per pixel")
+            x = self.cfg.opacity_mapping
+            exponent = 2 ** (x.initial + min(global_step / x.warm_up, 1) * (x.final - x.initial))
+            means, covariances, harmonics, opacities = self.gaussian_adapter(
+                context["extrinsics"], context["intrinsics"], raw_gaussians, depths.reshape(b, v, h * w),
+                densities.reshape(b, v, h * w), (h, w), opacity_exponent=exponent, gaussians_per_pixel=gpp)
         if visualization_dump is not None:
             visualization_dump["depth"] = rearrange(depths, "b v (h w) srf s -> b v h w srf s", h=h, w=w)
-        return Gaussians(
-            rearrange(gaussians.means, "b v r srf spp xyz -> b (v r srf spp) xyz"),
-            rearrange(gaussians.covariances, "b v r srf spp i j -> b (v r srf spp) i j"),
-            rearrange(gaussians.harmonics, "b v r srf spp c d_sh -> b (v r srf spp) c d_sh"),
-            rearrange(gaussians.opacities, "b v r srf spp -> b (v r srf spp)"),
-        )
+        return Gaussians(means, covariances, harmonics, opacities)
 
     def get_data_shim(self):
         """(reference :355-371) crop to a multiple of shim_patch_size * downscale_factor."""

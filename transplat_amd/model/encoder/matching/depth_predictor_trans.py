@@ -28,21 +28,21 @@ def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, nu
         cur_view_order = init_view_order[idx:] + init_view_order[:idx]
         feat_lists.append(rearrange(features[:, cur_view_order], "b v ... -> (v b) ..."))
         if v > 2:
-            cur = [extrinsics[:, v1].clone().detach().inverse() @ extrinsics[:, v0].clone().detach()
+            cur = [torch.linalg.inv_ex(extrinsics[:, v1].clone().detach())[0] @ extrinsics[:, v0].clone().detach()
                    for v0, v1 in zip(init_view_order, cur_view_order)]
             pose_curr_lists.append(torch.cat(cur, dim=0))
     if v == 2:
         pose_ref = extrinsics[:, 0].clone().detach()
         pose_tgt = extrinsics[:, 1].clone().detach()
-        pose = pose_tgt.inverse() @ pose_ref
-        pose_curr_lists = [torch.cat((pose, pose.inverse()), dim=0)]
+        pose = torch.linalg.inv_ex(pose_tgt)[0] @ pose_ref
+        pose_curr_lists = [torch.cat((pose, torch.linalg.inv_ex(pose)[0]), dim=0)]
     intr_curr = intrinsics[:, :, :3, :3].clone().detach()
     intr_curr[:, :, 0, :] *= float(w)
     intr_curr[:, :, 1, :] *= float(h)
     intr_curr = rearrange(intr_curr, "b v ... -> (v b) ...", b=b, v=v)
     min_depth = rearrange(1.0 / far.clone().detach(), "b v -> (v b) 1")
     max_depth = rearrange(1.0 / near.clone().detach(), "b v -> (v b) 1")
-    depth_candi_curr = (min_depth + torch.linspace(0.0, 1.0, num_samples).unsqueeze(0).to(min_depth.device)
+    depth_candi_curr = (min_depth + torch.linspace(0.0, 1.0, num_samples, device=min_depth.device).unsqueeze(0)
                         * (max_depth - min_depth)).type_as(features)
     depth_candi_curr = repeat(depth_candi_curr, "vb d -> vb d () ()")
     return feat_lists, intr_curr, pose_curr_lists, depth_candi_curr
@@ -104,7 +104,7 @@ class DepthPredictorTrans(nn.Module):
         camk = torch.eye(4, device=intr_curr.device).view(1, 4, 4).repeat(intr_curr.shape[0], 1, 1).float()
         camk[:, :3, :3] = intr_curr
         c2w = rearrange(extrinsics.clone().detach(), "b v ... -> (v b) ...", b=b, v=v)
-        img2world = torch.matmul(c2w, torch.inverse(camk)).reshape(-1, 16)
+        img2world = torch.matmul(c2w, torch.linalg.inv_ex(camk)[0]).reshape(-1, 16)
         pos_feature = self.cam_param_encoder(dino_feature, img2world)  # [(v b), C, h, w]
         # (b v)-ordered channel-last query positions: the reference's bev_pos after its permutes
         bev_pos = rearrange(pos_feature, "(v b) c h w -> (b v) (h w) c", v=v, b=b)

@@ -51,8 +51,8 @@ class UVSelfAttention(nn.Module):
         value = self.value_proj(value)
         offsets = self.sampling_offsets(query).view(bsv, nq, self.num_points, 2)
         weights = self.attention_weights(query).view(bsv, nq, self.num_points).softmax(-1)
-        normalizer = torch.tensor([bev_w, bev_h], dtype=offsets.dtype, device=offsets.device)
-        loc = ref_2d[:, :, None, :] + offsets / normalizer
+        # offset / (W, H) per coordinate (the reference divides by the spatial-shape tensor)
+        loc = ref_2d[:, :, None, :] + torch.stack((offsets[..., 0] / bev_w, offsets[..., 1] / bev_h), -1)
         out = kernels.msda(value, loc, weights, bev_h, bev_w)
         return self.dropout(self.output_proj(out)) + identity
 
