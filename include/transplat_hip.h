@@ -88,6 +88,13 @@ typedef struct tsplat_raster_desc {
 size_t tsplat_raster_workspace_bytes(int32_t num_gaussians, int32_t num_views, int32_t height,
                                      int32_t width, int32_t capacity);
 
+/* Byte offset inside the workspace of the uint32 total of (Gaussian, tile) instances the last
+ * tsplat_raster_fwd on that workspace generated: the reference forward's `num_rendered`
+ * (rasterize_points.cu RasterizeGaussiansCUDA return value). Valid after the call's stream
+ * completes; it may exceed `capacity` (then the status bit is set). */
+size_t tsplat_raster_num_rendered_offset(int32_t num_gaussians, int32_t num_views, int32_t height,
+                                         int32_t width);
+
 int tsplat_raster_fwd(const tsplat_raster_desc* desc,
                       const float* means, const float* cov, const float* shs,
                       const float* opacity, const float* viewmat, const float* projmat,

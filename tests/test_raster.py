@@ -217,3 +217,37 @@ def test_raster_capacity_overflow_is_reported(device):
     with pytest.raises(RuntimeError, match="capacity"):
         rasterize(gd["means"], gd["covariances"], gd["harmonics"], gd["opacities"], cams, hw, 3,
                   capacity=1000)
+
+
+@pytest.mark.gpu
+def test_raster_graph_replay_with_new_inputs(device):
+    """The rasterizer captured into a hipGraph and replayed over new Gaussians copied into the
+    static inputs gives the eager images bit-for-bit (its counters are reset inside the graph)."""
+    from transplat_amd.model.decoder.hip_splatting import check_status
+
+    hw = (64, 64)
+    batch = S.make_batch(1, image_shape=hw, device=device)
+    t = batch["target"]
+    cams = prepare_cameras(t["extrinsics"][0], t["intrinsics"][0], t["near"][0], t["far"][0],
+                           torch.zeros(3, 3, device=device))
+    scenes = [{k: v.to(device) for k, v in S.make_gaussians(1, image_shape=hw, scene_offset=o).items()}
+              for o in (0, 5, 9)]
+    run = lambda g: rasterize(g["means"], g["covariances"], g["harmonics"], g["opacities"], cams, hw, 3,
+                              check=False)[0]
+    eager = [run(g).clone() for g in scenes]
+    static = {k: v.clone() for k, v in scenes[0].items()}
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        run(static)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = run(static)
+    for i in (0, 1, 2, 1, 0):
+        for k in static:
+            static[k].copy_(scenes[i][k])
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager[i]), i
+    check_status(device)

@@ -8,7 +8,7 @@ mkdir -p $OUT
 TAG=${TAG:-r1}
 ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }   # 1 = test failures (no fault)
 if [ "${RUN_TESTS:-1}" = 1 ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-500} python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > $OUT/pytest_gpu_$TAG.log 2>&1; rc=$?
+  timeout -k 10 ${TEST_TIMEOUT:-500} python -m pytest ${PYTEST_TARGET:-tests} -m gpu -q ${PYTEST_ARGS:-} > $OUT/pytest_gpu_$TAG.log 2>&1; rc=$?
   echo "pytest rc=$rc"; tail -5 $OUT/pytest_gpu_$TAG.log
   ok $rc || exit $rc
 fi

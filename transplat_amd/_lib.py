@@ -38,6 +38,7 @@ SIGNATURES = {
     "tsplat_prof_enable": (ctypes.c_int, [_I32]),
     "tsplat_prof_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I32)]),
     "tsplat_raster_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, _I32, _I32, _I32]),
+    "tsplat_raster_num_rendered_offset": (ctypes.c_size_t, [_I32, _I32, _I32, _I32]),
     "tsplat_raster_fwd": (
         ctypes.c_int,
         [ctypes.POINTER(RasterDesc)] + [_P] * 15,

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "../../include/transplat_hip.h"
 
 #define TSPLAT_CHECK_LAUNCH()                                        \
@@ -25,6 +27,7 @@ constexpr int kWave = 64;
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 __host__ __device__ inline int ceil_div(int a, int b) { return (a + b - 1) / b; }
+__host__ __device__ inline size_t ceil_div(size_t a, size_t b) { return (a + b - 1) / b; }
 
 // Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): blocks that the dispatcher deals round-robin over the 8 XCDs are renumbered so that

@@ -152,6 +152,13 @@ __device__ __forceinline__ void sh_to_rgb(const float* __restrict__ sh, int M, i
     }
 }
 
+// --- K0: clear the per-tile counters (a kernel, not hipMemsetAsync: a memset captured into a
+// hipGraph was observed on ROCm 7.2 to leave garbage in the counters on the second replay) ---
+__global__ void __launch_bounds__(256) zero_kernel(uint4* __restrict__ p, size_t n4) {
+    for (size_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256)
+        p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 // --- K1: preprocess + per-tile instance counts ----------------------------------------------
 __global__ void __launch_bounds__(kPreThreads)
 preprocess_kernel(Params p, const float* __restrict__ means, const float* __restrict__ cov,
@@ -514,6 +521,12 @@ extern "C" size_t tsplat_raster_workspace_bytes(int32_t G, int32_t V, int32_t H,
     return total;
 }
 
+extern "C" size_t tsplat_raster_num_rendered_offset(int32_t G, int32_t V, int32_t H, int32_t W) {
+    const int T = ceil_div(W, kTile) * ceil_div(H, kTile);
+    const Workspace w = carve((void*)(uintptr_t)0x100000, G, V, T, 1, nullptr);  // layout only
+    return (size_t)((char*)(w.offsets + (size_t)V * T) - (char*)(uintptr_t)0x100000);
+}
+
 extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means, const float* cov,
                                  const float* shs, const float* opacity, const float* viewmat,
                                  const float* projmat, const float* campos, const float* tanfov,
@@ -545,7 +558,13 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
     Workspace ws = carve(workspace, p.G, p.V, p.T, p.capacity, nullptr);
 
     TSPLAT_PROF_BEGIN(prof::kRasterAll, stream);
-    TSPLAT_CHECK(hipMemsetAsync(ws.counts, 0, (size_t)2 * p.V * p.T * sizeof(uint32_t), stream));
+    {
+        // counts + cursor: 2 V T uint32, padded by carve()'s 256-byte alignment to whole uint4s
+        const size_t n4 = ceil_div((size_t)2 * p.V * p.T, (size_t)4);
+        const int blocks = (int)std::min<size_t>(ceil_div(n4, (size_t)256), 1024);
+        hipLaunchKernelGGL(zero_kernel, dim3(blocks), dim3(256), 0, stream, (uint4*)ws.counts, n4);
+        TSPLAT_CHECK_LAUNCH();
+    }
     dim3 pre_grid(ceil_div(p.G, kPreThreads), p.V);
     TSPLAT_PROF_BEGIN(prof::kRasterPreprocess, stream);
     hipLaunchKernelGGL(preprocess_kernel, pre_grid, dim3(kPreThreads), p.T * sizeof(uint32_t),

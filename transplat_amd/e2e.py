@@ -106,6 +106,7 @@ def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: s
             return model.test_step(data)
 
     info = {
+        "eager_step": lambda: model.test_step(data),
         "views_per_step": batch * data["target"]["near"].shape[1],
         "workload": f"e2e TranSplat test_step: {batch} scene(s) x (2 ctx -> 3 tgt) 256x256, "
                     f"dense layers {dense_dtype}, correlation/attention/raster fp32",

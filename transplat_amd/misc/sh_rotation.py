@@ -49,6 +49,12 @@ def _so3_generators(l: int) -> torch.Tensor:
     return torch.real(x)
 
 
+@lru_cache(maxsize=None)
+def _so3_generators_on(l: int, device: torch.device) -> torch.Tensor:
+    """Device-resident copy, made once (a host-to-device copy is not graph-capturable)."""
+    return _so3_generators(l).to(device)
+
+
 def _matrix_x(a):
     c, s, o, z = a.cos(), a.sin(), torch.ones_like(a), torch.zeros_like(a)
     return torch.stack([torch.stack([o, z, z], -1), torch.stack([z, c, -s], -1), torch.stack([z, s, c], -1)], -2)
@@ -87,7 +93,7 @@ def _expm(a: torch.Tensor, squarings: int = 6, terms: int = 16) -> torch.Tensor:
 
 def wigner_d(l: int, alpha, beta, gamma) -> torch.Tensor:
     """e3nn.o3.wigner_D(l, alpha, beta, gamma) -> [..., 2l+1, 2l+1] (float64)."""
-    gen = _so3_generators(l).to(alpha.device)
+    gen = _so3_generators_on(l, alpha.device)
     a = (alpha.double() % (2 * math.pi))[..., None, None]
     b = (beta.double() % (2 * math.pi))[..., None, None]
     c = (gamma.double() % (2 * math.pi))[..., None, None]

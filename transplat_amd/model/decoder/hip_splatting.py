@@ -89,16 +89,21 @@ def prepare_cameras(
 
 
 class _RasterState:
-    """Per-device workspace + sticky overflow status (grown on demand, never freed mid-run)."""
+    """Per-device workspace + sticky overflow status, grown on demand. A superseded workspace is
+    retired, not freed: a captured hipGraph may still hold its address."""
 
     def __init__(self):
         self.workspace: dict = {}
         self.status: dict = {}
+        self.last: dict = {}
+        self.retired: list = []
 
     def get(self, device, nbytes: int):
         key = (device.type, device.index)
         ws = self.workspace.get(key)
         if ws is None or ws.numel() < nbytes:
+            if ws is not None:
+                self.retired.append(ws)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
             self.workspace[key] = ws
         st = self.status.get(key)
@@ -111,8 +116,17 @@ class _RasterState:
 _STATE = _RasterState()
 
 
-def default_capacity(num_gaussians: int, num_views: int) -> int:
-    return max(1 << 20, 24 * num_gaussians * num_views)
+MAX_CAPACITY = 1 << 30  # 8 GiB of 8-byte instance keys
+
+
+def default_capacity(num_gaussians: int, num_views: int, height: int, width: int) -> int:
+    """The worst case, every Gaussian touching every 16x16 tile of every view, so a captured
+    graph can never overflow (the reference sizes its buffers from a host readback of the exact
+    count instead, which a graph cannot do). 8 bytes per instance: 0.8 GB for one 256x256 scene
+    x 3 views, 6.4 GB at batch 8, a small slice of 288 GB. Larger problems are capped at
+    MAX_CAPACITY and rely on the overflow status."""
+    tiles = ((height + 15) // 16) * ((width + 15) // 16)
+    return max(1, min(num_gaussians * num_views * tiles, MAX_CAPACITY))
 
 
 def rasterize(
@@ -149,7 +163,7 @@ def rasterize(
     f32 = lambda t: t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
     means, covariances, harmonics, opacities = map(f32, (means, covariances, harmonics, opacities))
     if capacity is None:
-        capacity = default_capacity(g, v)
+        capacity = default_capacity(g, v, h, w)
     nbytes = int(lib.tsplat_raster_workspace_bytes(g, v, h, w, capacity))
     ws, status = _STATE.get(dev, nbytes)
     color = torch.empty((v, 3, h, w), dtype=torch.float32, device=dev)
@@ -171,9 +185,17 @@ def rasterize(
         _lib.stream_ptr(dev),
     )
     _lib.check(rc, "tsplat_raster_fwd")
+    _STATE.last[(dev.type, dev.index)] = (ws, int(lib.tsplat_raster_num_rendered_offset(g, v, h, w)))
     if check:
         check_status(dev)
     return color, radii
+
+
+def num_rendered(device) -> int:
+    """(Gaussian, tile) instances generated by the last rasterize() on `device` (the reference
+    forward's num_rendered; syncs)."""
+    ws, off = _STATE.last[(device.type, device.index)]
+    return int(ws[off:off + 4].view(torch.int32).item())
 
 
 def check_status(device) -> None:

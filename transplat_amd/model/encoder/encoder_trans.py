@@ -133,7 +133,10 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         cnn_features = cnn_features.float()
 
         with bench("encoder_3_depth_anything"), torch.no_grad(), self._dense():
-            da_images = self.normalize_images(context["image"])[:, :, [2, 0, 1]]
+            # channel order (2, 0, 1) as the reference, by slicing: a list index would be a pageable
+            # host-to-device copy, which is not allowed inside hipGraph capture
+            da_images = self.normalize_images(context["image"])
+            da_images = torch.cat((da_images[:, :, 2:3], da_images[:, :, 0:2]), dim=2)
             da_images = da_images.reshape(b * v, 3, h, w)
             da_images = F.interpolate(da_images, (252, 252), mode="bilinear", align_corners=True)
             da_depth, out_feature = self.da_model(da_images)

@@ -26,7 +26,8 @@ def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, nu
     init_view_order = list(range(v))
     for idx in range(1, v):
         cur_view_order = init_view_order[idx:] + init_view_order[:idx]
-        feat_lists.append(rearrange(features[:, cur_view_order], "b v ... -> (v b) ..."))
+        # features[:, cur_view_order] as a roll (list indexing is a host copy: not graph-capturable)
+        feat_lists.append(rearrange(torch.roll(features, -idx, dims=1), "b v ... -> (v b) ..."))
         if v > 2:
             cur = [torch.linalg.inv_ex(extrinsics[:, v1].clone().detach())[0] @ extrinsics[:, v0].clone().detach()
                    for v0, v1 in zip(init_view_order, cur_view_order)]
