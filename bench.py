@@ -119,8 +119,7 @@ def cpu_baseline_e2e(model, seconds: float):
     from transplat_amd import synthetic as S
     from transplat_amd.model.decoder.hip_splatting import prepare_cameras
 
-    saved = {n: getattr(kernels, n) for n in ("window_attention", "uv_coarse", "uv_cross", "msda",
-                                              "gaussian_adapter")}
+    saved = {n: getattr(kernels, n) for n in E.KERNEL_RESTATEMENTS}
     for n in saved:
         setattr(kernels, n, getattr(E, n))
     threads = torch.get_num_threads()

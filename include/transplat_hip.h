@@ -42,7 +42,7 @@ int tsplat_version(void);
 /* Per-kernel timing with HIP events recorded on the launch stream around every launch of ONE
  * kernel (ids: 1 raster preprocess, 2 raster scan, 3 raster scatter, 4 raster render,
  * 5 uv coarse correlation, 6 uv cross correlation, 7 msda, 8 window attention, 9 the whole
- * rasterizer launch sequence; 0 = off).
+ * rasterizer launch sequence, 10 group norm (both launches); 0 = off).
  * tsplat_prof_read waits for the recorded events, returns the summed duration and the number of
  * launches timed since the last enable/read, and resets the record. Used by bench.py only. */
 int tsplat_prof_enable(int32_t kernel_id);
@@ -137,6 +137,27 @@ int tsplat_uv_cross_fwd(const float* value, const float* key, const float* cams,
 int tsplat_msda_fwd(const float* value, const float* loc, const float* weights, float* out,
                     int32_t n, int32_t height, int32_t width, int32_t channels, int32_t queries,
                     int32_t points, void* stream);
+
+/* Real-SH rotation matrices, block-diagonal over degrees 0..isqrt(d_sh)-1 (<= 4), one per
+ * camera: replaces the reference's e3nn call chain in rotate_sh (src/misc/sh_rotation.py:10-30:
+ * matrix_to_angles + wigner_D per degree). rotations [n, 3, 3] row-major float32 (the c2w
+ * rotation); basis = the constant e3nn x-to-y basis change P^l = exp(-pi/2 X_z), degrees 0..4
+ * packed row-major (1 + 9 + 25 + 49 + 81 = 165 float64, misc/sh_rotation.x_basis_packed);
+ * out [n, d_sh, d_sh] float32 (zeros off the diagonal blocks). */
+int tsplat_sh_rotation_fwd(const float* rotations, const double* basis, float* out, int32_t num_cameras,
+                           int32_t d_sh, void* stream);
+
+/* GroupNorm over NCHW fp32 with the following activation and residual add fused:
+ * y = act(group_norm(x) * gamma + beta) [+ residual], act 0 none, 1 SiLU, 2 GELU (erf).
+ * Replaces the U-Net / refine-head chains GroupNorm32 -> SiLU (-> + skip) and GroupNorm -> GELU
+ * (reference src/model/encoder/matching/ldm_unet/unet.py:177-370, util.py:189-208,
+ * depth_predictor_trans.py:142-206; torch.nn.functional.group_norm semantics: biased variance,
+ * rsqrt(var + eps)). workspace: tsplat_group_norm_workspace_bytes(n, c, hw, groups) bytes.
+ * residual may be NULL; x, residual and y are [n, c, hw] contiguous, y may not alias x. */
+size_t tsplat_group_norm_workspace_bytes(int32_t n, int32_t c, int64_t hw, int32_t groups);
+int tsplat_group_norm_fwd(const float* x, const float* gamma, const float* beta, const float* residual,
+                          float* y, void* workspace, int32_t n, int32_t c, int64_t hw, int32_t groups,
+                          float eps, int32_t act, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Gaussian adapter (encoder stage 5 + GaussianAdapter.forward, reference

@@ -234,3 +234,30 @@ def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape
     opac = 0.5 * (1 - (1 - densities) ** e + densities ** (1 / e)) / gaussians_per_pixel
     flat = lambda t: t.reshape(b, v * hw, *t.shape[3:])
     return flat(means), flat(cov), flat(harm), flat(opac)
+
+
+def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None):
+    """torch.nn.GroupNorm followed by the module chain's activation and residual add (reference
+    ldm_unet/unet.py:177-300 ResBlock: skip + SiLU(GN(conv)); :306-370 AttentionBlock:
+    x + GN(proj); depth_predictor_trans.py:142-206: GN -> GELU)."""
+    y = torch.nn.functional.group_norm(x.float(), num_groups, weight, bias, eps)
+    if act == "silu":
+        y = torch.nn.functional.silu(y)
+    elif act == "gelu":
+        y = torch.nn.functional.gelu(y)
+    if residual is not None:
+        y = residual.float() + y
+    return y
+
+
+def sh_rotation(rotations, d_sh: int):
+    """Per-camera block-diagonal real-SH rotation (the e3nn construction restated in
+    transplat_amd.misc.sh_rotation, float64 matrix exponentials)."""
+    from transplat_amd.misc.sh_rotation import sh_rotation_matrix
+
+    return sh_rotation_matrix(rotations.reshape(-1, 3, 3).double(), d_sh).float()
+
+
+# kernels.<name> -> oracle.<name>: what a CPU run of the module glue swaps in (tests, bench cpu leg)
+KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
+                       "sh_rotation")

@@ -15,7 +15,7 @@ def test_encoder_cpu_with_oracle_ops(monkeypatch):
     from transplat_amd import kernels
     from transplat_amd.model.encoder import EncoderTrans, EncoderTransCfg
 
-    for n in ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter"):
+    for n in E.KERNEL_RESTATEMENTS:
         monkeypatch.setattr(kernels, n, getattr(E, n))
     enc = S.init_synthetic_weights(EncoderTrans(EncoderTransCfg()).eval())
     batch = S.make_batch(1, image_shape=(128, 128))

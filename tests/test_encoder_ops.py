@@ -165,3 +165,32 @@ def test_gaussian_adapter_kernel(device):
         # products of three fp32 terms summed in a different order than torch's matmul)
         err = ((o - r).abs() / (r.abs() + 1e-3 * r.abs().max())).max().item()
         assert err < 2e-4, (name, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,groups,act,res", [
+    ((2, 128, 64, 64), 8, "silu", False), ((2, 32, 256, 256), 8, "silu", True), ((2, 128, 16, 16), 8, "none", True),
+    ((2, 32, 64, 64), 4, "gelu", False), ((3, 12, 5, 7), 4, "silu", True),  # odd HW: scalar path
+    ((2, 128, 4096), 8, "none", False)])
+def test_group_norm_kernel(device, shape, groups, act, res):
+    from transplat_amd import kernels as K
+
+    x = seeded(shape, 71) * 3 + 1.5  # non-zero mean: the Welford path matters
+    w = seeded((shape[1],), 72) * 0.5 + 1
+    b = seeded((shape[1],), 73) * 0.2
+    r = seeded(shape, 74) if res else None
+    ref = E.group_norm(x, groups, w, b, 1e-5, act, r)
+    out = K.group_norm(x.to(device), groups, w.to(device), b.to(device), 1e-5, act,
+                       r.to(device) if res else None).cpu()
+    assert (out - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_sh_rotation_op_matches_oracle(device):
+    from transplat_amd import kernels as K
+
+    _, _, _, ext, _ = _adapter_inputs()
+    rot = ext[..., :3, :3].reshape(-1, 3, 3)
+    ref = E.sh_rotation(rot, 25)
+    out = K.sh_rotation(rot.to(device), 25).cpu()
+    assert (out - ref).abs().max().item() < 2e-6

@@ -27,7 +27,7 @@ from transplat_amd import synthetic as S  # noqa: E402
 def cpu_ops(monkeypatch):
     from transplat_amd import kernels
 
-    for name in ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter"):
+    for name in E.KERNEL_RESTATEMENTS:
         monkeypatch.setattr(kernels, name, getattr(E, name))
     return torch.device("cpu")
 
@@ -137,7 +137,7 @@ def test_uv_transformers_gpu(device):
 # ------------------------------------------------------------------ U-Nets (MIOpen path)
 @pytest.mark.parametrize("tag,ch,mult,attn,hw", [("cv", 128, (1, 1, 1), (4,), 16),
                                                  ("depth", 32, (1, 1, 1, 1, 1), (16,), 32)])
-def test_unet_cpu(tag, ch, mult, attn, hw):
+def test_unet_cpu(cpu_ops, tag, ch, mult, attn, hw):
     from transplat_amd.model.encoder.matching.ldm_unet import UNetModel
 
     m = UNetModel(image_size=None, in_channels=ch, model_channels=ch, out_channels=ch, num_res_blocks=1,
@@ -147,6 +147,22 @@ def test_unet_cpu(tag, ch, mult, attn, hw):
     with torch.no_grad():
         y = m(seeded((2, ch, hw, hw), 601))
     _close(y, np.load(GOLD / f"unet_{tag}.npz")["out"], 1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag,ch,mult,attn,hw", [("cv", 128, (1, 1, 1), (4,), 16),
+                                                 ("depth", 32, (1, 1, 1, 1, 1), (16,), 32)])
+def test_unet_gpu(device, tag, ch, mult, attn, hw):
+    """The U-Nets with the fused GroupNorm(+SiLU, +residual) kernels vs the reference golden."""
+    from transplat_amd.model.encoder.matching.ldm_unet import UNetModel
+
+    m = UNetModel(image_size=None, in_channels=ch, model_channels=ch, out_channels=ch, num_res_blocks=1,
+                  attention_resolutions=attn, channel_mult=mult, num_head_channels=32, dims=2, postnorm=True,
+                  num_frames=2, use_cross_view_self_attn=True)
+    m = canonical_init(m, seed=41).eval().to(device)
+    with torch.no_grad():
+        y = m(seeded((2, ch, hw, hw), 601).to(device)).cpu()
+    _close(y, np.load(GOLD / f"unet_{tag}.npz")["out"], 1e-4)
 
 
 # ------------------------------------------------------------------ full depth predictor

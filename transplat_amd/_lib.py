@@ -47,6 +47,9 @@ SIGNATURES = {
     "tsplat_uv_cross_fwd": (ctypes.c_int, [_P] * 7 + [_I32] * 6 + [_P]),
     "tsplat_msda_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 6 + [_P]),
     "tsplat_win_attn_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 7 + [_P]),
+    "tsplat_group_norm_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, ctypes.c_int64, _I32]),
+    "tsplat_group_norm_fwd": (ctypes.c_int, [_P] * 6 + [_I32, _I32, ctypes.c_int64, _I32, ctypes.c_float, _I32, _P]),
+    "tsplat_sh_rotation_fwd": (ctypes.c_int, [_P] * 3 + [_I32] * 2 + [_P]),
     "tsplat_gaussian_adapter_fwd": (ctypes.c_int, [_P] * 9 + [_I32] * 6 + [ctypes.c_float] * 3 + [_I32, _P]),
 }
 
@@ -98,7 +101,8 @@ def stream_ptr(device: torch.device | None = None) -> int:
 
 
 PROF_IDS = {"raster_preprocess": 1, "raster_scan": 2, "raster_scatter": 3, "raster_render": 4,
-            "uv_coarse": 5, "uv_cross": 6, "msda": 7, "win_attn": 8, "raster": 9}
+            "uv_coarse": 5, "uv_cross": 6, "msda": 7, "win_attn": 8, "raster": 9,
+            "group_norm": 10}
 
 
 def prof_enable(name: str | None) -> None:

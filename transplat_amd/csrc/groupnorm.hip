@@ -1,0 +1,210 @@
+// GroupNorm (+ activation, + residual) over NCHW fp32, two launches.
+//
+// Replaces the GroupNorm -> SiLU/GELU (-> residual add) chains of the depth predictor's U-Nets
+// and refine heads (reference src/model/encoder/matching/ldm_unet/{unet.py:177-370, util.py:
+// 189-208}, depth_predictor_trans.py:142-206). PyTorch's ROCm GroupNorm launches one workgroup
+// per (sample, group) for the moments -- 16-64 workgroups on a 256-CU part, 37 us per call in the
+// r1 profile -- then a parameter kernel, an apply kernel and a separate activation.
+// Here: (1) every group is split into 4096-element chunks; a chunk's workgroup reduces it to a
+// Welford partial (mean, M2); (2) each apply workgroup combines its group's partials (Chan) and
+// normalises its chunk with the activation and optional residual fused: x is read twice (the
+// second time mostly from L2/MALL), y written once.
+#include "common.h"
+#include "prof.h"
+
+namespace tsplat {
+namespace gn {
+
+constexpr int kThreads = 256;
+constexpr int kChunk = 4096;  // elements per workgroup (16 per thread)
+
+struct Welford {
+    float n, mean, m2;
+};
+
+__device__ __forceinline__ Welford combine(Welford a, Welford b) {
+    const float n = a.n + b.n;
+    if (n == 0.f) return a;
+    const float d = b.mean - a.mean;
+    const float wb = b.n / n;
+    return {n, a.mean + d * wb, a.m2 + b.m2 + d * d * a.n * wb};
+}
+
+__device__ __forceinline__ Welford push(Welford w, float x) {
+    w.n += 1.f;
+    const float d = x - w.mean;
+    w.mean += d / w.n;
+    w.m2 += d * (x - w.mean);
+    return w;
+}
+
+__device__ __forceinline__ Welford wave_reduce(Welford w) {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        Welford o{__shfl_xor(w.n, off), __shfl_xor(w.mean, off), __shfl_xor(w.m2, off)};
+        w = combine(w, o);
+    }
+    return w;
+}
+
+// Welford over this workgroup's chunk -> partials[seg * S + chunk] = (mean, M2)
+template <bool VEC>
+__global__ void __launch_bounds__(kThreads)
+stats_kernel(const float* __restrict__ x, float2* __restrict__ partials, int64_t L, int S) {
+    const int chunk = blockIdx.x, seg = blockIdx.y, tid = threadIdx.x;
+    const int64_t start = (int64_t)chunk * kChunk;
+    const int n_local = (int)min((int64_t)kChunk, L - start);
+    const float* p = x + (int64_t)seg * L + start;
+    Welford w{0.f, 0.f, 0.f};
+    if (VEC) {
+#pragma unroll
+        for (int k = 0; k < kChunk / (4 * kThreads); ++k) {
+            const int i = (k * kThreads + tid) * 4;
+            if (i < n_local) {
+                const float4 v = *reinterpret_cast<const float4*>(p + i);
+                w = push(w, v.x);
+                w = push(w, v.y);
+                w = push(w, v.z);
+                w = push(w, v.w);
+            }
+        }
+    } else {
+        for (int i = tid; i < n_local; i += kThreads) w = push(w, p[i]);
+    }
+    w = wave_reduce(w);
+    __shared__ Welford sw[kThreads / kWave];
+    if ((tid & (kWave - 1)) == 0) sw[tid / kWave] = w;
+    __syncthreads();
+    if (tid == 0) {
+        Welford t = sw[0];
+#pragma unroll
+        for (int i = 1; i < kThreads / kWave; ++i) t = combine(t, sw[i]);
+        partials[(int64_t)seg * S + chunk] = make_float2(t.mean, t.m2);
+    }
+}
+
+template <int ACT>
+__device__ __forceinline__ float activate(float v) {
+    if (ACT == 1) return v / (1.0f + expf(-v));                     // SiLU
+    if (ACT == 2) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));  // GELU (erf)
+    return v;
+}
+
+template <bool VEC, int ACT, bool RES>
+__global__ void __launch_bounds__(kThreads)
+apply_kernel(const float* __restrict__ x, const float2* __restrict__ partials,
+             const float* __restrict__ gamma, const float* __restrict__ beta,
+             const float* __restrict__ res, float* __restrict__ y, int64_t L, int S, int HW, int C,
+             int cpg, int G, float eps) {
+    const int chunk = blockIdx.x, seg = blockIdx.y, tid = threadIdx.x;
+    __shared__ float s_scale_shift[2];
+    if (tid < kWave) {
+        // combine the group's S partials (chunk sizes are kChunk except the last)
+        Welford w{0.f, 0.f, 0.f};
+        for (int i = tid; i < S; i += kWave) {
+            const float2 pm = partials[(int64_t)seg * S + i];
+            const float n = (float)min((int64_t)kChunk, L - (int64_t)i * kChunk);
+            w = combine(w, Welford{n, pm.x, pm.y});
+        }
+        w = wave_reduce(w);
+        if (tid == 0) {
+            s_scale_shift[0] = w.mean;
+            s_scale_shift[1] = rsqrtf(w.m2 / (float)L + eps);
+        }
+    }
+    __syncthreads();
+    const float mean = s_scale_shift[0], rstd = s_scale_shift[1];
+    const int g = seg % G;
+    const int64_t start = (int64_t)chunk * kChunk;
+    const int n_local = (int)min((int64_t)kChunk, L - start);
+    const int64_t base = (int64_t)seg * L + start;
+    if (VEC) {
+#pragma unroll
+        for (int k = 0; k < kChunk / (4 * kThreads); ++k) {
+            const int i = (k * kThreads + tid) * 4;
+            if (i < n_local) {
+                const int c = g * cpg + (int)((start + i) / HW);  // HW % 4 == 0: one channel per float4
+                const float sc = rstd * gamma[c];
+                const float sh = beta[c] - sc * mean;
+                float4 v = *reinterpret_cast<const float4*>(x + base + i);
+                v.x = activate<ACT>(v.x * sc + sh);
+                v.y = activate<ACT>(v.y * sc + sh);
+                v.z = activate<ACT>(v.z * sc + sh);
+                v.w = activate<ACT>(v.w * sc + sh);
+                if (RES) {
+                    const float4 r = *reinterpret_cast<const float4*>(res + base + i);
+                    v.x += r.x;
+                    v.y += r.y;
+                    v.z += r.z;
+                    v.w += r.w;
+                }
+                *reinterpret_cast<float4*>(y + base + i) = v;
+            }
+        }
+    } else {
+        for (int i = tid; i < n_local; i += kThreads) {
+            const int c = g * cpg + (int)((start + i) / HW);
+            const float sc = rstd * gamma[c];
+            float v = activate<ACT>(x[base + i] * sc + (beta[c] - sc * mean));
+            if (RES) v += res[base + i];
+            y[base + i] = v;
+        }
+    }
+}
+
+}  // namespace gn
+}  // namespace tsplat
+
+using namespace tsplat;
+
+extern "C" size_t tsplat_group_norm_workspace_bytes(int32_t n, int32_t c, int64_t hw, int32_t groups) {
+    if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups) return 0;
+    const int64_t L = (int64_t)(c / groups) * hw;
+    const int64_t S = (L + gn::kChunk - 1) / gn::kChunk;
+    return (size_t)n * groups * S * sizeof(float2);
+}
+
+extern "C" int tsplat_group_norm_fwd(const float* x, const float* gamma, const float* beta,
+                                     const float* residual, float* y, void* workspace, int32_t n,
+                                     int32_t c, int64_t hw, int32_t groups, float eps, int32_t act,
+                                     void* stream_) {
+    using namespace tsplat::gn;
+    if (!x || !gamma || !beta || !y || !workspace) return TSPLAT_EINVAL;
+    if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups || act < 0 || act > 2 ||
+        hw > INT32_MAX)
+        return TSPLAT_EINVAL;
+    const int cpg = c / groups;
+    const int64_t L = (int64_t)cpg * hw;
+    const int64_t S = (L + kChunk - 1) / kChunk;
+    if (S > INT32_MAX || (int64_t)n * groups > 65535) return TSPLAT_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    const dim3 grid((unsigned)S, (unsigned)(n * groups));
+    const bool vec = (hw % 4 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
+                     (!residual || (uintptr_t)residual % 16 == 0);
+    float2* part = (float2*)workspace;
+    TSPLAT_PROF_BEGIN(prof::kGroupNorm, stream);
+    if (vec)
+        hipLaunchKernelGGL(stats_kernel<true>, grid, dim3(kThreads), 0, stream, x, part, L, (int)S);
+    else
+        hipLaunchKernelGGL(stats_kernel<false>, grid, dim3(kThreads), 0, stream, x, part, L, (int)S);
+    TSPLAT_CHECK_LAUNCH();
+#define TSPLAT_GN_APPLY(V, A, R)                                                                   \
+    hipLaunchKernelGGL((apply_kernel<V, A, R>), grid, dim3(kThreads), 0, stream, x, part, gamma,  \
+                       beta, residual, y, L, (int)S, (int)hw, c, cpg, groups, eps)
+#define TSPLAT_GN_ACT(V, R)              \
+    switch (act) {                       \
+        case 0: TSPLAT_GN_APPLY(V, 0, R); break; \
+        case 1: TSPLAT_GN_APPLY(V, 1, R); break; \
+        default: TSPLAT_GN_APPLY(V, 2, R); break; \
+    }
+    if (vec) {
+        if (residual) { TSPLAT_GN_ACT(true, true) } else { TSPLAT_GN_ACT(true, false) }
+    } else {
+        if (residual) { TSPLAT_GN_ACT(false, true) } else { TSPLAT_GN_ACT(false, false) }
+    }
+#undef TSPLAT_GN_ACT
+#undef TSPLAT_GN_APPLY
+    TSPLAT_PROF_END(prof::kGroupNorm, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

@@ -18,7 +18,8 @@ enum KernelId : int {
     kMsda = 7,
     kWinAttn = 8,
     kRasterAll = 9,   // the whole tsplat_raster_fwd launch sequence
-    kNumKernels = 10,
+    kGroupNorm = 10,  // both launches of tsplat_group_norm_fwd
+    kNumKernels = 11,
 };
 
 int active();                 // kernel id being timed (0 = off)

@@ -99,20 +99,55 @@ def adapter_cameras(extrinsics: torch.Tensor, intrinsics: torch.Tensor, image_sh
     return torch.cat([ext[:, :3, :3].reshape(-1, 9), ext[:, :3, 3], kinv.reshape(-1, 9), mult[:, None]], 1).contiguous()
 
 
+_ACTS = {"none": 0, "silu": 1, "gelu": 2}
+
+
+def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None):
+    """act(GroupNorm(x)) [+ residual] over [N, C, *spatial] fp32 (see tsplat_group_norm_fwd)."""
+    lib = _lib.load()
+    n, c = x.shape[:2]
+    hw = x[0, 0].numel()
+    xf = _f32(x)
+    res = _f32(residual) if residual is not None else None
+    if res is not None and res.shape != x.shape:
+        raise ValueError(f"residual {tuple(res.shape)} != input {tuple(x.shape)}")
+    y = torch.empty_like(xf)
+    ws = torch.empty(int(lib.tsplat_group_norm_workspace_bytes(n, c, hw, num_groups)), dtype=torch.uint8,
+                     device=x.device)
+    rc = lib.tsplat_group_norm_fwd(_lib.ptr(xf), _lib.ptr(_f32(weight)), _lib.ptr(_f32(bias)),
+                                   _lib.ptr(res) if res is not None else None, _lib.ptr(y), _lib.ptr(ws), n, c, hw,
+                                   num_groups, float(eps), _ACTS[act], _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_group_norm_fwd")
+    return y
+
+
+def sh_rotation(rotations, d_sh: int):
+    """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
+    wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""
+    from .misc.sh_rotation import x_basis_packed
+
+    lib = _lib.load()
+    rot = _f32(rotations.reshape(-1, 3, 3))
+    n = rot.shape[0]
+    out = torch.empty((n, d_sh, d_sh), device=rot.device)
+    rc = lib.tsplat_sh_rotation_fwd(_lib.ptr(rot), _lib.ptr(x_basis_packed(rot.device)), _lib.ptr(out), n, d_sh,
+                                    _lib.stream_ptr(rot.device))
+    _lib.check(rc, "tsplat_sh_rotation_fwd")
+    return out
+
+
 def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape, scale_min: float,
                      scale_max: float, opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1):
     """Raw head output -> Gaussians (see oracle.gaussian_adapter). raw [B, V, HW, 9 + 3 d_sh];
     depths, densities [B, V, HW]; extrinsics [B, V, 4, 4]; intrinsics [B, V, 3, 3]
     -> means [B, V*HW, 3], covariances [B, V*HW, 3, 3], harmonics [B, V*HW, 3, d_sh], opacities [B, V*HW]."""
-    from .misc.sh_rotation import sh_rotation_matrix
-
     lib = _lib.load()
     b, v, hw, r = raw.shape
     d_sh = (r - 9) // 3
     h, w = image_shape
     raw, depths, densities = _f32(raw), _f32(depths), _f32(densities)
     cams = adapter_cameras(extrinsics, intrinsics, image_shape)
-    shrot = sh_rotation_matrix(extrinsics.reshape(-1, 4, 4)[:, :3, :3], d_sh).float().contiguous()
+    shrot = sh_rotation(extrinsics.reshape(-1, 4, 4)[:, :3, :3], d_sh)
     dev = raw.device
     g = v * hw
     means = torch.empty((b, g, 3), device=dev)

@@ -110,6 +110,14 @@ def sh_rotation_matrix(rotations: torch.Tensor, d_sh: int) -> torch.Tensor:
     return out
 
 
+@lru_cache(maxsize=None)
+def x_basis_packed(device: torch.device) -> torch.Tensor:
+    """The constant P^l = exp(-pi/2 X_z), l = 0..4, packed row-major (165 float64): e3nn's x
+    rotation is P exp(t X_y) P^T. Device-resident, built once (kernel tsplat_sh_rotation_fwd)."""
+    blocks = [_expm(-math.pi / 2 * _so3_generators(l)[2]).reshape(-1) for l in range(5)]
+    return torch.cat(blocks).contiguous().to(device)
+
+
 def rotate_sh(sh_coefficients: torch.Tensor, rotations: torch.Tensor) -> torch.Tensor:
     """sh [..., n] rotated by the per-camera rotation [..., 3, 3] (broadcast over pixels)."""
     n = sh_coefficients.shape[-1]

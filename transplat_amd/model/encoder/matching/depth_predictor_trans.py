@@ -14,7 +14,7 @@ from torch import nn
 
 from ...utils.cam_param_encoder import cam_param_encoder
 from ...utils.uv_transformer import UVTransformer
-from .ldm_unet import UNetModel
+from .ldm_unet import UNetModel, run_sequential
 
 
 def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, num_samples):
@@ -134,7 +134,8 @@ class DepthPredictorTrans(nn.Module):
                                             features)
         raw_correlation_in = torch.cat((raw_correlation_in, feat01), dim=1)
 
-        raw_correlation = self.corr_refine_net(raw_correlation_in) + self.regressor_residual(raw_correlation_in)
+        raw_correlation = (run_sequential(self.corr_refine_net, raw_correlation_in)
+                           + self.regressor_residual(raw_correlation_in))
         pdf = F.softmax(self.depth_head_lowres(raw_correlation), dim=1)
         coarse_disps = (disp_candi_curr * pdf).sum(dim=1, keepdim=True)
         pdf_max = torch.max(pdf, dim=1, keepdim=True)[0]
@@ -144,7 +145,7 @@ class DepthPredictorTrans(nn.Module):
 
         proj_feat_in_fullres = self.upsampler(torch.cat((feat01, cnn_features), dim=1))
         proj_feature = self.proj_feature(proj_feat_in_fullres)
-        refine_out = self.refine_unet(torch.cat((extra_info["images"], da_depth, proj_feature, fullres_disps,
+        refine_out = run_sequential(self.refine_unet, torch.cat((extra_info["images"], da_depth, proj_feature, fullres_disps,
                                                  pdf_max), dim=1))
 
         raw_gaussians = self.to_gaussians(torch.cat([refine_out, extra_info["images"], proj_feat_in_fullres], dim=1))

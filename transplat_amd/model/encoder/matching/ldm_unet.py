@@ -5,7 +5,9 @@ Only the configuration the depth predictor instantiates is built: postnorm ResBl
 down/up-sampling, legacy QKV attention at the requested resolutions with views folded into the
 token axis, middle block = ResBlock, Identity, ResBlock. Module indices and parameter names
 follow the reference (`input_blocks.{i}.{j}`, `middle_block.{0,2}`, `output_blocks.{i}.{j}`,
-`out.{0,1}`) so checkpoint keys load. Convolutions and GEMMs run on MIOpen / hipBLASLt.
+`out.{0,1}`) so checkpoint keys load. Convolutions and GEMMs run on MIOpen / hipBLASLt; every
+GroupNorm runs as one fused gfx950 kernel pair together with the activation and residual add
+that follow it in the reference's module chain (kernels.group_norm).
 """
 from __future__ import annotations
 
@@ -16,10 +18,40 @@ import torch.nn.functional as F
 from einops import rearrange
 from torch import nn
 
+from .... import kernels
+
+_ACT_OF = {nn.SiLU: "silu", nn.GELU: "gelu"}
+
+
+def gn_act(norm: nn.GroupNorm, x, act: str = "none", residual=None):
+    """act(norm(x)) [+ residual] in one fused kernel, computed in fp32 and returned in x's dtype
+    (GroupNorm32 semantics: the reference normalises in float and casts back)."""
+    y = kernels.group_norm(x, norm.num_groups, norm.weight, norm.bias, norm.eps, act, residual)
+    return y.type(x.dtype)
+
+
+def run_sequential(seq: nn.Sequential, x):
+    """Run an nn.Sequential, fusing each GroupNorm with a SiLU / GELU that directly follows it."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, nn.GroupNorm):
+            nxt = mods[i + 1] if i + 1 < len(mods) else None
+            act = _ACT_OF.get(type(nxt)) if nxt is not None else None
+            if isinstance(nxt, nn.GELU) and nxt.approximate != "none":
+                act = None
+            x = gn_act(m, x, act or "none")
+            i += 2 if act else 1
+            continue
+        x = m(x)
+        i += 1
+    return x
+
 
 class GroupNorm32(nn.GroupNorm):
     def forward(self, x):
-        return super().forward(x.float()).type(x.dtype)
+        return gn_act(self, x)
 
 
 def normalization(channels):
@@ -45,7 +77,9 @@ class ResBlock(nn.Module):
                                 else nn.Conv2d(channels, self.out_channels, 1))
 
     def forward(self, x):
-        return self.skip_connection(x) + self.out_layers(self.in_layers(x))
+        # skip + SiLU(GN(conv(SiLU(GN(conv(x)))))): both GN + SiLU pairs and the residual fused
+        h = gn_act(self.in_layers[1], self.in_layers[0](x), "silu")
+        return gn_act(self.out_layers[1], self.out_layers[0](h), "silu", residual=self.skip_connection(x))
 
 
 class QKVAttentionLegacy(nn.Module):
@@ -89,8 +123,8 @@ class AttentionBlock(nn.Module):
     def forward(self, x):
         b, c, *spatial = x.shape
         x = x.reshape(b, c, -1)
-        h = self.norm(self.proj_out(self.attention(self.qkv(x))))
-        return (x + h).reshape(b, c, *spatial)
+        h = self.proj_out(self.attention(self.qkv(x)))
+        return gn_act(self.norm, h, residual=x).reshape(b, c, *spatial)
 
 
 class Downsample(nn.Module):
@@ -166,4 +200,4 @@ class UNetModel(nn.Module):
         h = self.middle_block(h)
         for module in self.output_blocks:
             h = module(torch.cat([h, hs.pop()], dim=1))
-        return self.out(h)
+        return run_sequential(self.out, h)
