@@ -182,8 +182,14 @@ int tsplat_gaussian_adapter_fwd(const float* raw, const float* depths, const flo
  *   q [batch, H*W, C]; k, v [batch, key_views, H*W, C] (key_views = 1 for two views);
  *   out [batch, H*W, C]; C must be 128; window pixels and window pixels * key_views must be
  *   multiples of 64. with_shift rolls by half a window and applies the -100 region mask.
+ *   Replaces single_head_split_window_attention (reference
+ *   src/model/encoder/backbone/multiview_transformer.py:57-206).
+ *   workspace: tsplat_win_attn_workspace_bytes(...) bytes (split-key partials; may be 0, then
+ *   workspace may be NULL).
  * ---------------------------------------------------------------------------------------- */
-int tsplat_win_attn_fwd(const float* q, const float* k, const float* v, float* out,
+size_t tsplat_win_attn_workspace_bytes(int32_t batch, int32_t height, int32_t width, int32_t key_views,
+                                       int32_t splits);
+int tsplat_win_attn_fwd(const float* q, const float* k, const float* v, float* out, void* workspace,
                         int32_t batch, int32_t height, int32_t width, int32_t channels,
                         int32_t key_views, int32_t splits, int32_t with_shift, void* stream);
 

@@ -1,0 +1,34 @@
+"""Microbenchmark of the window-attention kernel alone (2-view 64x64 map, splits 2, C=128: the
+transformer's shape at 256x256 input). Prints average µs per call (HIP events) and TFLOP/s.
+Variants via env TSPLAT_WINATTN / TSPLAT_WINATTN_KSPLIT (see csrc/winattn.hip)."""
+import argparse
+import os
+
+import torch
+
+from transplat_amd import _lib, kernels
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--batch", type=int, default=2)
+ap.add_argument("--hw", type=int, default=64)
+ap.add_argument("--iters", type=int, default=50)
+ap.add_argument("--shift", type=int, default=1)
+args = ap.parse_args()
+dev = torch.device("cuda:0")
+_lib.load()
+b, hw = args.batch, args.hw
+g = torch.Generator(device=dev).manual_seed(0)
+q, k, v = (torch.randn((b, hw * hw, 128), device=dev, generator=g) for _ in range(3))
+for _ in range(3):
+    kernels.window_attention(q, k, v, hw, hw, 2, bool(args.shift))
+torch.cuda.synchronize()
+_lib.prof_enable("win_attn")  # HIP events around the kernel launches only (no Python overhead)
+for _ in range(args.iters):
+    kernels.window_attention(q, k, v, hw, hw, 2, bool(args.shift))
+ms, n = _lib.prof_read()
+_lib.prof_enable(None)
+us = ms / n * 1e3
+L = (hw // 2) ** 2
+flops = 4 * b * 4 * L * L * 128
+print(f"variant={os.environ.get('TSPLAT_WINATTN', 'default')} ksplit={os.environ.get('TSPLAT_WINATTN_KSPLIT', 'auto')} "
+      f"b={b} hw={hw}: {us:.1f} us/call, {flops / us / 1e6:.1f} TFLOP/s", flush=True)

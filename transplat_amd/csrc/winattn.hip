@@ -11,7 +11,10 @@
 // (the reference allocates rolled copies, a [K^2, L, L] mask and [8, L, L] fp32 scores per call).
 //
 // Kernel: flash-style, one workgroup = 4 waves = 64 queries of one window; each wave owns 16
-// queries. Exact-fp32 MFMA (v_mfma_f32_16x16x4_f32) for both contractions:
+// queries. The keys of a window are split into ksplit ranges (one workgroup each, partials merged
+// by a small combine kernel) so the 2-view 64x64 map (128 query blocks) still fills 256 CUs
+// twice over; the next K/V tile's global loads are issued before the current tile's MFMAs.
+// Exact-fp32 MFMA (v_mfma_f32_16x16x4_f32) for both contractions:
 //   S^T[key, q] = K Q^T   (keys on MFMA rows, queries on lanes -> per-query softmax stats are
 //                          per-lane, no cross-lane transpose)
 //   O^T[d, q]  += V^T P^T (the S^T accumulator IS the P^T B-operand: lane (q, g) holds keys
@@ -19,6 +22,9 @@
 // K and V tiles of 64 keys are gathered by pixel index into LDS (K XOR-swizzled per 16-B chunk so
 // the 16 row reads of a ds_read_b128 group hit distinct banks; V rows padded to 132 floats so the
 // column reads of the two half-waves hit disjoint banks).
+#include <stdlib.h>
+#include <string.h>
+
 #include "common.h"
 #include "prof.h"
 
@@ -35,8 +41,21 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 struct Params {
     int H, W, splits, shift, m, L;  // L = window pixels
+    int ksplit, keys_per_split;     // key range [s * keys_per_split, (s+1) * keys_per_split)
     float scale;
 };
+
+// split-key partials of one workgroup (64 queries): O (unnormalised, [64][128]), m, l
+struct Partials {
+    float* o;
+    float* m;
+    float* l;
+};
+
+// row of query t (in-window index) of window wi, batch b, key split ks in the partial arrays
+__device__ __forceinline__ size_t pidx(const Params& p, int b, int wi, int ks, int t) {
+    return (((size_t)b * p.splits * p.splits + wi) * p.ksplit + ks) * p.L + t;
+}
 
 // original pixel of in-window position t of window wi after the roll by -shift
 __device__ __forceinline__ int win_pixel(const Params& p, int wi, int t) {
@@ -61,14 +80,51 @@ __device__ __forceinline__ int win_region(const Params& p, int wi, int t) {
     return by * 3 + bx;
 }
 
+// K / V rows of one 64-key tile held in registers between the global gather and the LDS store
+// (the next tile's loads are in flight while the current tile is computed)
+struct TileRegs {
+    float4 k[8], v[8];
+};
+
+__device__ __forceinline__ void load_tile(const Params& p, int wi, const float* kb, const float* vb,
+                                          size_t HW, int k0, int tid, TileRegs& t, int& region) {
+    const int r = tid >> 2, part = tid & 3;  // key row, 32-float quarter
+    const int j = k0 + r;
+    const int tk = j / p.m, vi = j - tk * p.m;
+    const int kpix = win_pixel(p, wi, tk);
+    const float4* ks = reinterpret_cast<const float4*>(kb + ((size_t)vi * HW + kpix) * kC + 32 * part);
+    const float4* vs = reinterpret_cast<const float4*>(vb + ((size_t)vi * HW + kpix) * kC + 32 * part);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        t.k[i] = ks[i];
+        t.v[i] = vs[i];
+    }
+    region = p.shift ? win_region(p, wi, j % p.L) : 0;
+}
+
+__device__ __forceinline__ void store_tile(float* sK, float* sV, int* sKeyRegion, int tid,
+                                           const TileRegs& t, int region, bool shift) {
+    const int r = tid >> 2, part = tid & 3;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int chunk = part * 8 + i;      // 16-B chunk in the 512-B row
+        const int phys = chunk ^ (r & 15);   // XOR swizzle (low 4 bits)
+        *reinterpret_cast<float4*>(&sK[r * kC + phys * 4]) = t.k[i];
+        *reinterpret_cast<float4*>(&sV[r * kVStride + chunk * 4]) = t.v[i];
+    }
+    if (part == 0 && shift) sKeyRegion[r] = region;
+}
+
+// grid (query blocks, windows, batch * ksplit); ksplit > 1 writes Partials, else `out`
 __global__ void __launch_bounds__(kThreads)
 win_attn_f32_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
-                    const float* __restrict__ v, float* __restrict__ out) {
+                    const float* __restrict__ v, float* __restrict__ out, Partials part) {
     __shared__ __attribute__((aligned(16))) float sK[kBK * kC];
     __shared__ __attribute__((aligned(16))) float sV[kBK * kVStride];
     __shared__ int sKeyRegion[kBK];
 
-    const int qblk = blockIdx.x, wi = blockIdx.y, b = blockIdx.z;
+    const int qblk = blockIdx.x, wi = blockIdx.y;
+    const int b = blockIdx.z / p.ksplit, ks = blockIdx.z - b * p.ksplit;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int g = lane >> 4, ql = lane & 15;
     const size_t HW = (size_t)p.H * p.W;
@@ -98,26 +154,14 @@ win_attn_f32_kernel(Params p, const float* __restrict__ q, const float* __restri
     for (int i = 0; i < 8; ++i) o[i] = floatx4{0.f, 0.f, 0.f, 0.f};
     float m_run = -INFINITY, l_run = 0.f;
 
-    const int nkeys = p.L * p.m;
-    for (int k0 = 0; k0 < nkeys; k0 += kBK) {
-        // ---- gather the K / V tile (64 keys x 128 ch) into LDS: 4 threads per key row
-        {
-            const int r = tid >> 2, part = tid & 3;  // row, 32-float quarter
-            const int j = k0 + r;
-            const int tk = j / p.m, vi = j - tk * p.m;
-            const int kpix = win_pixel(p, wi, tk);
-            const float4* ks = reinterpret_cast<const float4*>(kb + ((size_t)vi * HW + kpix) * kC + 32 * part);
-            const float4* vs = reinterpret_cast<const float4*>(vb + ((size_t)vi * HW + kpix) * kC + 32 * part);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int chunk = part * 8 + i;               // 16-B chunk in the 512-B row
-                const int phys = chunk ^ (r & 15);            // XOR swizzle (low 4 bits)
-                *reinterpret_cast<float4*>(&sK[r * kC + phys * 4]) = ks[i];
-                *reinterpret_cast<float4*>(&sV[r * kVStride + chunk * 4]) = vs[i];
-            }
-            if (part == 0 && p.shift) sKeyRegion[r] = win_region(p, wi, j % p.L);
-        }
+    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
+    TileRegs tr;
+    int treg;
+    load_tile(p, wi, kb, vb, HW, kbeg, tid, tr, treg);
+    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
+        store_tile(sK, sV, sKeyRegion, tid, tr, treg, p.shift != 0);
         __syncthreads();
+        if (k0 + kBK < kend) load_tile(p, wi, kb, vb, HW, k0 + kBK, tid, tr, treg);
 
         // ---- S^T = K Q^T for 4 tiles of 16 keys
         floatx4 s[4];
@@ -187,13 +231,239 @@ win_attn_f32_kernel(Params p, const float* __restrict__ q, const float* __restri
         __syncthreads();
     }
 
-    // ---- epilogue: O^T[d = 16dt + 4g + r][q] / l -> out[qpix][d]
-    const float inv = 1.0f / l_run;
-    float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * g;
+    if (p.ksplit == 1) {
+        // ---- epilogue: O^T[d = 16dt + 4g + r][q] / l -> out[qpix][d]
+        const float inv = 1.0f / l_run;
+        float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * g;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-        float4 t4 = make_float4(o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
-        *reinterpret_cast<float4*>(dst + 16 * dt) = t4;
+        for (int dt = 0; dt < 8; ++dt) {
+            float4 t4 = make_float4(o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+            *reinterpret_cast<float4*>(dst + 16 * dt) = t4;
+        }
+    } else {
+        // ---- split-key partial: unnormalised O, running max and sum of this key range
+        const size_t row = pidx(p, b, wi, ks, tq);
+        float* dst = part.o + row * kC + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+            *reinterpret_cast<float4*>(dst + 16 * dt) = make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+        if (g == 0) {
+            part.m[row] = m_run;
+            part.l[row] = l_run;
+        }
+    }
+}
+
+// combine the ksplit partials of each query: out = sum_s e^(m_s - M) O_s / sum_s e^(m_s - M) l_s
+// grid (L / 8, windows, batch); 32 threads per query, one float4 of channels each (1024+
+// workgroups for the 2-view map: the partials are the only HBM/MALL traffic of the split)
+__global__ void __launch_bounds__(kThreads)
+win_attn_combine_kernel(Params p, Partials part, float* __restrict__ out) {
+    const int wi = blockIdx.y, b = blockIdx.z;
+    const int tq = blockIdx.x * (kThreads / 32) + (threadIdx.x >> 5), c4 = threadIdx.x & 31;
+    const size_t HW = (size_t)p.H * p.W;
+    float M = -INFINITY;
+    for (int s = 0; s < p.ksplit; ++s) M = fmaxf(M, part.m[pidx(p, b, wi, s, tq)]);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    float L = 0.f;
+    for (int s = 0; s < p.ksplit; ++s) {
+        const size_t row = pidx(p, b, wi, s, tq);
+        const float w = __expf(part.m[row] - M);
+        L += w * part.l[row];
+        const float4 t4 = reinterpret_cast<const float4*>(part.o + row * kC)[c4];
+        acc.x += w * t4.x;
+        acc.y += w * t4.y;
+        acc.z += w * t4.z;
+        acc.w += w * t4.w;
+    }
+    const float inv = 1.0f / L;
+    const int qpix = win_pixel(p, wi, tq);
+    reinterpret_cast<float4*>(out + ((size_t)b * HW + qpix) * kC)[c4] =
+        make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+}
+
+// ============================================================================================
+// 32x32x2 variant (window pixels % 128 == 0): one workgroup = 4 waves x 32 queries; every MFMA
+// moves 32 FLOP per operand element (2x the 16x16x4 form) and has 64-cycle issue = dependent
+// latency, so single accumulator chains run at rate. Operand maps (lane l, c = l & 31, h = l >> 5):
+//   QK step i (0..63) contracts channels {i, 64 + i}: A = K[key c][64h + i] (LDS, K rows
+//     XOR-swizzled by 16-B chunk), B = Q[query c][64h + i] (registers, pre-scaled);
+//     S^T[key][q]: lane holds q = c, keys 8(r >> 2) + 4h + (r & 3) in register r.
+//   PV step r contracts keys {8(r >> 2) + (r & 3) + 4h'}: B = the S^T register r itself,
+//     A = V^T[d][that key] read as one ds_read_b128 per 4 steps from a transposed V tile.
+// ============================================================================================
+constexpr int kQW = 32;              // queries per wave
+constexpr int kBQ3 = 4 * kQW;        // queries per workgroup
+constexpr int kVtStride = kBK + 4;   // transposed V row (floats)
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// PREFETCH: the next tile's K/V rows are loaded into registers while the current tile is computed
+// (needs the 512-VGPR budget of one wave per SIMD); otherwise two workgroups per CU overlap.
+template <bool PREFETCH>
+__global__ void __launch_bounds__(kThreads, PREFETCH ? 1 : 2)
+win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
+                       const float* __restrict__ v, float* __restrict__ out, Partials part) {
+    __shared__ __attribute__((aligned(16))) float sK[kBK * kC];
+    __shared__ __attribute__((aligned(16))) float sVt[kC * kVtStride];
+    __shared__ int sKeyRegion[kBK];
+
+    const int qblk = blockIdx.x, wi = blockIdx.y;
+    const int b = blockIdx.z / p.ksplit, ks = blockIdx.z - b * p.ksplit;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const size_t HW = (size_t)p.H * p.W;
+    const float* qb = q + (size_t)b * HW * kC;
+    const float* kb = k + (size_t)b * p.m * HW * kC;
+    const float* vb = v + (size_t)b * p.m * HW * kC;
+
+    // gather: thread = (key row tid & 63, 32-channel quarter tid >> 6)
+    const int grow = tid & 63, gpart = tid >> 6;
+    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
+    float4 kv[8], vv[8];
+    int kreg = 0;
+    auto gather = [&](int k0) {  // global -> registers
+        const int j = k0 + grow;
+        const int tk = j / p.m, vi = j - tk * p.m;
+        const int kpix = win_pixel(p, wi, tk);
+        const float4* ksrc = reinterpret_cast<const float4*>(kb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
+        const float4* vsrc = reinterpret_cast<const float4*>(vb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            kv[i] = ksrc[i];
+            vv[i] = vsrc[i];
+        }
+        kreg = p.shift ? win_region(p, wi, j % p.L) : 0;
+    };
+    if (PREFETCH) gather(kbeg);
+
+    const int tq = qblk * kBQ3 + wid * kQW + c;
+    const int qpix = win_pixel(p, wi, tq);
+    const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+    float qr[64];
+    {
+        const float4* src = reinterpret_cast<const float4*>(qb + (size_t)qpix * kC + 64 * h);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float4 t4 = src[i];
+            qr[4 * i] = t4.x * p.scale;
+            qr[4 * i + 1] = t4.y * p.scale;
+            qr[4 * i + 2] = t4.z * p.scale;
+            qr[4 * i + 3] = t4.w * p.scale;
+        }
+    }
+    floatx16 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
+        if (!PREFETCH) gather(k0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int chunk = 8 * gpart + i;
+            *reinterpret_cast<float4*>(&sK[grow * kC + ((chunk ^ (grow & 15)) * 4)]) = kv[i];
+            sVt[(4 * chunk + 0) * kVtStride + grow] = vv[i].x;
+            sVt[(4 * chunk + 1) * kVtStride + grow] = vv[i].y;
+            sVt[(4 * chunk + 2) * kVtStride + grow] = vv[i].z;
+            sVt[(4 * chunk + 3) * kVtStride + grow] = vv[i].w;
+        }
+        if (gpart == 0 && p.shift) sKeyRegion[grow] = kreg;
+        __syncthreads();
+        if (PREFETCH && k0 + kBK < kend) gather(k0 + kBK);
+
+        // ---- S^T = K Q^T, two 32-key subtiles
+        floatx16 s[2];
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            const int row = 32 * sub + c;
+            floatx16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+            for (int i4 = 0; i4 < 16; ++i4) {
+                const int chunk = 16 * h + i4;
+                const float4 kk = *reinterpret_cast<const float4*>(&sK[row * kC + ((chunk ^ (row & 15)) * 4)]);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.x, qr[4 * i4 + 0], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.y, qr[4 * i4 + 1], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.z, qr[4 * i4 + 2], acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.w, qr[4 * i4 + 3], acc, 0, 0, 0);
+            }
+            s[sub] = acc;
+        }
+        // ---- mask + online softmax (lane = query c; its keys 32 sub + 8(r >> 2) + 4h + (r & 3))
+        float bmax = -INFINITY;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float x = s[sub][r];
+                if (p.shift)
+                    x += (sKeyRegion[32 * sub + 8 * (r >> 2) + 4 * h + (r & 3)] == qreg) ? 0.0f : -100.0f;
+                s[sub][r] = x;
+                bmax = fmaxf(bmax, x);
+            }
+        bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+        const float m_new = fmaxf(m_run, bmax);
+        const float corr = __expf(m_run - m_new);
+        float bsum = 0.f;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = __expf(s[sub][r] - m_new);
+                s[sub][r] = e;
+                bsum += e;
+            }
+        bsum += __shfl_xor(bsum, 32);
+        l_run = l_run * corr + bsum;
+        m_run = m_new;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+
+        // ---- O^T += V^T P^T
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt) {
+                    const float4 vt = *reinterpret_cast<const float4*>(
+                        &sVt[(32 * dt + c) * kVtStride + 32 * sub + 8 * u + 4 * h]);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt.x, s[sub][4 * u + 0], o[dt], 0, 0, 0);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt.y, s[sub][4 * u + 1], o[dt], 0, 0, 0);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt.z, s[sub][4 * u + 2], o[dt], 0, 0, 0);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt.w, s[sub][4 * u + 3], o[dt], 0, 0, 0);
+                }
+        __syncthreads();
+    }
+
+    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
+    if (p.ksplit == 1) {
+        const float inv = 1.0f / l_run;
+        float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                *reinterpret_cast<float4*>(dst + 32 * dt + 8 * u) =
+                    make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv, o[dt][4 * u + 2] * inv,
+                                o[dt][4 * u + 3] * inv);
+    } else {
+        const size_t row = pidx(p, b, wi, ks, tq);
+        float* dst = part.o + row * kC + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                *reinterpret_cast<float4*>(dst + 32 * dt + 8 * u) =
+                    make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
+        if (h == 0) {
+            part.m[row] = m_run;
+            part.l[row] = l_run;
+        }
     }
 }
 
@@ -202,10 +472,53 @@ win_attn_f32_kernel(Params p, const float* __restrict__ q, const float* __restri
 
 using namespace tsplat;
 
+// keys are split so a launch fills the 256 CUs: >= 512 workgroups for the 16x16 kernel (two per
+// CU), >= 256 for the 32x32 kernel (one per CU, software-pipelined)
+static int choose_ksplit(int base_wgs, int key_tiles, int target) {
+    int ks = 1;
+    while (base_wgs * ks < target && ks * 2 <= key_tiles && key_tiles % (ks * 2) == 0 && ks < 8) ks *= 2;
+    return ks;
+}
+
+// Tuning knobs (benchmarking only): TSPLAT_WINATTN=16 forces the 16x16x4 kernel, =32p the
+// register-prefetch 32x32x2 variant; TSPLAT_WINATTN_KSPLIT forces the key split.
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+static bool env_is(const char* name, const char* val) {
+    const char* e = getenv(name);
+    return e && !strcmp(e, val);
+}
+
+// query-block size of the kernel used for window size L (128: 32x32x2 kernel, 64: 16x16x4)
+static int query_block(int L) {
+    if (env_is("TSPLAT_WINATTN", "16")) return tsplat::winattn::kBQ;
+    return L % tsplat::winattn::kBQ3 == 0 ? tsplat::winattn::kBQ3 : tsplat::winattn::kBQ;
+}
+static int pick_ksplit(int base, int key_tiles, int qb) {
+    const int forced = env_int("TSPLAT_WINATTN_KSPLIT", 0);
+    if (forced > 0 && key_tiles % forced == 0) return forced;
+    const bool pf = env_is("TSPLAT_WINATTN", "32p");
+    return choose_ksplit(base, key_tiles, qb == tsplat::winattn::kBQ3 && pf ? 256 : 512);
+}
+
+extern "C" size_t tsplat_win_attn_workspace_bytes(int32_t batch, int32_t height, int32_t width,
+                                                  int32_t key_views, int32_t splits) {
+    using namespace tsplat::winattn;
+    if (batch <= 0 || key_views <= 0 || splits <= 0 || height % splits || width % splits) return 0;
+    const int L = (height / splits) * (width / splits);
+    if (L % kBQ || (L * key_views) % kBK) return 0;
+    const int base = (L / query_block(L)) * splits * splits * batch;
+    const int ks = pick_ksplit(base, L * key_views / kBK, query_block(L));
+    if (ks == 1) return 0;
+    return (size_t)batch * splits * splits * ks * L * (kC + 2) * sizeof(float);
+}
+
 extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* v, float* out,
-                                   int32_t batch, int32_t height, int32_t width, int32_t channels,
-                                   int32_t key_views, int32_t splits, int32_t with_shift,
-                                   void* stream_) {
+                                   void* workspace, int32_t batch, int32_t height, int32_t width,
+                                   int32_t channels, int32_t key_views, int32_t splits,
+                                   int32_t with_shift, void* stream_) {
     using namespace tsplat::winattn;
     if (!q || !k || !v || !out) return TSPLAT_EINVAL;
     if (channels != kC || batch <= 0 || key_views <= 0 || splits <= 0) return TSPLAT_EINVAL;
@@ -220,10 +533,30 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     if (with_shift && (height / splits) / 2 != (width / splits) / 2) return TSPLAT_EINVAL;
     if (p.L % kBQ || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
+    const int qb = query_block(p.L);
+    const int base = (p.L / qb) * splits * splits * batch;
+    p.ksplit = pick_ksplit(base, p.L * p.m / kBK, qb);
+    p.keys_per_split = p.L * p.m / p.ksplit;
+    Partials part{nullptr, nullptr, nullptr};
+    if (p.ksplit > 1) {
+        if (!workspace) return TSPLAT_EINVAL;
+        const size_t n = (size_t)batch * splits * splits * p.ksplit * p.L;
+        part.o = (float*)workspace;
+        part.m = part.o + n * kC;
+        part.l = part.m + n;
+    }
     hipStream_t stream = (hipStream_t)stream_;
-    dim3 grid(p.L / kBQ, splits * splits, batch);
+    const dim3 grid(p.L / qb, splits * splits, batch * p.ksplit);
     TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
-    hipLaunchKernelGGL(win_attn_f32_kernel, grid, dim3(kThreads), 0, stream, p, q, k, v, out);
+    if (qb == kBQ3 && env_is("TSPLAT_WINATTN", "32p"))
+        hipLaunchKernelGGL(win_attn_f32x32_kernel<true>, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
+    else if (qb == kBQ3)
+        hipLaunchKernelGGL(win_attn_f32x32_kernel<false>, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
+    else
+        hipLaunchKernelGGL(win_attn_f32_kernel, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
+    if (p.ksplit > 1)
+        hipLaunchKernelGGL(win_attn_combine_kernel, dim3(p.L / (kThreads / 32), splits * splits, batch),
+                           dim3(kThreads), 0, stream, p, part, out);
     TSPLAT_PROF_END(prof::kWinAttn, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

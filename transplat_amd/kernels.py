@@ -33,8 +33,10 @@ def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool)
     m = 1 if k.dim() == 3 else k.shape[1]
     q, k, v = _f32(q), _f32(k), _f32(v)
     out = torch.empty((b, l, c), dtype=torch.float32, device=q.device)
-    rc = lib.tsplat_win_attn_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(out), b, h, w, c, m,
-                                 num_splits, int(with_shift), _lib.stream_ptr(q.device))
+    nbytes = int(lib.tsplat_win_attn_workspace_bytes(b, h, w, m, num_splits))
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=q.device) if nbytes else None
+    rc = lib.tsplat_win_attn_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(out), _lib.ptr(ws), b, h, w, c,
+                                 m, num_splits, int(with_shift), _lib.stream_ptr(q.device))
     _lib.check(rc, "tsplat_win_attn_fwd")
     return out
 

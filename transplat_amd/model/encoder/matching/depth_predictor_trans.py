@@ -17,9 +17,11 @@ from ...utils.uv_transformer import UVTransformer
 from .ldm_unet import UNetModel, run_sequential
 
 
+@torch.autocast("cuda", enabled=False)
 def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, num_samples):
     """(reference :59-109) per-view features, pixel intrinsics, relative poses and disparity
-    candidates 1/far + linspace(0, 1, D) (1/near - 1/far), all in (v b) order."""
+    candidates 1/far + linspace(0, 1, D) (1/near - 1/far), all in (v b) order. Camera math stays
+    fp32 when the dense layers run under bf16 autocast."""
     b, v, _, h, w = features.shape
     feat_lists = [rearrange(features, "b v ... -> (v b) ...")]
     pose_curr_lists = []
@@ -101,11 +103,12 @@ class DepthPredictorTrans(nn.Module):
     def match_two(self, intr_curr, pose_curr, extrinsics, disp_candi_curr, dino_feature, features):
         """(reference :236-290) coarse then fine correlation for a pair of views -> [(v b), D, h, w]."""
         b, v, c, h, w = features.shape
-        cameras = (intr_curr, pose_curr, disp_candi_curr.flatten(1))
-        camk = torch.eye(4, device=intr_curr.device).view(1, 4, 4).repeat(intr_curr.shape[0], 1, 1).float()
-        camk[:, :3, :3] = intr_curr
-        c2w = rearrange(extrinsics.clone().detach(), "b v ... -> (v b) ...", b=b, v=v)
-        img2world = torch.matmul(c2w, torch.linalg.inv_ex(camk)[0]).reshape(-1, 16)
+        cameras = (intr_curr, pose_curr, disp_candi_curr.flatten(1).float())
+        with torch.autocast("cuda", enabled=False):
+            camk = torch.eye(4, device=intr_curr.device).view(1, 4, 4).repeat(intr_curr.shape[0], 1, 1).float()
+            camk[:, :3, :3] = intr_curr
+            c2w = rearrange(extrinsics.clone().detach(), "b v ... -> (v b) ...", b=b, v=v)
+            img2world = torch.matmul(c2w, torch.linalg.inv_ex(camk)[0]).reshape(-1, 16)
         pos_feature = self.cam_param_encoder(dino_feature, img2world)  # [(v b), C, h, w]
         # (b v)-ordered channel-last query positions: the reference's bev_pos after its permutes
         bev_pos = rearrange(pos_feature, "(v b) c h w -> (b v) (h w) c", v=v, b=b)
