@@ -181,7 +181,7 @@ int tsplat_gaussian_adapter_fwd(const float* raw, const float* depths, const flo
  * Shifted-window attention of the multi-view transformer (exact fp32 MFMA):
  *   q [batch, H*W, C]; k, v [batch, key_views, H*W, C] (key_views = 1 for two views);
  *   out [batch, H*W, C]; C must be 128; window pixels and window pixels * key_views must be
- *   multiples of 64. with_shift rolls by half a window and applies the -100 region mask.
+ *   multiples of 64. with_shift rolls by half a window per axis and applies the -100 region mask.
  *   Replaces single_head_split_window_attention (reference
  *   src/model/encoder/backbone/multiview_transformer.py:57-206).
  *   workspace: tsplat_win_attn_workspace_bytes(...) bytes (split-key partials; may be 0, then

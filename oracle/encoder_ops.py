@@ -13,19 +13,19 @@ import torch
 
 
 # --------------------------------------------------------------------- window attention (T2, T3)
-def _window_pixel_index(h: int, w: int, splits: int, shift: int) -> torch.Tensor:
-    """[K*K, L] original pixel of every (window, in-window position) after a roll by -shift.
+def _window_pixel_index(h: int, w: int, splits: int, shift_h: int, shift_w: int) -> torch.Tensor:
+    """[K*K, L] original pixel of every (window, in-window position) after the roll.
 
     Restates split_feature (reference unimatch/utils.py:34-59: windows ordered (row-split,
-    col-split), positions row-major) applied to torch.roll(x, (-shift, -shift)) (reference
-    multiview_transformer.py:91-98): rolled[y, x] = x_orig[(y + shift) % h, (x + shift) % w].
+    col-split), positions row-major) applied to torch.roll(x, (-shift_h, -shift_w)) (reference
+    multiview_transformer.py:91-98): rolled[y, x] = x_orig[(y + shift_h) % h, (x + shift_w) % w].
     """
     wh, ww = h // splits, w // splits
     idx = []
     for sy in range(splits):
         for sx in range(splits):
-            yy = (torch.arange(wh) + sy * wh + shift) % h
-            xx = (torch.arange(ww) + sx * ww + shift) % w
+            yy = (torch.arange(wh) + sy * wh + shift_h) % h
+            xx = (torch.arange(ww) + sx * ww + shift_w) % w
             idx.append((yy[:, None] * w + xx[None, :]).reshape(-1))
     return torch.stack(idx)
 
@@ -63,9 +63,9 @@ def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool)
         k = k[:, None]
         v = v[:, None]
     m = k.shape[1]
-    wh = h // num_splits
-    shift = wh // 2 if with_shift else 0
-    pix = _window_pixel_index(h, w, num_splits, shift)  # [K2, L]
+    wh, ww = h // num_splits, w // num_splits
+    # shift_size_h / _w = window // 2 per axis (reference :93-94)
+    pix = _window_pixel_index(h, w, num_splits, wh // 2 if with_shift else 0, ww // 2 if with_shift else 0)
     k2, L = pix.shape
     out = torch.empty_like(q)
     if with_shift:

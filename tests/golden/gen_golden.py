@@ -245,6 +245,35 @@ def gen_depth_predictor():
          raw_rows=raw_s)
 
 
+def gen_depth_predictor_v3():
+    """Three context views (DTU-style nctx = 3 at 256x256): the reference's pairwise match_two
+    averaging path (depth_predictor_trans.py:351-373)."""
+    dp = imp("src.model.encoder.matching.depth_predictor_trans")
+    from transplat_amd import synthetic as S
+
+    m = dp.DepthPredictorTrans(
+        feature_channels=128, upscale_factor=4, num_depth_candidates=128,
+        costvolume_unet_feat_dim=128, costvolume_unet_channel_mult=(1, 1, 1),
+        costvolume_unet_attn_res=(4,), gaussian_raw_channels=84, gaussians_per_pixel=1,
+        num_views=3, depth_unet_feat_dim=32, depth_unet_attn_res=[16],
+        depth_unet_channel_mult=[1, 1, 1, 1, 1], DA_size=64)
+    m = canonical_init(m, seed=33).eval()
+    ctx = S.make_batch(1, num_context=3, image_shape=(256, 256))["context"]
+    feats = seeded((1, 3, 128, 64, 64), 511, 0.5)
+    cnn = seeded((1, 3, 128, 64, 64), 512, 0.5)
+    da_depth = seeded((1, 3, 1, 256, 256), 513, 1.0, kind="rand")
+    dino = seeded((1, 3, 64, 144, 144), 514, 0.5)
+    extra = {"images": ctx["image"].permute(1, 0, 2, 3, 4).reshape(3, 3, 256, 256), "scene_names": None}
+    with torch.no_grad():
+        depths, dens, raw = m(feats, ctx["intrinsics"], ctx["extrinsics"], ctx["near"], ctx["far"],
+                              gaussians_per_pixel=1, deterministic=True, extra_info=extra,
+                              cnn_features=cnn, da_depth=da_depth, dino_feature=dino)
+    idx, raw_s = subset_rows(raw.reshape(-1, raw.shape[-1]), 4096, 9)
+    didx, d_s = subset_rows(depths.flatten(), 16384, 10)
+    save("depth_predictor_v3", depth_idx=didx, depths=d_s, densities=dens.flatten()[didx], raw_idx=idx,
+         raw_rows=raw_s)
+
+
 def gen_unet():
     un = imp("src.model.encoder.matching.ldm_unet.unet")
     for tag, ch, mult, attn, hw in (("cv", 128, (1, 1, 1), (4,), 16), ("depth", 32, (1, 1, 1, 1, 1), (16,), 32)):
@@ -308,6 +337,7 @@ ALL = {
     "uv": gen_uv,
     "unet": gen_unet,
     "depth_predictor": gen_depth_predictor,
+    "depth_predictor_v3": gen_depth_predictor_v3,
     "depth_anything": gen_depth_anything,
     "covariance": gen_covariance,
 }

@@ -49,3 +49,19 @@ def test_e2e_graph_matches_eager(device):
     torch.cuda.synchronize()
     assert (out2 - eager2).abs().mean().item() < 1e-4
     assert (out2 - out).abs().mean().item() > 1e-3  # a different scene really went through the graph
+
+
+@pytest.mark.gpu
+def test_e2e_three_context_views(device):
+    """nctx = 3 (the DTU setting at the reference's 256x256): V = 3 window attention (two key
+    views), pairwise cost-volume averaging, U-Nets with three frames, 3 x 65,536 Gaussians."""
+    from transplat_amd.e2e import build_model
+
+    model = build_model(device, num_context_views=3)
+    data = S.make_batch(1, num_context=3, image_shape=(256, 256), device=device)
+    with torch.no_grad():
+        g = model.encoder(model.data_shim(data)["context"], 0, deterministic=True)
+        out = model.test_step(data).color
+    torch.cuda.synchronize()
+    assert g.means.shape == (1, 3 * 256 * 256, 3)
+    assert out.shape == (1, 3, 3, 256, 256) and torch.isfinite(out).all()

@@ -194,3 +194,18 @@ def test_sh_rotation_op_matches_oracle(device):
     ref = E.sh_rotation(rot, 25)
     out = K.sh_rotation(rot.to(device), 25).cpu()
     assert (out - ref).abs().max().item() < 2e-6
+
+
+@pytest.mark.gpu
+def test_window_attention_dtu_stress(device):
+    """C5 stress: 3 context views at 512x384 -> a 128x96 feature map, 2 windows per side
+    (L = 3072 queries, 6144 keys over two key views), shifted layer."""
+    from transplat_amd import kernels as K
+
+    h, w = 96, 128
+    q = seeded((1, h * w, 128), 81)
+    k = seeded((1, 2, h * w, 128), 82)
+    v = seeded((1, 2, h * w, 128), 83)
+    ref = E.window_attention(q, k, v, h, w, 2, True)
+    out = K.window_attention(q.to(device), k.to(device), v.to(device), h, w, 2, True).cpu()
+    assert (out - ref).abs().max().item() < 2e-4

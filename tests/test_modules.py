@@ -166,29 +166,33 @@ def test_unet_gpu(device, tag, ch, mult, attn, hw):
 
 
 # ------------------------------------------------------------------ full depth predictor
-def _depth_predictor(dev):
+_DP_CASES = {2: ("depth_predictor", 31, (501, 502, 503, 504)), 3: ("depth_predictor_v3", 33, (511, 512, 513, 514))}
+
+
+def _depth_predictor(dev, nv=2):
     from transplat_amd.model.encoder.matching.depth_predictor_trans import DepthPredictorTrans
 
+    _, seed, sd = _DP_CASES[nv]
     m = DepthPredictorTrans(
         feature_channels=128, upscale_factor=4, num_depth_candidates=128, costvolume_unet_feat_dim=128,
         costvolume_unet_channel_mult=(1, 1, 1), costvolume_unet_attn_res=(4,), gaussian_raw_channels=84,
-        gaussians_per_pixel=1, num_views=2, depth_unet_feat_dim=32, depth_unet_attn_res=[16],
+        gaussians_per_pixel=1, num_views=nv, depth_unet_feat_dim=32, depth_unet_attn_res=[16],
         depth_unet_channel_mult=[1, 1, 1, 1, 1], DA_size=64)
-    m = canonical_init(m, seed=31).eval().to(dev)
-    ctx = {k: v.to(dev) for k, v in S.make_batch(1, image_shape=(256, 256))["context"].items()}
-    feats = seeded((1, 2, 128, 64, 64), 501, 0.5).to(dev)
-    cnn = seeded((1, 2, 128, 64, 64), 502, 0.5).to(dev)
-    da_depth = seeded((1, 2, 1, 256, 256), 503, 1.0, kind="rand").to(dev)
-    dino = seeded((1, 2, 64, 144, 144), 504, 0.5).to(dev)
-    extra = {"images": ctx["image"].permute(1, 0, 2, 3, 4).reshape(2, 3, 256, 256), "scene_names": None}
+    m = canonical_init(m, seed=seed).eval().to(dev)
+    ctx = {k: v.to(dev) for k, v in S.make_batch(1, num_context=nv, image_shape=(256, 256))["context"].items()}
+    feats = seeded((1, nv, 128, 64, 64), sd[0], 0.5).to(dev)
+    cnn = seeded((1, nv, 128, 64, 64), sd[1], 0.5).to(dev)
+    da_depth = seeded((1, nv, 1, 256, 256), sd[2], 1.0, kind="rand").to(dev)
+    dino = seeded((1, nv, 64, 144, 144), sd[3], 0.5).to(dev)
+    extra = {"images": ctx["image"].permute(1, 0, 2, 3, 4).reshape(nv, 3, 256, 256), "scene_names": None}
     depths, dens, raw = m(feats, ctx["intrinsics"], ctx["extrinsics"], ctx["near"], ctx["far"],
                           gaussians_per_pixel=1, deterministic=True, extra_info=extra, cnn_features=cnn,
                           da_depth=da_depth, dino_feature=dino)
     return depths.flatten().cpu(), dens.flatten().cpu(), raw.reshape(-1, raw.shape[-1]).cpu()
 
 
-def _check_depth_predictor(out, rel):
-    g = np.load(GOLD / "depth_predictor.npz")
+def _check_depth_predictor(out, rel, nv=2):
+    g = np.load(GOLD / f"{_DP_CASES[nv][0]}.npz")
     depths, dens, raw = out
     idx = torch.tensor(g["depth_idx"])
     _close(depths[idx], g["depths"], rel)
@@ -196,13 +200,15 @@ def _check_depth_predictor(out, rel):
     _close(raw[torch.tensor(g["raw_idx"])], g["raw_rows"], rel)
 
 
-def test_depth_predictor_cpu(cpu_ops):
-    _check_depth_predictor(_run(cpu_ops, _depth_predictor), 1e-3)
+@pytest.mark.parametrize("nv", [2, 3])
+def test_depth_predictor_cpu(cpu_ops, nv):
+    _check_depth_predictor(_run(cpu_ops, lambda d: _depth_predictor(d, nv)), 1e-3, nv)
 
 
 @pytest.mark.gpu
-def test_depth_predictor_gpu(device):
-    _check_depth_predictor(_run(device, _depth_predictor), 2e-3)
+@pytest.mark.parametrize("nv", [2, 3])
+def test_depth_predictor_gpu(device, nv):
+    _check_depth_predictor(_run(device, lambda d: _depth_predictor(d, nv)), 2e-3, nv)
 
 
 # ------------------------------------------------------------------ Depth-Anything-V2 ViT-B

@@ -251,3 +251,16 @@ def test_raster_graph_replay_with_new_inputs(device):
         torch.cuda.synchronize()
         assert torch.equal(out, eager[i]), i
     check_status(device)
+
+
+@pytest.mark.gpu
+def test_raster_dtu_stress_parity(device):
+    """C5 stress: G = 3 x 512 x 384 = 589,824 Gaussians from three context views rendered at
+    512x384 (32 x 24 tiles): long per-tile lists exercise the in-global sort path of the render
+    kernel. Bit-exact against the oracle like every other case."""
+    hw = (384, 512)
+    g = S.make_gaussians(1, num_context=3, image_shape=hw)
+    assert g["means"].shape[1] == 589_824
+    cams = _target_cams(S.make_batch(1, num_context=3, num_target=1, image_shape=hw), hw)
+    color, radii, color_ref, radii_ref, counts = _run_both(g, cams, hw, 1, 3, device)
+    _assert_parity(color, radii, color_ref, radii_ref)

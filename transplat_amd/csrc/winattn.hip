@@ -4,7 +4,7 @@
 // (src/model/encoder/backbone/multiview_transformer.py:57-206, both the 2-view and the multi-view
 // branch) with the Swin mask of `generate_shift_window_attn_mask` (:17-54):
 //   out[p] = softmax(q_p K_w^T / sqrt(C) + mask) V_w over the window w containing p, where windows
-//   are the K x K splits of the map rolled by (-shift, -shift) (shift = window/2 on odd layers),
+//   are the K x K splits of the map rolled by (-window_h/2, -window_w/2) on shifted layers,
 //   keys of m views are ordered pixel-major / view-minor and the -100 region mask is tiled
 //   view-major, so key j uses mask column j mod L (the reference's V >= 3 indexing, reproduced).
 // The roll, the window partition and the mask are index arithmetic here: nothing is materialised
@@ -40,7 +40,8 @@ constexpr int kVStride = kC + 4;  // padded V row (floats)
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 struct Params {
-    int H, W, splits, shift, m, L;  // L = window pixels
+    int H, W, splits, shift, m, L;  // L = window pixels; shift != 0: shifted (masked) layer
+    int shift_h, shift_w;           // roll of the shifted layer: half a window per axis
     int ksplit, keys_per_split;     // key range [s * keys_per_split, (s+1) * keys_per_split)
     float scale;
 };
@@ -62,8 +63,8 @@ __device__ __forceinline__ int win_pixel(const Params& p, int wi, int t) {
     const int wh = p.H / p.splits, ww = p.W / p.splits;
     const int sy = wi / p.splits, sx = wi % p.splits;
     const int ty = t / ww, tx = t - ty * ww;
-    int y = sy * wh + ty + p.shift;
-    int x = sx * ww + tx + p.shift;
+    int y = sy * wh + ty + p.shift_h;
+    int x = sx * ww + tx + p.shift_w;
     if (y >= p.H) y -= p.H;
     if (x >= p.W) x -= p.W;
     return y * p.W + x;
@@ -529,8 +530,10 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     p.splits = splits;
     p.m = key_views;
     p.L = (height / splits) * (width / splits);
-    p.shift = with_shift ? (height / splits) / 2 : 0;
-    if (with_shift && (height / splits) / 2 != (width / splits) / 2) return TSPLAT_EINVAL;
+    p.shift_h = with_shift ? (height / splits) / 2 : 0;
+    p.shift_w = with_shift ? (width / splits) / 2 : 0;
+    p.shift = with_shift ? 1 : 0;
+    if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
     if (p.L % kBQ || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
     const int qb = query_block(p.L);

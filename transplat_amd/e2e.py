@@ -45,9 +45,9 @@ class TransplatModel(torch.nn.Module):
         return missing, unexpected
 
 
-def build_model(device, dense_dtype: str = "fp32", seed: int = 0) -> TransplatModel:
+def build_model(device, dense_dtype: str = "fp32", seed: int = 0, num_context_views: int = 2) -> TransplatModel:
     torch.manual_seed(seed)
-    cfg = EncoderTransCfg(dense_dtype=dense_dtype)
+    cfg = EncoderTransCfg(dense_dtype=dense_dtype, num_context_views=num_context_views)
     model = TransplatModel(cfg, DecoderSplattingHIPCfg(check_overflow=False))
     S.init_synthetic_weights(model.encoder, seed)
     return model.eval().to(device)

@@ -51,6 +51,11 @@ def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, nu
     return feat_lists, intr_curr, pose_curr_lists, depth_candi_curr
 
 
+# view pairs matched for V > 2 in the reference's order (depth_predictor_trans.py:351-414): the ring
+# (i, i+1) first, then for V = 4 the diagonals (0, 2), (1, 3)
+_VIEW_PAIRS = {3: ((0, 1), (1, 2), (2, 0)), 4: ((0, 1), (1, 2), (2, 3), (3, 0), (0, 2), (1, 3))}
+
+
 class DepthPredictorTrans(nn.Module):
     def __init__(self, feature_channels=128, upscale_factor=4, num_depth_candidates=32, costvolume_unet_feat_dim=128,
                  costvolume_unet_channel_mult=(1, 1, 1), costvolume_unet_attn_res=(), gaussian_raw_channels=-1,
@@ -118,6 +123,30 @@ class DepthPredictorTrans(nn.Module):
         corr = self.fine_transformer([features], corr, w, h, bev_pos=bev_pos, cameras=cameras, channel_last=feat_cl)
         return rearrange(corr, "(b v) (h w) c -> (v b) c h w", b=b, v=v, h=h, w=w)
 
+    def match_pairs(self, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr, dino_feature, features):
+        """(reference :351-414) V = 3 / 4: match_two on every pair of _VIEW_PAIRS[V], then each view's
+        correlation is the mean of its halves over the pairs that contain it, taken in the
+        reference's order (pairs where it comes first, then pairs where it comes second).
+        pose_curr_lists[k] holds inv(E[(a + k + 1) % V]) E[a] for view a, so pair (a, c) uses
+        lists[(c - a - 1) % V][a] and lists[(a - c - 1) % V][c]. Generalised to batch b > 1 by
+        taking (v b) blocks (the reference indexes single rows, i.e. assumes b = 1)."""
+        b, v = features.shape[:2]
+        blk = lambda t, a: t[a * b:(a + 1) * b]
+        parts = []
+        for a, c in _VIEW_PAIRS[v]:
+            pose = torch.cat((blk(pose_curr_lists[(c - a - 1) % v], a), blk(pose_curr_lists[(a - c - 1) % v], c)))
+            pair = lambda t: torch.cat((blk(t, a), blk(t, c)))
+            corr = self.match_two(pair(intr_curr), pose, torch.stack((extrinsics[:, a], extrinsics[:, c]), 1),
+                                  pair(disp_candi_curr), pair(dino_feature),
+                                  torch.stack((features[:, a], features[:, c]), 1))
+            parts.append((corr[:b], corr[b:]))
+        per_view = []
+        for k in range(v):
+            halves = [p[0] for (a, _), p in zip(_VIEW_PAIRS[v], parts) if a == k]
+            halves += [p[1] for (_, c), p in zip(_VIEW_PAIRS[v], parts) if c == k]
+            per_view.append(torch.stack(halves, dim=0).mean(dim=0))
+        return torch.cat(per_view, dim=0)  # (v b)
+
     def forward(self, features, intrinsics, extrinsics, near, far, gaussians_per_pixel=1, deterministic=True,
                 extra_info=None, cnn_features=None, da_depth=None, dino_feature=None, benchmarker=None):
         b, v, c, h, w = features.shape
@@ -131,10 +160,14 @@ class DepthPredictorTrans(nn.Module):
         feat_comb_lists, intr_curr, pose_curr_lists, disp_candi_curr = prepare_feat_proj_data_lists(
             features, intrinsics, extrinsics, near, far, num_samples=self.num_depth_candidates)
         feat01 = feat_comb_lists[0]
-        if v != 2:
-            raise NotImplementedError("V > 2 context views: pairwise match_two averaging not built yet")
-        raw_correlation_in = self.match_two(intr_curr, pose_curr_lists[0], extrinsics, disp_candi_curr, dino_feature,
-                                            features)
+        if v == 2:
+            raw_correlation_in = self.match_two(intr_curr, pose_curr_lists[0], extrinsics, disp_candi_curr,
+                                                dino_feature, features)
+        elif v in _VIEW_PAIRS:
+            raw_correlation_in = self.match_pairs(intr_curr, pose_curr_lists, extrinsics, disp_candi_curr,
+                                                  dino_feature, features)
+        else:
+            raise NotImplementedError(f"{v} context views (the reference handles 2, 3 and 4)")
         raw_correlation_in = torch.cat((raw_correlation_in, feat01), dim=1)
 
         raw_correlation = (run_sequential(self.corr_refine_net, raw_correlation_in)
