@@ -193,6 +193,15 @@ int tsplat_win_attn_fwd(const float* q, const float* k, const float* v, float* o
                         int32_t batch, int32_t height, int32_t width, int32_t channels,
                         int32_t key_views, int32_t splits, int32_t with_shift, void* stream);
 
+/* bf16 variant (config C3): q, k, v, out are bf16 (raw 16-bit storage), same layouts and
+ * semantics; bf16 MFMA with fp32 accumulation and an fp32 softmax (P rounded to bf16 for the
+ * PV product). Window pixels must be a multiple of 128. */
+size_t tsplat_win_attn_bf16_workspace_bytes(int32_t batch, int32_t height, int32_t width, int32_t key_views,
+                                            int32_t splits);
+int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void* v, void* out, void* workspace,
+                             int32_t batch, int32_t height, int32_t width, int32_t channels,
+                             int32_t key_views, int32_t splits, int32_t with_shift, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

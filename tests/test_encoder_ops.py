@@ -209,3 +209,21 @@ def test_window_attention_dtu_stress(device):
     ref = E.window_attention(q, k, v, h, w, 2, True)
     out = K.window_attention(q.to(device), k.to(device), v.to(device), h, w, 2, True).cpu()
     assert (out - ref).abs().max().item() < 2e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,m,shift,b", [(64, 1, False, 2), (64, 1, True, 2), (64, 2, True, 3), (32, 1, True, 16)])
+def test_window_attention_bf16_kernel(device, hw, m, shift, b):
+    """bf16 MFMA variant (config C3) vs the fp32 oracle on the same bf16-rounded inputs: P is
+    rounded to bf16 for the PV product, so the bound is bf16-level (1.5e-2 absolute on O(1)
+    outputs)."""
+    from transplat_amd import kernels as K
+
+    q = seeded((b, hw * hw, 128), 91).bfloat16()
+    k = (seeded((b, m, hw * hw, 128), 92) if m > 1 else seeded((b, hw * hw, 128), 92)).bfloat16()
+    v = seeded(k.shape, 93).bfloat16()
+    ref = E.window_attention(q.float(), k.float(), v.float(), hw, hw, 2, shift)
+    out = K.window_attention(q.to(device), k.to(device), v.to(device), hw, hw, 2, shift)
+    assert out.dtype == torch.bfloat16
+    err = (out.float().cpu() - ref).abs().max().item()
+    assert err < 1.5e-2, err

@@ -13,12 +13,14 @@ ap.add_argument("--batch", type=int, default=2)
 ap.add_argument("--hw", type=int, default=64)
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--shift", type=int, default=1)
+ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 _lib.load()
 b, hw = args.batch, args.hw
 g = torch.Generator(device=dev).manual_seed(0)
-q, k, v = (torch.randn((b, hw * hw, 128), device=dev, generator=g) for _ in range(3))
+dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+q, k, v = (torch.randn((b, hw * hw, 128), device=dev, generator=g).to(dt) for _ in range(3))
 for _ in range(3):
     kernels.window_attention(q, k, v, hw, hw, 2, bool(args.shift))
 torch.cuda.synchronize()
@@ -30,5 +32,5 @@ _lib.prof_enable(None)
 us = ms / n * 1e3
 L = (hw // 2) ** 2
 flops = 4 * b * 4 * L * L * 128
-print(f"variant={os.environ.get('TSPLAT_WINATTN', 'default')} ksplit={os.environ.get('TSPLAT_WINATTN_KSPLIT', 'auto')} "
+print(f"{args.dtype} variant={os.environ.get('TSPLAT_WINATTN', 'default')} ksplit={os.environ.get('TSPLAT_WINATTN_KSPLIT', 'auto')} "
       f"b={b} hw={hw}: {us:.1f} us/call, {flops / us / 1e6:.1f} TFLOP/s", flush=True)

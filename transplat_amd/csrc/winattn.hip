@@ -258,8 +258,15 @@ win_attn_f32_kernel(Params p, const float* __restrict__ q, const float* __restri
 // combine the ksplit partials of each query: out = sum_s e^(m_s - M) O_s / sum_s e^(m_s - M) l_s
 // grid (L / 8, windows, batch); 32 threads per query, one float4 of channels each (1024+
 // workgroups for the 2-view map: the partials are the only HBM/MALL traffic of the split)
+__device__ __forceinline__ void store4(float* dst, float4 v) { *reinterpret_cast<float4*>(dst) = v; }
+__device__ __forceinline__ void store4(__bf16* dst, float4 v) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<bf16x4*>(dst) = bf16x4{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+}
+
+template <typename OutT>
 __global__ void __launch_bounds__(kThreads)
-win_attn_combine_kernel(Params p, Partials part, float* __restrict__ out) {
+win_attn_combine_kernel(Params p, Partials part, OutT* __restrict__ out) {
     const int wi = blockIdx.y, b = blockIdx.z;
     const int tq = blockIdx.x * (kThreads / 32) + (threadIdx.x >> 5), c4 = threadIdx.x & 31;
     const size_t HW = (size_t)p.H * p.W;
@@ -279,8 +286,7 @@ win_attn_combine_kernel(Params p, Partials part, float* __restrict__ out) {
     }
     const float inv = 1.0f / L;
     const int qpix = win_pixel(p, wi, tq);
-    reinterpret_cast<float4*>(out + ((size_t)b * HW + qpix) * kC)[c4] =
-        make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv);
+    store4(out + ((size_t)b * HW + qpix) * kC + 4 * c4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
 }
 
 // ============================================================================================
@@ -468,6 +474,171 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
     }
 }
 
+
+// ============================================================================================
+// bf16 variant (config C3: bf16 attention): v_mfma_f32_32x32x16_bf16, fp32 accumulation and
+// fp32 softmax, bf16 in/out. One workgroup = 4 waves x 32 queries, 64-key tiles in LDS as bf16
+// (K rows XOR-swizzled per 16-B chunk, V transposed). Operand maps (lane l, c = l & 31,
+// h = l >> 5, fragment element j = 0..7):
+//   QK step i (0..7): A = K[key c][16i + 8h + j], B = Q[query c][16i + 8h + j] (registers).
+//   S^T tile: lane holds query c, keys 8(r >> 2) + 4h + (r & 3) in register r.
+//   PV k-step s (16 keys) takes the S^T registers 8s..8s+7 packed to bf16 as the B operand
+//   (element j <-> key 16s + 8(j >> 2) + 4h + (j & 3)); A = V^T[d][same keys] from LDS.
+// ============================================================================================
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+constexpr int kVtStrideH = kBK + 8;  // transposed V row (bf16 elements)
+
+__global__ void __launch_bounds__(kThreads, 2)
+win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                     const __bf16* __restrict__ v, __bf16* __restrict__ out, Partials part) {
+    __shared__ __attribute__((aligned(16))) __bf16 sK[kBK * kC];
+    __shared__ __attribute__((aligned(16))) __bf16 sVt[kC * kVtStrideH];
+    __shared__ int sKeyRegion[kBK];
+
+    const int qblk = blockIdx.x, wi = blockIdx.y;
+    const int b = blockIdx.z / p.ksplit, ks = blockIdx.z - b * p.ksplit;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const size_t HW = (size_t)p.H * p.W;
+    const __bf16* qb = q + (size_t)b * HW * kC;
+    const __bf16* kb = k + (size_t)b * p.m * HW * kC;
+    const __bf16* vb = v + (size_t)b * p.m * HW * kC;
+
+    const int tq = qblk * kBQ3 + wid * kQW + c;
+    const int qpix = win_pixel(p, wi, tq);
+    const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+    bf16x8 qf[8];
+    {
+        const bf16x8* src = reinterpret_cast<const bf16x8*>(qb + (size_t)qpix * kC + 8 * h);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qf[i] = src[2 * i];
+    }
+    floatx16 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    const int grow = tid & 63, gpart = tid >> 6;  // key row, 32-channel quarter (64 B)
+    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
+    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
+        {
+            const int j = k0 + grow;
+            const int tk = j / p.m, vi = j - tk * p.m;
+            const int kpix = win_pixel(p, wi, tk);
+            const bf16x8* ksrc = reinterpret_cast<const bf16x8*>(kb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
+            const bf16x8* vsrc = reinterpret_cast<const bf16x8*>(vb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
+            bf16x8 kv[4], vv[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                kv[i] = ksrc[i];
+                vv[i] = vsrc[i];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int chunk = 4 * gpart + i;  // 16-B chunk (8 channels) of the 256-B row
+                *reinterpret_cast<bf16x8*>(&sK[grow * kC + ((chunk ^ (grow & 15)) * 8)]) = kv[i];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sVt[(8 * chunk + e) * kVtStrideH + grow] = vv[i][e];
+            }
+            if (gpart == 0 && p.shift) sKeyRegion[grow] = win_region(p, wi, j % p.L);
+        }
+        __syncthreads();
+
+        // ---- S^T = K Q^T (two 32-key subtiles), scaled in fp32
+        floatx16 s[2];
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            const int row = 32 * sub + c;
+            floatx16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int chunk = 2 * i + h;
+                const bf16x8 kk = *reinterpret_cast<const bf16x8*>(&sK[row * kC + ((chunk ^ (row & 15)) * 8)]);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[i], acc, 0, 0, 0);
+            }
+            s[sub] = acc;
+        }
+        // ---- mask + online softmax (fp32)
+        float bmax = -INFINITY;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                float x = s[sub][r] * p.scale;
+                if (p.shift)
+                    x += (sKeyRegion[32 * sub + 8 * (r >> 2) + 4 * h + (r & 3)] == qreg) ? 0.0f : -100.0f;
+                s[sub][r] = x;
+                bmax = fmaxf(bmax, x);
+            }
+        bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+        const float m_new = fmaxf(m_run, bmax);
+        const float corr = __expf(m_run - m_new);
+        float bsum = 0.f;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = __expf(s[sub][r] - m_new);
+                s[sub][r] = e;
+                bsum += e;
+            }
+        bsum += __shfl_xor(bsum, 32);
+        l_run = l_run * corr + bsum;
+        m_run = m_new;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+
+        // ---- O^T += V^T P^T: 4 k-steps of 16 keys
+#pragma unroll
+        for (int ksx = 0; ksx < 4; ++ksx) {
+            const int sub = ksx >> 1, st = ksx & 1;
+            bf16x8 pf;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) pf[e] = (__bf16)s[sub][8 * st + e];
+            const int key0 = 16 * ksx + 4 * h;  // keys key0 + 0..3 and key0 + 8 + 0..3
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const __bf16* vrow = &sVt[(32 * dt + c) * kVtStrideH];
+                const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vrow + key0);
+                const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vrow + key0 + 8);
+                const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+
+    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
+    if (p.ksplit == 1) {
+        const float inv = 1.0f / l_run;
+        __bf16* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                store4(dst + 32 * dt + 8 * u, make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv,
+                                                          o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
+    } else {
+        const size_t row = pidx(p, b, wi, ks, tq);
+        float* dst = part.o + row * kC + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                *reinterpret_cast<float4*>(dst + 32 * dt + 8 * u) =
+                    make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
+        if (h == 0) {
+            part.m[row] = m_run;
+            part.l[row] = l_run;
+        }
+    }
+}
+
 }  // namespace winattn
 }  // namespace tsplat
 
@@ -558,8 +729,64 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     else
         hipLaunchKernelGGL(win_attn_f32_kernel, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
     if (p.ksplit > 1)
-        hipLaunchKernelGGL(win_attn_combine_kernel, dim3(p.L / (kThreads / 32), splits * splits, batch),
+        hipLaunchKernelGGL(win_attn_combine_kernel<float>, dim3(p.L / (kThreads / 32), splits * splits, batch),
                            dim3(kThreads), 0, stream, p, part, out);
+    TSPLAT_PROF_END(prof::kWinAttn, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" size_t tsplat_win_attn_bf16_workspace_bytes(int32_t batch, int32_t height, int32_t width,
+                                                       int32_t key_views, int32_t splits) {
+    using namespace tsplat::winattn;
+    if (batch <= 0 || key_views <= 0 || splits <= 0 || height % splits || width % splits) return 0;
+    const int L = (height / splits) * (width / splits);
+    if (L % kBQ3 || (L * key_views) % kBK) return 0;
+    const int base = (L / kBQ3) * splits * splits * batch;
+    const int ks = choose_ksplit(base, L * key_views / kBK, 512);
+    if (ks == 1) return 0;
+    return (size_t)batch * splits * splits * ks * L * (kC + 2) * sizeof(float);
+}
+
+extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void* v, void* out,
+                                        void* workspace, int32_t batch, int32_t height, int32_t width,
+                                        int32_t channels, int32_t key_views, int32_t splits,
+                                        int32_t with_shift, void* stream_) {
+    using namespace tsplat::winattn;
+    if (!q || !k || !v || !out) return TSPLAT_EINVAL;
+    if (channels != kC || batch <= 0 || key_views <= 0 || splits <= 0) return TSPLAT_EINVAL;
+    if (height % splits || width % splits) return TSPLAT_EINVAL;
+    Params p;
+    p.H = height;
+    p.W = width;
+    p.splits = splits;
+    p.m = key_views;
+    p.L = (height / splits) * (width / splits);
+    p.shift_h = with_shift ? (height / splits) / 2 : 0;
+    p.shift_w = with_shift ? (width / splits) / 2 : 0;
+    p.shift = with_shift ? 1 : 0;
+    if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
+    if (p.L % kBQ3 || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
+    p.scale = 1.0f / sqrtf((float)kC);
+    const int base = (p.L / kBQ3) * splits * splits * batch;
+    p.ksplit = choose_ksplit(base, p.L * p.m / kBK, 512);
+    p.keys_per_split = p.L * p.m / p.ksplit;
+    Partials part{nullptr, nullptr, nullptr};
+    if (p.ksplit > 1) {
+        if (!workspace) return TSPLAT_EINVAL;
+        const size_t n = (size_t)batch * splits * splits * p.ksplit * p.L;
+        part.o = (float*)workspace;
+        part.m = part.o + n * kC;
+        part.l = part.m + n;
+    }
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
+    hipLaunchKernelGGL(win_attn_bf16_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
+                       dim3(kThreads), 0, stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
+                       (__bf16*)out, part);
+    if (p.ksplit > 1)
+        hipLaunchKernelGGL(win_attn_combine_kernel<__bf16>, dim3(p.L / (kThreads / 32), splits * splits, batch),
+                           dim3(kThreads), 0, stream, p, part, (__bf16*)out);
     TSPLAT_PROF_END(prof::kWinAttn, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

@@ -27,10 +27,21 @@ def pack_cameras(intr: torch.Tensor, pose: torch.Tensor) -> torch.Tensor:
 
 def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool):
     """Shifted-window attention (reference single_head_split_window_attention).
-    q [B, L, C]; k, v [B, L, C] or [B, m, L, C] -> [B, L, C] fp32."""
+    q [B, L, C]; k, v [B, L, C] or [B, m, L, C] -> [B, L, C]. bf16 inputs (the dense layers under
+    bf16 autocast) run the bf16-MFMA kernel and return bf16; everything else runs exact fp32."""
     lib = _lib.load()
     b, l, c = q.shape
     m = 1 if k.dim() == 3 else k.shape[1]
+    wl = (h // num_splits) * (w // num_splits)
+    if q.dtype == k.dtype == v.dtype == torch.bfloat16 and wl % 128 == 0:
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        out = torch.empty((b, l, c), dtype=torch.bfloat16, device=q.device)
+        nbytes = int(lib.tsplat_win_attn_bf16_workspace_bytes(b, h, w, m, num_splits))
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=q.device) if nbytes else None
+        rc = lib.tsplat_win_attn_bf16_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(out), _lib.ptr(ws), b, h,
+                                          w, c, m, num_splits, int(with_shift), _lib.stream_ptr(q.device))
+        _lib.check(rc, "tsplat_win_attn_bf16_fwd")
+        return out
     q, k, v = _f32(q), _f32(k), _f32(v)
     out = torch.empty((b, l, c), dtype=torch.float32, device=q.device)
     nbytes = int(lib.tsplat_win_attn_workspace_bytes(b, h, w, m, num_splits))
