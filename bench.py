@@ -27,6 +27,7 @@ import torch.distributed as dist
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md chip table)
 FP32_MFMA_PEAK_TFS = 157.3  # v_mfma_f32_16x16x4_f32 dense peak (= FP32 vector peak)
+BF16_MFMA_PEAK_TFS = 2500.0  # dense bf16 MFMA peak (no 2:1 sparsity), MI355X_MICROARCH.md
 RASTER_BYTES_PER_VIEW = None  # computed: G*(12+24+4*d_sh*3+4) + H*W*12
 
 
@@ -89,7 +90,7 @@ def build_raster_workload(batch: int, device, scene_offset: int):
     return step, info, cpu_inputs
 
 
-def e2e_roofline_info(kernel: str, batch: int) -> dict:
+def e2e_roofline_info(kernel: str, batch: int, dense_dtype: str = "fp32") -> dict:
     """Algorithmic HBM bytes (or FLOPs) per launch of the hand-written encoder kernels at 256x256,
     2 views, D = 128, C = 128, per SURVEY §8d (units per launch = `batch` scenes)."""
     hw, c, d, p = 64 * 64, 128, 128, 4
@@ -98,12 +99,18 @@ def e2e_roofline_info(kernel: str, batch: int) -> dict:
         # value (other view) + key + offsets + logits + output, fp32, each read once
         per = n * hw * (c * 4 + c * 4 + d * p * 2 * 4 + d * p * 4 + d * 4)
         return {"dominant": kernel, "alg_bytes_per_launch": per, "bound": "hbm"}
+    if kernel == "uv_cross_table":
+        # the [HW, HW] correlation table + offsets + logits + output, each read / written once
+        per = n * hw * (hw * 4 + d * p * 2 * 4 + d * p * 4 + d * 4)
+        return {"dominant": kernel, "alg_bytes_per_launch": per, "bound": "hbm"}
     if kernel == "uv_coarse":
         per = n * hw * (c * 4 + d * 4) + n * hw * c * 4  # own + other features, output
         return {"dominant": kernel, "alg_bytes_per_launch": per, "bound": "hbm"}
     if kernel == "win_attn":
         # 4 L S d FLOPs per window, 8 windows per scene-call (v = 2), fp32 MFMA
-        return {"dominant": kernel, "alg_flops_per_launch": 4 * 1024 * 1024 * 128 * 8 * batch, "bound": "mfma"}
+        # bf16 dense mode runs the bf16-MFMA kernel (priced against the dense bf16 peak)
+        return {"dominant": kernel, "alg_flops_per_launch": 4 * 1024 * 1024 * 128 * 8 * batch, "bound": "mfma",
+                "peak_tflops": BF16_MFMA_PEAK_TFS if dense_dtype == "bf16" else FP32_MFMA_PEAK_TFS}
     if kernel == "raster":
         return {"dominant": kernel, "alg_bytes_per_launch": raster_bytes_per_view(131072, 25, 256, 256) * 3 * batch,
                 "bound": "hbm"}
@@ -195,7 +202,7 @@ def main():
 
         step, info, model = build_e2e_workload(args.batch, device, scene_offset=rank * args.batch,
                                                dense_dtype=args.dense_dtype, graph=not args.no_graph)
-        info.update(e2e_roofline_info(args.dominant or "uv_cross", args.batch))
+        info.update(e2e_roofline_info(args.dominant or "win_attn", args.batch, args.dense_dtype))
         cpu_inputs = ("e2e", model)
     if args.dominant and args.workload == "raster":
         info["dominant"] = args.dominant
@@ -238,7 +245,7 @@ def main():
     avg_ms = ms / launches
     if info.get("bound", "hbm") == "mfma":
         achieved = info["alg_flops_per_launch"] / (avg_ms * 1e-3) / 1e12
-        peak, unit = FP32_MFMA_PEAK_TFS, "TFLOP/s"
+        peak, unit = info.get("peak_tflops", FP32_MFMA_PEAK_TFS), "TFLOP/s"
     else:
         achieved = info["alg_bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
         peak, unit = HBM_PEAK_GBS, "GB/s"

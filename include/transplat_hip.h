@@ -42,7 +42,8 @@ int tsplat_version(void);
 /* Per-kernel timing with HIP events recorded on the launch stream around every launch of ONE
  * kernel (ids: 1 raster preprocess, 2 raster scan, 3 raster scatter, 4 raster render,
  * 5 uv coarse correlation, 6 uv cross correlation, 7 msda, 8 window attention, 9 the whole
- * rasterizer launch sequence, 10 group norm (both launches); 0 = off).
+ * rasterizer launch sequence, 10 group norm (both launches), 11 uv cross through the
+ * correlation table; 0 = off).
  * tsplat_prof_read waits for the recorded events, returns the summed duration and the number of
  * launches timed since the last enable/read, and resets the record. Used by bench.py only. */
 int tsplat_prof_enable(int32_t kernel_id);
@@ -129,6 +130,15 @@ int tsplat_uv_cross_fwd(const float* value, const float* key, const float* cams,
                         const float* disp, const float* offsets, const float* logits, float* out,
                         int32_t batch, int32_t height, int32_t width, int32_t channels,
                         int32_t depths, int32_t points, void* stream);
+
+/* Fine cross correlation, table form: identical semantics to tsplat_uv_cross_fwd with the
+ * channel dot products precomputed, table[(b v)][p][q] = sum_c key[p][c] value_other[q][c]
+ * ([2*batch, H*W, H*W] fp32, e.g. one batched library GEMM), so each (pixel, depth) gathers
+ * 4 points x 4 bilinear corners of scalars: out = (1/channels) sum_pt softmax_pt sum_corner
+ * b * table[p][corner]. Same cams / disp / offsets / logits / out layouts. */
+int tsplat_uv_cross_table_fwd(const float* table, const float* cams, const float* disp, const float* offsets,
+                              const float* logits, float* out, int32_t batch, int32_t height, int32_t width,
+                              int32_t channels, int32_t depths, int32_t points, void* stream);
 
 /* Single-level single-head multi-scale deformable attention (mmcv ms_deform_attn_forward with
  * num_levels = num_heads = 1): out[i, q] = sum_pt weights[i, q, pt] * bilinear(value[i],

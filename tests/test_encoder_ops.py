@@ -106,17 +106,21 @@ def test_uv_coarse_kernel(device, hw, b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hw,b", [(16, 1), (24, 2)])
-def test_uv_cross_kernel(device, hw, b):
+@pytest.mark.parametrize("hw,b,variant", [(16, 1, "table"), (24, 2, "table"), (64, 1, "table"), (16, 1, "direct"),
+                                          (24, 2, "direct")])
+def test_uv_cross_kernel(device, hw, b, variant):
+    """Both forms of the fine cross correlation: the correlation-table gather (default) and the
+    direct feature-row sampling kernel."""
     from transplat_amd import kernels as K
 
+    op = K.uv_cross if variant == "table" else K.uv_cross_direct
     intr, pose, disp = _cams(b, hw)
     value = seeded((b, 2, hw * hw, 128), 41)
     key = seeded((b, 2, hw * hw, 128), 42)
     offsets = seeded((b * 2, hw * hw, 128 * 4 * 2), 43, 2.0)
     logits = seeded((b * 2, hw * hw, 128 * 4), 44)
     ref = E.uv_cross(value, key, intr, pose, disp, offsets, logits, hw, hw)
-    out = K.uv_cross(*(t.to(device) for t in (value, key, intr, pose, disp, offsets, logits)), hw, hw).cpu()
+    out = op(*(t.to(device) for t in (value, key, intr, pose, disp, offsets, logits)), hw, hw).cpu()
     assert (out - ref).abs().max().item() < 1e-4
 
 

@@ -45,6 +45,7 @@ SIGNATURES = {
     ),
     "tsplat_uv_coarse_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 5 + [_P]),
     "tsplat_uv_cross_fwd": (ctypes.c_int, [_P] * 7 + [_I32] * 6 + [_P]),
+    "tsplat_uv_cross_table_fwd": (ctypes.c_int, [_P] * 6 + [_I32] * 6 + [_P]),
     "tsplat_msda_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 6 + [_P]),
     "tsplat_win_attn_workspace_bytes": (ctypes.c_size_t, [_I32] * 5),
     "tsplat_win_attn_fwd": (ctypes.c_int, [_P] * 5 + [_I32] * 7 + [_P]),
@@ -105,7 +106,7 @@ def stream_ptr(device: torch.device | None = None) -> int:
 
 PROF_IDS = {"raster_preprocess": 1, "raster_scan": 2, "raster_scatter": 3, "raster_render": 4,
             "uv_coarse": 5, "uv_cross": 6, "msda": 7, "win_attn": 8, "raster": 9,
-            "group_norm": 10}
+            "group_norm": 10, "uv_cross_table": 11}
 
 
 def prof_enable(name: str | None) -> None:

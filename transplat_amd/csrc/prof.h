@@ -19,7 +19,8 @@ enum KernelId : int {
     kWinAttn = 8,
     kRasterAll = 9,   // the whole tsplat_raster_fwd launch sequence
     kGroupNorm = 10,  // both launches of tsplat_group_norm_fwd
-    kNumKernels = 11,
+    kUvCrossTable = 11,
+    kNumKernels = 12,
 };
 
 int active();                 // kernel id being timed (0 = off)

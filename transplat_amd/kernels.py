@@ -69,7 +69,29 @@ def uv_coarse(feat, intr, pose, disp, h: int, w: int):
 
 def uv_cross(value, key, intr, pose, disp, offsets, logits, h: int, w: int):
     """Fine cross correlation. value, key [B, 2, HW, C]; offsets [B*2, HW, D*P*2];
-    logits [B*2, HW, D*P] -> [B*2, HW, D] (see oracle.uv_cross)."""
+    logits [B*2, HW, D*P] -> [B*2, HW, D] (see oracle.uv_cross).
+
+    Two steps: the correlation table G[(b v)] = key_v value_(1-v)^T [HW, HW] as one batched
+    fp32 library GEMM (hipBLASLt, MFMA; autocast off so it stays fp32), then
+    tsplat_uv_cross_table_fwd gathers 4 points x 4 bilinear corners of G per (pixel, depth)."""
+    lib = _lib.load()
+    b, _, hw, c = value.shape
+    d = disp.shape[1]
+    p = logits.shape[-1] // d
+    value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
+    cams = pack_cameras(intr, pose)
+    with torch.autocast("cuda", enabled=False):
+        table = torch.bmm(key.reshape(b * 2, hw, c), torch.flip(value, dims=[1]).reshape(b * 2, hw, c).transpose(1, 2))
+    out = torch.empty((b * 2, hw, d), dtype=torch.float32, device=value.device)
+    rc = lib.tsplat_uv_cross_table_fwd(_lib.ptr(table), _lib.ptr(cams), _lib.ptr(disp), _lib.ptr(offsets),
+                                       _lib.ptr(logits), _lib.ptr(out), b, h, w, c, d, p, _lib.stream_ptr(value.device))
+    _lib.check(rc, "tsplat_uv_cross_table_fwd")
+    return out
+
+
+def uv_cross_direct(value, key, intr, pose, disp, offsets, logits, h: int, w: int):
+    """The same op in one gather kernel without the table (tsplat_uv_cross_fwd: 16 feature-row
+    samples per (pixel, depth)); kept as the table-free variant (no [HW, HW] buffer)."""
     lib = _lib.load()
     b, _, hw, c = value.shape
     d = disp.shape[1]
