@@ -21,6 +21,7 @@ import json
 import os
 import platform
 import time
+from pathlib import Path
 
 import torch
 import torch.distributed as dist
@@ -88,6 +89,19 @@ def build_raster_workload(batch: int, device, scene_offset: int):
     }
     cpu_inputs = ({k: t.cpu() for k, t in g.items()}, cams.to("cpu"), hw, v)
     return step, info, cpu_inputs
+
+
+def committed_traffic(kernel: str, dense_dtype: str, batch: int):
+    """HBM traffic per launch of `kernel` from the newest committed PMC digest
+    (profiles/<round>/traffic_<kernel>_<dtype>_b<batch>.json, written by tools/pmc_traffic.py from
+    separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same workload), or None."""
+    root = Path(__file__).resolve().parent / "profiles"
+    name = f"traffic_{kernel}_{dense_dtype}_b{batch}.json"
+    for d in sorted((p for p in root.glob("*") if p.is_dir()), reverse=True):
+        f = d / name
+        if f.exists():
+            return json.loads(f.read_text())["traffic_bytes_per_launch"], str(f.relative_to(root.parent))
+    return None, None
 
 
 def e2e_roofline_info(kernel: str, batch: int, dense_dtype: str = "fp32") -> dict:
@@ -250,6 +264,8 @@ def main():
         achieved = info["alg_bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
         peak, unit = HBM_PEAK_GBS, "GB/s"
 
+    traffic, traffic_src = committed_traffic(info["dominant"], args.dense_dtype, args.batch)
+
     views = world * info["views_per_step"] * args.steps
     result = {
         "metric": "novel views/sec at 256x256, 2 ctx views; PSNR parity vs reference",
@@ -278,7 +294,9 @@ def main():
             "peak": peak,
             "unit": unit,
             "frac": achieved / peak,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes/launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)",
+            "traffic_source": traffic_src,
             "avg_launch_ms": avg_ms,
             "launches": launches,
         },

@@ -1,9 +1,4 @@
-cd $GRAFT_REPO_ROOT
-export PYTHONPATH=$GRAFT_REPO_ROOT
-timeout -k 10 300 python -m pytest tests/test_encoder_ops.py tests/test_modules.py -q -m gpu > gpurun_out/t.log 2>&1; tail -3 gpurun_out/t.log
-for dom in uv_cross_table win_attn; do
-timeout -k 10 400 python bench.py --steps 20 --warmup 3 --dominant $dom --no-cpu-baseline > gpurun_out/b_$dom.log 2>&1 || { tail -5 gpurun_out/b_$dom.log; exit 1; }
-tail -1 gpurun_out/b_$dom.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"],1), "views/s", round(d["ms_per_step"],2), "ms", d["roofline"])'
-done
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_r1o -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $GRAFT_REPO_ROOT/gpurun_out/prof_r1o.log 2>&1 || exit 1
+R=$GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES -d $R/gpurun_out/rr_pmc -o run --output-format csv -- python3 $R/bench.py --workload raster --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/rr_pmc.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_TRANS_F32 SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS -d $R/gpurun_out/rr_pmc2 -o run --output-format csv -- python3 $R/bench.py --workload raster --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/rr_pmc2.log 2>&1 || exit 1

@@ -29,3 +29,14 @@ if [ "${RUN_PROF:-1}" = 1 ]; then
   echo "prof rc=$rc"; tail -3 $OUT/prof_$TAG.log
   find $OUT/prof_$TAG -name "*stats*" | head
 fi
+if [ "${RUN_PMC:-0}" = 1 ]; then
+  # HBM traffic of the dominant kernel: FETCH_SIZE and WRITE_SIZE in separate passes (eager launches)
+  cd /tmp && export TMPDIR=/tmp
+  DOM=${PMC_KERNEL:-win_attn}
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 400 rocprofv3 --pmc $C -d $OUT/pmc_${TAG}_$C -o run --output-format csv -- \
+        python3 $R/bench.py ${BENCH_ARGS:-} --steps 3 --warmup 1 --no-graph --no-cpu-baseline --dominant $DOM > $OUT/pmc_${TAG}_$C.log 2>&1; rc=$?
+    echo "pmc $C rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+  done
+fi

@@ -47,8 +47,10 @@ __constant__ float kSH_C4[9] = {2.5033429417967046f, -1.7701307697799304f, 0.946
 
 // exp(x) for x <= 0 (Cephes range reduction + degree-5 polynomial). Identical op sequence in
 // oracle/raster_ref.c so both sides produce the same float.
-__device__ __forceinline__ float exp_neg(float x) {
-    if (x < -87.0f) return 0.0f;
+// Branch-free on the GPU (the x < -87 case is a select, not exec-mask flow); bitwise the same.
+__device__ __forceinline__ float exp_neg(float x_in) {
+    const bool underflow = x_in < -87.0f;
+    const float x = underflow ? 0.0f : x_in;
     float kf = rintf(x * 1.44269504088896341f);
     float r = x - kf * 0.693359375f;
     r = r - kf * -2.12194440e-4f;
@@ -61,7 +63,7 @@ __device__ __forceinline__ float exp_neg(float x) {
     p = p * r + 5.0000001201e-1f;
     p = p * z + r + 1.0f;
     int k = (int)kf;
-    return p * __int_as_float((k + 127) << 23);
+    return underflow ? 0.0f : p * __int_as_float((k + 127) << 23);
 }
 
 struct Workspace {
@@ -413,7 +415,7 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     __shared__ float4 s_xy[kTileThreads];
     __shared__ float4 s_co[kTileThreads];
     __shared__ float4 s_rgb[kTileThreads];
-    __shared__ uint16_t s_list[kTileThreads / kWave][kTileThreads];
+    __shared__ __attribute__((aligned(8))) uint16_t s_list[kTileThreads / kWave][kTileThreads];
 
     const int v = blockIdx.y;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -448,17 +450,26 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     const size_t vbase = (size_t)v * p.G;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
 
-    for (int b0 = 0; b0 < n; b0 += kTileThreads) {
-        if (__syncthreads_count(done) == kTileThreads) break;
-        const int k = b0 + threadIdx.x;
+    // this thread's record of the next batch, fetched from global memory one batch ahead so the
+    // gather latency hides behind the current batch's blending
+    float4 r_xy = make_float4(0.f, 0.f, 0.f, 0.f), r_co = r_xy, r_rgb = r_xy;
+    auto fetch = [&](int k) {
         if (k < n) {
             const uint64_t key = in_lds ? skeys[k] : gkeys[k];
             const size_t id = vbase + (uint32_t)(key & 0xffffffffu);
-            s_xy[threadIdx.x] = ws.xy[id];
-            s_co[threadIdx.x] = ws.conic_o[id];
-            s_rgb[threadIdx.x] = ws.rgbd[id];
+            r_xy = ws.xy[id];
+            r_co = ws.conic_o[id];
+            r_rgb = ws.rgbd[id];
         }
+    };
+    fetch(threadIdx.x);
+    for (int b0 = 0; b0 < n; b0 += kTileThreads) {
+        if (__syncthreads_count(done) == kTileThreads) break;
+        s_xy[threadIdx.x] = r_xy;
+        s_co[threadIdx.x] = r_co;
+        s_rgb[threadIdx.x] = r_rgb;
         __syncthreads();
+        fetch(b0 + kTileThreads + threadIdx.x);
         const int cnt = min(kTileThreads, n - b0);
         // order-preserving compaction of this wave's candidates
         int m = 0;
@@ -476,12 +487,9 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
             m += __popcll(mask);
         }
         __syncthreads();
-        for (int i = 0; i < m; ++i) {
-            if (__all(done)) break;
-            const int e = s_list[wid][i];
-            const float4 xy = s_xy[e];
-            const float4 co = s_co[e];
-            const float4 c = s_rgb[e];
+        // blend in list order; 4 entries' LDS reads are issued together so the dependent
+        // index -> record loads overlap (the per-pixel operation sequence is unchanged)
+        auto blend = [&](const float4 xy, const float4 co, const float4 c) {
             const float dx = xy.x - pfx, dy = xy.y - pfy;
             const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
             const float alpha = fminf(0.99f, co.w * exp_neg(power));
@@ -495,6 +503,25 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
             C2 = acc ? C2 + c.z * alpha * T : C2;
             T = acc ? test_T : T;
             done = done || stop;
+        };
+        int i = 0;
+        for (; i + 4 <= m; i += 4) {
+            if (__all(done)) break;
+            const uint2 ids = *reinterpret_cast<const uint2*>(&s_list[wid][i]);
+            const int e0 = ids.x & 0xffff, e1 = ids.x >> 16, e2 = ids.y & 0xffff, e3 = ids.y >> 16;
+            const float4 xy0 = s_xy[e0], co0 = s_co[e0], c0 = s_rgb[e0];
+            const float4 xy1 = s_xy[e1], co1 = s_co[e1], c1 = s_rgb[e1];
+            const float4 xy2 = s_xy[e2], co2 = s_co[e2], c2 = s_rgb[e2];
+            const float4 xy3 = s_xy[e3], co3 = s_co[e3], c3 = s_rgb[e3];
+            blend(xy0, co0, c0);
+            blend(xy1, co1, c1);
+            blend(xy2, co2, c2);
+            blend(xy3, co3, c3);
+        }
+        for (; i < m; ++i) {
+            if (__all(done)) break;
+            const int e = s_list[wid][i];
+            blend(s_xy[e], s_co[e], s_rgb[e]);
         }
     }
     if (inside) {

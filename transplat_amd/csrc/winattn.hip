@@ -313,7 +313,7 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
                        const float* __restrict__ v, float* __restrict__ out, Partials part) {
     __shared__ __attribute__((aligned(16))) float sK[kBK * kC];
     __shared__ __attribute__((aligned(16))) float sVt[kC * kVtStride];
-    __shared__ int sKeyRegion[kBK];
+    __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
 
     const int qblk = blockIdx.x, wi = blockIdx.y;
     const int b = blockIdx.z / p.ksplit, ks = blockIdx.z - b * p.ksplit;
@@ -381,37 +381,55 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
         __syncthreads();
         if (PREFETCH && k0 + kBK < kend) gather(k0 + kBK);
 
-        // ---- S^T = K Q^T, two 32-key subtiles
+        // ---- S^T = K Q^T, two 32-key subtiles as two interleaved accumulator chains; the next
+        // K chunk pair is read from LDS before the current chunk's 8 MFMAs
         floatx16 s[2];
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-            const int row = 32 * sub + c;
-            floatx16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+        for (int r = 0; r < 16; ++r) s[0][r] = s[1][r] = 0.f;
+        {
+            auto kread = [&](int sub, int i4) {
+                const int row = 32 * sub + c;
+                return *reinterpret_cast<const float4*>(&sK[row * kC + (((16 * h + i4) ^ (row & 15)) * 4)]);
+            };
+            float4 ka0 = kread(0, 0), ka1 = kread(1, 0);
 #pragma unroll
             for (int i4 = 0; i4 < 16; ++i4) {
-                const int chunk = 16 * h + i4;
-                const float4 kk = *reinterpret_cast<const float4*>(&sK[row * kC + ((chunk ^ (row & 15)) * 4)]);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.x, qr[4 * i4 + 0], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.y, qr[4 * i4 + 1], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.z, qr[4 * i4 + 2], acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(kk.w, qr[4 * i4 + 3], acc, 0, 0, 0);
+                float4 kn0 = ka0, kn1 = ka1;
+                if (i4 + 1 < 16) {
+                    kn0 = kread(0, i4 + 1);
+                    kn1 = kread(1, i4 + 1);
+                }
+                s[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka0.x, qr[4 * i4 + 0], s[0], 0, 0, 0);
+                s[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka1.x, qr[4 * i4 + 0], s[1], 0, 0, 0);
+                s[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka0.y, qr[4 * i4 + 1], s[0], 0, 0, 0);
+                s[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka1.y, qr[4 * i4 + 1], s[1], 0, 0, 0);
+                s[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka0.z, qr[4 * i4 + 2], s[0], 0, 0, 0);
+                s[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka1.z, qr[4 * i4 + 2], s[1], 0, 0, 0);
+                s[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka0.w, qr[4 * i4 + 3], s[0], 0, 0, 0);
+                s[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka1.w, qr[4 * i4 + 3], s[1], 0, 0, 0);
+                ka0 = kn0;
+                ka1 = kn1;
             }
-            s[sub] = acc;
         }
         // ---- mask + online softmax (lane = query c; its keys 32 sub + 8(r >> 2) + 4h + (r & 3))
+        if (p.shift) {
+            // region ids of the lane's 4-key runs as int4 LDS reads, branch-free select
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int4 rg = *reinterpret_cast<const int4*>(&sKeyRegion[32 * sub + 8 * u + 4 * h]);
+                    s[sub][4 * u + 0] += rg.x == qreg ? 0.0f : -100.0f;
+                    s[sub][4 * u + 1] += rg.y == qreg ? 0.0f : -100.0f;
+                    s[sub][4 * u + 2] += rg.z == qreg ? 0.0f : -100.0f;
+                    s[sub][4 * u + 3] += rg.w == qreg ? 0.0f : -100.0f;
+                }
+        }
         float bmax = -INFINITY;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float x = s[sub][r];
-                if (p.shift)
-                    x += (sKeyRegion[32 * sub + 8 * (r >> 2) + 4 * h + (r & 3)] == qreg) ? 0.0f : -100.0f;
-                s[sub][r] = x;
-                bmax = fmaxf(bmax, x);
-            }
+            for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[sub][r]);
         bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
         const float m_new = fmaxf(m_run, bmax);
         const float corr = __expf(m_run - m_new);
@@ -430,20 +448,21 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
 
-        // ---- O^T += V^T P^T
+        // ---- O^T += V^T P^T: per 4-key run, the four d tiles' chains interleaved
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < 4; ++u) {
+                float4 vt[4];
 #pragma unroll
-                for (int dt = 0; dt < 4; ++dt) {
-                    const float4 vt = *reinterpret_cast<const float4*>(
-                        &sVt[(32 * dt + c) * kVtStride + 32 * sub + 8 * u + 4 * h]);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt.x, s[sub][4 * u + 0], o[dt], 0, 0, 0);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt.y, s[sub][4 * u + 1], o[dt], 0, 0, 0);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt.z, s[sub][4 * u + 2], o[dt], 0, 0, 0);
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt.w, s[sub][4 * u + 3], o[dt], 0, 0, 0);
-                }
+                for (int dt = 0; dt < 4; ++dt)
+                    vt[dt] = *reinterpret_cast<const float4*>(&sVt[(32 * dt + c) * kVtStride + 32 * sub + 8 * u + 4 * h]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int dt = 0; dt < 4; ++dt)
+                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt[dt][j], s[sub][4 * u + j], o[dt], 0, 0, 0);
+            }
         __syncthreads();
     }
 
@@ -494,7 +513,7 @@ win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __res
                      const __bf16* __restrict__ v, __bf16* __restrict__ out, Partials part) {
     __shared__ __attribute__((aligned(16))) __bf16 sK[kBK * kC];
     __shared__ __attribute__((aligned(16))) __bf16 sVt[kC * kVtStrideH];
-    __shared__ int sKeyRegion[kBK];
+    __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
 
     const int qblk = blockIdx.x, wi = blockIdx.y;
     const int b = blockIdx.z / p.ksplit, ks = blockIdx.z - b * p.ksplit;
@@ -547,34 +566,47 @@ win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __res
         }
         __syncthreads();
 
-        // ---- S^T = K Q^T (two 32-key subtiles), scaled in fp32
+        // ---- S^T = K Q^T (two 32-key subtiles, interleaved chains), scaled in fp32
         floatx16 s[2];
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-            const int row = 32 * sub + c;
-            floatx16 acc;
+        for (int r = 0; r < 16; ++r) s[0][r] = s[1][r] = 0.f;
+        {
+            bf16x8 kk[2][8];
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int row = 32 * sub + c, chunk = 2 * i + h;
+                    kk[sub][i] = *reinterpret_cast<const bf16x8*>(&sK[row * kC + ((chunk ^ (row & 15)) * 8)]);
+                }
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const int chunk = 2 * i + h;
-                const bf16x8 kk = *reinterpret_cast<const bf16x8*>(&sK[row * kC + ((chunk ^ (row & 15)) * 8)]);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk, qf[i], acc, 0, 0, 0);
+                s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk[0][i], qf[i], s[0], 0, 0, 0);
+                s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk[1][i], qf[i], s[1], 0, 0, 0);
             }
-            s[sub] = acc;
         }
-        // ---- mask + online softmax (fp32)
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[sub][r] *= p.scale;
+        // ---- mask (int4 region reads, branch-free) + online softmax (fp32)
+        if (p.shift) {
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int4 rg = *reinterpret_cast<const int4*>(&sKeyRegion[32 * sub + 8 * u + 4 * h]);
+                    s[sub][4 * u + 0] += rg.x == qreg ? 0.0f : -100.0f;
+                    s[sub][4 * u + 1] += rg.y == qreg ? 0.0f : -100.0f;
+                    s[sub][4 * u + 2] += rg.z == qreg ? 0.0f : -100.0f;
+                    s[sub][4 * u + 3] += rg.w == qreg ? 0.0f : -100.0f;
+                }
+        }
         float bmax = -INFINITY;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                float x = s[sub][r] * p.scale;
-                if (p.shift)
-                    x += (sKeyRegion[32 * sub + 8 * (r >> 2) + 4 * h + (r & 3)] == qreg) ? 0.0f : -100.0f;
-                s[sub][r] = x;
-                bmax = fmaxf(bmax, x);
-            }
+            for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[sub][r]);
         bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
         const float m_new = fmaxf(m_run, bmax);
         const float corr = __expf(m_run - m_new);
