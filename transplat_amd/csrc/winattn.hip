@@ -289,6 +289,56 @@ win_attn_combine_kernel(Params p, Partials part, OutT* __restrict__ out) {
     store4(out + ((size_t)b * HW + qpix) * kC + 4 * c4, make_float4(acc.x * inv, acc.y * inv, acc.z * inv, acc.w * inv));
 }
 
+// x32 / bf16 kernels store each wave's unnormalised O^T tile lane-contiguously: float4 number
+// (dt * 4 + u) * 64 + lane of the wave's 16-KB slot holds O^T[d = 32 dt + 8u + 4h .. +3][query c]
+// (lane = c + 32 h). Slot of (b, wi, ks, query block, wave) in the partial buffer (floats):
+__device__ __forceinline__ size_t lane_tile_base(const Params& p, int b, int wi, int ks, int qblk, int wid) {
+    const size_t nqb = (size_t)p.L / 128;
+    return ((((size_t)b * p.splits * p.splits + wi) * p.ksplit + ks) * nqb + qblk) * 128 * kC + (size_t)wid * 32 * kC;
+}
+
+// combine for the lane-contiguous layout: grid (L / 128 * 16, windows, batch), 256 threads; a
+// workgroup owns 256 consecutive float4s of one 128-query block (one wave slot's quarter, i.e.
+// 32 queries): it forms those queries' weights e^(m_s - M) / L in LDS, then reads every partial
+// float4 coalesced
+template <typename OutT>
+__global__ void __launch_bounds__(kThreads)
+win_attn_combine_x32_kernel(Params p, Partials part, OutT* __restrict__ out) {
+    __shared__ float s_w[8][32];
+    const int qblk = blockIdx.x >> 4, part16 = blockIdx.x & 15, wi = blockIdx.y, b = blockIdx.z;
+    const int t = threadIdx.x;
+    const int idx = part16 * kThreads + t;  // float4 index within the 128-query block
+    const int wid = idx >> 10, rem = idx & 1023, du = rem >> 6, lane = rem & 63;
+    const int c = lane & 31, h = lane >> 5, dt = du >> 2, u = du & 3;
+    const size_t HW = (size_t)p.H * p.W;
+    if (t < 32) {
+        const int tq = qblk * 128 + wid * 32 + t;
+        float M = -INFINITY;
+        for (int s = 0; s < p.ksplit; ++s) M = fmaxf(M, part.m[pidx(p, b, wi, s, tq)]);
+        float L = 0.f;
+        for (int s = 0; s < p.ksplit; ++s) {
+            const size_t row = pidx(p, b, wi, s, tq);
+            const float w = __expf(part.m[row] - M);
+            s_w[s][t] = w;
+            L += w * part.l[row];
+        }
+        const float inv = 1.0f / L;
+        for (int s = 0; s < p.ksplit; ++s) s_w[s][t] *= inv;
+    }
+    __syncthreads();
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = 0; s < p.ksplit; ++s) {
+        const float4 v = reinterpret_cast<const float4*>(part.o + lane_tile_base(p, b, wi, s, qblk, 0))[idx];
+        const float w = s_w[s][c];
+        acc.x += w * v.x;
+        acc.y += w * v.y;
+        acc.z += w * v.z;
+        acc.w += w * v.w;
+    }
+    const int qpix = win_pixel(p, wi, qblk * 128 + wid * 32 + c);
+    store4(out + ((size_t)b * HW + qpix) * kC + 32 * dt + 8 * u + 4 * h, acc);
+}
+
 // ============================================================================================
 // 32x32x2 variant (window pixels % 128 == 0): one workgroup = 4 waves x 32 queries; every MFMA
 // moves 32 FLOP per operand element (2x the 16x16x4 form) and has 64-cycle issue = dependent
@@ -478,14 +528,14 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
                     make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv, o[dt][4 * u + 2] * inv,
                                 o[dt][4 * u + 3] * inv);
     } else {
+        // lane-contiguous partial tile: each store instruction writes one 1-KB run
         const size_t row = pidx(p, b, wi, ks, tq);
-        float* dst = part.o + row * kC + 4 * h;
+        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, wid)) + lane;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                *reinterpret_cast<float4*>(dst + 32 * dt + 8 * u) =
-                    make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
+                dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
         if (h == 0) {
             part.m[row] = m_run;
             part.l[row] = l_run;
@@ -656,14 +706,14 @@ win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __res
                 store4(dst + 32 * dt + 8 * u, make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv,
                                                           o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
     } else {
+        // lane-contiguous partial tile: each store instruction writes one 1-KB run
         const size_t row = pidx(p, b, wi, ks, tq);
-        float* dst = part.o + row * kC + 4 * h;
+        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, wid)) + lane;
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                *reinterpret_cast<float4*>(dst + 32 * dt + 8 * u) =
-                    make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
+                dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
         if (h == 0) {
             part.m[row] = m_run;
             part.l[row] = l_run;
@@ -760,7 +810,10 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
         hipLaunchKernelGGL(win_attn_f32x32_kernel<false>, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
     else
         hipLaunchKernelGGL(win_attn_f32_kernel, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
-    if (p.ksplit > 1)
+    if (p.ksplit > 1 && qb == kBQ3)
+        hipLaunchKernelGGL(win_attn_combine_x32_kernel<float>, dim3(p.L / kBQ3 * 16, splits * splits, batch),
+                           dim3(kThreads), 0, stream, p, part, out);
+    else if (p.ksplit > 1)
         hipLaunchKernelGGL(win_attn_combine_kernel<float>, dim3(p.L / (kThreads / 32), splits * splits, batch),
                            dim3(kThreads), 0, stream, p, part, out);
     TSPLAT_PROF_END(prof::kWinAttn, stream);
@@ -817,7 +870,7 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
                        dim3(kThreads), 0, stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
                        (__bf16*)out, part);
     if (p.ksplit > 1)
-        hipLaunchKernelGGL(win_attn_combine_kernel<__bf16>, dim3(p.L / (kThreads / 32), splits * splits, batch),
+        hipLaunchKernelGGL(win_attn_combine_x32_kernel<__bf16>, dim3(p.L / kBQ3 * 16, splits * splits, batch),
                            dim3(kThreads), 0, stream, p, part, (__bf16*)out);
     TSPLAT_PROF_END(prof::kWinAttn, stream);
     TSPLAT_CHECK_LAUNCH();
