@@ -17,7 +17,8 @@
  *     ndc2Pix, getRect (16x16 tiles, (int) truncation), empty rect culled, SH -> RGB (+0.5, >= 0)
  *   binning: every (gaussian, tile) instance ordered by (tile, depth, gaussian id) — the order of
  *     the stable radix sort over id-ordered duplicates keyed (tile << 32 | depth bits)
- *   render: per pixel at integer coordinates, front to back: power = -0.5(a dx^2 + c dy^2) - b dx dy,
+ *   render: per pixel at integer coordinates, front to back (explicit fmaf where the kernel uses
+ *     v_fma_f32, identical sequence): power = -0.5(a dx^2 + c dy^2) - b dx dy,
  *     skip power > 0, alpha = min(0.99, o exp(power)), skip alpha < 1/255, stop when
  *     T (1 - alpha) < 1e-4, C += rgb alpha T; out = C + T bg.
  * Parity: unpinned against the reference CUDA binary (not available anywhere);
@@ -53,21 +54,22 @@ static uint32_t float_to_bits(float f) {
     return u;
 }
 
-/* exp(x), x <= 0: Cephes reduction + degree-5 polynomial (same op order as the kernel). */
+/* exp(x), x <= 0: Cephes reduction + degree-5 polynomial with explicit fmaf (same op order as
+ * the kernel; fmaf is correctly rounded on both sides). */
 static float ref_exp_neg(float x) {
     if (x < -87.0f) return 0.0f;
-    float kf = rintf(x * 1.44269504088896341f);
-    float r = x - kf * 0.693359375f;
-    r = r - kf * -2.12194440e-4f;
-    float z = r * r;
+    const float kf = rintf(x * 1.44269504088896341f);
+    float r = fmaf(kf, -0.693359375f, x);
+    r = fmaf(kf, 2.12194440e-4f, r);
+    const float z = r * r;
     float p = 1.9875691500e-4f;
-    p = p * r + 1.3981999507e-3f;
-    p = p * r + 8.3334519073e-3f;
-    p = p * r + 4.1665795894e-2f;
-    p = p * r + 1.6666665459e-1f;
-    p = p * r + 5.0000001201e-1f;
-    p = p * z + r + 1.0f;
-    int k = (int)kf;
+    p = fmaf(p, r, 1.3981999507e-3f);
+    p = fmaf(p, r, 8.3334519073e-3f);
+    p = fmaf(p, r, 4.1665795894e-2f);
+    p = fmaf(p, r, 1.6666665459e-1f);
+    p = fmaf(p, r, 5.0000001201e-1f);
+    p = fmaf(p, z, r) + 1.0f;
+    const int k = (int)kf;
     return p * bits_to_float((uint32_t)(k + 127) << 23);
 }
 
@@ -254,15 +256,17 @@ long tsplat_ref_raster_view(int G, int H, int W, int M, int deg, const float* me
                 for (long k = offs[t]; k < offs[t + 1]; ++k) {
                     const Rec* q = &rec[(uint32_t)(keys[k] & 0xffffffffu)];
                     const float dx = q->px - pfx, dy = q->py - pfy;
-                    const float power = -0.5f * (q->ca * dx * dx + q->cc * dy * dy) - q->cb * dx * dy;
+                    const float quad = fmaf(q->ca * dx, dx, (q->cc * dy) * dy);
+                    const float power = fmaf(-0.5f, quad, -((q->cb * dx) * dy));
                     if (power > 0.0f) continue;
                     const float alpha = fminf(0.99f, q->op * ref_exp_neg(power));
                     if (alpha < 1.0f / 255.0f) continue;
-                    const float test_T = Tr * (1.0f - alpha);
+                    const float test_T = fmaf(-alpha, Tr, Tr);
                     if (test_T < 0.0001f) break;
-                    C0 = C0 + q->r * alpha * Tr;
-                    C1 = C1 + q->g * alpha * Tr;
-                    C2 = C2 + q->b * alpha * Tr;
+                    const float w = alpha * Tr;
+                    C0 = fmaf(q->r, w, C0);
+                    C1 = fmaf(q->g, w, C1);
+                    C2 = fmaf(q->b, w, C2);
                     Tr = test_T;
                 }
                 const size_t pix = (size_t)pyi * W + pxi;

@@ -45,24 +45,24 @@ __constant__ float kSH_C4[9] = {2.5033429417967046f, -1.7701307697799304f, 0.946
                                 -0.6690465435572892f, 0.10578554691520431f, -0.6690465435572892f,
                                 0.47308734787878004f, -1.7701307697799304f, 0.6258357354491761f};
 
-// exp(x) for x <= 0 (Cephes range reduction + degree-5 polynomial). Identical op sequence in
-// oracle/raster_ref.c so both sides produce the same float.
+// exp(x) for x <= 0 (Cephes range reduction + degree-5 polynomial, written with explicit fmaf).
+// Identical op sequence in oracle/raster_ref.c so both sides produce the same float.
 // Branch-free on the GPU (the x < -87 case is a select, not exec-mask flow); bitwise the same.
 __device__ __forceinline__ float exp_neg(float x_in) {
     const bool underflow = x_in < -87.0f;
     const float x = underflow ? 0.0f : x_in;
-    float kf = rintf(x * 1.44269504088896341f);
-    float r = x - kf * 0.693359375f;
-    r = r - kf * -2.12194440e-4f;
-    float z = r * r;
+    const float kf = rintf(x * 1.44269504088896341f);
+    float r = fmaf(kf, -0.693359375f, x);
+    r = fmaf(kf, 2.12194440e-4f, r);
+    const float z = r * r;
     float p = 1.9875691500e-4f;
-    p = p * r + 1.3981999507e-3f;
-    p = p * r + 8.3334519073e-3f;
-    p = p * r + 4.1665795894e-2f;
-    p = p * r + 1.6666665459e-1f;
-    p = p * r + 5.0000001201e-1f;
-    p = p * z + r + 1.0f;
-    int k = (int)kf;
+    p = fmaf(p, r, 1.3981999507e-3f);
+    p = fmaf(p, r, 8.3334519073e-3f);
+    p = fmaf(p, r, 4.1665795894e-2f);
+    p = fmaf(p, r, 1.6666665459e-1f);
+    p = fmaf(p, r, 5.0000001201e-1f);
+    p = fmaf(p, z, r) + 1.0f;
+    const int k = (int)kf;
     return underflow ? 0.0f : p * __int_as_float((k + 127) << 23);
 }
 
@@ -489,18 +489,22 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
         __syncthreads();
         // blend in list order; 4 entries' LDS reads are issued together so the dependent
         // index -> record loads overlap (the per-pixel operation sequence is unchanged)
+        // power = -0.5 (a dx^2 + c dy^2) - b dx dy, alpha = min(0.99, o e^power), T' = T (1 - alpha),
+        // C += rgb alpha T, written with explicit fmaf (same sequence in oracle/raster_ref.c)
         auto blend = [&](const float4 xy, const float4 co, const float4 c) {
             const float dx = xy.x - pfx, dy = xy.y - pfy;
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+            const float quad = fmaf(co.x * dx, dx, (co.z * dy) * dy);
+            const float power = fmaf(-0.5f, quad, -((co.y * dx) * dy));
             const float alpha = fminf(0.99f, co.w * exp_neg(power));
-            const float test_T = T * (1.0f - alpha);
+            const float test_T = fmaf(-alpha, T, T);
             // reference order: skip power > 0, skip alpha < 1/255, stop if test_T < 1e-4
             const bool contrib = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
             const bool stop = contrib && (test_T < 0.0001f);
             const bool acc = contrib && !stop;
-            C0 = acc ? C0 + c.x * alpha * T : C0;
-            C1 = acc ? C1 + c.y * alpha * T : C1;
-            C2 = acc ? C2 + c.z * alpha * T : C2;
+            const float w = alpha * T;
+            C0 = acc ? fmaf(c.x, w, C0) : C0;
+            C1 = acc ? fmaf(c.y, w, C1) : C1;
+            C2 = acc ? fmaf(c.z, w, C2) : C2;
             T = acc ? test_T : T;
             done = done || stop;
         };
