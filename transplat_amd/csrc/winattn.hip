@@ -545,6 +545,234 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
 
 
 // ============================================================================================
+// Key-pair variant of the 32x32x2 kernel (for launches that need a key split): a workgroup of
+// 4 waves owns 64 queries; waves (2g, 2g + 1) share query group g and take the low / high 32 keys
+// of every 64-key tile, so each workgroup covers twice the keys of the 128-query kernel at the
+// same work. The two halves merge their (max, sum, O) in LDS at the end, which halves the
+// global split (and its partial traffic and combine) for the same number of workgroups.
+// Partials use the 128-query lane-contiguous layout (wave slot = 2 (qblk & 1) + g), so the same
+// combine kernel applies.
+// ============================================================================================
+__global__ void __launch_bounds__(kThreads, 2)
+win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
+                         const float* __restrict__ v, float* __restrict__ out, Partials part) {
+    __shared__ __attribute__((aligned(16))) float sK[kBK * kC];
+    __shared__ __attribute__((aligned(16))) float sVt[kC * kVtStride];
+    __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
+
+    const int qblk = blockIdx.x, wi = blockIdx.y;  // qblk: 64-query block
+    const int b = blockIdx.z / p.ksplit, ks = blockIdx.z - b * p.ksplit;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int qg = wid >> 1, kh = wid & 1;
+    const int c = lane & 31, h = lane >> 5;
+    const size_t HW = (size_t)p.H * p.W;
+    const float* qb = q + (size_t)b * HW * kC;
+    const float* kb = k + (size_t)b * p.m * HW * kC;
+    const float* vb = v + (size_t)b * p.m * HW * kC;
+
+    const int tq = qblk * 64 + qg * 32 + c;
+    const int qpix = win_pixel(p, wi, tq);
+    const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+    float qr[64];
+    {
+        const float4* src = reinterpret_cast<const float4*>(qb + (size_t)qpix * kC + 64 * h);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float4 t4 = src[i];
+            qr[4 * i] = t4.x * p.scale;
+            qr[4 * i + 1] = t4.y * p.scale;
+            qr[4 * i + 2] = t4.z * p.scale;
+            qr[4 * i + 3] = t4.w * p.scale;
+        }
+    }
+    floatx16 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    // staging (T14 split): the next tile's K rows are loaded into registers during this tile's
+    // QK^T and written to LDS after the barrier that retires K(t); the same registers then carry
+    // V(t+1) during PV(t). One 8 x float4 register set, three barriers per tile.
+    const int grow = tid & 63, gpart = tid >> 6;
+    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
+    const int row = 32 * kh + c;  // this lane's key row (A operand) within the tile
+    float4 stg[8];
+    int stg_region = 0;
+    auto row_src = [&](const float* base, int k0) {
+        const int j = k0 + grow;
+        const int tk = j / p.m, vi = j - tk * p.m;
+        return reinterpret_cast<const float4*>(base + ((size_t)vi * HW + win_pixel(p, wi, tk)) * kC + 32 * gpart);
+    };
+    auto load_k = [&](int k0) {
+        const float4* src = row_src(kb, k0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stg[i] = src[i];
+        stg_region = p.shift ? win_region(p, wi, (k0 + grow) % p.L) : 0;
+    };
+    auto load_v = [&](int k0) {
+        const float4* src = row_src(vb, k0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stg[i] = src[i];
+    };
+    auto store_k = [&]() {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int chunk = 8 * gpart + i;
+            *reinterpret_cast<float4*>(&sK[grow * kC + ((chunk ^ (grow & 15)) * 4)]) = stg[i];
+        }
+        if (gpart == 0 && p.shift) sKeyRegion[grow] = stg_region;
+    };
+    auto store_v = [&]() {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int chunk = 8 * gpart + i;
+            sVt[(4 * chunk + 0) * kVtStride + grow] = stg[i].x;
+            sVt[(4 * chunk + 1) * kVtStride + grow] = stg[i].y;
+            sVt[(4 * chunk + 2) * kVtStride + grow] = stg[i].z;
+            sVt[(4 * chunk + 3) * kVtStride + grow] = stg[i].w;
+        }
+    };
+    load_k(kbeg);
+    store_k();
+    load_v(kbeg);
+    store_v();
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
+        const bool has_next = k0 + kBK < kend;
+        if (has_next) load_k(k0 + kBK);
+
+        // ---- S^T for this wave's 32 keys (one chain: 32x32x2 issue interval = dependent latency;
+        // the next K chunk is read before the current chunk's MFMAs)
+        floatx16 s;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = 0.f;
+        {
+            auto kread = [&](int i4) {
+                return *reinterpret_cast<const float4*>(&sK[row * kC + (((16 * h + i4) ^ (row & 15)) * 4)]);
+            };
+            float4 ka = kread(0);
+#pragma unroll
+            for (int i4 = 0; i4 < 16; ++i4) {
+                const float4 nk = i4 + 1 < 16 ? kread(i4 + 1) : ka;
+                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.x, qr[4 * i4 + 0], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.y, qr[4 * i4 + 1], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.z, qr[4 * i4 + 2], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.w, qr[4 * i4 + 3], s, 0, 0, 0);
+                ka = nk;
+            }
+        }
+        if (p.shift) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int4 rg = *reinterpret_cast<const int4*>(&sKeyRegion[32 * kh + 8 * u + 4 * h]);
+                s[4 * u + 0] += rg.x == qreg ? 0.0f : -100.0f;
+                s[4 * u + 1] += rg.y == qreg ? 0.0f : -100.0f;
+                s[4 * u + 2] += rg.z == qreg ? 0.0f : -100.0f;
+                s[4 * u + 3] += rg.w == qreg ? 0.0f : -100.0f;
+            }
+        }
+        float bmax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[r]);
+        bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+        const float m_new = fmaxf(m_run, bmax);
+        const float corr = __expf(m_run - m_new);
+        float bsum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float e = __expf(s[r] - m_new);
+            s[r] = e;
+            bsum += e;
+        }
+        bsum += __shfl_xor(bsum, 32);
+        l_run = l_run * corr + bsum;
+        m_run = m_new;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+
+        __syncthreads();  // every wave is done with K(t) / regions(t)
+        if (has_next) {
+            store_k();
+            load_v(k0 + kBK);
+        }
+
+        // ---- O^T += V^T P^T over this wave's 32 keys, the four d tiles' chains interleaved
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int dp = 0; dp < 4; dp += 2) {
+                const float4 v0 = *reinterpret_cast<const float4*>(&sVt[(32 * dp + c) * kVtStride + 32 * kh + 8 * u + 4 * h]);
+                const float4 v1 = *reinterpret_cast<const float4*>(&sVt[(32 * dp + 32 + c) * kVtStride + 32 * kh + 8 * u + 4 * h]);
+                o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.x, s[4 * u + 0], o[dp], 0, 0, 0);
+                o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.x, s[4 * u + 0], o[dp + 1], 0, 0, 0);
+                o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.y, s[4 * u + 1], o[dp], 0, 0, 0);
+                o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.y, s[4 * u + 1], o[dp + 1], 0, 0, 0);
+                o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.z, s[4 * u + 2], o[dp], 0, 0, 0);
+                o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.z, s[4 * u + 2], o[dp + 1], 0, 0, 0);
+                o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.w, s[4 * u + 3], o[dp], 0, 0, 0);
+                o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.w, s[4 * u + 3], o[dp + 1], 0, 0, 0);
+            }
+        __syncthreads();  // every wave is done with V(t)
+        if (has_next) {
+            store_v();
+            __syncthreads();
+        }
+    }
+
+    // ---- merge the two key halves of each query group through LDS (sK / sVt are free now)
+    float* so = sK + qg * 64 * 64;          // [16 regs x 4 dt][64 lanes] of the high-key wave
+    float* sml = sVt + qg * 128;            // [64 lanes] m, [64 lanes] l
+    if (kh == 1) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) so[(dt * 16 + r) * 64 + lane] = o[dt][r];
+        sml[lane] = m_run;
+        sml[64 + lane] = l_run;
+    }
+    __syncthreads();
+    if (kh == 1) return;
+    {
+        const float m1 = sml[lane], l1 = sml[64 + lane];
+        const float M = fmaxf(m_run, m1);
+        const float a0 = __expf(m_run - M), a1 = __expf(m1 - M);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) o[dt][r] = o[dt][r] * a0 + so[(dt * 16 + r) * 64 + lane] * a1;
+        l_run = l_run * a0 + l1 * a1;
+        m_run = M;
+    }
+
+    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
+    if (p.ksplit == 1) {
+        const float inv = 1.0f / l_run;
+        float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                *reinterpret_cast<float4*>(dst + 32 * dt + 8 * u) =
+                    make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv, o[dt][4 * u + 2] * inv,
+                                o[dt][4 * u + 3] * inv);
+    } else {
+        const size_t prow = pidx(p, b, wi, ks, tq);
+        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk >> 1, 2 * (qblk & 1) + qg)) + lane;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
+        if (h == 0) {
+            part.m[prow] = m_run;
+            part.l[prow] = l_run;
+        }
+    }
+}
+
+// ============================================================================================
 // bf16 variant (config C3: bf16 attention): v_mfma_f32_32x32x16_bf16, fp32 accumulation and
 // fp32 softmax, bf16 in/out. One workgroup = 4 waves x 32 queries, 64-key tiles in LDS as bf16
 // (K rows XOR-swizzled per 16-B chunk, V transposed). Operand maps (lane l, c = l & 31,
@@ -792,6 +1020,10 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     const int qb = query_block(p.L);
     const int base = (p.L / qb) * splits * splits * batch;
     p.ksplit = pick_ksplit(base, p.L * p.m / kBK, qb);
+    // key-pair kernel: 64-query workgroups (twice the blocks), half the global key split
+    const bool pair = qb == kBQ3 && (p.ksplit > 1 || env_is("TSPLAT_WINATTN", "pair")) &&
+                      !env_is("TSPLAT_WINATTN", "32") && !env_is("TSPLAT_WINATTN", "32p");
+    if (pair) p.ksplit = std::max(1, p.ksplit / 2);
     p.keys_per_split = p.L * p.m / p.ksplit;
     Partials part{nullptr, nullptr, nullptr};
     if (p.ksplit > 1) {
@@ -804,7 +1036,10 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     hipStream_t stream = (hipStream_t)stream_;
     const dim3 grid(p.L / qb, splits * splits, batch * p.ksplit);
     TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
-    if (qb == kBQ3 && env_is("TSPLAT_WINATTN", "32p"))
+    if (pair)
+        hipLaunchKernelGGL(win_attn_f32_pair_kernel, dim3(p.L / 64, splits * splits, batch * p.ksplit),
+                           dim3(kThreads), 0, stream, p, q, k, v, out, part);
+    else if (qb == kBQ3 && env_is("TSPLAT_WINATTN", "32p"))
         hipLaunchKernelGGL(win_attn_f32x32_kernel<true>, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
     else if (qb == kBQ3)
         hipLaunchKernelGGL(win_attn_f32x32_kernel<false>, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
