@@ -65,3 +65,31 @@ def test_gather_world2_gloo():
         assert p.exitcode == 0
     assert [r[0] for r in res] == [0, 1, 2, 3, 4]
     assert all(r[2] == 3 for r in res) and all(r[1] > 15 for r in res)
+
+
+def test_index_batch_places_targets():
+    scenes = ev.load_index(INDEX)
+    key, entry = scenes[0]
+    b = ev.index_batch(0, key, entry, image_shape=(32, 32))
+    assert b["context"]["image"].shape == (1, 2, 3, 32, 32) and b["target"]["image"].shape == (1, 3, 3, 32, 32)
+    c0, c1 = entry["context"]
+    t = b["target"]["extrinsics"][0, :, 0, 3]  # x translation along the unit baseline
+    expect = torch.tensor([(f - c0) / (c1 - c0) for f in entry["target"]], dtype=torch.float32)
+    assert torch.allclose(t, expect, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_evaluate_cli_small_index(device):
+    """C1 plumbing on the GPU: the reference's re10k_small evaluation index through the full
+    model (synthetic frames and weights), one JSON summary."""
+    import json
+    import subprocess
+    import sys
+
+    repo = Path(__file__).resolve().parents[1]
+    out = subprocess.run([sys.executable, "-m", "transplat_amd.evaluate", "--index", str(INDEX)], cwd=repo,
+                         capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    summary = json.loads(out.stdout.strip().splitlines()[-1])
+    assert summary["scenes"] == 2 and summary["views"] == 6
+    assert summary["psnr"] == summary["psnr"]  # finite

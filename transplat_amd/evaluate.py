@@ -90,3 +90,58 @@ def summarize(results: list[SceneResult]) -> dict:
         "views": sum(r.n_views for r in results),
         "seconds": sum(r.seconds for r in results),
     }
+
+
+def index_batch(idx: int, key: str, entry: dict, image_shape=(256, 256), device="cpu") -> dict:
+    """Synthetic stand-in for the re10k chunk reader: the index entry's frame numbers place the
+    targets along the context baseline (t = (frame - ctx0) / (ctx1 - ctx0)), the scene index
+    seeds the images. Real frames replace this once the dataset is available."""
+    from . import synthetic as S
+
+    c0, c1 = entry["context"][0], entry["context"][-1]
+    span = max(c1 - c0, 1)
+    ts = [(t - c0) / span for t in entry["target"]]
+    return S.make_batch(1, num_context=len(entry["context"]), num_target=len(ts), image_shape=image_shape,
+                        scene_offset=idx, device=device, target_ts=ts)
+
+
+def main(argv=None):
+    """`python -m transplat_amd.evaluate --index <evaluation_index.json>` (one process per GPU under
+    torch.distributed.run; RCCL for the final gather). Prints one JSON summary on rank 0."""
+    import argparse
+    import os
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--index", required=True)
+    ap.add_argument("--checkpoint", default=None, help="reference Lightning checkpoint (loaded weights_only)")
+    ap.add_argument("--dense-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--limit", type=int, default=None, help="first N scenes of the index")
+    args = ap.parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    device = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(device)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+    from .e2e import build_model
+
+    model = build_model(device, args.dense_dtype)
+    if args.checkpoint:
+        model.load_checkpoint(args.checkpoint)
+    scenes = load_index(args.index)[: args.limit]
+    step = lambda batch: model.test_step(batch).color
+    results = evaluate(step, [(k, v) for k, v in scenes],
+                       lambda i, kv: index_batch(i, kv[0], kv[1], device=device), device, rank, world)
+    if rank == 0:
+        summary = summarize(results)
+        summary.update({"index": str(args.index), "world": world, "weights": args.checkpoint or "synthetic",
+                        "data": "synthetic frames at the index's frame positions"})
+        print(json.dumps(summary), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

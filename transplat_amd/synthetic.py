@@ -59,8 +59,10 @@ def make_batch(
     device="cpu",
     near: float = 1.0,
     far: float = 100.0,
+    target_ts=None,
 ) -> dict:
-    """A `BatchedExample`-like dict with 'context' and 'target' views for `batch` scenes."""
+    """A `BatchedExample`-like dict with 'context' and 'target' views for `batch` scenes.
+    `target_ts` places the targets along the context baseline (default evenly spaced)."""
     h, w = image_shape
     ctx_imgs, tgt_imgs = [], []
     for i in range(batch):
@@ -68,7 +70,7 @@ def make_batch(
         ctx_imgs.append(torch.rand((num_context, 3, h, w), generator=gen))
         tgt_imgs.append(torch.rand((num_target, 3, h, w), generator=gen))
     ctx_ext = context_extrinsics(num_context)
-    ts = tuple((k + 1) / (num_target + 1) for k in range(num_target))
+    ts = tuple(target_ts) if target_ts is not None else tuple((k + 1) / (num_target + 1) for k in range(num_target))
     tgt_ext = target_extrinsics(ctx_ext, ts)
 
     def views(imgs, ext, n):
