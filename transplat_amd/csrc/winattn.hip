@@ -818,31 +818,63 @@ win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __res
         for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
     float m_run = -INFINITY, l_run = 0.f;
 
-    const int grow = tid & 63, gpart = tid >> 6;  // key row, 32-channel quarter (64 B)
+    // gather: thread = (key row grow, 32-channel quarter gpart). The next tile's rows are loaded
+    // into registers right after this tile's barrier and written to LDS after the end-of-tile
+    // barrier (issue early / write late). V is transposed in the write: lanes 2r and 2r + 1 (keys
+    // 2r, 2r + 1) swap half their channels so each writes 32-bit (key pair) words.
+    const int grow = tid & 63, gpart = tid >> 6;
     const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
-    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
-        {
-            const int j = k0 + grow;
-            const int tk = j / p.m, vi = j - tk * p.m;
-            const int kpix = win_pixel(p, wi, tk);
-            const bf16x8* ksrc = reinterpret_cast<const bf16x8*>(kb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
-            const bf16x8* vsrc = reinterpret_cast<const bf16x8*>(vb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
-            bf16x8 kv[4], vv[4];
+    bf16x8 kv[4], vv[4];
+    int kreg = 0;
+    auto gather = [&](int k0) {
+        const int j = k0 + grow;
+        const int tk = j / p.m, vi = j - tk * p.m;
+        const int kpix = win_pixel(p, wi, tk);
+        const bf16x8* ksrc = reinterpret_cast<const bf16x8*>(kb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
+        const bf16x8* vsrc = reinterpret_cast<const bf16x8*>(vb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                kv[i] = ksrc[i];
-                vv[i] = vsrc[i];
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int chunk = 4 * gpart + i;  // 16-B chunk (8 channels) of the 256-B row
-                *reinterpret_cast<bf16x8*>(&sK[grow * kC + ((chunk ^ (grow & 15)) * 8)]) = kv[i];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) sVt[(8 * chunk + e) * kVtStrideH + grow] = vv[i][e];
-            }
-            if (gpart == 0 && p.shift) sKeyRegion[grow] = win_region(p, wi, j % p.L);
+        for (int i = 0; i < 4; ++i) {
+            kv[i] = ksrc[i];
+            vv[i] = vsrc[i];
         }
+        kreg = p.shift ? win_region(p, wi, j % p.L) : 0;
+    };
+    auto stage = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int chunk = 4 * gpart + i;  // 16-B chunk (8 channels) of the 256-B row
+            *reinterpret_cast<bf16x8*>(&sK[grow * kC + ((chunk ^ (grow & 15)) * 8)]) = kv[i];
+        }
+        // V^T: lane pair (even key e, odd key e + 1); even lane writes channels 0..15 of the
+        // quarter, odd lane 16..31, each as (V[e][d], V[e+1][d]) words
+        const bool odd = grow & 1;
+        const int key0 = grow & ~1;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            // give away the half the partner writes, receive the partner's half of mine
+            const bf16x8 mine = odd ? vv[2 + i] : vv[i];
+            const bf16x8 give = odd ? vv[i] : vv[2 + i];
+            typedef int intx4 __attribute__((ext_vector_type(4)));
+            const intx4 gi = __builtin_bit_cast(intx4, give);
+            intx4 ri;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) ri[w] = __shfl_xor(gi[w], 1);
+            const bf16x8 other = __builtin_bit_cast(bf16x8, ri);
+            const int c0 = 32 * gpart + 16 * (odd ? 1 : 0) + 8 * i;  // first channel of this 8-run
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+                const bf16x2 pr = odd ? bf16x2{other[e], mine[e]} : bf16x2{mine[e], other[e]};
+                *reinterpret_cast<bf16x2*>(&sVt[(c0 + e) * kVtStrideH + key0]) = pr;
+            }
+        }
+        if (gpart == 0 && p.shift) sKeyRegion[grow] = kreg;
+    };
+    gather(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
+        stage();
         __syncthreads();
+        if (k0 + kBK < kend) gather(k0 + kBK);
 
         // ---- S^T = K Q^T (two 32-key subtiles, interleaved chains), scaled in fp32
         floatx16 s[2];
