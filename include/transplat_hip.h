@@ -157,15 +157,17 @@ int tsplat_msda_fwd(const float* value, const float* loc, const float* weights, 
 int tsplat_sh_rotation_fwd(const float* rotations, const double* basis, float* out, int32_t num_cameras,
                            int32_t d_sh, void* stream);
 
-/* GroupNorm over NCHW fp32 with the following activation and residual add fused:
- * y = act(group_norm(x) * gamma + beta) [+ residual], act 0 none, 1 SiLU, 2 GELU (erf).
+/* GroupNorm over NCHW fp32 with the producing convolution's bias, the following activation and
+ * the residual add fused: y = act(group_norm(x + pre_bias[c]) * gamma + beta) [+ residual],
+ * act 0 none, 1 SiLU, 2 GELU (erf); pre_bias and residual may be NULL.
  * Replaces the U-Net / refine-head chains GroupNorm32 -> SiLU (-> + skip) and GroupNorm -> GELU
  * (reference src/model/encoder/matching/ldm_unet/unet.py:177-370, util.py:189-208,
  * depth_predictor_trans.py:142-206; torch.nn.functional.group_norm semantics: biased variance,
  * rsqrt(var + eps)). workspace: tsplat_group_norm_workspace_bytes(n, c, hw, groups) bytes.
  * residual may be NULL; x, residual and y are [n, c, hw] contiguous, y may not alias x. */
 size_t tsplat_group_norm_workspace_bytes(int32_t n, int32_t c, int64_t hw, int32_t groups);
-int tsplat_group_norm_fwd(const float* x, const float* gamma, const float* beta, const float* residual,
+int tsplat_group_norm_fwd(const float* x, const float* pre_bias, const float* gamma, const float* beta,
+                          const float* residual,
                           float* y, void* workspace, int32_t n, int32_t c, int64_t hw, int32_t groups,
                           float eps, int32_t act, void* stream);
 

@@ -236,11 +236,14 @@ def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape
     return flat(means), flat(cov), flat(harm), flat(opac)
 
 
-def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None):
+def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None, pre_bias=None):
     """torch.nn.GroupNorm followed by the module chain's activation and residual add (reference
     ldm_unet/unet.py:177-300 ResBlock: skip + SiLU(GN(conv)); :306-370 AttentionBlock:
     x + GN(proj); depth_predictor_trans.py:142-206: GN -> GELU)."""
-    y = torch.nn.functional.group_norm(x.float(), num_groups, weight, bias, eps)
+    x = x.float()
+    if pre_bias is not None:  # the producing convolution's bias (reference: conv2d with bias)
+        x = x + pre_bias.float().view(1, -1, *([1] * (x.dim() - 2)))
+    y = torch.nn.functional.group_norm(x, num_groups, weight, bias, eps)
     if act == "silu":
         y = torch.nn.functional.silu(y)
     elif act == "gelu":

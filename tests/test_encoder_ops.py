@@ -172,20 +172,23 @@ def test_gaussian_adapter_kernel(device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape,groups,act,res", [
-    ((2, 128, 64, 64), 8, "silu", False), ((2, 32, 256, 256), 8, "silu", True), ((2, 128, 16, 16), 8, "none", True),
-    ((2, 32, 64, 64), 4, "gelu", False), ((3, 12, 5, 7), 4, "silu", True),  # odd HW: scalar path
-    ((2, 128, 4096), 8, "none", False)])
-def test_group_norm_kernel(device, shape, groups, act, res):
+@pytest.mark.parametrize("shape,groups,act,res,pb", [
+    ((2, 128, 64, 64), 8, "silu", False, False), ((2, 32, 256, 256), 8, "silu", True, True),
+    ((2, 128, 16, 16), 8, "none", True, False), ((2, 32, 64, 64), 4, "gelu", False, True),
+    ((3, 12, 5, 7), 4, "silu", True, True),  # odd HW: scalar path
+    ((2, 128, 4096), 8, "none", False, True)])
+def test_group_norm_kernel(device, shape, groups, act, res, pb):
+    """GroupNorm (+ folded conv bias, + SiLU/GELU, + residual) vs torch on CPU."""
     from transplat_amd import kernels as K
 
     x = seeded(shape, 71) * 3 + 1.5  # non-zero mean: the Welford path matters
     w = seeded((shape[1],), 72) * 0.5 + 1
     b = seeded((shape[1],), 73) * 0.2
     r = seeded(shape, 74) if res else None
-    ref = E.group_norm(x, groups, w, b, 1e-5, act, r)
+    bias = seeded((shape[1],), 75) if pb else None
+    ref = E.group_norm(x, groups, w, b, 1e-5, act, r, bias)
     out = K.group_norm(x.to(device), groups, w.to(device), b.to(device), 1e-5, act,
-                       r.to(device) if res else None).cpu()
+                       r.to(device) if res else None, bias.to(device) if pb else None).cpu()
     assert (out - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
 
 

@@ -48,28 +48,34 @@ __device__ __forceinline__ Welford wave_reduce(Welford w) {
 }
 
 // Welford over this workgroup's chunk -> partials[seg * S + chunk] = (mean, M2)
+// pb (may be null): per-channel bias of the producing convolution, added on the fly (the conv
+// runs without its bias, so PyTorch's separate broadcast add disappears)
 template <bool VEC>
 __global__ void __launch_bounds__(kThreads)
-stats_kernel(const float* __restrict__ x, float2* __restrict__ partials, int64_t L, int S) {
+stats_kernel(const float* __restrict__ x, const float* __restrict__ pb, float2* __restrict__ partials,
+             int64_t L, int S, int HW, int cpg, int G) {
     const int chunk = blockIdx.x, seg = blockIdx.y, tid = threadIdx.x;
     const int64_t start = (int64_t)chunk * kChunk;
     const int n_local = (int)min((int64_t)kChunk, L - start);
     const float* p = x + (int64_t)seg * L + start;
+    const int c0 = (seg % G) * cpg;
     Welford w{0.f, 0.f, 0.f};
     if (VEC) {
 #pragma unroll
         for (int k = 0; k < kChunk / (4 * kThreads); ++k) {
             const int i = (k * kThreads + tid) * 4;
             if (i < n_local) {
+                const float b = pb ? pb[c0 + (int)((start + i) / HW)] : 0.f;
                 const float4 v = *reinterpret_cast<const float4*>(p + i);
-                w = push(w, v.x);
-                w = push(w, v.y);
-                w = push(w, v.z);
-                w = push(w, v.w);
+                w = push(w, v.x + b);
+                w = push(w, v.y + b);
+                w = push(w, v.z + b);
+                w = push(w, v.w + b);
             }
         }
     } else {
-        for (int i = tid; i < n_local; i += kThreads) w = push(w, p[i]);
+        for (int i = tid; i < n_local; i += kThreads)
+            w = push(w, p[i] + (pb ? pb[c0 + (int)((start + i) / HW)] : 0.f));
     }
     w = wave_reduce(w);
     __shared__ Welford sw[kThreads / kWave];
@@ -92,7 +98,7 @@ __device__ __forceinline__ float activate(float v) {
 
 template <bool VEC, int ACT, bool RES>
 __global__ void __launch_bounds__(kThreads)
-apply_kernel(const float* __restrict__ x, const float2* __restrict__ partials,
+apply_kernel(const float* __restrict__ x, const float* __restrict__ pb, const float2* __restrict__ partials,
              const float* __restrict__ gamma, const float* __restrict__ beta,
              const float* __restrict__ res, float* __restrict__ y, int64_t L, int S, int HW, int C,
              int cpg, int G, float eps) {
@@ -126,7 +132,12 @@ apply_kernel(const float* __restrict__ x, const float2* __restrict__ partials,
                 const int c = g * cpg + (int)((start + i) / HW);  // HW % 4 == 0: one channel per float4
                 const float sc = rstd * gamma[c];
                 const float sh = beta[c] - sc * mean;
+                const float b = pb ? pb[c] : 0.f;
                 float4 v = *reinterpret_cast<const float4*>(x + base + i);
+                v.x += b;
+                v.y += b;
+                v.z += b;
+                v.w += b;
                 v.x = activate<ACT>(v.x * sc + sh);
                 v.y = activate<ACT>(v.y * sc + sh);
                 v.z = activate<ACT>(v.z * sc + sh);
@@ -145,7 +156,7 @@ apply_kernel(const float* __restrict__ x, const float2* __restrict__ partials,
         for (int i = tid; i < n_local; i += kThreads) {
             const int c = g * cpg + (int)((start + i) / HW);
             const float sc = rstd * gamma[c];
-            float v = activate<ACT>(x[base + i] * sc + (beta[c] - sc * mean));
+            float v = activate<ACT>((x[base + i] + (pb ? pb[c] : 0.f)) * sc + (beta[c] - sc * mean));
             if (RES) v += res[base + i];
             y[base + i] = v;
         }
@@ -164,7 +175,7 @@ extern "C" size_t tsplat_group_norm_workspace_bytes(int32_t n, int32_t c, int64_
     return (size_t)n * groups * S * sizeof(float2);
 }
 
-extern "C" int tsplat_group_norm_fwd(const float* x, const float* gamma, const float* beta,
+extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, const float* gamma, const float* beta,
                                      const float* residual, float* y, void* workspace, int32_t n,
                                      int32_t c, int64_t hw, int32_t groups, float eps, int32_t act,
                                      void* stream_) {
@@ -184,12 +195,14 @@ extern "C" int tsplat_group_norm_fwd(const float* x, const float* gamma, const f
     float2* part = (float2*)workspace;
     TSPLAT_PROF_BEGIN(prof::kGroupNorm, stream);
     if (vec)
-        hipLaunchKernelGGL(stats_kernel<true>, grid, dim3(kThreads), 0, stream, x, part, L, (int)S);
+        hipLaunchKernelGGL(stats_kernel<true>, grid, dim3(kThreads), 0, stream, x, pre_bias, part, L, (int)S,
+                           (int)hw, cpg, groups);
     else
-        hipLaunchKernelGGL(stats_kernel<false>, grid, dim3(kThreads), 0, stream, x, part, L, (int)S);
+        hipLaunchKernelGGL(stats_kernel<false>, grid, dim3(kThreads), 0, stream, x, pre_bias, part, L, (int)S,
+                           (int)hw, cpg, groups);
     TSPLAT_CHECK_LAUNCH();
 #define TSPLAT_GN_APPLY(V, A, R)                                                                   \
-    hipLaunchKernelGGL((apply_kernel<V, A, R>), grid, dim3(kThreads), 0, stream, x, part, gamma,  \
+    hipLaunchKernelGGL((apply_kernel<V, A, R>), grid, dim3(kThreads), 0, stream, x, pre_bias, part, gamma,  \
                        beta, residual, y, L, (int)S, (int)hw, c, cpg, groups, eps)
 #define TSPLAT_GN_ACT(V, R)              \
     switch (act) {                       \

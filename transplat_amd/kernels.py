@@ -137,8 +137,9 @@ def adapter_cameras(extrinsics: torch.Tensor, intrinsics: torch.Tensor, image_sh
 _ACTS = {"none": 0, "silu": 1, "gelu": 2}
 
 
-def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None):
-    """act(GroupNorm(x)) [+ residual] over [N, C, *spatial] fp32 (see tsplat_group_norm_fwd)."""
+def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None, pre_bias=None):
+    """act(GroupNorm(x + pre_bias)) [+ residual] over [N, C, *spatial] fp32 (see
+    tsplat_group_norm_fwd); pre_bias is the bias of a convolution that ran without it."""
     lib = _lib.load()
     n, c = x.shape[:2]
     hw = x[0, 0].numel()
@@ -149,7 +150,8 @@ def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", 
     y = torch.empty_like(xf)
     ws = torch.empty(int(lib.tsplat_group_norm_workspace_bytes(n, c, hw, num_groups)), dtype=torch.uint8,
                      device=x.device)
-    rc = lib.tsplat_group_norm_fwd(_lib.ptr(xf), _lib.ptr(_f32(weight)), _lib.ptr(_f32(bias)),
+    pb = _f32(pre_bias) if pre_bias is not None else None
+    rc = lib.tsplat_group_norm_fwd(_lib.ptr(xf), _lib.ptr(pb), _lib.ptr(_f32(weight)), _lib.ptr(_f32(bias)),
                                    _lib.ptr(res) if res is not None else None, _lib.ptr(y), _lib.ptr(ws), n, c, hw,
                                    num_groups, float(eps), _ACTS[act], _lib.stream_ptr(x.device))
     _lib.check(rc, "tsplat_group_norm_fwd")

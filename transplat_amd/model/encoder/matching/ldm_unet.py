@@ -23,11 +23,25 @@ from .... import kernels
 _ACT_OF = {nn.SiLU: "silu", nn.GELU: "gelu"}
 
 
-def gn_act(norm: nn.GroupNorm, x, act: str = "none", residual=None):
-    """act(norm(x)) [+ residual] in one fused kernel, computed in fp32 and returned in x's dtype
-    (GroupNorm32 semantics: the reference normalises in float and casts back)."""
-    y = kernels.group_norm(x, norm.num_groups, norm.weight, norm.bias, norm.eps, act, residual)
+def gn_act(norm: nn.GroupNorm, x, act: str = "none", residual=None, pre_bias=None):
+    """act(norm(x + pre_bias)) [+ residual] in one fused kernel, computed in fp32 and returned in
+    x's dtype (GroupNorm32 semantics: the reference normalises in float and casts back)."""
+    y = kernels.group_norm(x, norm.num_groups, norm.weight, norm.bias, norm.eps, act, residual, pre_bias)
     return y.type(x.dtype)
+
+
+def conv_nobias(conv: nn.Module, x):
+    """The convolution without its bias (the following fused GroupNorm adds it)."""
+    if isinstance(conv, nn.Conv2d):
+        return F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+    return F.conv1d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+def conv_gn_act(conv: nn.Module, norm: nn.GroupNorm, x, act: str = "none", residual=None):
+    """conv -> GroupNorm -> act (-> + residual) with the conv bias folded into the norm kernel."""
+    if conv.bias is None:
+        return gn_act(norm, conv(x), act, residual)
+    return gn_act(norm, conv_nobias(conv, x), act, residual, pre_bias=conv.bias)
 
 
 def run_sequential(seq: nn.Sequential, x):
@@ -36,6 +50,14 @@ def run_sequential(seq: nn.Sequential, x):
     i = 0
     while i < len(mods):
         m = mods[i]
+        if isinstance(m, (nn.Conv1d, nn.Conv2d)) and i + 1 < len(mods) and isinstance(mods[i + 1], nn.GroupNorm):
+            nxt = mods[i + 2] if i + 2 < len(mods) else None
+            act = _ACT_OF.get(type(nxt)) if nxt is not None else None
+            if isinstance(nxt, nn.GELU) and nxt.approximate != "none":
+                act = None
+            x = conv_gn_act(m, mods[i + 1], x, act or "none")
+            i += 3 if act else 2
+            continue
         if isinstance(m, nn.GroupNorm):
             nxt = mods[i + 1] if i + 1 < len(mods) else None
             act = _ACT_OF.get(type(nxt)) if nxt is not None else None
@@ -78,8 +100,8 @@ class ResBlock(nn.Module):
 
     def forward(self, x):
         # skip + SiLU(GN(conv(SiLU(GN(conv(x)))))): both GN + SiLU pairs and the residual fused
-        h = gn_act(self.in_layers[1], self.in_layers[0](x), "silu")
-        return gn_act(self.out_layers[1], self.out_layers[0](h), "silu", residual=self.skip_connection(x))
+        h = conv_gn_act(self.in_layers[0], self.in_layers[1], x, "silu")
+        return conv_gn_act(self.out_layers[0], self.out_layers[1], h, "silu", residual=self.skip_connection(x))
 
 
 class QKVAttentionLegacy(nn.Module):
@@ -123,8 +145,8 @@ class AttentionBlock(nn.Module):
     def forward(self, x):
         b, c, *spatial = x.shape
         x = x.reshape(b, c, -1)
-        h = self.proj_out(self.attention(self.qkv(x)))
-        return gn_act(self.norm, h, residual=x).reshape(b, c, *spatial)
+        h = self.attention(self.qkv(x))
+        return conv_gn_act(self.proj_out, self.norm, h, residual=x).reshape(b, c, *spatial)
 
 
 class Downsample(nn.Module):
