@@ -58,6 +58,18 @@ __device__ __forceinline__ size_t pidx(const Params& p, int b, int wi, int ks, i
     return (((size_t)b * p.splits * p.splits + wi) * p.ksplit + ks) * p.L + t;
 }
 
+// Logical (x, y, z) of this workgroup after the bijective XCD remap of its linear id: the
+// dispatcher deals consecutive ids round-robin over the 8 XCDs, so without the remap the query
+// blocks of one window (which all read the same K/V) would land on 8 different L2s.
+__device__ __forceinline__ void xcd_block_coords(int& x, int& y, int& z) {
+    const int X = gridDim.x, Y = gridDim.y;
+    const int n = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+    const int m = xcd_remap(n, X * Y * gridDim.z);
+    x = m % X;
+    y = (m / X) % Y;
+    z = m / (X * Y);
+}
+
 // original pixel of in-window position t of window wi after the roll by -shift
 __device__ __forceinline__ int win_pixel(const Params& p, int wi, int t) {
     const int wh = p.H / p.splits, ww = p.W / p.splits;
@@ -365,8 +377,9 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
     __shared__ __attribute__((aligned(16))) float sVt[kC * kVtStride];
     __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
 
-    const int qblk = blockIdx.x, wi = blockIdx.y;
-    const int b = blockIdx.z / p.ksplit, ks = blockIdx.z - b * p.ksplit;
+    int qblk, wi, bz;
+    xcd_block_coords(qblk, wi, bz);
+    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int c = lane & 31, h = lane >> 5;
     const size_t HW = (size_t)p.H * p.W;
@@ -560,8 +573,9 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
     __shared__ __attribute__((aligned(16))) float sVt[kC * kVtStride];
     __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
 
-    const int qblk = blockIdx.x, wi = blockIdx.y;  // qblk: 64-query block
-    const int b = blockIdx.z / p.ksplit, ks = blockIdx.z - b * p.ksplit;
+    int qblk, wi, bz;  // qblk: 64-query block
+    xcd_block_coords(qblk, wi, bz);
+    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int qg = wid >> 1, kh = wid & 1;
     const int c = lane & 31, h = lane >> 5;
@@ -793,8 +807,9 @@ win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __res
     __shared__ __attribute__((aligned(16))) __bf16 sVt[kC * kVtStrideH];
     __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
 
-    const int qblk = blockIdx.x, wi = blockIdx.y;
-    const int b = blockIdx.z / p.ksplit, ks = blockIdx.z - b * p.ksplit;
+    int qblk, wi, bz;
+    xcd_block_coords(qblk, wi, bz);
+    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int c = lane & 31, h = lane >> 5;
     const size_t HW = (size_t)p.H * p.W;
