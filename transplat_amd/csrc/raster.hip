@@ -402,6 +402,86 @@ __device__ __forceinline__ void bitonic_sort(Ptr buf, int n) {
     }
 }
 
+// Register-resident bitonic sort of the n <= kSortCap keys in `buf` (LDS), ascending. Thread t
+// holds positions t*E .. t*E + E - 1 (E = P / 256 for P = next_pow2(n) >= 256; positions >= n
+// are +inf). The network is unrolled at compile time (template over log2 P), so every register
+// index is static: stages whose partner distance j is below E run in registers, j < 64 E
+// exchange with the partner lane by shuffles, and only j >= 64 E (at most 3 stages for 4096
+// keys) go through LDS with barriers -- instead of one barrier-separated LDS pass per stage.
+template <int E>
+__device__ __forceinline__ void cas_step(uint64_t (&v)[E], int t, int k, int j, uint64_t* buf) {
+    if (j < E) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int f = e ^ j;
+            if (f > e) {
+                const bool asc = (((t * E + e) & k) == 0);
+                const uint64_t a = v[e], b = v[f];
+                const bool sw = asc ? (a > b) : (a < b);
+                v[e] = sw ? b : a;
+                v[f] = sw ? a : b;
+            }
+        }
+    } else if (j < 64 * E) {
+        const int lane_xor = j / E;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = t * E + e;
+            const uint32_t lo = __shfl_xor((uint32_t)v[e], lane_xor);
+            const uint32_t hi = __shfl_xor((uint32_t)(v[e] >> 32), lane_xor);
+            const uint64_t other = ((uint64_t)hi << 32) | lo;
+            const bool take_min = ((i & j) == 0) == ((i & k) == 0);
+            const uint64_t mn = v[e] < other ? v[e] : other, mx = v[e] < other ? other : v[e];
+            v[e] = take_min ? mn : mx;
+        }
+    } else {
+        __syncthreads();  // previous readers of buf are done
+#pragma unroll
+        for (int e = 0; e < E; ++e) buf[t * E + e] = v[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const int i = t * E + e;
+            const uint64_t other = buf[i ^ j];
+            const bool take_min = ((i & j) == 0) == ((i & k) == 0);
+            const uint64_t mn = v[e] < other ? v[e] : other, mx = v[e] < other ? other : v[e];
+            v[e] = take_min ? mn : mx;
+        }
+    }
+}
+
+template <int LOGP>
+__device__ __forceinline__ void bitonic_sort_regs_p(uint64_t* buf, int n) {
+    constexpr int P = 1 << LOGP;
+    constexpr int E = P / kTileThreads;
+    const int t = threadIdx.x;
+    uint64_t v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = t * E + e;
+        v[e] = i < n ? buf[i] : ~0ull;
+    }
+#pragma unroll
+    for (int lk = 1; lk <= LOGP; ++lk)
+#pragma unroll
+        for (int lj = lk - 1; lj >= 0; --lj) cas_step<E>(v, t, 1 << lk, 1 << lj, buf);
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = t * E + e;
+        if (i < n) buf[i] = v[e];
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void bitonic_sort_regs(uint64_t* buf, int n) {
+    if (n <= 256) bitonic_sort_regs_p<8>(buf, n);
+    else if (n <= 512) bitonic_sort_regs_p<9>(buf, n);
+    else if (n <= 1024) bitonic_sort_regs_p<10>(buf, n);
+    else if (n <= 2048) bitonic_sort_regs_p<11>(buf, n);
+    else bitonic_sort_regs_p<12>(buf, n);
+}
+
 // --- K4: per-tile depth sort + front-to-back alpha blending ---------------------------------
 // One workgroup per (tile, view); each wave owns an 8x8 pixel block. Gaussians are staged in
 // batches of 256 in LDS; every wave then compacts, in depth order, the entries whose
@@ -432,7 +512,7 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     if (in_lds) {
         for (int i = threadIdx.x; i < n; i += kTileThreads) skeys[i] = gkeys[i];
         __syncthreads();
-        bitonic_sort(skeys, n);
+        bitonic_sort_regs(skeys, n);
     } else {
         bitonic_sort(gkeys, n);  // rare: very long tile list, sorted in place in global memory
     }
