@@ -50,13 +50,22 @@ def parse():
 
 
 def init_dist():
+    """One process per GPU (torch.distributed.run env). RCCL ("nccl") by default; the rehearsal
+    override TSPLAT_DIST_BACKEND=gloo (with LOCAL_RANK folded onto the visible GPUs) lets the N > 1
+    path run on a single-GPU box — the timing all-reduce is the only collective either way."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("TSPLAT_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -235,7 +244,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=device if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     from transplat_amd.model.decoder.hip_splatting import check_status
