@@ -483,19 +483,20 @@ __device__ __forceinline__ void bitonic_sort_regs(uint64_t* buf, int n) {
 }
 
 // --- K4: per-tile depth sort + front-to-back alpha blending ---------------------------------
-// One workgroup per (tile, view); each wave owns an 8x8 pixel block. Gaussians are staged in
-// batches of 256 in LDS; every wave then compacts, in depth order, the entries whose
-// alpha >= 1/255 ellipse can touch its block (conservative, so exact) and blends only those
-// with branch-free selects (no exec-mask flow per Gaussian), leaving as soon as all its 64
-// pixels are saturated.
+// One workgroup per (tile, view); the tile list is sorted in registers/LDS, then each wave owns
+// an 8x8 pixel block and walks the sorted list on its own in 64-entry chunks (no workgroup
+// barriers, so a wave never waits for a busier neighbour): the chunk's records are fetched one
+// chunk ahead, the entries whose alpha >= 1/255 box can touch the block are compacted in depth
+// order into the wave's LDS slot (conservative, so exact) and blended branch-free; the wave
+// leaves as soon as all its 64 pixels are saturated.
 __global__ void __launch_bounds__(kTileThreads)
 render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_color,
               Workspace ws) {
     __shared__ uint64_t skeys[kSortCap];
-    __shared__ float4 s_xy[kTileThreads];
-    __shared__ float4 s_co[kTileThreads];
-    __shared__ float4 s_rgb[kTileThreads];
-    __shared__ __attribute__((aligned(8))) uint16_t s_list[kTileThreads / kWave][kTileThreads];
+    // per-wave compacted records of the current 64-entry chunk (waves progress independently)
+    __shared__ float4 s_wxy[kTileThreads / kWave][kWave];
+    __shared__ float4 s_wco[kTileThreads / kWave][kWave];
+    __shared__ float4 s_wrgb[kTileThreads / kWave][kWave];
 
     const int v = blockIdx.y;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
@@ -516,6 +517,7 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     } else {
         bitonic_sort(gkeys, n);  // rare: very long tile list, sorted in place in global memory
     }
+    // no workgroup barrier below this point: each wave walks the sorted list on its own
 
     const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
     const int lx = (wid & 1) * 8 + (lane & 7), ly = (wid >> 1) * 8 + (lane >> 3);
@@ -529,12 +531,36 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
     const size_t vbase = (size_t)v * p.G;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
+    float4* w_xy = s_wxy[wid];
+    float4* w_co = s_wco[wid];
+    float4* w_rgb = s_wrgb[wid];
 
-    // this thread's record of the next batch, fetched from global memory one batch ahead so the
-    // gather latency hides behind the current batch's blending
+    // power = -0.5 (a dx^2 + c dy^2) - b dx dy, alpha = min(0.99, o e^power), T' = T (1 - alpha),
+    // C += rgb alpha T, written with explicit fmaf (same sequence in oracle/raster_ref.c)
+    auto blend = [&](const float4 xy, const float4 co, const float4 c) {
+        const float dx = xy.x - pfx, dy = xy.y - pfy;
+        const float quad = fmaf(co.x * dx, dx, (co.z * dy) * dy);
+        const float power = fmaf(-0.5f, quad, -((co.y * dx) * dy));
+        const float alpha = fminf(0.99f, co.w * exp_neg(power));
+        const float test_T = fmaf(-alpha, T, T);
+        // reference order: skip power > 0, skip alpha < 1/255, stop if test_T < 1e-4
+        const bool contrib = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const bool stop = contrib && (test_T < 0.0001f);
+        const bool acc = contrib && !stop;
+        const float w = alpha * T;
+        C0 = acc ? fmaf(c.x, w, C0) : C0;
+        C1 = acc ? fmaf(c.y, w, C1) : C1;
+        C2 = acc ? fmaf(c.z, w, C2) : C2;
+        T = acc ? test_T : T;
+        done = done || stop;
+    };
+
+    // this lane's record of the next 64-entry chunk, fetched one chunk ahead
     float4 r_xy = make_float4(0.f, 0.f, 0.f, 0.f), r_co = r_xy, r_rgb = r_xy;
+    bool r_valid = false;
     auto fetch = [&](int k) {
-        if (k < n) {
+        r_valid = k < n;
+        if (r_valid) {
             const uint64_t key = in_lds ? skeys[k] : gkeys[k];
             const size_t id = vbase + (uint32_t)(key & 0xffffffffu);
             r_xy = ws.xy[id];
@@ -542,71 +568,40 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
             r_rgb = ws.rgbd[id];
         }
     };
-    fetch(threadIdx.x);
-    for (int b0 = 0; b0 < n; b0 += kTileThreads) {
-        if (__syncthreads_count(done) == kTileThreads) break;
-        s_xy[threadIdx.x] = r_xy;
-        s_co[threadIdx.x] = r_co;
-        s_rgb[threadIdx.x] = r_rgb;
-        __syncthreads();
-        fetch(b0 + kTileThreads + threadIdx.x);
-        const int cnt = min(kTileThreads, n - b0);
-        // order-preserving compaction of this wave's candidates
-        int m = 0;
-#pragma unroll
-        for (int c = 0; c < kTileThreads / kWave; ++c) {
-            const int e = c * kWave + lane;
-            bool hit = false;
-            if (e < cnt) {
-                const float4 xy = s_xy[e];
-                hit = !(xy.x + xy.z < wx0 || xy.x - xy.z > wx1 || xy.y + xy.w < wy0 ||
-                        xy.y - xy.w > wy1);
-            }
-            const uint64_t mask = __ballot(hit);
-            if (hit) s_list[wid][m + __popcll(mask & lt_mask)] = (uint16_t)e;
-            m += __popcll(mask);
+    fetch(lane);
+    for (int c0 = 0; c0 < n; c0 += kWave) {
+        if (__all(done)) break;
+        const float4 xy = r_xy, co = r_co, rgb = r_rgb;
+        const bool valid = r_valid;
+        fetch(c0 + kWave + lane);
+        // order-preserving compaction of the chunk's entries whose alpha >= 1/255 box touches
+        // this wave's 8x8 block
+        const bool hit = valid && !(xy.x + xy.z < wx0 || xy.x - xy.z > wx1 || xy.y + xy.w < wy0 ||
+                                    xy.y - xy.w > wy1);
+        const uint64_t mask = __ballot(hit);
+        const int m = __popcll(mask);
+        if (hit) {
+            const int pos = __popcll(mask & lt_mask);
+            w_xy[pos] = xy;
+            w_co[pos] = co;
+            w_rgb[pos] = rgb;
         }
-        __syncthreads();
-        // blend in list order; 4 entries' LDS reads are issued together so the dependent
-        // index -> record loads overlap (the per-pixel operation sequence is unchanged)
-        // power = -0.5 (a dx^2 + c dy^2) - b dx dy, alpha = min(0.99, o e^power), T' = T (1 - alpha),
-        // C += rgb alpha T, written with explicit fmaf (same sequence in oracle/raster_ref.c)
-        auto blend = [&](const float4 xy, const float4 co, const float4 c) {
-            const float dx = xy.x - pfx, dy = xy.y - pfy;
-            const float quad = fmaf(co.x * dx, dx, (co.z * dy) * dy);
-            const float power = fmaf(-0.5f, quad, -((co.y * dx) * dy));
-            const float alpha = fminf(0.99f, co.w * exp_neg(power));
-            const float test_T = fmaf(-alpha, T, T);
-            // reference order: skip power > 0, skip alpha < 1/255, stop if test_T < 1e-4
-            const bool contrib = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-            const bool stop = contrib && (test_T < 0.0001f);
-            const bool acc = contrib && !stop;
-            const float w = alpha * T;
-            C0 = acc ? fmaf(c.x, w, C0) : C0;
-            C1 = acc ? fmaf(c.y, w, C1) : C1;
-            C2 = acc ? fmaf(c.z, w, C2) : C2;
-            T = acc ? test_T : T;
-            done = done || stop;
-        };
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         int i = 0;
         for (; i + 4 <= m; i += 4) {
-            if (__all(done)) break;
-            const uint2 ids = *reinterpret_cast<const uint2*>(&s_list[wid][i]);
-            const int e0 = ids.x & 0xffff, e1 = ids.x >> 16, e2 = ids.y & 0xffff, e3 = ids.y >> 16;
-            const float4 xy0 = s_xy[e0], co0 = s_co[e0], c0 = s_rgb[e0];
-            const float4 xy1 = s_xy[e1], co1 = s_co[e1], c1 = s_rgb[e1];
-            const float4 xy2 = s_xy[e2], co2 = s_co[e2], c2 = s_rgb[e2];
-            const float4 xy3 = s_xy[e3], co3 = s_co[e3], c3 = s_rgb[e3];
-            blend(xy0, co0, c0);
-            blend(xy1, co1, c1);
-            blend(xy2, co2, c2);
-            blend(xy3, co3, c3);
+            const float4 xy0 = w_xy[i], co0 = w_co[i], c0v = w_rgb[i];
+            const float4 xy1 = w_xy[i + 1], co1 = w_co[i + 1], c1v = w_rgb[i + 1];
+            const float4 xy2 = w_xy[i + 2], co2 = w_co[i + 2], c2v = w_rgb[i + 2];
+            const float4 xy3 = w_xy[i + 3], co3 = w_co[i + 3], c3v = w_rgb[i + 3];
+            blend(xy0, co0, c0v);
+            blend(xy1, co1, c1v);
+            blend(xy2, co2, c2v);
+            blend(xy3, co3, c3v);
         }
-        for (; i < m; ++i) {
-            if (__all(done)) break;
-            const int e = s_list[wid][i];
-            blend(s_xy[e], s_co[e], s_rgb[e]);
-        }
+        for (; i < m; ++i) blend(w_xy[i], w_co[i], w_rgb[i]);
+        __builtin_amdgcn_wave_barrier();  // reads of this chunk's records precede the next writes
     }
     if (inside) {
         const size_t hw = (size_t)p.H * p.W;
