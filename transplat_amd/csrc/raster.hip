@@ -482,6 +482,29 @@ __device__ __forceinline__ void bitonic_sort_regs(uint64_t* buf, int n) {
     else bitonic_sort_regs_p<12>(buf, n);
 }
 
+// Exact culling of one Gaussian against a pixel block: does the alpha >= 1/255 ellipse
+// {d : a dx^2 + 2 b dx dy + c dy^2 <= q}, q = 2 ln(255 o), meet the rectangle of pixel centres
+// [x0, x1] x [y0, y1]? The minimum of the (convex) quadratic over the rectangle is 0 when the
+// centre is inside, else it lies on an edge (1-D minimisation, clamped). Conservative margins
+// (relative 1e-3 on q plus 1e-3 absolute) keep every contributing Gaussian (the blend's float
+// arithmetic differs from this by a few ulps), so images are unchanged; culls the corners the
+// axis-aligned box test keeps for rotated / elongated splats.
+__device__ __forceinline__ bool ellipse_meets_block(float mx, float my, float4 co, float x0, float x1,
+                                                    float y0, float y1) {
+    const float a = co.x, b = co.y, c = co.z;
+    const float q = 2.0f * __logf(255.0f * co.w) * 1.001f + 1e-3f;
+    const float X0 = x0 - mx, X1 = x1 - mx, Y0 = y0 - my, Y1 = y1 - my;
+    if (X0 <= 0.f && X1 >= 0.f && Y0 <= 0.f && Y1 >= 0.f) return true;
+    if (!(a > 0.f && c > 0.f)) return true;  // degenerate: keep (the box test decided)
+    auto Qf = [&](float dx, float dy) { return a * dx * dx + 2.0f * b * dx * dy + c * dy * dy; };
+    const float ia = 1.0f / a, ic = 1.0f / c;
+    const float qx0 = Qf(X0, fminf(fmaxf(-b * X0 * ic, Y0), Y1));
+    const float qx1 = Qf(X1, fminf(fmaxf(-b * X1 * ic, Y0), Y1));
+    const float qy0 = Qf(fminf(fmaxf(-b * Y0 * ia, X0), X1), Y0);
+    const float qy1 = Qf(fminf(fmaxf(-b * Y1 * ia, X0), X1), Y1);
+    return fminf(fminf(qx0, qx1), fminf(qy0, qy1)) <= q;
+}
+
 // --- K4: per-tile depth sort + front-to-back alpha blending ---------------------------------
 // One workgroup per (tile, view); the tile list is sorted in registers/LDS, then each wave owns
 // an 8x8 pixel block and walks the sorted list on its own in 64-entry chunks (no workgroup
@@ -576,8 +599,9 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
         fetch(c0 + kWave + lane);
         // order-preserving compaction of the chunk's entries whose alpha >= 1/255 box touches
         // this wave's 8x8 block
-        const bool hit = valid && !(xy.x + xy.z < wx0 || xy.x - xy.z > wx1 || xy.y + xy.w < wy0 ||
-                                    xy.y - xy.w > wy1);
+        bool hit = valid && !(xy.x + xy.z < wx0 || xy.x - xy.z > wx1 || xy.y + xy.w < wy0 ||
+                              xy.y - xy.w > wy1);
+        if (hit) hit = ellipse_meets_block(xy.x, xy.y, co, wx0, wx1, wy0, wy1);
         const uint64_t mask = __ballot(hit);
         const int m = __popcll(mask);
         if (hit) {
