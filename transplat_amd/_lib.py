@@ -12,7 +12,8 @@ from pathlib import Path
 
 import torch
 
-_LIB_PATH = Path(__file__).resolve().parent / "libtransplat_hip.so"
+# TSPLAT_LIB (benchmarking only) points at an alternative build of the same library
+_LIB_PATH = Path(os.environ.get("TSPLAT_LIB") or Path(__file__).resolve().parent / "libtransplat_hip.so")
 _lib = None
 
 

@@ -31,6 +31,54 @@
 namespace tsplat {
 namespace winattn {
 
+// TSPLAT_WA_ABL (diagnostic builds only, never the shipped library): removes one phase of the
+// key-pair kernel's tile loop to attribute its time (results are wrong in such a build)
+#ifndef TSPLAT_WA_ABL
+#define TSPLAT_WA_ABL 0
+#endif
+constexpr int kAbl = TSPLAT_WA_ABL;
+
+// TSPLAT_WA_STAMP (diagnostic builds only): per-wave s_memtime sums of the key-pair kernel's loop
+// segments, read back with tsplat_diag_wa_stamps(); shares are meaningful, the build's time is not
+#ifndef TSPLAT_WA_STAMP
+#define TSPLAT_WA_STAMP 0
+#endif
+constexpr int kStampSegs = 10;
+constexpr int kStampWaves = 8192;
+#if TSPLAT_WA_STAMP
+__device__ unsigned long long g_wa_stamp[kStampWaves][kStampSegs];
+#define WA_STAMP(seg)                                                                        \
+    do {                                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+        unsigned long long _t;                                                               \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");           \
+        stamp_acc[seg] += _t - stamp_prev;                                                   \
+        stamp_prev = _t;                                                                     \
+        __builtin_amdgcn_sched_barrier(0);                                                   \
+    } while (0)
+#else
+#define WA_STAMP(seg) \
+    do {              \
+    } while (0)
+#endif
+
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kLn2 = 0.6931471805599453f;
+constexpr float kMaskLog2 = -100.0f * kLog2e;  // the reference's -100 mask, log2 domain
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// max / sum of lanes l and l ^ 32 (the two half-waves), in VALU via v_permlane32_swap instead of
+// an LDS-routed ds_bpermute: swap(x, x) returns (x[row 0], x[row 1]) in every lane
+__device__ __forceinline__ float halves_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halves_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 constexpr int kC = 128;          // channels (d_model of the reference transformer)
 constexpr int kBQ = 64;          // queries per workgroup
 constexpr int kBK = 64;          // keys per LDS tile
@@ -43,8 +91,15 @@ struct Params {
     int H, W, splits, shift, m, L;  // L = window pixels; shift != 0: shifted (masked) layer
     int shift_h, shift_w;           // roll of the shifted layer: half a window per axis
     int ksplit, keys_per_split;     // key range [s * keys_per_split, (s+1) * keys_per_split)
+    int wh, ww, ww_log2;            // window rows / columns; log2(ww), or -1 if not a power of 2
     float scale;
 };
+
+// t / ww and t % ww without a per-lane integer division when the window width is a power of 2
+__device__ __forceinline__ void win_split(const Params& p, int t, int& ty, int& tx) {
+    ty = p.ww_log2 >= 0 ? (t >> p.ww_log2) : t / p.ww;
+    tx = t - ty * p.ww;
+}
 
 // split-key partials of one workgroup (64 queries): O (unnormalised, [64][128]), m, l
 struct Partials {
@@ -72,11 +127,11 @@ __device__ __forceinline__ void xcd_block_coords(int& x, int& y, int& z) {
 
 // original pixel of in-window position t of window wi after the roll by -shift
 __device__ __forceinline__ int win_pixel(const Params& p, int wi, int t) {
-    const int wh = p.H / p.splits, ww = p.W / p.splits;
-    const int sy = wi / p.splits, sx = wi % p.splits;
-    const int ty = t / ww, tx = t - ty * ww;
-    int y = sy * wh + ty + p.shift_h;
-    int x = sx * ww + tx + p.shift_w;
+    const int sy = wi / p.splits, sx = wi - sy * p.splits;
+    int ty, tx;
+    win_split(p, t, ty, tx);
+    int y = sy * p.wh + ty + p.shift_h;
+    int x = sx * p.ww + tx + p.shift_w;
     if (y >= p.H) y -= p.H;
     if (x >= p.W) x -= p.W;
     return y * p.W + x;
@@ -84,13 +139,21 @@ __device__ __forceinline__ int win_pixel(const Params& p, int wi, int t) {
 
 // Swin region id of in-window position t of window wi (on the rolled grid)
 __device__ __forceinline__ int win_region(const Params& p, int wi, int t) {
-    const int wh = p.H / p.splits, ww = p.W / p.splits;
-    const int sy = wi / p.splits, sx = wi % p.splits;
-    const int ty = t / ww, tx = t - ty * ww;
-    const int Y = sy * wh + ty, X = sx * ww + tx;
-    const int by = Y < p.H - wh ? 0 : (Y < p.H - wh / 2 ? 1 : 2);
-    const int bx = X < p.W - ww ? 0 : (X < p.W - ww / 2 ? 1 : 2);
+    const int sy = wi / p.splits, sx = wi - sy * p.splits;
+    int ty, tx;
+    win_split(p, t, ty, tx);
+    const int Y = sy * p.wh + ty, X = sx * p.ww + tx;
+    const int by = Y < p.H - p.wh ? 0 : (Y < p.H - p.wh / 2 ? 1 : 2);
+    const int bx = X < p.W - p.ww ? 0 : (X < p.W - p.ww / 2 ? 1 : 2);
     return by * 3 + bx;
+}
+
+// key j of a window (pixel-major, view-minor over m key views): offset of its row in the
+// [m, H*W] key/value maps and its mask region (mask column j mod L, the reference's tiling)
+__device__ __forceinline__ void key_row(const Params& p, int wi, size_t HW, int j, size_t& off, int& region) {
+    const int tk = p.m == 1 ? j : j / p.m, vi = j - tk * p.m;
+    off = (size_t)vi * HW + win_pixel(p, wi, tk);
+    region = p.shift ? win_region(p, wi, p.m == 1 ? j : j % p.L) : 0;
 }
 
 // K / V rows of one 64-key tile held in registers between the global gather and the LDS store
@@ -208,7 +271,7 @@ win_attn_f32_kernel(Params p, const float* __restrict__ q, const float* __restri
                 bmax = fmaxf(bmax, x);
             }
         bmax = fmaxf(bmax, __shfl_xor(bmax, 16));
-        bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+        bmax = halves_max(bmax);
         const float m_new = fmaxf(m_run, bmax);
         const float corr = __expf(m_run - m_new);
         float bsum = 0.f;
@@ -221,7 +284,7 @@ win_attn_f32_kernel(Params p, const float* __restrict__ q, const float* __restri
                 bsum += e;
             }
         bsum += __shfl_xor(bsum, 16);
-        bsum += __shfl_xor(bsum, 32);
+        bsum = halves_sum(bsum);
         l_run = l_run * corr + bsum;
         m_run = m_new;
 #pragma unroll
@@ -493,7 +556,7 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
             for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[sub][r]);
-        bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+        bmax = halves_max(bmax);
         const float m_new = fmaxf(m_run, bmax);
         const float corr = __expf(m_run - m_new);
         float bsum = 0.f;
@@ -505,7 +568,7 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
                 s[sub][r] = e;
                 bsum += e;
             }
-        bsum += __shfl_xor(bsum, 32);
+        bsum = halves_sum(bsum);
         l_run = l_run * corr + bsum;
         m_run = m_new;
 #pragma unroll
@@ -573,6 +636,10 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
     __shared__ __attribute__((aligned(16))) float sVt[kC * kVtStride];
     __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
 
+#if TSPLAT_WA_STAMP
+    unsigned long long stamp_acc[kStampSegs] = {}, stamp_prev;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_prev)::"memory");
+#endif
     int qblk, wi, bz;  // qblk: 64-query block
     xcd_block_coords(qblk, wi, bz);
     const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
@@ -587,16 +654,19 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
     const int tq = qblk * 64 + qg * 32 + c;
     const int qpix = win_pixel(p, wi, tq);
     const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+    // scores are kept in the log2 domain (Q pre-scaled by log2(e) / sqrt(C), mask -100 log2(e)) so
+    // the softmax exponentials are bare v_exp_f32; m is converted back to natural log for partials
+    const float qscale = p.scale * kLog2e;
     float qr[64];
     {
         const float4* src = reinterpret_cast<const float4*>(qb + (size_t)qpix * kC + 64 * h);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const float4 t4 = src[i];
-            qr[4 * i] = t4.x * p.scale;
-            qr[4 * i + 1] = t4.y * p.scale;
-            qr[4 * i + 2] = t4.z * p.scale;
-            qr[4 * i + 3] = t4.w * p.scale;
+            qr[4 * i] = t4.x * qscale;
+            qr[4 * i + 1] = t4.y * qscale;
+            qr[4 * i + 2] = t4.z * qscale;
+            qr[4 * i + 3] = t4.w * qscale;
         }
     }
     floatx16 o[4];
@@ -608,25 +678,22 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
 
     // staging (T14 split): the next tile's K rows are loaded into registers during this tile's
     // QK^T and written to LDS after the barrier that retires K(t); the same registers then carry
-    // V(t+1) during PV(t). One 8 x float4 register set, three barriers per tile.
+    // V(t+1) during PV(t). One 8 x float4 register set, two barriers per tile: V(t+1) is stored
+    // after the second and first read after the next tile's first.
     const int grow = tid & 63, gpart = tid >> 6;
     const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
     const int row = 32 * kh + c;  // this lane's key row (A operand) within the tile
     float4 stg[8];
     int stg_region = 0;
-    auto row_src = [&](const float* base, int k0) {
-        const int j = k0 + grow;
-        const int tk = j / p.m, vi = j - tk * p.m;
-        return reinterpret_cast<const float4*>(base + ((size_t)vi * HW + win_pixel(p, wi, tk)) * kC + 32 * gpart);
-    };
+    size_t stg_off = 0;  // row offset of this thread's key in the tile being staged (K, then V)
     auto load_k = [&](int k0) {
-        const float4* src = row_src(kb, k0);
+        key_row(p, wi, HW, k0 + grow, stg_off, stg_region);
+        const float4* src = reinterpret_cast<const float4*>(kb + stg_off * kC + 32 * gpart);
 #pragma unroll
         for (int i = 0; i < 8; ++i) stg[i] = src[i];
-        stg_region = p.shift ? win_region(p, wi, (k0 + grow) % p.L) : 0;
     };
-    auto load_v = [&](int k0) {
-        const float4* src = row_src(vb, k0);
+    auto load_v = [&]() {
+        const float4* src = reinterpret_cast<const float4*>(vb + stg_off * kC + 32 * gpart);
 #pragma unroll
         for (int i = 0; i < 8; ++i) stg[i] = src[i];
     };
@@ -650,12 +717,13 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
     };
     load_k(kbeg);
     store_k();
-    load_v(kbeg);
+    load_v();
     store_v();
     __syncthreads();
+    WA_STAMP(0);  // prologue
     for (int k0 = kbeg; k0 < kend; k0 += kBK) {
         const bool has_next = k0 + kBK < kend;
-        if (has_next) load_k(k0 + kBK);
+        if (has_next && kAbl != 3) load_k(k0 + kBK);
 
         // ---- S^T for this wave's 32 keys (one chain: 32x32x2 issue interval = dependent latency;
         // the next K chunk is read before the current chunk's MFMAs)
@@ -670,6 +738,7 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
 #pragma unroll
             for (int i4 = 0; i4 < 16; ++i4) {
                 const float4 nk = i4 + 1 < 16 ? kread(i4 + 1) : ka;
+                if (kAbl == 6) { s[i4] += ka.x * qr[4 * i4]; ka = nk; continue; }
                 s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.x, qr[4 * i4 + 0], s, 0, 0, 0);
                 s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.y, qr[4 * i4 + 1], s, 0, 0, 0);
                 s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.z, qr[4 * i4 + 2], s, 0, 0, 0);
@@ -677,46 +746,57 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
                 ka = nk;
             }
         }
+        WA_STAMP(1);  // QK issue
         if (p.shift) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int4 rg = *reinterpret_cast<const int4*>(&sKeyRegion[32 * kh + 8 * u + 4 * h]);
-                s[4 * u + 0] += rg.x == qreg ? 0.0f : -100.0f;
-                s[4 * u + 1] += rg.y == qreg ? 0.0f : -100.0f;
-                s[4 * u + 2] += rg.z == qreg ? 0.0f : -100.0f;
-                s[4 * u + 3] += rg.w == qreg ? 0.0f : -100.0f;
+                s[4 * u + 0] += rg.x == qreg ? 0.0f : kMaskLog2;
+                s[4 * u + 1] += rg.y == qreg ? 0.0f : kMaskLog2;
+                s[4 * u + 2] += rg.z == qreg ? 0.0f : kMaskLog2;
+                s[4 * u + 3] += rg.w == qreg ? 0.0f : kMaskLog2;
             }
         }
-        float bmax = -INFINITY;
+        if (kAbl != 1) {
+            float bmax = -INFINITY;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[r]);
-        bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
-        const float m_new = fmaxf(m_run, bmax);
-        const float corr = __expf(m_run - m_new);
-        float bsum = 0.f;
+            for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[r]);
+            bmax = halves_max(bmax);
+            const float m_new = fmaxf(m_run, bmax);
+            // rescale only when some query's running max moved (corr is exactly 1 otherwise)
+            if (__any(m_new > m_run)) {
+                const float corr = fast_exp2(m_run - m_new);
+                l_run *= corr;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float e = __expf(s[r] - m_new);
-            s[r] = e;
-            bsum += e;
+                for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+                m_run = m_new;
+            }
+            float bsum = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = fast_exp2(s[r] - m_run);
+                s[r] = e;
+                bsum += e;
+            }
+            bsum = halves_sum(bsum);
+            l_run += bsum;
         }
-        bsum += __shfl_xor(bsum, 32);
-        l_run = l_run * corr + bsum;
-        m_run = m_new;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
 
-        __syncthreads();  // every wave is done with K(t) / regions(t)
+        WA_STAMP(2);  // mask + softmax (waits for the QK MFMAs)
+        if (kAbl != 2) __syncthreads();  // every wave is done with K(t) / regions(t)
+        WA_STAMP(3);  // barrier 1
         if (has_next) {
-            store_k();
-            load_v(k0 + kBK);
+            if (kAbl != 4) store_k();
+            if (kAbl != 3) load_v();
         }
+        WA_STAMP(4);  // store K(t+1) (waits for its loads), issue V(t+1) loads
 
         // ---- O^T += V^T P^T over this wave's 32 keys, the four d tiles' chains interleaved
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int dp = 0; dp < 4; dp += 2) {
+                if (kAbl == 5) break;
                 const float4 v0 = *reinterpret_cast<const float4*>(&sVt[(32 * dp + c) * kVtStride + 32 * kh + 8 * u + 4 * h]);
                 const float4 v1 = *reinterpret_cast<const float4*>(&sVt[(32 * dp + 32 + c) * kVtStride + 32 * kh + 8 * u + 4 * h]);
                 o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.x, s[4 * u + 0], o[dp], 0, 0, 0);
@@ -728,11 +808,12 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
                 o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.w, s[4 * u + 3], o[dp], 0, 0, 0);
                 o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.w, s[4 * u + 3], o[dp + 1], 0, 0, 0);
             }
-        __syncthreads();  // every wave is done with V(t)
-        if (has_next) {
-            store_v();
-            __syncthreads();
-        }
+        WA_STAMP(5);  // PV issue
+        if (kAbl != 2) __syncthreads();  // every wave is done with V(t); K(t+1) is visible
+        WA_STAMP(6);  // barrier 2 (waits for the PV MFMAs)
+        // V(t+1) becomes visible at the next tile's first barrier, before its PV reads
+        if (has_next && kAbl != 4) store_v();
+        WA_STAMP(7);  // store V(t+1)
     }
 
     // ---- merge the two key halves of each query group through LDS (sK / sVt are free now)
@@ -747,11 +828,19 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
         sml[64 + lane] = l_run;
     }
     __syncthreads();
+#if TSPLAT_WA_STAMP
+    WA_STAMP(8);  // merge
+    {
+        const int wave_id = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + wid;
+        if (lane == 0 && wave_id < kStampWaves)
+            for (int i = 0; i < kStampSegs; ++i) g_wa_stamp[wave_id][i] = stamp_acc[i];
+    }
+#endif
     if (kh == 1) return;
     {
         const float m1 = sml[lane], l1 = sml[64 + lane];
         const float M = fmaxf(m_run, m1);
-        const float a0 = __expf(m_run - M), a1 = __expf(m1 - M);
+        const float a0 = fast_exp2(m_run - M), a1 = fast_exp2(m1 - M);
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
@@ -780,7 +869,7 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
             for (int u = 0; u < 4; ++u)
                 dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
         if (h == 0) {
-            part.m[prow] = m_run;
+            part.m[prow] = m_run * kLn2;
             part.l[prow] = l_run;
         }
     }
@@ -932,7 +1021,7 @@ win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __res
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
             for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[sub][r]);
-        bmax = fmaxf(bmax, __shfl_xor(bmax, 32));
+        bmax = halves_max(bmax);
         const float m_new = fmaxf(m_run, bmax);
         const float corr = __expf(m_run - m_new);
         float bsum = 0.f;
@@ -944,7 +1033,7 @@ win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __res
                 s[sub][r] = e;
                 bsum += e;
             }
-        bsum += __shfl_xor(bsum, 32);
+        bsum = halves_sum(bsum);
         l_run = l_run * corr + bsum;
         m_run = m_new;
 #pragma unroll
@@ -1061,6 +1150,9 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     p.shift_h = with_shift ? (height / splits) / 2 : 0;
     p.shift_w = with_shift ? (width / splits) / 2 : 0;
     p.shift = with_shift ? 1 : 0;
+    p.wh = height / splits;
+    p.ww = width / splits;
+    p.ww_log2 = (p.ww & (p.ww - 1)) == 0 ? __builtin_ctz(p.ww) : -1;
     if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
     if (p.L % kBQ || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
@@ -1132,6 +1224,9 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     p.shift_h = with_shift ? (height / splits) / 2 : 0;
     p.shift_w = with_shift ? (width / splits) / 2 : 0;
     p.shift = with_shift ? 1 : 0;
+    p.wh = height / splits;
+    p.ww = width / splits;
+    p.ww_log2 = (p.ww & (p.ww - 1)) == 0 ? __builtin_ctz(p.ww) : -1;
     if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
     if (p.L % kBQ3 || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
@@ -1158,3 +1253,14 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
+
+#if TSPLAT_WA_STAMP
+extern "C" int tsplat_diag_wa_stamps(unsigned long long* host, int waves) {
+    using namespace tsplat::winattn;
+    if (waves > kStampWaves) waves = kStampWaves;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wa_stamp), sizeof(unsigned long long) * kStampSegs * waves, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess
+               ? waves
+               : -1;
+}
+#endif
