@@ -430,10 +430,10 @@ constexpr int kVtStride = kBK + 4;   // transposed V row (floats)
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-// PREFETCH: the next tile's K/V rows are loaded into registers while the current tile is computed
-// (needs the 512-VGPR budget of one wave per SIMD); otherwise two workgroups per CU overlap.
-template <bool PREFETCH>
-__global__ void __launch_bounds__(kThreads, PREFETCH ? 1 : 2)
+// Staging is the T14 split of the key-pair kernel below: K(t+1) is loaded into registers during
+// QK(t) and stored after the barrier that retires K(t); the same registers then carry V(t+1)
+// during PV(t). Two barriers per tile, two workgroups per CU.
+__global__ void __launch_bounds__(kThreads, 2)
 win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
                        const float* __restrict__ v, float* __restrict__ out, Partials part) {
     __shared__ __attribute__((aligned(16))) float sK[kBK * kC];
@@ -450,41 +450,59 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
     const float* kb = k + (size_t)b * p.m * HW * kC;
     const float* vb = v + (size_t)b * p.m * HW * kC;
 
-    // gather: thread = (key row tid & 63, 32-channel quarter tid >> 6)
+    // staging: thread = (key row tid & 63, 32-channel quarter tid >> 6)
     const int grow = tid & 63, gpart = tid >> 6;
     const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
-    float4 kv[8], vv[8];
-    int kreg = 0;
-    auto gather = [&](int k0) {  // global -> registers
-        const int j = k0 + grow;
-        const int tk = j / p.m, vi = j - tk * p.m;
-        const int kpix = win_pixel(p, wi, tk);
-        const float4* ksrc = reinterpret_cast<const float4*>(kb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
-        const float4* vsrc = reinterpret_cast<const float4*>(vb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
+    float4 stg[8];
+    int stg_region = 0;
+    size_t stg_off = 0;
+    auto load_k = [&](int k0) {
+        key_row(p, wi, HW, k0 + grow, stg_off, stg_region);
+        const float4* src = reinterpret_cast<const float4*>(kb + stg_off * kC + 32 * gpart);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stg[i] = src[i];
+    };
+    auto load_v = [&]() {
+        const float4* src = reinterpret_cast<const float4*>(vb + stg_off * kC + 32 * gpart);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stg[i] = src[i];
+    };
+    auto store_k = [&]() {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            kv[i] = ksrc[i];
-            vv[i] = vsrc[i];
+            const int chunk = 8 * gpart + i;
+            *reinterpret_cast<float4*>(&sK[grow * kC + ((chunk ^ (grow & 15)) * 4)]) = stg[i];
         }
-        kreg = p.shift ? win_region(p, wi, j % p.L) : 0;
+        if (gpart == 0 && p.shift) sKeyRegion[grow] = stg_region;
     };
-    if (PREFETCH) gather(kbeg);
+    auto store_v = [&]() {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int chunk = 8 * gpart + i;
+            sVt[(4 * chunk + 0) * kVtStride + grow] = stg[i].x;
+            sVt[(4 * chunk + 1) * kVtStride + grow] = stg[i].y;
+            sVt[(4 * chunk + 2) * kVtStride + grow] = stg[i].z;
+            sVt[(4 * chunk + 3) * kVtStride + grow] = stg[i].w;
+        }
+    };
 
     const int tq = qblk * kBQ3 + wid * kQW + c;
     const int qpix = win_pixel(p, wi, tq);
     const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+    // log2-domain scores (see the key-pair kernel)
+    const float qscale = p.scale * kLog2e;
     float qr[64];
-    {
+    auto load_q = [&]() {
         const float4* src = reinterpret_cast<const float4*>(qb + (size_t)qpix * kC + 64 * h);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const float4 t4 = src[i];
-            qr[4 * i] = t4.x * p.scale;
-            qr[4 * i + 1] = t4.y * p.scale;
-            qr[4 * i + 2] = t4.z * p.scale;
-            qr[4 * i + 3] = t4.w * p.scale;
+            qr[4 * i] = t4.x * qscale;
+            qr[4 * i + 1] = t4.y * qscale;
+            qr[4 * i + 2] = t4.z * qscale;
+            qr[4 * i + 3] = t4.w * qscale;
         }
-    }
+    };
     floatx16 o[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -492,49 +510,44 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
         for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
     float m_run = -INFINITY, l_run = 0.f;
 
-    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
-        if (!PREFETCH) gather(k0);
+    {
+        // prologue: tile 0's K and V rows are in flight together with Q (one exposed round trip)
+        load_k(kbeg);
+        float4 vrow[8];
+        const float4* vsrc = reinterpret_cast<const float4*>(vb + stg_off * kC + 32 * gpart);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int chunk = 8 * gpart + i;
-            *reinterpret_cast<float4*>(&sK[grow * kC + ((chunk ^ (grow & 15)) * 4)]) = kv[i];
-            sVt[(4 * chunk + 0) * kVtStride + grow] = vv[i].x;
-            sVt[(4 * chunk + 1) * kVtStride + grow] = vv[i].y;
-            sVt[(4 * chunk + 2) * kVtStride + grow] = vv[i].z;
-            sVt[(4 * chunk + 3) * kVtStride + grow] = vv[i].w;
-        }
-        if (gpart == 0 && p.shift) sKeyRegion[grow] = kreg;
-        __syncthreads();
-        if (PREFETCH && k0 + kBK < kend) gather(k0 + kBK);
+        for (int i = 0; i < 8; ++i) vrow[i] = vsrc[i];
+        load_q();
+        store_k();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) stg[i] = vrow[i];
+        store_v();
+    }
+    __syncthreads();
+    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
+        const bool has_next = k0 + kBK < kend;
+        if (has_next) load_k(k0 + kBK);
 
-        // ---- S^T = K Q^T, two 32-key subtiles as two interleaved accumulator chains; the next
-        // K chunk pair is read from LDS before the current chunk's 8 MFMAs
+        // ---- S^T = K Q^T, the two 32-key subtiles one after the other (a single 32x32x2 chain
+        // runs at rate); the next K chunk is read from LDS before the current chunk's MFMAs
         floatx16 s[2];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) s[0][r] = s[1][r] = 0.f;
-        {
-            auto kread = [&](int sub, int i4) {
-                const int row = 32 * sub + c;
+        for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[sub][r] = 0.f;
+            const int row = 32 * sub + c;
+            auto kread = [&](int i4) {
                 return *reinterpret_cast<const float4*>(&sK[row * kC + (((16 * h + i4) ^ (row & 15)) * 4)]);
             };
-            float4 ka0 = kread(0, 0), ka1 = kread(1, 0);
+            float4 ka = kread(0);
 #pragma unroll
             for (int i4 = 0; i4 < 16; ++i4) {
-                float4 kn0 = ka0, kn1 = ka1;
-                if (i4 + 1 < 16) {
-                    kn0 = kread(0, i4 + 1);
-                    kn1 = kread(1, i4 + 1);
-                }
-                s[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka0.x, qr[4 * i4 + 0], s[0], 0, 0, 0);
-                s[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka1.x, qr[4 * i4 + 0], s[1], 0, 0, 0);
-                s[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka0.y, qr[4 * i4 + 1], s[0], 0, 0, 0);
-                s[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka1.y, qr[4 * i4 + 1], s[1], 0, 0, 0);
-                s[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka0.z, qr[4 * i4 + 2], s[0], 0, 0, 0);
-                s[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka1.z, qr[4 * i4 + 2], s[1], 0, 0, 0);
-                s[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka0.w, qr[4 * i4 + 3], s[0], 0, 0, 0);
-                s[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka1.w, qr[4 * i4 + 3], s[1], 0, 0, 0);
-                ka0 = kn0;
-                ka1 = kn1;
+                const float4 nk = i4 + 1 < 16 ? kread(i4 + 1) : ka;
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.x, qr[4 * i4 + 0], s[sub], 0, 0, 0);
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.y, qr[4 * i4 + 1], s[sub], 0, 0, 0);
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.z, qr[4 * i4 + 2], s[sub], 0, 0, 0);
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.w, qr[4 * i4 + 3], s[sub], 0, 0, 0);
+                ka = nk;
             }
         }
         // ---- mask + online softmax (lane = query c; its keys 32 sub + 8(r >> 2) + 4h + (r & 3))
@@ -545,10 +558,10 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int4 rg = *reinterpret_cast<const int4*>(&sKeyRegion[32 * sub + 8 * u + 4 * h]);
-                    s[sub][4 * u + 0] += rg.x == qreg ? 0.0f : -100.0f;
-                    s[sub][4 * u + 1] += rg.y == qreg ? 0.0f : -100.0f;
-                    s[sub][4 * u + 2] += rg.z == qreg ? 0.0f : -100.0f;
-                    s[sub][4 * u + 3] += rg.w == qreg ? 0.0f : -100.0f;
+                    s[sub][4 * u + 0] += rg.x == qreg ? 0.0f : kMaskLog2;
+                    s[sub][4 * u + 1] += rg.y == qreg ? 0.0f : kMaskLog2;
+                    s[sub][4 * u + 2] += rg.z == qreg ? 0.0f : kMaskLog2;
+                    s[sub][4 * u + 3] += rg.w == qreg ? 0.0f : kMaskLog2;
                 }
         }
         float bmax = -INFINITY;
@@ -558,38 +571,50 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
             for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[sub][r]);
         bmax = halves_max(bmax);
         const float m_new = fmaxf(m_run, bmax);
-        const float corr = __expf(m_run - m_new);
+        if (__any(m_new > m_run)) {  // exact: corr == 1 for every lane otherwise
+            const float corr = fast_exp2(m_run - m_new);
+            l_run *= corr;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+            m_run = m_new;
+        }
         float bsum = 0.f;
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float e = __expf(s[sub][r] - m_new);
+                const float e = fast_exp2(s[sub][r] - m_run);
                 s[sub][r] = e;
                 bsum += e;
             }
-        bsum = halves_sum(bsum);
-        l_run = l_run * corr + bsum;
-        m_run = m_new;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+        l_run += halves_sum(bsum);
+
+        __syncthreads();  // every wave is done with K(t) / regions(t)
+        if (has_next) {
+            store_k();
+            load_v();
+        }
 
         // ---- O^T += V^T P^T: per 4-key run, the four d tiles' chains interleaved
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                float4 vt[4];
+            for (int u = 0; u < 4; ++u)
 #pragma unroll
-                for (int dt = 0; dt < 4; ++dt)
-                    vt[dt] = *reinterpret_cast<const float4*>(&sVt[(32 * dt + c) * kVtStride + 32 * sub + 8 * u + 4 * h]);
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int dt = 0; dt < 4; ++dt)
-                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(vt[dt][j], s[sub][4 * u + j], o[dt], 0, 0, 0);
-            }
-        __syncthreads();
+                for (int dp = 0; dp < 4; dp += 2) {
+                    const float4 v0 = *reinterpret_cast<const float4*>(&sVt[(32 * dp + c) * kVtStride + 32 * sub + 8 * u + 4 * h]);
+                    const float4 v1 = *reinterpret_cast<const float4*>(&sVt[(32 * dp + 32 + c) * kVtStride + 32 * sub + 8 * u + 4 * h]);
+                    o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.x, s[sub][4 * u + 0], o[dp], 0, 0, 0);
+                    o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.x, s[sub][4 * u + 0], o[dp + 1], 0, 0, 0);
+                    o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.y, s[sub][4 * u + 1], o[dp], 0, 0, 0);
+                    o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.y, s[sub][4 * u + 1], o[dp + 1], 0, 0, 0);
+                    o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.z, s[sub][4 * u + 2], o[dp], 0, 0, 0);
+                    o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.z, s[sub][4 * u + 2], o[dp + 1], 0, 0, 0);
+                    o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.w, s[sub][4 * u + 3], o[dp], 0, 0, 0);
+                    o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.w, s[sub][4 * u + 3], o[dp + 1], 0, 0, 0);
+                }
+        __syncthreads();  // every wave is done with V(t); K(t+1) is visible
+        if (has_next) store_v();  // read after the next tile's first barrier
     }
 
     // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
@@ -613,7 +638,7 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
             for (int u = 0; u < 4; ++u)
                 dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
         if (h == 0) {
-            part.m[row] = m_run;
+            part.m[row] = m_run * kLn2;  // natural-log domain for the combine
             part.l[row] = l_run;
         }
     }
@@ -1098,8 +1123,8 @@ static int choose_ksplit(int base_wgs, int key_tiles, int target) {
     return ks;
 }
 
-// Tuning knobs (benchmarking only): TSPLAT_WINATTN=16 forces the 16x16x4 kernel, =32p the
-// register-prefetch 32x32x2 variant; TSPLAT_WINATTN_KSPLIT forces the key split.
+// Tuning knobs (benchmarking only): TSPLAT_WINATTN=16 forces the 16x16x4 kernel, =32 the 128-query
+// 32x32x2 kernel, =pair the key-pair kernel; TSPLAT_WINATTN_KSPLIT forces the key split.
 static int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     return e ? atoi(e) : dflt;
@@ -1114,11 +1139,12 @@ static int query_block(int L) {
     if (env_is("TSPLAT_WINATTN", "16")) return tsplat::winattn::kBQ;
     return L % tsplat::winattn::kBQ3 == 0 ? tsplat::winattn::kBQ3 : tsplat::winattn::kBQ;
 }
+// 128-query kernel: one workgroup per CU is enough (measured: b = 2 at 256 workgroups beats 512,
+// and the key-pair kernel); the 16x16x4 kernel wants two per CU
 static int pick_ksplit(int base, int key_tiles, int qb) {
     const int forced = env_int("TSPLAT_WINATTN_KSPLIT", 0);
     if (forced > 0 && key_tiles % forced == 0) return forced;
-    const bool pf = env_is("TSPLAT_WINATTN", "32p");
-    return choose_ksplit(base, key_tiles, qb == tsplat::winattn::kBQ3 && pf ? 256 : 512);
+    return choose_ksplit(base, key_tiles, qb == tsplat::winattn::kBQ3 ? 256 : 512);
 }
 
 extern "C" size_t tsplat_win_attn_workspace_bytes(int32_t batch, int32_t height, int32_t width,
@@ -1160,8 +1186,7 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     const int base = (p.L / qb) * splits * splits * batch;
     p.ksplit = pick_ksplit(base, p.L * p.m / kBK, qb);
     // key-pair kernel: 64-query workgroups (twice the blocks), half the global key split
-    const bool pair = qb == kBQ3 && (p.ksplit > 1 || env_is("TSPLAT_WINATTN", "pair")) &&
-                      !env_is("TSPLAT_WINATTN", "32") && !env_is("TSPLAT_WINATTN", "32p");
+    const bool pair = qb == kBQ3 && env_is("TSPLAT_WINATTN", "pair");
     if (pair) p.ksplit = std::max(1, p.ksplit / 2);
     p.keys_per_split = p.L * p.m / p.ksplit;
     Partials part{nullptr, nullptr, nullptr};
@@ -1178,10 +1203,8 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     if (pair)
         hipLaunchKernelGGL(win_attn_f32_pair_kernel, dim3(p.L / 64, splits * splits, batch * p.ksplit),
                            dim3(kThreads), 0, stream, p, q, k, v, out, part);
-    else if (qb == kBQ3 && env_is("TSPLAT_WINATTN", "32p"))
-        hipLaunchKernelGGL(win_attn_f32x32_kernel<true>, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
     else if (qb == kBQ3)
-        hipLaunchKernelGGL(win_attn_f32x32_kernel<false>, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
+        hipLaunchKernelGGL(win_attn_f32x32_kernel, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
     else
         hipLaunchKernelGGL(win_attn_f32_kernel, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
     if (p.ksplit > 1 && qb == kBQ3)
