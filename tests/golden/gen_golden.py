@@ -307,6 +307,29 @@ def gen_covariance():
     save("covariance", cov=gs.build_covariance(s, q))
 
 
+def gen_crop_shim():
+    """Test-time crop shim (LANCZOS rescale through uint8 + centre crop) and patch shim."""
+    sys.modules.setdefault("src.dataset", types.ModuleType("src.dataset"))
+    sys.modules["src.dataset"].__path__ = [str(Path(sys.modules["src"].__path__[0]) / "dataset")]
+    sh = types.ModuleType("src.dataset.shims")
+    sh.__path__ = [sys.modules["src.dataset"].__path__[0] + "/shims"]
+    sys.modules["src.dataset.shims"] = sh
+    crop = imp("src.dataset.shims.crop_shim")
+    patch = imp("src.dataset.shims.patch_shim")
+    img = seeded((2, 3, 90, 160), 901, kind="rand")
+    k = torch.eye(3).repeat(2, 1, 1)
+    k[:, 0, 0], k[:, 1, 1], k[:, 0, 2], k[:, 1, 2] = 0.9, 1.6, 0.5, 0.5
+    ex = {"context": {"image": img, "intrinsics": k}, "target": {"image": img[:1], "intrinsics": k[:1]}}
+    out = crop.apply_crop_shim(ex, (64, 64))
+    pimg = seeded((1, 2, 3, 70, 66), 902, kind="rand")
+    pk = k.unsqueeze(0)
+    pout = patch.apply_patch_shim({"context": {"image": pimg, "intrinsics": pk},
+                                   "target": {"image": pimg, "intrinsics": pk}}, 14)
+    save("crop_shim", image=img, intrinsics=k, out_image=out["context"]["image"],
+         out_intrinsics=out["context"]["intrinsics"], patch_image=pimg, patch_intrinsics=pk,
+         patch_out_image=pout["context"]["image"], patch_out_intrinsics=pout["context"]["intrinsics"])
+
+
 def gen_state_dict_keys():
     """Parameter names + shapes of the reference submodules an `encoder.*` checkpoint holds."""
     import json
@@ -340,6 +363,7 @@ ALL = {
     "depth_predictor_v3": gen_depth_predictor_v3,
     "depth_anything": gen_depth_anything,
     "covariance": gen_covariance,
+    "crop_shim": gen_crop_shim,
 }
 
 

@@ -82,6 +82,27 @@ def evaluate(step: Callable[[dict], torch.Tensor], scenes: list, make_batch: Cal
     return gather_results(local, device, world)
 
 
+def evaluate_stream(step: Callable[[dict], torch.Tensor], examples, device: torch.device, rank: int = 0,
+                    world: int = 1) -> list[SceneResult]:
+    """Like `evaluate`, over an iterable of ready batches (the chunk reader): example i of the
+    stream is scene i, and rank r keeps i = r, r + N, ... (every rank decodes the same stream
+    order, so the split matches the index-driven one)."""
+    local = []
+    for idx, batch in enumerate(examples):
+        if idx % world != rank:
+            continue
+        batch = {k: ({kk: vv.to(device) for kk, vv in v.items()} if isinstance(v, dict) else v)
+                 for k, v in batch.items()}
+        t0 = time.perf_counter()
+        color = step(batch)
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+        psnr = compute_psnr(batch["target"]["image"][0], color[0]).mean().item()
+        local.append(SceneResult(idx, psnr, int(color.shape[1]), dt))
+    return gather_results(local, device, world)
+
+
 def summarize(results: list[SceneResult]) -> dict:
     n = len(results)
     return {
@@ -116,6 +137,9 @@ def main(argv=None):
     ap.add_argument("--checkpoint", default=None, help="reference Lightning checkpoint (loaded weights_only)")
     ap.add_argument("--dense-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--limit", type=int, default=None, help="first N scenes of the index")
+    ap.add_argument("--data-root", action="append", default=None,
+                    help="dataset root holding test/*.torch chunks (repeatable); real frames instead of synthetic")
+    ap.add_argument("--experiment", choices=["re10k", "acid", "dtu"], default="re10k")
     args = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -130,14 +154,26 @@ def main(argv=None):
     model = build_model(device, args.dense_dtype)
     if args.checkpoint:
         model.load_checkpoint(args.checkpoint)
-    scenes = load_index(args.index)[: args.limit]
     step = lambda batch: model.test_step(batch).color
-    results = evaluate(step, [(k, v) for k, v in scenes],
-                       lambda i, kv: index_batch(i, kv[0], kv[1], device=device), device, rank, world)
+    if args.data_root:
+        from itertools import islice
+
+        from .dataset import EXPERIMENTS, ChunkDatasetCfg, ChunkTestDataset
+
+        cfg = ChunkDatasetCfg(roots=tuple(args.data_root), **EXPERIMENTS[args.experiment])
+        ds = ChunkTestDataset.from_index_file(cfg, args.index)
+        stream = (ChunkTestDataset.batch(ex) for ex in islice(iter(ds), args.limit))
+        results = evaluate_stream(step, stream, device, rank, world)
+        data = f"{args.experiment} chunks under {args.data_root}"
+    else:
+        scenes = load_index(args.index)[: args.limit]
+        results = evaluate(step, [(k, v) for k, v in scenes],
+                           lambda i, kv: index_batch(i, kv[0], kv[1], device=device), device, rank, world)
+        data = "synthetic frames at the index's frame positions"
     if rank == 0:
         summary = summarize(results)
         summary.update({"index": str(args.index), "world": world, "weights": args.checkpoint or "synthetic",
-                        "data": "synthetic frames at the index's frame positions"})
+                        "data": data})
         print(json.dumps(summary), flush=True)
     if world > 1:
         dist.destroy_process_group()
