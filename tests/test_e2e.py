@@ -65,3 +65,42 @@ def test_e2e_three_context_views(device):
     torch.cuda.synchronize()
     assert g.means.shape == (1, 3 * 256 * 256, 3)
     assert out.shape == (1, 3, 3, 256, 256) and torch.isfinite(out).all()
+
+
+@pytest.mark.gpu
+def test_bf16_weight_precast_keeps_outputs(device):
+    """bf16 dense mode stores conv / linear weights in bf16 once (e2e.precast_autocast_weights)
+    instead of letting autocast re-cast them each step. The bf16 values are the same (checked
+    parameter by parameter); params used outside autocast (norms, HIP kernels, fp32 islands) stay
+    fp32. Library algorithm choices differ between the two models, so the rendered views are
+    compared through their distance to the fp32 model: the pre-cast model must be as close to it
+    as the re-casting one."""
+    from transplat_amd import e2e
+
+    data = S.make_batch(1, image_shape=(256, 256), device=device)
+    cast = e2e.build_model(device, "bf16")
+
+    def fresh(dtype):
+        torch.manual_seed(0)
+        cfg = e2e.EncoderTransCfg(dense_dtype=dtype)
+        m = e2e.TransplatModel(cfg, e2e.DecoderSplattingHIPCfg(check_overflow=False))
+        S.init_synthetic_weights(m.encoder, 0)
+        return m.eval().to(device)
+
+    plain, ref = fresh("bf16"), fresh("fp32")
+    n_bf16 = sum(p.dtype == torch.bfloat16 for p in cast.parameters())
+    assert n_bf16 > 300
+    for (name, p), q in zip(cast.named_parameters(), plain.parameters()):
+        if p.dtype == torch.bfloat16:
+            assert "norm" not in name.split(".")[-2]
+            assert torch.equal(p, q.to(torch.bfloat16))
+        else:
+            assert torch.equal(p, q)
+    with torch.no_grad():
+        a = cast.test_step(data).color.float()
+        b = plain.test_step(data).color.float()
+        r = ref.test_step(data).color.float()
+    torch.cuda.synchronize()
+    assert torch.isfinite(a).all()
+    ea, eb = (a - r).abs().mean().item(), (b - r).abs().mean().item()
+    assert ea < 1.5 * eb + 1e-3, (ea, eb)

@@ -63,12 +63,17 @@ def test_camera_prep_matches_reference_golden():
 
 # ------------------------------------------------------------------ HIP kernels vs oracle
 @pytest.mark.gpu
-@pytest.mark.parametrize("hw,m,shift", [(16, 1, False), (16, 1, True), (16, 2, True), (64, 1, False),
-                                        (64, 1, True), (64, 2, True), (32, 2, False)])
-def test_window_attention_kernel(device, hw, m, shift):
+@pytest.mark.parametrize("variant", ["auto", "quad"])
+@pytest.mark.parametrize("hw,m,shift,b", [(16, 1, False, 2), (16, 1, True, 2), (16, 2, True, 2), (64, 1, False, 2),
+                                          (64, 1, True, 2), (64, 2, True, 2), (32, 2, False, 2), (64, 1, True, 8)])
+def test_window_attention_kernel(device, monkeypatch, hw, m, shift, b, variant):
+    """auto: the 128-query 32x32x2 kernel with its global key split + combine (b = 2 at 64x64), without
+    split at b = 8, the 64-query 16x16x4 kernel for 8x8 windows; "quad": the opt-in split-free kernel
+    (4 waves x key quarters on 32 queries) where its shapes allow, else the same defaults."""
     from transplat_amd import kernels as K
 
-    b = 2
+    if variant != "auto":
+        monkeypatch.setenv("TSPLAT_WINATTN", variant)
     q = seeded((b, hw * hw, 128), 11)
     k = seeded((b, m, hw * hw, 128), 12) if m > 1 else seeded((b, hw * hw, 128), 12)
     v = seeded(k.shape, 13)

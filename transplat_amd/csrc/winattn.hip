@@ -901,6 +901,219 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
 }
 
 // ============================================================================================
+// Quad kernel (launches whose 128-query blocks cannot fill the chip, e.g. the 2-view 64x64 map
+// at batch 1: 64 blocks): one workgroup = 4 INDEPENDENT waves on the same 32 queries, wave w
+// taking the w-th quarter of the window's keys, merged once through LDS at the end. No global
+// key split: no partial slabs in HBM and no combine launch; 256 workgroups of 32 queries fill
+// the 256 CUs once. Each wave stages its own 32-key K / V tiles (no workgroup barrier in the
+// loop): tile t+1's rows are loaded into registers during tile t's MFMAs and stored after them.
+//   loads: instruction i covers 8 key rows x 128 B (rows 8 (i & 3) + (lane >> 3), 128-B segment
+//          i >> 2), i.e. whole cache lines; a lane holds 4 rows' pieces.
+//   K: row-major, 16-B chunks XOR-swizzled by row (the x32 kernel's S^T = K Q^T reads, 1 subtile).
+//   V: row-major, rows padded to 136 floats: the O^T += V^T P^T A operand of lane (c, h) is
+//      V[key 8u + 4h + j][32 dt + c], one ds_read_b32 per MFMA, the two half-waves (key + 4)
+//      on disjoint banks.
+// ============================================================================================
+constexpr int kQT = 32;             // keys per wave tile
+constexpr int kVRow = kC + 8;       // padded V row (floats)
+constexpr int kQuadWave = kQT * kC + kQT * kVRow + kQT;  // floats of one wave's LDS region
+
+__global__ void __launch_bounds__(kThreads, 1)
+win_attn_f32_quad_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
+                         const float* __restrict__ v, float* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) float smem[4 * kQuadWave];
+    __shared__ float sML[4][2][kQW];
+
+    int qblk, wi, b;
+    xcd_block_coords(qblk, wi, b);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const size_t HW = (size_t)p.H * p.W;
+    const float* qb = q + (size_t)b * HW * kC;
+    const float* kb = k + (size_t)b * p.m * HW * kC;
+    const float* vb = v + (size_t)b * p.m * HW * kC;
+    float* sK = smem + wid * kQuadWave;
+    float* sV = sK + kQT * kC;
+    int* sReg = reinterpret_cast<int*>(sV + kQT * kVRow);
+
+    const int nkeys = p.L * p.m / 4;
+    const int kbeg = wid * nkeys, kend = kbeg + nkeys;
+    const int lrow = lane >> 3, lseg = lane & 7;  // row within an 8-row group, 16-B piece of a 128-B segment
+    floatx4 stk[16], stv[16];  // vector types: plain loads, no memcpy (which stays in scratch)
+    int rreg[4];
+#define QUAD_LOAD_TILE(k0_)                                                                      \
+    {                                                                                            \
+        size_t roff[4];                                                                          \
+        _Pragma("unroll") for (int g = 0; g < 4; ++g)                                            \
+            key_row(p, wi, HW, (k0_) + 8 * g + lrow, roff[g], rreg[g]);                          \
+        _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                         \
+            const size_t o_ = roff[i & 3] * kC + 32 * (i >> 2) + 4 * lseg;                       \
+            stk[i] = *reinterpret_cast<const floatx4*>(kb + o_);                                  \
+            stv[i] = *reinterpret_cast<const floatx4*>(vb + o_);                                  \
+        }                                                                                        \
+    }
+#define QUAD_STORE_TILE()                                                                        \
+    {                                                                                            \
+        _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                         \
+            const int row = 8 * (i & 3) + lrow, chunk = 8 * (i >> 2) + lseg;                    \
+            *reinterpret_cast<floatx4*>(&sK[row * kC + ((chunk ^ (row & 15)) * 4)]) = stk[i];     \
+            *reinterpret_cast<floatx4*>(&sV[row * kVRow + chunk * 4]) = stv[i];                 \
+        }                                                                                        \
+        if (p.shift && lseg == 0) {                                                              \
+            _Pragma("unroll") for (int g = 0; g < 4; ++g) sReg[8 * g + lrow] = rreg[g];          \
+        }                                                                                        \
+    }
+
+    const int tq = qblk * kQW + c;
+    const int qpix = win_pixel(p, wi, tq);
+    const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+    const float qscale = p.scale * kLog2e;  // log2-domain scores (see the key-pair kernel)
+    float qr[64];
+    QUAD_LOAD_TILE(kbeg);
+    {
+        const float4* src = reinterpret_cast<const float4*>(qb + (size_t)qpix * kC + 64 * h);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float4 t4 = src[i];
+            qr[4 * i] = t4.x * qscale;
+            qr[4 * i + 1] = t4.y * qscale;
+            qr[4 * i + 2] = t4.z * qscale;
+            qr[4 * i + 3] = t4.w * qscale;
+        }
+    }
+    floatx16 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    QUAD_STORE_TILE();
+
+    for (int k0 = kbeg; k0 < kend; k0 += kQT) {
+        // this wave's LDS stores of tile t are complete before any lane reads them
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const bool has_next = k0 + kQT < kend;
+        if (has_next) QUAD_LOAD_TILE(k0 + kQT);
+
+        // ---- S^T = K Q^T over the tile's 32 keys (lane = query c; keys 8(r >> 2) + 4h + (r & 3))
+        floatx16 s;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = 0.f;
+        {
+            auto kread = [&](int i4) {
+                return *reinterpret_cast<const float4*>(&sK[c * kC + (((16 * h + i4) ^ (c & 15)) * 4)]);
+            };
+            float4 ka = kread(0);
+#pragma unroll
+            for (int i4 = 0; i4 < 16; ++i4) {
+                const float4 nk = i4 + 1 < 16 ? kread(i4 + 1) : ka;
+                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.x, qr[4 * i4 + 0], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.y, qr[4 * i4 + 1], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.z, qr[4 * i4 + 2], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.w, qr[4 * i4 + 3], s, 0, 0, 0);
+                ka = nk;
+            }
+        }
+        if (p.shift) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int4 rg = *reinterpret_cast<const int4*>(&sReg[8 * u + 4 * h]);
+                s[4 * u + 0] += rg.x == qreg ? 0.0f : kMaskLog2;
+                s[4 * u + 1] += rg.y == qreg ? 0.0f : kMaskLog2;
+                s[4 * u + 2] += rg.z == qreg ? 0.0f : kMaskLog2;
+                s[4 * u + 3] += rg.w == qreg ? 0.0f : kMaskLog2;
+            }
+        }
+        float bmax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[r]);
+        bmax = halves_max(bmax);
+        const float m_new = fmaxf(m_run, bmax);
+        if (__any(m_new > m_run)) {  // exact: corr == 1 for every lane otherwise
+            const float corr = fast_exp2(m_run - m_new);
+            l_run *= corr;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+            m_run = m_new;
+        }
+        float bsum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float e = fast_exp2(s[r] - m_run);
+            s[r] = e;
+            bsum += e;
+        }
+        l_run += halves_sum(bsum);
+
+        // ---- O^T += V^T P^T: k-step (u, j) contracts keys {8u + j, 8u + 4 + j} (lane halves)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float* vrow = &sV[(8 * u + 4 * h + j) * kVRow + c];
+                const float a0 = vrow[0], a1 = vrow[32], a2 = vrow[64], a3 = vrow[96];
+                o[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, s[4 * u + j], o[0], 0, 0, 0);
+                o[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, s[4 * u + j], o[1], 0, 0, 0);
+                o[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, s[4 * u + j], o[2], 0, 0, 0);
+                o[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a3, s[4 * u + j], o[3], 0, 0, 0);
+            }
+        if (has_next) QUAD_STORE_TILE();  // waits for tile t+1's loads; every lane's reads of tile t are done
+    }
+
+    // ---- merge the four key quarters: wave w finishes output d tile w.
+    // Own region, own (finished) loop: park the three d tiles other waves finish, then one barrier.
+    if (h == 0) {
+        sML[wid][0][c] = m_run;
+        sML[wid][1][c] = l_run;
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+        if (dt == wid) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sK[(dt * 16 + r) * 64 + lane] = o[dt][r];
+    }
+    __syncthreads();
+    float mw[4], M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        mw[w] = sML[w][0][c];
+        M = fmaxf(M, mw[w]);
+    }
+    float a[4], L = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        a[w] = fast_exp2(mw[w] - M);
+        L += a[w] * sML[w][1][c];
+    }
+    const float inv = 1.0f / L;
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        if (w == wid) {
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)  // compile-time register index (o[wid] would spill)
+                if (dt == wid)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[r] += a[w] * o[dt][r];
+        } else {
+            const float* src = smem + w * kQuadWave + wid * 16 * 64 + lane;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] += a[w] * src[r * 64];
+        }
+    }
+    // O^T[d = 32 wid + 8u + 4h + j][q = c] in acc[4u + j]
+    float* dst = out + ((size_t)b * HW + qpix) * kC + 32 * wid + 4 * h;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        *reinterpret_cast<float4*>(dst + 8 * u) =
+            make_float4(acc[4 * u] * inv, acc[4 * u + 1] * inv, acc[4 * u + 2] * inv, acc[4 * u + 3] * inv);
+#undef QUAD_LOAD_TILE
+#undef QUAD_STORE_TILE
+}
+
+// ============================================================================================
 // bf16 variant (config C3: bf16 attention): v_mfma_f32_32x32x16_bf16, fp32 accumulation and
 // fp32 softmax, bf16 in/out. One workgroup = 4 waves x 32 queries, 64-key tiles in LDS as bf16
 // (K rows XOR-swizzled per 16-B chunk, V transposed). Operand maps (lane l, c = l & 31,
@@ -1147,6 +1360,17 @@ static int pick_ksplit(int base, int key_tiles, int qb) {
     return choose_ksplit(base, key_tiles, qb == tsplat::winattn::kBQ3 ? 256 : 512);
 }
 
+// quad kernel (no global key split): opt-in with TSPLAT_WINATTN=quad where its shape constraints
+// hold. Measured on MI355X (2-view 64x64 map, b = 2, shifted): 59.7 us vs 56.9 us for the 128-query
+// kernel with its 4-way key split + combine, and 115 vs 96.5 us at b = 4, so the split kernels stay
+// the default: one wave per SIMD re-reading a quarter of the window's K/V per 32 queries (1 MB per
+// workgroup through L2) costs more than the partial slabs it avoids.
+static bool use_quad(int L, int m, int base128) {
+    (void)base128;
+    if (L % tsplat::winattn::kQW || (L * m) % (4 * tsplat::winattn::kQT)) return false;
+    return env_is("TSPLAT_WINATTN", "quad");
+}
+
 extern "C" size_t tsplat_win_attn_workspace_bytes(int32_t batch, int32_t height, int32_t width,
                                                   int32_t key_views, int32_t splits) {
     using namespace tsplat::winattn;
@@ -1154,6 +1378,7 @@ extern "C" size_t tsplat_win_attn_workspace_bytes(int32_t batch, int32_t height,
     const int L = (height / splits) * (width / splits);
     if (L % kBQ || (L * key_views) % kBK) return 0;
     const int base = (L / query_block(L)) * splits * splits * batch;
+    if (use_quad(L, key_views, (L / kBQ3) * splits * splits * batch)) return 0;
     const int ks = pick_ksplit(base, L * key_views / kBK, query_block(L));
     if (ks == 1) return 0;
     return (size_t)batch * splits * splits * ks * L * (kC + 2) * sizeof(float);
@@ -1182,6 +1407,17 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
     if (p.L % kBQ || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
+    hipStream_t stream = (hipStream_t)stream_;
+    if (use_quad(p.L, p.m, (p.L / kBQ3) * splits * splits * batch)) {
+        p.ksplit = 1;
+        p.keys_per_split = p.L * p.m;
+        TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
+        hipLaunchKernelGGL(win_attn_f32_quad_kernel, dim3(p.L / kQW, splits * splits, batch), dim3(kThreads), 0,
+                           stream, p, q, k, v, out);
+        TSPLAT_PROF_END(prof::kWinAttn, stream);
+        TSPLAT_CHECK_LAUNCH();
+        return TSPLAT_OK;
+    }
     const int qb = query_block(p.L);
     const int base = (p.L / qb) * splits * splits * batch;
     p.ksplit = pick_ksplit(base, p.L * p.m / kBK, qb);
@@ -1197,7 +1433,6 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
         part.m = part.o + n * kC;
         part.l = part.m + n;
     }
-    hipStream_t stream = (hipStream_t)stream_;
     const dim3 grid(p.L / qb, splits * splits, batch * p.ksplit);
     TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
     if (pair)

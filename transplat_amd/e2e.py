@@ -50,7 +50,55 @@ def build_model(device, dense_dtype: str = "fp32", seed: int = 0, num_context_vi
     cfg = EncoderTransCfg(dense_dtype=dense_dtype, num_context_views=num_context_views)
     model = TransplatModel(cfg, DecoderSplattingHIPCfg(check_overflow=False))
     S.init_synthetic_weights(model.encoder, seed)
-    return model.eval().to(device)
+    model = model.eval().to(device)
+    if dense_dtype == "bf16" and torch.device(device).type == "cuda":
+        example = S.make_batch(1, num_context=num_context_views, image_shape=(256, 256), device=device)
+        precast_autocast_weights(model, example)
+    return model
+
+
+_AUTOCAST_MATMULS = None
+
+
+def precast_autocast_weights(model: torch.nn.Module, example: dict) -> int:
+    """Store once, in bf16, every parameter whose only uses are conv / linear calls under bf16
+    autocast. Autocast would otherwise re-cast those fp32 weights on every step (its cast cache
+    lives only as long as one autocast region): ~600 cast kernels per captured step. The values the
+    convolutions see are identical (the same round-to-nearest cast, done once). Uses are recorded by
+    a TorchFunctionMode over one eager test_step; a parameter used anywhere else (norms, HIP
+    kernels, autocast-disabled regions) stays fp32. Returns the number of parameters cast."""
+    import torch.nn.functional as F
+    from torch.overrides import TorchFunctionMode
+
+    global _AUTOCAST_MATMULS
+    if _AUTOCAST_MATMULS is None:
+        _AUTOCAST_MATMULS = {F.conv1d, F.conv2d, F.conv3d, F.linear, F.conv_transpose1d, F.conv_transpose2d,
+                             torch.conv2d, torch.conv1d, torch.conv_transpose2d}
+    params = {id(p): p for p in model.parameters()}
+    ok: dict[int, bool] = {}
+
+    class _Record(TorchFunctionMode):
+        def __torch_function__(self, func, types, args=(), kwargs=None):
+            kwargs = kwargs or {}
+            castable = func in _AUTOCAST_MATMULS and torch.is_autocast_enabled("cuda")
+            for a in (*args, *kwargs.values()):
+                if isinstance(a, (list, tuple)):
+                    for x in a:
+                        if id(x) in params:
+                            ok[id(x)] = False
+                elif id(a) in params:
+                    ok[id(a)] = ok.get(id(a), True) and castable
+            return func(*args, **kwargs)
+
+    with torch.no_grad(), _Record():
+        model.test_step(example)
+    n = 0
+    for pid, good in ok.items():
+        p = params[pid]
+        if good and p.dtype == torch.float32:
+            p.data = p.data.to(torch.bfloat16)
+            n += 1
+    return n
 
 
 class GraphedStep:
