@@ -44,8 +44,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=1, help="scenes per step per GPU")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--conv-search", action="store_true",
-                    help="let MIOpen search convolution algorithms (torch.backends.cudnn.benchmark)")
+    ap.add_argument("--no-conv-search", action="store_true",
+                    help="MIOpen's default convolution algorithm choice instead of its measured search "
+                         "(torch.backends.cudnn.benchmark, on by default: +2.4%% e2e at b = 1)")
     return ap.parse_args()
 
 
@@ -212,7 +213,7 @@ def main():
     world, rank, local = init_dist()
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
-    if args.conv_search:
+    if not args.no_conv_search:
         torch.backends.cudnn.benchmark = True
     from transplat_amd import _lib
 

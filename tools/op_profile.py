@@ -25,18 +25,18 @@ with torch.no_grad():
         torch.cuda.synchronize()
 print(prof.key_averages(group_by_input_shape=True).table(sort_by="cuda_time_total", row_limit=60, max_name_column_width=40,
                                                          max_shapes_column_width=80), flush=True)
-# GPU time of leaf ops by (op, first repo frame)
+# GPU time launched directly by each CPU op, by (op, innermost repo frame)
 agg = collections.defaultdict(lambda: [0, 0.0])
 for ev in prof.events():
-    dt = getattr(ev, "device_time_total", 0) or getattr(ev, "cuda_time_total", 0)
-    if not dt or ev.cpu_children:
+    dt = getattr(ev, "self_device_time_total", 0) or getattr(ev, "self_cuda_time_total", 0)
+    if not dt or ev.device_type != torch.autograd.DeviceType.CPU:
         continue
     frames = [f for f in (ev.stack or []) if "transplat_amd" in f]
-    where = frames[0] if frames else "?"
+    where = frames[0].split("transplat_amd/")[-1] if frames else "?"
     a = agg[(ev.name, where)]
     a[0] += 1
     a[1] += dt
 rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
 print("\n== GPU time by (op, call site)")
-for (name, where), (n, us) in rows[:80]:
+for (name, where), (n, us) in rows[:120]:
     print(f"{us:9.1f}us {n:4d}x {name[:34]:34s} {where}")

@@ -22,6 +22,8 @@
 // so bitwise agreement is what makes an L-inf 1e-4 image check meaningful.
 #pragma clang fp contract(off)
 
+#include <stdlib.h>
+
 #include "common.h"
 #include "prof.h"
 
@@ -66,6 +68,29 @@ __device__ __forceinline__ float exp_neg(float x_in) {
     return underflow ? 0.0f : p * __int_as_float((k + 127) << 23);
 }
 
+// Two exp_neg evaluations in packed fp32 (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32: both
+// halves IEEE-identical to the scalar ops). Underflow is a clamp instead of a select: for
+// x < -87 the result is a tiny positive number where exp_neg returns 0, and alpha < 1/255 either
+// way, so every blend decision -- and therefore the image -- is unchanged.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f32x2 exp_neg2(f32x2 x_in) {
+    const f32x2 x = {fmaxf(x_in.x, -87.0f), fmaxf(x_in.y, -87.0f)};
+    const f32x2 t = x * 1.44269504088896341f;
+    const f32x2 kf = {rintf(t.x), rintf(t.y)};
+    f32x2 r = pk_fma(kf, (f32x2)(-0.693359375f), x);
+    r = pk_fma(kf, (f32x2)(2.12194440e-4f), r);
+    const f32x2 z = r * r;
+    f32x2 q = pk_fma((f32x2)(1.9875691500e-4f), r, (f32x2)(1.3981999507e-3f));
+    q = pk_fma(q, r, (f32x2)(8.3334519073e-3f));
+    q = pk_fma(q, r, (f32x2)(4.1665795894e-2f));
+    q = pk_fma(q, r, (f32x2)(1.6666665459e-1f));
+    q = pk_fma(q, r, (f32x2)(5.0000001201e-1f));
+    q = pk_fma(q, z, r) + 1.0f;
+    const f32x2 sc = {__int_as_float(((int)kf.x + 127) << 23), __int_as_float(((int)kf.y + 127) << 23)};
+    return q * sc;
+}
+
 struct Workspace {
     float4* xy;          // [V*G] pixel-space mean + half-extents of the alpha >= 1/255 ellipse
     float4* conic_o;     // [V*G] conic (a, b, c) + opacity
@@ -101,6 +126,7 @@ __host__ __device__ inline Workspace carve(void* base, int G, int V, int T, int 
 
 struct Params {
     int G, V, vps, H, W, M, deg, tiles_x, tiles_y, T, capacity;
+    int diag;  // timing diagnostics only (TSPLAT_RASTER_DIAG; output is wrong when != 0)
 };
 
 __device__ __forceinline__ void get_rect(float px, float py, int r, int tx, int ty, int& x0,
@@ -536,7 +562,9 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     if (in_lds) {
         for (int i = threadIdx.x; i < n; i += kTileThreads) skeys[i] = gkeys[i];
         __syncthreads();
-        bitonic_sort_regs(skeys, n);
+        if (p.diag == 3) return;  // key load only
+        if (p.diag != 1) bitonic_sort_regs(skeys, n);
+        if (p.diag == 2) return;  // key load + sort
     } else {
         bitonic_sort(gkeys, n);  // rare: very long tile list, sorted in place in global memory
     }
@@ -576,6 +604,35 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
         C2 = acc ? fmaf(c.z, w, C2) : C2;
         T = acc ? test_T : T;
         done = done || stop;
+    };
+
+    // two consecutive entries: their alphas do not depend on T, so power / exp / alpha run as
+    // packed fp32 pairs; the T / C updates stay sequential in depth order (bitwise the same as two
+    // blend() calls: same floats in every decision, a non-accumulating entry adds c * 0 = +0)
+    auto blend2 = [&](const float4 xa, const float4 ca, const float4 cola, const float4 xb, const float4 cb,
+                      const float4 colb) {
+        const f32x2 dx = (f32x2){xa.x, xb.x} - pfx, dy = (f32x2){xa.y, xb.y} - pfy;
+        const f32x2 ka = {ca.x, cb.x}, kb = {ca.y, cb.y}, kc = {ca.z, cb.z}, op = {ca.w, cb.w};
+        const f32x2 quad = pk_fma(ka * dx, dx, (kc * dy) * dy);
+        const f32x2 power = pk_fma((f32x2)(-0.5f), quad, -((kb * dx) * dy));
+        const f32x2 oe = op * exp_neg2(power);
+        const float al[2] = {fminf(0.99f, oe.x), fminf(0.99f, oe.y)};
+        const float pw[2] = {power.x, power.y};
+        const float4 col[2] = {cola, colb};
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const float alpha = al[t];
+            const float test_T = fmaf(-alpha, T, T);
+            const bool contrib = !done && !(pw[t] > 0.0f) && !(alpha < 1.0f / 255.0f);
+            const bool stop = contrib && (test_T < 0.0001f);
+            const bool acc = contrib && !stop;
+            const float w = acc ? alpha * T : 0.0f;
+            C0 = fmaf(col[t].x, w, C0);
+            C1 = fmaf(col[t].y, w, C1);
+            C2 = fmaf(col[t].z, w, C2);
+            T = acc ? test_T : T;
+            done = done || stop;
+        }
     };
 
     // this lane's record of the next 64-entry chunk, fetched one chunk ahead
@@ -619,10 +676,8 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
             const float4 xy1 = w_xy[i + 1], co1 = w_co[i + 1], c1v = w_rgb[i + 1];
             const float4 xy2 = w_xy[i + 2], co2 = w_co[i + 2], c2v = w_rgb[i + 2];
             const float4 xy3 = w_xy[i + 3], co3 = w_co[i + 3], c3v = w_rgb[i + 3];
-            blend(xy0, co0, c0v);
-            blend(xy1, co1, c1v);
-            blend(xy2, co2, c2v);
-            blend(xy3, co3, c3v);
+            blend2(xy0, co0, c0v, xy1, co1, c1v);
+            blend2(xy2, co2, c2v, xy3, co3, c3v);
         }
         for (; i < m; ++i) blend(w_xy[i], w_co[i], w_rgb[i]);
         __builtin_amdgcn_wave_barrier();  // reads of this chunk's records precede the next writes
@@ -684,6 +739,10 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
     p.tiles_y = ceil_div(p.H, kTile);
     p.T = p.tiles_x * p.tiles_y;
     p.capacity = d->capacity;
+    {
+        const char* e = getenv("TSPLAT_RASTER_DIAG");
+        p.diag = e ? atoi(e) : 0;
+    }
     if ((size_t)p.T * 2 * sizeof(uint32_t) > 64 * 1024) return TSPLAT_EINVAL;  // LDS histogram
     Workspace ws = carve(workspace, p.G, p.V, p.T, p.capacity, nullptr);
 
