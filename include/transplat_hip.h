@@ -214,6 +214,23 @@ int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void* v, void* 
                              int32_t batch, int32_t height, int32_t width, int32_t channels,
                              int32_t key_views, int32_t splits, int32_t with_shift, void* stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Fused linear of the multi-view transformer (exact fp32 MFMA), replacing the nn.Linear +
+ * torch.cat + nn.GELU + nn.LayerNorm + residual-add chains of TransformerLayer.forward
+ * (reference src/model/encoder/backbone/multiview_transformer.py:327-407):
+ *   out[M, N] = epilogue([x1 | x2] w^T), x1 [M, k1], x2 [M, k2] (x2 may be NULL when k2 = 0),
+ *   w [N, k1 + k2] row-major (nn.Linear weight); k1, k2 multiples of 64, N a multiple of 128.
+ *   flags: 16 + bias[N]; 1 exact-erf GELU; 2 LayerNorm over the row (N must be 128; biased
+ *   variance, rsqrt(var + ln_eps), ln_gamma / ln_beta [128]); 4 + residual [M, N];
+ *   8 split: column block j of 128 is written to out + j * split_stride as its own [M, 128]
+ *   matrix (not with 4); 32 GELU of the INPUT: exact-erf GELU applied to [x1 | x2] as it is
+ *   loaded (the producing layer's activation; N must be 128). Epilogues applied in that order.
+ * ---------------------------------------------------------------------------------------- */
+int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x2, int32_t k2, const float* w,
+                          const float* bias, const float* ln_gamma, const float* ln_beta, float ln_eps,
+                          const float* residual, float* out, int64_t split_stride, int32_t M, int32_t N,
+                          int32_t flags, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -262,5 +262,24 @@ def sh_rotation(rotations, d_sh: int):
 
 
 # kernels.<name> -> oracle.<name>: what a CPU run of the module glue swaps in (tests, bench cpu leg)
+def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, residual=None, split: bool = False,
+                 gelu_in: bool = False):
+    """CPU restatement of kernels.fused_linear: the reference TransformerLayer's chain
+    (multiview_transformer.py:327-407) torch.cat -> nn.Linear -> nn.GELU -> nn.LayerNorm -> + x."""
+    x = torch.cat([x1, x2], dim=-1) if x2 is not None else x1
+    if gelu_in:
+        x = torch.nn.functional.gelu(x)
+    y = torch.nn.functional.linear(x, weight, bias)
+    if gelu:
+        y = torch.nn.functional.gelu(y)
+    if ln is not None:
+        y = torch.nn.functional.layer_norm(y, (y.shape[-1],), ln[0], ln[1], ln[2])
+    if residual is not None:
+        y = residual + y
+    if split:
+        return [t.contiguous() for t in y.split(128, dim=-1)]
+    return y
+
+
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
-                       "sh_rotation")
+                       "sh_rotation", "fused_linear")

@@ -5,6 +5,7 @@ Tolerances: the window attention runs exact-fp32 MFMA but with a different summa
 exp2-based softmax than torch: 2e-4 absolute on O(1) outputs. The correlation kernels sum 128
 products in a different order than MSDA+mean: 1e-4 absolute (outputs are O(1)).
 """
+import math
 import sys
 from pathlib import Path
 
@@ -239,3 +240,34 @@ def test_window_attention_bf16_kernel(device, hw, m, shift, b):
     assert out.dtype == torch.bfloat16
     err = (out.float().cpu() - ref).abs().max().item()
     assert err < 1.5e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k1,k2,n,gelu,ln,res,split,bias,gin", [
+    (8192, 128, 0, 384, False, False, False, True, False, False),    # self-attention q | k | v
+    (8192, 128, 0, 128, False, True, True, False, False, False),     # merge + norm1 + residual
+    (1000, 128, 128, 1024, True, False, False, False, False, False),  # [x | msg] + GELU, ragged M
+    (8192, 1024, 0, 128, False, True, True, False, False, True),     # GELU(h) mlp[2] + norm2 + res
+    (96, 64, 0, 256, True, False, False, False, True, False),        # bias path, tiny M
+])
+def test_fused_linear_kernel(device, m, k1, k2, n, gelu, ln, res, split, bias, gin):
+    """tsplat_linear_f32_fwd vs the CPU restatement of the reference TransformerLayer chain
+    (exact fp32 MFMA; only the summation order differs)."""
+    from transplat_amd import kernels as K
+
+    x1 = seeded((m, k1), 31)
+    x2 = seeded((m, k2), 32) if k2 else None
+    w = seeded((n, k1 + k2), 33) / math.sqrt(k1 + k2)
+    b = seeded((n,), 34) if bias else None
+    lnp = (seeded((n,), 35) * 0.1 + 1.0, seeded((n,), 36) * 0.1, 1e-5) if ln else None
+    r = seeded((m, n), 37) if res else None
+    ref = E.fused_linear(x1, w, x2=x2, bias=b, gelu=gelu, ln=lnp, residual=r, split=split, gelu_in=gin)
+    d = lambda t: t.to(device) if t is not None else None
+    out = K.fused_linear(d(x1), d(w), x2=d(x2), bias=d(b), gelu=gelu,
+                         ln=(d(lnp[0]), d(lnp[1]), lnp[2]) if ln else None, residual=d(r), split=split,
+                         gelu_in=gin)
+    if split:
+        assert len(out) == n // 128 and all(o.is_contiguous() and o.shape == (m, 128) for o in out)
+        out, ref = torch.cat(out, -1), torch.cat(ref, -1)
+    err = (out.cpu() - ref).abs().max().item()
+    assert err < 2e-4 * max(1.0, ref.abs().max().item()), err

@@ -1,0 +1,6 @@
+export PYTHONPATH=$PWD
+O=gpurun_out/lin; mkdir -p $O
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_encoder_ops.py -m gpu -k "fused_linear" > $O/test.log 2>&1; rc=$?; tail -3 $O/test.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 120 python tools/bench_linear.py || exit 1
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/b0.log 2>&1 || exit 1
+tail -1 $O/b0.log | cut -c1-200

@@ -1,0 +1,49 @@
+"""Microbenchmark of tsplat_linear_f32_fwd on the multi-view transformer's shapes at b = 1
+(8,192 rows = 2 views x 64 x 64): HIP events around the launches, µs per call and TFLOP/s against
+the 157.3 TF fp32-MFMA peak; next to torch's hipBLASLt F.linear for the plain GEMM part."""
+import torch
+import torch.nn.functional as F
+
+from transplat_amd import _lib, kernels as K
+
+dev = torch.device("cuda:0")
+_lib.load()
+g = torch.Generator(device=dev).manual_seed(0)
+r = lambda *s: torch.randn(s, device=dev, generator=g)
+M = 8192
+cases = [  # name, k1, k2, n, kwargs
+    ("qkv", 128, 0, 384, dict(split=True)),
+    ("merge+ln+res", 128, 0, 128, dict(ln=True, res=True)),
+    ("fc1+gelu [x|m]", 128, 128, 1024, dict(gelu=True)),
+    ("fc2+ln+res", 1024, 0, 128, dict(ln=True, res=True)),
+    ("gelu>fc2+ln+res", 1024, 0, 128, dict(ln=True, res=True, gelu_in=True)),
+]
+for name, k1, k2, n, kw in cases:
+    x1, x2 = r(M, k1), (r(M, k2) if k2 else None)
+    w = r(n, k1 + k2)
+    ln = (r(n), r(n), 1e-5) if kw.get("ln") else None
+    res = r(M, n) if kw.get("res") else None
+    call = lambda: K.fused_linear(x1, w, x2=x2, gelu=kw.get("gelu", False), ln=ln, residual=res,
+                                  split=kw.get("split", False), gelu_in=kw.get("gelu_in", False))
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize()
+    _lib.prof_enable("linear")
+    for _ in range(50):
+        call()
+    ms, cnt = _lib.prof_read()
+    _lib.prof_enable(None)
+    us = ms / cnt * 1e3
+    xx = torch.cat([x1, x2], -1) if k2 else x1
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        F.linear(xx, w)
+    e0.record()
+    for _ in range(50):
+        F.linear(xx, w)
+    e1.record()
+    torch.cuda.synchronize()
+    tus = e0.elapsed_time(e1) / 50 * 1e3
+    fl = 2.0 * M * (k1 + k2) * n
+    print(f"{name:16s} M={M} K={k1 + k2} N={n}: fused {us:6.1f} us ({fl / us / 1e6:5.1f} TF, "
+          f"{fl / us / 1e6 / 157.3 * 100:4.1f} %)   torch F.linear {tus:6.1f} us", flush=True)

@@ -56,6 +56,8 @@ SIGNATURES = {
     "tsplat_group_norm_fwd": (ctypes.c_int, [_P] * 7 + [_I32, _I32, ctypes.c_int64, _I32, ctypes.c_float, _I32, _P]),
     "tsplat_sh_rotation_fwd": (ctypes.c_int, [_P] * 3 + [_I32] * 2 + [_P]),
     "tsplat_gaussian_adapter_fwd": (ctypes.c_int, [_P] * 9 + [_I32] * 6 + [ctypes.c_float] * 3 + [_I32, _P]),
+    "tsplat_linear_f32_fwd": (ctypes.c_int, [_P, _I32, _P, _I32] + [_P] * 4 + [ctypes.c_float, _P, _P, ctypes.c_int64]
+                              + [_I32] * 3 + [_P]),
 }
 
 ERRORS = {-1: "invalid argument", -2: "HIP launch error"}
@@ -107,7 +109,7 @@ def stream_ptr(device: torch.device | None = None) -> int:
 
 PROF_IDS = {"raster_preprocess": 1, "raster_scan": 2, "raster_scatter": 3, "raster_render": 4,
             "uv_coarse": 5, "uv_cross": 6, "msda": 7, "win_attn": 8, "raster": 9,
-            "group_norm": 10, "uv_cross_table": 11}
+            "group_norm": 10, "uv_cross_table": 11, "linear": 12}
 
 
 def prof_enable(name: str | None) -> None:

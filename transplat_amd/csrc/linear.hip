@@ -1,0 +1,283 @@
+// Row-block fp32 GEMM with fused epilogues for the multi-view transformer's linears on gfx950.
+//
+// Semantics (reference TransformerLayer.forward, src/model/encoder/backbone/multiview_transformer.py
+// :327-407, single head, no biases): per layer
+//   q, k, v = x Wq^T, y Wk^T, y Wv^T                        (q_proj / k_proj / v_proj)
+//   m = norm1(attn Wmerge^T)                                 (merge + LayerNorm, eps 1e-5)
+//   self layer:      out = x + m
+//   cross/FFN layer: out = x + norm2(GELU([x | m] W1^T) W2^T) (mlp = Linear, exact GELU, Linear)
+// One launch computes out[M, N] = epilogue([x1 | x2] W^T) with
+//   x1 [M, k1], x2 [M, k2] (the concatenation is never materialised), W [N, k1 + k2] (nn.Linear),
+//   epilogue = (+ bias) -> (exact-erf GELU) -> (LayerNorm over N = 128 with gamma / beta) ->
+//   (+ residual [M, N]); "split" writes column block j of 128 to out + j * split_stride.
+// Replaces per layer up to 11 PyTorch launches (3-4 hipBLASLt GEMMs, cat, GELU, 2 LayerNorms, add).
+//
+// Kernel: one workgroup = 4 waves = BM (32 or 64) rows x 128 columns; wave w owns columns
+// [32 w, 32 w + 32) as BM / 32 v_mfma_f32_32x32x2_f32 accumulators (exact fp32). A = W (MFMA rows =
+// output columns), B = X^T (MFMA columns = output rows), so lane (m, h) ends with 16 columns of ONE
+// output row per accumulator: the row-wise LayerNorm needs only in-lane sums, one half-wave swap
+// and a 4-wave LDS exchange. K is walked in 64-wide chunks staged through LDS (rows XOR-swizzled
+// per 16-B chunk, ping-pong buffers) with two register stages in flight (see linear_f32_kernel).
+#include "common.h"
+#include "prof.h"
+
+namespace tsplat {
+namespace linear {
+
+constexpr int kBN = 128;  // columns per workgroup
+constexpr int kBK = 64;   // K chunk
+constexpr int kThreads = 512;  // 8 waves: two per SIMD
+
+enum Flags : int { kGelu = 1, kLayerNorm = 2, kResidual = 4, kSplit = 8, kBias = 16, kGeluIn = 32 };
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+struct Args {
+    const float* x1;
+    const float* x2;
+    const float* w;
+    const float* bias;
+    const float* gamma;
+    const float* beta;
+    const float* res;
+    float* out;
+    long long split_stride;
+    float eps;
+    int k1, k2, M, N, flags;
+};
+
+__device__ __forceinline__ float halves_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// One K chunk in flight in registers: thread = 16-B chunk (tid & 15) of rows (tid >> 4) + 32 i.
+template <int BM>
+struct Stage {
+    floatx4 x[BM / 32], w[kBN / 32];
+};
+
+template <int BM>
+__device__ __forceinline__ void stage_load(const Args& a, int m0, int n0, int K, int ck, int tid, Stage<BM>& st) {
+    const int srow = tid >> 4, sq = tid & 15;
+    const int k0 = ck * kBK;
+    const bool first = k0 < a.k1;
+    const float* xs = first ? a.x1 : a.x2;
+    const int ld = first ? a.k1 : a.k2, kk = first ? k0 : k0 - a.k1;
+#pragma unroll
+    for (int i = 0; i < BM / 32; ++i) {
+        const int m = m0 + srow + 32 * i;
+        st.x[i] = m < a.M ? *reinterpret_cast<const floatx4*>(xs + (size_t)m * ld + kk + 4 * sq) : (floatx4)(0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < kBN / 32; ++i)
+        st.w[i] = *reinterpret_cast<const floatx4*>(a.w + (size_t)(n0 + srow + 32 * i) * K + k0 + 4 * sq);
+}
+
+template <int BM>
+__device__ __forceinline__ void stage_store(float* sX, float* sW, int tid, const Stage<BM>& st, bool gelu_in) {
+    const int srow = tid >> 4, sq = tid & 15;
+#pragma unroll
+    for (int i = 0; i < BM / 32; ++i) {
+        const int r = srow + 32 * i;
+        floatx4 x = st.x[i];
+        if (gelu_in) x = (floatx4){gelu_erf(x.x), gelu_erf(x.y), gelu_erf(x.z), gelu_erf(x.w)};
+        *reinterpret_cast<floatx4*>(&sX[r * kBK + ((sq ^ (r & 15)) * 4)]) = x;
+    }
+#pragma unroll
+    for (int i = 0; i < kBN / 32; ++i) {
+        const int r = srow + 32 * i;
+        *reinterpret_cast<floatx4*>(&sW[r * kBK + ((sq ^ (r & 15)) * 4)]) = st.w[i];
+    }
+}
+
+// The k-steps of one chunk this wave owns: k-step t contracts chunk channels {t, 32 + t} (lane
+// half h supplies channel 32 h + t), t in [8 q0, 8 q0 + 8 NQ) in 16-B units; rows xr0 .. xr0 + 31
+template <int NQ>
+__device__ __forceinline__ void chunk_mfma(const float* sX, const float* sW, int wrow, int xr, int h, int q0,
+                                           floatx16& acc) {
+    auto rd = [&](const float* base, int row, int q4) {
+        const int lq = 8 * h + q0 + q4;  // logical 16-B chunk
+        return *reinterpret_cast<const floatx4*>(&base[row * kBK + ((lq ^ (row & 15)) * 4)]);
+    };
+    floatx4 wn = rd(sW, wrow, 0), xn = rd(sX, xr, 0);
+#pragma unroll
+    for (int q4 = 0; q4 < NQ; ++q4) {
+        // the next 16-B operands are read before this unit's four MFMAs
+        const floatx4 wa = wn, xb = xn;
+        if (q4 + 1 < NQ) {
+            wn = rd(sW, wrow, q4 + 1);
+            xn = rd(sX, xr, q4 + 1);
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the MFMAs (no re-sinking)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.x, xb.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.y, xb.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.z, xb.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wa.w, xb.w, acc, 0, 0, 0);
+    }
+}
+
+// 8 waves = 4 column blocks of 32 x 2. BM = 64: the second index is the row half (each wave one
+// 32x32 accumulator over all of K). BM = 32 (grids too small to fill the chip with 64-row
+// blocks): the second index is a K half inside every chunk, the halves are summed through LDS
+// before the epilogue. Pipeline: LDS ping-pong (one barrier per chunk) and two register stages,
+// so chunk t+2's global loads are issued before chunk t's MFMAs and stored to LDS only after
+// chunk t+1's; the loop is unrolled by two so every register stage index is static.
+template <int BM>
+__global__ void __launch_bounds__(kThreads)
+linear_f32_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) float sX[2][BM * kBK];
+    __shared__ __attribute__((aligned(16))) float sW[2][kBN * kBK];
+    __shared__ float sRed[4][BM];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const int cb = wid & 3, sel = wid >> 2;  // column block, row half (BM 64) or K half (BM 32)
+    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * kBN;
+    const int K = a.k1 + a.k2;
+    const int nchunks = K / kBK;
+    const int wrow = 32 * cb + c;                     // this lane's W row (output column)
+    const int xr = BM == 64 ? 32 * sel + c : c;       // this lane's X row
+    const int q0 = BM == 64 ? 0 : 4 * sel;            // first 16-B unit of the wave's k-steps
+    constexpr int NQ = BM == 64 ? 8 : 4;
+    const bool gelu_in = a.flags & kGeluIn;  // GELU of the producing layer applied to X on its way to LDS
+
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    Stage<BM> s0, s1;
+    stage_load<BM>(a, m0, n0, K, 0, tid, s0);
+    if (nchunks > 1) stage_load<BM>(a, m0, n0, K, 1, tid, s1);
+    stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in);
+    __syncthreads();
+    for (int ck = 0; ck < nchunks; ck += 2) {
+        // even chunk ck (buffer 0); s1 holds chunk ck + 1, s0 is free
+        if (ck + 2 < nchunks) stage_load<BM>(a, m0, n0, K, ck + 2, tid, s0);
+        chunk_mfma<NQ>(sX[0], sW[0], wrow, xr, h, q0, acc);
+        if (ck + 1 >= nchunks) break;
+        stage_store<BM>(sX[1], sW[1], tid, s1, gelu_in);
+        __syncthreads();
+        // odd chunk ck + 1 (buffer 1); s0 holds chunk ck + 2, s1 is free
+        if (ck + 3 < nchunks) stage_load<BM>(a, m0, n0, K, ck + 3, tid, s1);
+        chunk_mfma<NQ>(sX[1], sW[1], wrow, xr, h, q0, acc);
+        if (ck + 2 >= nchunks) break;
+        stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in);
+        __syncthreads();
+    }
+    __syncthreads();  // every wave is done with the LDS tiles
+    if (BM == 32) {   // sum the two K halves: waves 4..7 hand their accumulators to waves 0..3
+        float* park = sW[0] + cb * 16 * 64;
+        if (sel == 1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) park[r * 64 + lane] = acc[r];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[r] += park[r * 64 + lane];
+    }
+    // BM = 32: waves 4..7 stay (for the barriers below) but store nothing
+    const bool active = BM == 64 || sel == 0;
+
+    // acc[r] = Y[row m0 + mr][column n0 + 32 cb + 8 (r >> 2) + 4 h + (r & 3)]. LayerNorm row
+    // statistics: the 4 column-block waves of a row group exchange partial sums through sRed.
+    const int nb = n0 + 32 * cb + 4 * h;
+    const int mr = xr;
+    const int m = m0 + mr;
+    floatx16& y = acc;
+    if (a.flags & kBias) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const floatx4 b = *reinterpret_cast<const floatx4*>(a.bias + nb + 8 * u);
+            y[4 * u] += b.x;
+            y[4 * u + 1] += b.y;
+            y[4 * u + 2] += b.z;
+            y[4 * u + 3] += b.w;
+        }
+    }
+    if (a.flags & kGelu) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) y[r] = gelu_erf(y[r]);
+    }
+    if (a.flags & kLayerNorm) {  // N == 128: the workgroup holds whole rows
+        float s = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s += y[r];
+        s = halves_sum(s);
+        if (h == 0 && active) sRed[cb][mr] = s;
+        __syncthreads();
+        const float mean = (sRed[0][mr] + sRed[1][mr] + sRed[2][mr] + sRed[3][mr]) * (1.0f / kBN);
+        __syncthreads();
+        float v = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float d = y[r] - mean;
+            v += d * d;
+        }
+        v = halves_sum(v);
+        if (h == 0 && active) sRed[cb][mr] = v;
+        __syncthreads();
+        const float var = (sRed[0][mr] + sRed[1][mr] + sRed[2][mr] + sRed[3][mr]) * (1.0f / kBN);
+        const float rstd = rsqrtf(var + a.eps);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const floatx4 g = *reinterpret_cast<const floatx4*>(a.gamma + nb + 8 * u);
+            const floatx4 bt = *reinterpret_cast<const floatx4*>(a.beta + nb + 8 * u);
+            y[4 * u] = (y[4 * u] - mean) * rstd * g.x + bt.x;
+            y[4 * u + 1] = (y[4 * u + 1] - mean) * rstd * g.y + bt.y;
+            y[4 * u + 2] = (y[4 * u + 2] - mean) * rstd * g.z + bt.z;
+            y[4 * u + 3] = (y[4 * u + 3] - mean) * rstd * g.w + bt.w;
+        }
+    }
+    if (!active || m >= a.M) return;
+    float* dst;
+    int col0;
+    if (a.flags & kSplit) {  // column block j of 128 -> its own [M, 128] matrix
+        dst = a.out + (size_t)(nb / kBN) * a.split_stride + (size_t)m * kBN;
+        col0 = nb % kBN;
+    } else {
+        dst = a.out + (size_t)m * a.N;
+        col0 = nb;
+    }
+    const float* res = (a.flags & kResidual) ? a.res + (size_t)m * a.N : nullptr;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        floatx4 o = {y[4 * u], y[4 * u + 1], y[4 * u + 2], y[4 * u + 3]};
+        if (res) o += *reinterpret_cast<const floatx4*>(res + nb + 8 * u);
+        *reinterpret_cast<floatx4*>(dst + col0 + 8 * u) = o;
+    }
+}
+
+}  // namespace linear
+}  // namespace tsplat
+
+using namespace tsplat;
+
+extern "C" int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x2, int32_t k2, const float* w,
+                                     const float* bias, const float* ln_gamma, const float* ln_beta,
+                                     float ln_eps, const float* residual, float* out, int64_t split_stride,
+                                     int32_t M, int32_t N, int32_t flags, void* stream_) {
+    using namespace tsplat::linear;
+    if (!x1 || !w || !out || M <= 0 || N <= 0 || k1 <= 0 || k2 < 0) return TSPLAT_EINVAL;
+    if (k1 % kBK || k2 % kBK || N % kBN || (k2 > 0 && !x2)) return TSPLAT_EINVAL;
+    if ((flags & kGeluIn) && N != kBN) return TSPLAT_EINVAL;  // each X element staged exactly once
+    if ((flags & kBias) && !bias) return TSPLAT_EINVAL;
+    if ((flags & kLayerNorm) && (N != kBN || !ln_gamma || !ln_beta)) return TSPLAT_EINVAL;
+    if ((flags & kResidual) && (!residual || (flags & kSplit))) return TSPLAT_EINVAL;
+    if ((flags & kSplit) && split_stride < (int64_t)M * kBN) return TSPLAT_EINVAL;
+    Args a{x1, x2, w, bias, ln_gamma, ln_beta, residual, out, split_stride, ln_eps, k1, k2, M, N, flags};
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(prof::kLinear, stream);
+    // 64-row blocks when that still fills the 256 CUs, else 32-row blocks with the K halves split
+    // over the wave pairs (a 128-column GEMM of 8,192 rows: 256 workgroups)
+    const bool tall = (long long)((M + 63) / 64) * (N / kBN) >= 256;
+    if (tall)
+        hipLaunchKernelGGL(linear_f32_kernel<64>, dim3((M + 63) / 64, N / kBN), dim3(kThreads), 0, stream, a);
+    else
+        hipLaunchKernelGGL(linear_f32_kernel<32>, dim3((M + 31) / 32, N / kBN), dim3(kThreads), 0, stream, a);
+    TSPLAT_PROF_END(prof::kLinear, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

@@ -20,7 +20,8 @@ enum KernelId : int {
     kRasterAll = 9,   // the whole tsplat_raster_fwd launch sequence
     kGroupNorm = 10,  // both launches of tsplat_group_norm_fwd
     kUvCrossTable = 11,
-    kNumKernels = 12,
+    kLinear = 12,     // tsplat_linear_f32_fwd
+    kNumKernels = 13,
 };
 
 int active();                 // kernel id being timed (0 = off)

@@ -158,6 +158,50 @@ def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", 
     return y
 
 
+_LIN_GELU, _LIN_LN, _LIN_RES, _LIN_SPLIT, _LIN_BIAS, _LIN_GELU_IN = 1, 2, 4, 8, 16, 32
+
+
+def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, residual=None, split: bool = False,
+                 gelu_in: bool = False):
+    """epilogue([x1 | x2] weight^T) in one exact-fp32 MFMA launch (tsplat_linear_f32_fwd):
+    (+ bias) -> (exact GELU) -> (LayerNorm with ln = (gamma, beta, eps), N = 128) -> (+ residual);
+    gelu_in applies exact GELU to the input first (the producing layer's activation, N = 128).
+    x1 [..., k1], x2 [..., k2] (concatenated along the last axis without materialising it);
+    split=True returns the N / 128 column blocks as separate contiguous [..., 128] tensors."""
+    lib = _lib.load()
+    lead = x1.shape[:-1]
+    k1 = x1.shape[-1]
+    k2 = x2.shape[-1] if x2 is not None else 0
+    n = weight.shape[0]
+    if weight.shape[1] != k1 + k2:
+        raise ValueError(f"weight {tuple(weight.shape)} does not match k1 + k2 = {k1 + k2}")
+    a = _f32(x1).reshape(-1, k1)
+    m = a.shape[0]
+    b = _f32(x2).reshape(-1, k2) if x2 is not None else None
+    if b is not None and b.shape[0] != m:
+        raise ValueError("x1 and x2 row counts differ")
+    flags = (_LIN_GELU if gelu else 0) | (_LIN_LN if ln is not None else 0) | (_LIN_BIAS if bias is not None else 0)
+    flags |= _LIN_GELU_IN if gelu_in else 0
+    res = None
+    if residual is not None:
+        res = _f32(residual).reshape(m, n)
+        flags |= _LIN_RES
+    if split:
+        flags |= _LIN_SPLIT
+        out = torch.empty((n // 128, m, 128), dtype=torch.float32, device=x1.device)
+    else:
+        out = torch.empty((m, n), dtype=torch.float32, device=x1.device)
+    g, bt, eps = (_f32(ln[0]), _f32(ln[1]), float(ln[2])) if ln is not None else (None, None, 0.0)
+    bb = _f32(bias) if bias is not None else None
+    rc = lib.tsplat_linear_f32_fwd(_lib.ptr(a), k1, _lib.ptr(b), k2, _lib.ptr(_f32(weight)), _lib.ptr(bb),
+                                   _lib.ptr(g), _lib.ptr(bt), eps, _lib.ptr(res), _lib.ptr(out), m * 128, m, n,
+                                   flags, _lib.stream_ptr(x1.device))
+    _lib.check(rc, "tsplat_linear_f32_fwd")
+    if split:
+        return [t.reshape(*lead, 128) for t in out.unbind(0)]
+    return out.reshape(*lead, n)
+
+
 def sh_rotation(rotations, d_sh: int):
     """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
     wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""

@@ -40,8 +40,42 @@ class TransformerLayer(nn.Module):
             )
             self.norm2 = nn.LayerNorm(d_model)
 
+    def _cat_weights(self, names: tuple[str, ...]) -> torch.Tensor:
+        """[len(names) * d, d] concatenation of projection weights, cached until a weight changes
+        (one fused launch computes q, k, v / k, v)."""
+        ws = [getattr(self, n).weight for n in names]
+        key = tuple((w.data_ptr(), w._version) for w in ws)
+        cache = self.__dict__.setdefault("_wcat", {})
+        hit = cache.get(names)
+        if hit is None or hit[0] != key:
+            hit = (key, torch.cat([w.detach() for w in ws], dim=0).contiguous())
+            cache[names] = hit
+        return hit[1]
+
+    def _forward_fused(self, source, target, height, width, attn_num_splits):
+        """fp32 path: 4-5 kernels.fused_linear launches (exact fp32 MFMA, epilogues fused) around
+        the attention kernel instead of ~12 PyTorch launches; same math as forward() below."""
+        K = kernels
+        if target is source:
+            query, key, value = K.fused_linear(source, self._cat_weights(("q_proj", "k_proj", "v_proj")), split=True)
+        else:
+            query = K.fused_linear(source, self.q_proj.weight)
+            key, value = K.fused_linear(target, self._cat_weights(("k_proj", "v_proj")), split=True)
+        message = K.window_attention(query, key, value, height, width, attn_num_splits, self.with_shift)
+        ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        if self.no_ffn:
+            return K.fused_linear(message, self.merge.weight, ln=ln1, residual=source)
+        message = K.fused_linear(message, self.merge.weight, ln=ln1)
+        # mlp[0] is the one large plain GEMM of the layer (8192 x 256 x 1024 at b = 1): hipBLASLt
+        # runs it at 103 TF, above this build's kernel (66 TF); its GELU moves into mlp[2]'s load
+        hidden = self.mlp[0](torch.cat([source, message], dim=-1))
+        ln2 = (self.norm2.weight, self.norm2.bias, self.norm2.eps)
+        return K.fused_linear(hidden, self.mlp[2].weight, ln=ln2, residual=source, gelu_in=True)
+
     def forward(self, source, target, height=None, width=None, attn_num_splits=None, **kwargs):
         # source [B, L, C]; target [B, L, C] (self) or [B, V-1, L, C] (cross)
+        if source.dtype == torch.float32 and self.dim == 128 and not torch.is_autocast_enabled(source.device.type):
+            return self._forward_fused(source, target, height, width, attn_num_splits)
         query = self.q_proj(source)
         key = self.k_proj(target)
         value = self.v_proj(target)
