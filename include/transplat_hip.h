@@ -205,6 +205,16 @@ int tsplat_win_attn_fwd(const float* q, const float* k, const float* v, float* o
                         int32_t batch, int32_t height, int32_t width, int32_t channels,
                         int32_t key_views, int32_t splits, int32_t with_shift, void* stream);
 
+/* Split-key form of the same attention for a consumer that folds the combine into its own
+ * prologue: tsplat_win_attn_split() returns the key split the 128-query kernel uses for the shape
+ * (> 1: split, 1: none, 0: another kernel serves it); tsplat_win_attn_partials_fwd runs only the
+ * main kernel and leaves the partials (unnormalised O, max in natural log, sum) in workspace
+ * (tsplat_win_attn_workspace_bytes bytes), for tsplat_linear_f32_attn_merge_fwd. */
+int32_t tsplat_win_attn_split(int32_t batch, int32_t height, int32_t width, int32_t key_views, int32_t splits);
+int tsplat_win_attn_partials_fwd(const float* q, const float* k, const float* v, void* workspace, int32_t batch,
+                                 int32_t height, int32_t width, int32_t channels, int32_t key_views,
+                                 int32_t splits, int32_t with_shift, void* stream);
+
 /* bf16 variant (config C3): q, k, v, out are bf16 (raw 16-bit storage), same layouts and
  * semantics; bf16 MFMA with fp32 accumulation and an fp32 softmax (P rounded to bf16 for the
  * PV product). Window pixels must be a multiple of 128. */
@@ -230,6 +240,17 @@ int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x2, int32_t 
                           const float* bias, const float* ln_gamma, const float* ln_beta, float ln_eps,
                           const float* residual, float* out, int64_t split_stride, int32_t M, int32_t N,
                           int32_t flags, void* stream);
+
+/* The merge projection of a transformer layer reading the attention output still split over
+ * key ranges: out = epilogue(combine(partials) w^T) with combine = sum_s e^(m_s - M) O_s /
+ * sum_s e^(m_s - M) l_s per query (the combine launch of tsplat_win_attn_fwd, moved into this
+ * kernel's operand staging). partials as left by tsplat_win_attn_partials_fwd for the same
+ * (batch, height, width, key_views, splits, with_shift); out [batch, height*width, N] in pixel
+ * order; w [N, 128]; flags as tsplat_linear_f32_fwd (2 LayerNorm, 4 residual; no 8/16/32). */
+int tsplat_linear_f32_attn_merge_fwd(const float* partials, int32_t batch, int32_t height, int32_t width,
+                                     int32_t key_views, int32_t splits, int32_t with_shift, const float* w,
+                                     const float* ln_gamma, const float* ln_beta, float ln_eps,
+                                     const float* residual, float* out, int32_t N, int32_t flags, void* stream);
 
 #ifdef __cplusplus
 }

@@ -281,5 +281,12 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     return y
 
 
+def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, merge_weight, ln, residual=None):
+    """CPU restatement of kernels.attention_merge: window attention, merge Linear, LayerNorm,
+    optional residual (reference multiview_transformer.py:327-407)."""
+    msg = window_attention(q, k, v, h, w, num_splits, with_shift)
+    return fused_linear(msg, merge_weight, ln=ln, residual=residual)
+
+
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
-                       "sh_rotation", "fused_linear")
+                       "sh_rotation", "fused_linear", "attention_merge")

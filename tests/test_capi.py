@@ -13,7 +13,7 @@ def declared_symbols():
     names = set()
     for h in (ROOT / "include").glob("*.h"):
         text = h.read_text()
-        names |= set(re.findall(r"^\s*(?:int|size_t|void)\s+\**(tsplat_\w+)\s*\(", text, re.M))
+        names |= set(re.findall(r"^\s*(?:int|int32_t|int64_t|size_t|void)\s+\**(tsplat_\w+)\s*\(", text, re.M))
     return sorted(names)
 
 

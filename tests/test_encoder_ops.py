@@ -271,3 +271,28 @@ def test_fused_linear_kernel(device, m, k1, k2, n, gelu, ln, res, split, bias, g
         out, ref = torch.cat(out, -1), torch.cat(ref, -1)
     err = (out.cpu() - ref).abs().max().item()
     assert err < 2e-4 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,m,shift,b,res", [(64, 1, True, 2, True), (64, 1, False, 2, False), (64, 2, True, 3, True),
+                                              (32, 1, True, 2, False), (64, 1, True, 8, True)])
+def test_attention_merge_kernel(device, hw, m, shift, b, res):
+    """Window attention + merge Linear + LayerNorm (+ residual) with the split-key combine folded
+    into the merge kernel (tsplat_win_attn_partials_fwd + tsplat_linear_f32_attn_merge_fwd; key
+    splits 4 / 8 here, b = 8 takes the unsplit path) vs the CPU restatement."""
+    from transplat_amd import _lib
+    from transplat_amd import kernels as K
+
+    q = seeded((b, hw * hw, 128), 41)
+    k = seeded((b, m, hw * hw, 128), 42) if m > 1 else seeded((b, hw * hw, 128), 42)
+    v = seeded(k.shape, 43)
+    wm = seeded((128, 128), 44) / math.sqrt(128)
+    ln = (seeded((128,), 45) * 0.1 + 1.0, seeded((128,), 46) * 0.1, 1e-5)
+    r = seeded((b, hw * hw, 128), 47) if res else None
+    ks = int(_lib.load().tsplat_win_attn_split(b, hw, hw, m, 2))
+    assert (ks > 1) == (b < 8)
+    ref = E.attention_merge(q, k, v, hw, hw, 2, shift, wm, ln, residual=r)
+    d = lambda t: t.to(device) if t is not None else None
+    out = K.attention_merge(d(q), d(k), d(v), hw, hw, 2, shift, d(wm), (d(ln[0]), d(ln[1]), ln[2]), residual=d(r))
+    err = (out.cpu() - ref).abs().max().item()
+    assert err < 1e-3, err

@@ -47,7 +47,65 @@ struct Args {
     long long split_stride;
     float eps;
     int k1, k2, M, N, flags;
+    // X = combined split-key attention partials (tsplat_win_attn_partials_fwd layout), see
+    // tsplat_linear_f32_attn_merge_fwd: o / m / l arrays and the window geometry
+    const float* po;
+    const float* pm;
+    const float* pl;
+    int aks, aH, aW, aS, aL, awh, aww, ash, asw;
 };
+
+constexpr int kMaxSplit = 8;
+
+// Per-thread source of one X row when X is the attention output still split over key ranges:
+// float offset of (row, split 0, this query's lane) in o, the split stride, the combine weights
+struct AttnRow {
+    size_t obase;
+    float w[kMaxSplit];
+};
+
+__device__ __forceinline__ void attn_row(const Args& a, int m, AttnRow& r) {
+    const int HW = a.aH * a.aW;
+    const int b = m / HW, pix = m - b * HW;
+    const int y = pix / a.aW, x = pix - y * a.aW;
+    int Y = y - a.ash, X = x - a.asw;  // position on the rolled grid (the attention rolled by -shift)
+    if (Y < 0) Y += a.aH;
+    if (X < 0) X += a.aW;
+    const int sy = Y / a.awh, sx = X / a.aww;
+    const int wi = sy * a.aS + sx, t = (Y - sy * a.awh) * a.aww + (X - sx * a.aww);
+    const size_t win = (size_t)b * a.aS * a.aS + wi;
+    const int nqb = a.aL / 128;
+    r.obase = ((win * a.aks * nqb + (t >> 7)) * 128 + 32 * ((t >> 5) & 3)) * 128 + 4 * (t & 31);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int s = 0; s < kMaxSplit; ++s)
+        if (s < a.aks) mx = fmaxf(mx, a.pm[(win * a.aks + s) * a.aL + t]);
+    float L = 0.f;
+#pragma unroll
+    for (int s = 0; s < kMaxSplit; ++s) {
+        r.w[s] = 0.f;
+        if (s < a.aks) {
+            const size_t row = (win * a.aks + s) * a.aL + t;
+            r.w[s] = __expf(a.pm[row] - mx);
+            L += r.w[s] * a.pl[row];
+        }
+    }
+    const float inv = 1.0f / L;
+#pragma unroll
+    for (int s = 0; s < kMaxSplit; ++s) r.w[s] *= inv;
+}
+
+// channels k .. k+3 of the combined attention row: O^T[d][q] float4 (dt * 4 + u) * 64 + lane of
+// the wave slot holds d = 32 dt + 8 u + 4 h + (0..3) for lane = q + 32 h
+__device__ __forceinline__ floatx4 attn_x4(const Args& a, const AttnRow& r, int k) {
+    const size_t sstride = (size_t)(a.aL / 128) * 128 * 128;
+    const size_t off = r.obase + ((size_t)(((k >> 5) * 4 + ((k >> 3) & 3)) * 64 + 32 * ((k >> 2) & 1))) * 4;
+    floatx4 acc = (floatx4)(0.f);
+#pragma unroll
+    for (int s = 0; s < kMaxSplit; ++s)
+        if (s < a.aks) acc += r.w[s] * *reinterpret_cast<const floatx4*>(a.po + off + s * sstride);
+    return acc;
+}
 
 __device__ __forceinline__ float halves_sum(float x) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -60,17 +118,24 @@ struct Stage {
     floatx4 x[BM / 32], w[kBN / 32];
 };
 
-template <int BM>
-__device__ __forceinline__ void stage_load(const Args& a, int m0, int n0, int K, int ck, int tid, Stage<BM>& st) {
+template <int BM, bool ATTN>
+__device__ __forceinline__ void stage_load(const Args& a, int m0, int n0, int K, int ck, int tid, Stage<BM>& st,
+                                           const AttnRow (&ar)[BM / 32]) {
     const int srow = tid >> 4, sq = tid & 15;
     const int k0 = ck * kBK;
-    const bool first = k0 < a.k1;
-    const float* xs = first ? a.x1 : a.x2;
-    const int ld = first ? a.k1 : a.k2, kk = first ? k0 : k0 - a.k1;
+    if (ATTN) {
 #pragma unroll
-    for (int i = 0; i < BM / 32; ++i) {
-        const int m = m0 + srow + 32 * i;
-        st.x[i] = m < a.M ? *reinterpret_cast<const floatx4*>(xs + (size_t)m * ld + kk + 4 * sq) : (floatx4)(0.f);
+        for (int i = 0; i < BM / 32; ++i)
+            st.x[i] = m0 + srow + 32 * i < a.M ? attn_x4(a, ar[i], k0 + 4 * sq) : (floatx4)(0.f);
+    } else {
+        const bool first = k0 < a.k1;
+        const float* xs = first ? a.x1 : a.x2;
+        const int ld = first ? a.k1 : a.k2, kk = first ? k0 : k0 - a.k1;
+#pragma unroll
+        for (int i = 0; i < BM / 32; ++i) {
+            const int m = m0 + srow + 32 * i;
+            st.x[i] = m < a.M ? *reinterpret_cast<const floatx4*>(xs + (size_t)m * ld + kk + 4 * sq) : (floatx4)(0.f);
+        }
     }
 #pragma unroll
     for (int i = 0; i < kBN / 32; ++i)
@@ -126,7 +191,7 @@ __device__ __forceinline__ void chunk_mfma(const float* sX, const float* sW, int
 // before the epilogue. Pipeline: LDS ping-pong (one barrier per chunk) and two register stages,
 // so chunk t+2's global loads are issued before chunk t's MFMAs and stored to LDS only after
 // chunk t+1's; the loop is unrolled by two so every register stage index is static.
-template <int BM>
+template <int BM, bool ATTN>
 __global__ void __launch_bounds__(kThreads)
 linear_f32_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) float sX[2][BM * kBK];
@@ -149,19 +214,27 @@ linear_f32_kernel(Args a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     Stage<BM> s0, s1;
-    stage_load<BM>(a, m0, n0, K, 0, tid, s0);
-    if (nchunks > 1) stage_load<BM>(a, m0, n0, K, 1, tid, s1);
+    AttnRow ar[BM / 32];
+    if (ATTN) {
+#pragma unroll
+        for (int i = 0; i < BM / 32; ++i) {
+            const int m = m0 + (tid >> 4) + 32 * i;
+            if (m < a.M) attn_row(a, m, ar[i]);
+        }
+    }
+    stage_load<BM, ATTN>(a, m0, n0, K, 0, tid, s0, ar);
+    if (nchunks > 1) stage_load<BM, ATTN>(a, m0, n0, K, 1, tid, s1, ar);
     stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in);
     __syncthreads();
     for (int ck = 0; ck < nchunks; ck += 2) {
         // even chunk ck (buffer 0); s1 holds chunk ck + 1, s0 is free
-        if (ck + 2 < nchunks) stage_load<BM>(a, m0, n0, K, ck + 2, tid, s0);
+        if (ck + 2 < nchunks) stage_load<BM, ATTN>(a, m0, n0, K, ck + 2, tid, s0, ar);
         chunk_mfma<NQ>(sX[0], sW[0], wrow, xr, h, q0, acc);
         if (ck + 1 >= nchunks) break;
         stage_store<BM>(sX[1], sW[1], tid, s1, gelu_in);
         __syncthreads();
         // odd chunk ck + 1 (buffer 1); s0 holds chunk ck + 2, s1 is free
-        if (ck + 3 < nchunks) stage_load<BM>(a, m0, n0, K, ck + 3, tid, s1);
+        if (ck + 3 < nchunks) stage_load<BM, ATTN>(a, m0, n0, K, ck + 3, tid, s1, ar);
         chunk_mfma<NQ>(sX[1], sW[1], wrow, xr, h, q0, acc);
         if (ck + 2 >= nchunks) break;
         stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in);
@@ -268,15 +341,55 @@ extern "C" int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x
     if ((flags & kResidual) && (!residual || (flags & kSplit))) return TSPLAT_EINVAL;
     if ((flags & kSplit) && split_stride < (int64_t)M * kBN) return TSPLAT_EINVAL;
     Args a{x1, x2, w, bias, ln_gamma, ln_beta, residual, out, split_stride, ln_eps, k1, k2, M, N, flags};
+    a.po = a.pm = a.pl = nullptr;
     hipStream_t stream = (hipStream_t)stream_;
     TSPLAT_PROF_BEGIN(prof::kLinear, stream);
     // 64-row blocks when that still fills the 256 CUs, else 32-row blocks with the K halves split
     // over the wave pairs (a 128-column GEMM of 8,192 rows: 256 workgroups)
     const bool tall = (long long)((M + 63) / 64) * (N / kBN) >= 256;
     if (tall)
-        hipLaunchKernelGGL(linear_f32_kernel<64>, dim3((M + 63) / 64, N / kBN), dim3(kThreads), 0, stream, a);
+        hipLaunchKernelGGL((linear_f32_kernel<64, false>), dim3((M + 63) / 64, N / kBN), dim3(kThreads), 0, stream, a);
     else
-        hipLaunchKernelGGL(linear_f32_kernel<32>, dim3((M + 31) / 32, N / kBN), dim3(kThreads), 0, stream, a);
+        hipLaunchKernelGGL((linear_f32_kernel<32, false>), dim3((M + 31) / 32, N / kBN), dim3(kThreads), 0, stream, a);
+    TSPLAT_PROF_END(prof::kLinear, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int32_t tsplat_win_attn_split(int32_t batch, int32_t height, int32_t width, int32_t key_views,
+                                         int32_t splits);
+
+extern "C" int tsplat_linear_f32_attn_merge_fwd(const float* partials, int32_t batch, int32_t height, int32_t width,
+                                                int32_t key_views, int32_t splits, int32_t with_shift,
+                                                const float* w, const float* ln_gamma, const float* ln_beta,
+                                                float ln_eps, const float* residual, float* out, int32_t N,
+                                                int32_t flags, void* stream_) {
+    using namespace tsplat::linear;
+    if (!partials || !w || !out || N <= 0 || N % kBN) return TSPLAT_EINVAL;
+    const int ks = tsplat_win_attn_split(batch, height, width, key_views, splits);
+    if (ks <= 1 || ks > kMaxSplit) return TSPLAT_EINVAL;
+    if (flags & (kSplit | kGeluIn)) return TSPLAT_EINVAL;
+    if ((flags & kLayerNorm) && (N != kBN || !ln_gamma || !ln_beta)) return TSPLAT_EINVAL;
+    if ((flags & kResidual) && !residual) return TSPLAT_EINVAL;
+    if (flags & kBias) return TSPLAT_EINVAL;
+    const int M = batch * height * width;
+    Args a{nullptr, nullptr, w, nullptr, ln_gamma, ln_beta, residual, out, 0, ln_eps, kBN, 0, M, N, flags};
+    a.aks = ks;
+    a.aH = height;
+    a.aW = width;
+    a.aS = splits;
+    a.awh = height / splits;
+    a.aww = width / splits;
+    a.aL = a.awh * a.aww;
+    a.ash = with_shift ? a.awh / 2 : 0;
+    a.asw = with_shift ? a.aww / 2 : 0;
+    const size_t n = (size_t)batch * splits * splits * ks * a.aL;
+    a.po = partials;
+    a.pm = partials + n * kBN;
+    a.pl = a.pm + n;
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(prof::kLinear, stream);
+    hipLaunchKernelGGL((linear_f32_kernel<32, true>), dim3((M + 31) / 32, N / kBN), dim3(kThreads), 0, stream, a);
     TSPLAT_PROF_END(prof::kLinear, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

@@ -1453,6 +1453,58 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     return TSPLAT_OK;
 }
 
+// Key split the exact-fp32 128-query kernel uses for this launch shape (the same decision as
+// tsplat_win_attn_fwd): > 1 means the call runs main + combine and tsplat_win_attn_partials_fwd
+// may be used instead; 1 = no split; 0 = another kernel serves this shape.
+extern "C" int32_t tsplat_win_attn_split(int32_t batch, int32_t height, int32_t width, int32_t key_views,
+                                         int32_t splits) {
+    using namespace tsplat::winattn;
+    if (batch <= 0 || key_views <= 0 || splits <= 0 || height % splits || width % splits) return 0;
+    const int L = (height / splits) * (width / splits);
+    if (L % kBQ3 || (L * key_views) % kBK || getenv("TSPLAT_WINATTN")) return 0;
+    const int base = (L / kBQ3) * splits * splits * batch;
+    return pick_ksplit(base, L * key_views / kBK, kBQ3);
+}
+
+// The main kernel only: the split-key partials (O unnormalised, m in natural log, l) stay in
+// `workspace` for a consumer that folds the combine into its own prologue (the merge projection,
+// tsplat_linear_f32_attn_merge_fwd). Only for shapes where tsplat_win_attn_split() > 1.
+extern "C" int tsplat_win_attn_partials_fwd(const float* q, const float* k, const float* v, void* workspace,
+                                            int32_t batch, int32_t height, int32_t width, int32_t channels,
+                                            int32_t key_views, int32_t splits, int32_t with_shift, void* stream_) {
+    using namespace tsplat::winattn;
+    if (!q || !k || !v || !workspace || channels != kC) return TSPLAT_EINVAL;
+    const int ks = tsplat_win_attn_split(batch, height, width, key_views, splits);
+    if (ks <= 1) return TSPLAT_EINVAL;
+    Params p;
+    p.H = height;
+    p.W = width;
+    p.splits = splits;
+    p.m = key_views;
+    p.L = (height / splits) * (width / splits);
+    p.shift_h = with_shift ? (height / splits) / 2 : 0;
+    p.shift_w = with_shift ? (width / splits) / 2 : 0;
+    p.shift = with_shift ? 1 : 0;
+    p.wh = height / splits;
+    p.ww = width / splits;
+    p.ww_log2 = (p.ww & (p.ww - 1)) == 0 ? __builtin_ctz(p.ww) : -1;
+    if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
+    p.scale = 1.0f / sqrtf((float)kC);
+    p.ksplit = ks;
+    p.keys_per_split = p.L * p.m / p.ksplit;
+    const size_t n = (size_t)batch * splits * splits * p.ksplit * p.L;
+    Partials part{(float*)workspace, nullptr, nullptr};
+    part.m = part.o + n * kC;
+    part.l = part.m + n;
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
+    hipLaunchKernelGGL(win_attn_f32x32_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit), dim3(kThreads),
+                       0, stream, p, q, k, v, nullptr, part);
+    TSPLAT_PROF_END(prof::kWinAttn, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
 extern "C" size_t tsplat_win_attn_bf16_workspace_bytes(int32_t batch, int32_t height, int32_t width,
                                                        int32_t key_views, int32_t splits) {
     using namespace tsplat::winattn;

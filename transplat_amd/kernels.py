@@ -202,6 +202,41 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     return out.reshape(*lead, n)
 
 
+def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, merge_weight, ln, residual=None):
+    """norm(window_attention(q, k, v) merge_weight^T) [+ residual] for the fp32 transformer layer.
+    Where the attention kernel splits the keys (b = 1 at 64x64), the combine of its partials runs
+    in the merge kernel's operand staging (tsplat_win_attn_partials_fwd +
+    tsplat_linear_f32_attn_merge_fwd: no combine launch, no [B, L, 128] attention output);
+    otherwise window_attention + fused_linear."""
+    lib = _lib.load()
+    b, l, c = q.shape
+    m = 1 if k.dim() == 3 else k.shape[1]
+    fp32 = q.dtype == k.dtype == v.dtype == torch.float32
+    ks = int(lib.tsplat_win_attn_split(b, h, w, m, num_splits)) if fp32 and c == 128 else 0
+    if ks <= 1:
+        msg = window_attention(q, k, v, h, w, num_splits, with_shift)
+        return fused_linear(msg, merge_weight, ln=ln, residual=residual)
+    q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+    ws = torch.empty(int(lib.tsplat_win_attn_workspace_bytes(b, h, w, m, num_splits)), dtype=torch.uint8,
+                     device=q.device)
+    rc = lib.tsplat_win_attn_partials_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(ws), b, h, w, c, m,
+                                          num_splits, int(with_shift), _lib.stream_ptr(q.device))
+    _lib.check(rc, "tsplat_win_attn_partials_fwd")
+    n = merge_weight.shape[0]
+    out = torch.empty((b, l, n), dtype=torch.float32, device=q.device)
+    flags = _LIN_LN if ln is not None else 0
+    res = None
+    if residual is not None:
+        res = _f32(residual)
+        flags |= _LIN_RES
+    g, bt, eps = (_f32(ln[0]), _f32(ln[1]), float(ln[2])) if ln is not None else (None, None, 0.0)
+    rc = lib.tsplat_linear_f32_attn_merge_fwd(_lib.ptr(ws), b, h, w, m, num_splits, int(with_shift),
+                                              _lib.ptr(_f32(merge_weight)), _lib.ptr(g), _lib.ptr(bt), eps,
+                                              _lib.ptr(res), _lib.ptr(out), n, flags, _lib.stream_ptr(q.device))
+    _lib.check(rc, "tsplat_linear_f32_attn_merge_fwd")
+    return out
+
+
 def sh_rotation(rotations, d_sh: int):
     """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
     wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""

@@ -61,11 +61,12 @@ class TransformerLayer(nn.Module):
         else:
             query = K.fused_linear(source, self.q_proj.weight)
             key, value = K.fused_linear(target, self._cat_weights(("k_proj", "v_proj")), split=True)
-        message = K.window_attention(query, key, value, height, width, attn_num_splits, self.with_shift)
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
         if self.no_ffn:
-            return K.fused_linear(message, self.merge.weight, ln=ln1, residual=source)
-        message = K.fused_linear(message, self.merge.weight, ln=ln1)
+            return K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
+                                     self.merge.weight, ln1, residual=source)
+        message = K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
+                                    self.merge.weight, ln1)
         # mlp[0] is the one large plain GEMM of the layer (8192 x 256 x 1024 at b = 1): hipBLASLt
         # runs it at 103 TF, above this build's kernel (66 TF); its GELU moves into mlp[2]'s load
         hidden = self.mlp[0](torch.cat([source, message], dim=-1))
