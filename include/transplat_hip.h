@@ -252,6 +252,11 @@ int tsplat_linear_f32_attn_merge_fwd(const float* partials, int32_t batch, int32
                                      const float* ln_gamma, const float* ln_beta, float ln_eps,
                                      const float* residual, float* out, int32_t N, int32_t flags, void* stream);
 
+/* Batched inverse of n row-major dim x dim fp32 matrices (dim 2..4): the camera algebra's
+ * torch.inverse calls (reference depth_predictor_trans.py:36-49,88-98, encoder_trans.py:181-190,
+ * cuda_splatting.py:93-96), Gauss-Jordan with partial pivoting, one thread per matrix. */
+int tsplat_small_inverse(const float* in, float* out, int32_t n, int32_t dim, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -296,3 +296,24 @@ def test_attention_merge_kernel(device, hw, m, shift, b, res):
     out = K.attention_merge(d(q), d(k), d(v), hw, hw, 2, shift, d(wm), (d(ln[0]), d(ln[1]), ln[2]), residual=d(r))
     err = (out.cpu() - ref).abs().max().item()
     assert err < 1e-3, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d", [2, 3, 4])
+def test_small_inverse_kernel(device, d):
+    """tsplat_small_inverse vs float64 torch.linalg.inv on camera-like matrices (rigid c2w with
+    translation, normalised / pixel intrinsics) and random well-conditioned ones, incl. rows that
+    need pivoting."""
+    from transplat_amd import kernels as K
+
+    g = torch.Generator().manual_seed(d)
+    a = torch.randn((257, d, d), generator=g) + 3.0 * torch.eye(d)
+    a[::7] = a[::7].flip(-2)  # zero-free but pivot-requiring row orders
+    if d >= 3:
+        k = torch.eye(d).repeat(16, 1, 1)
+        k[:, 0, 0], k[:, 1, 1], k[:, 0, 2], k[:, 1, 2] = 250.0, 260.0, 128.0, 127.5
+        a = torch.cat([a, k])
+    ref = torch.linalg.inv(a.double())
+    out = K.small_inverse(a.to(device)).cpu().double()
+    rel = ((out - ref).abs().amax((-2, -1)) / ref.abs().amax((-2, -1))).max().item()
+    assert rel < 1e-5, rel

@@ -8,6 +8,7 @@ from __future__ import annotations
 import torch
 from einops import einsum
 from torch import Tensor
+from .. import kernels
 
 
 def homogenize_points(points: Tensor) -> Tensor:
@@ -28,7 +29,7 @@ def transform_cam2world(homogeneous_coordinates: Tensor, extrinsics: Tensor) -> 
 
 def unproject(coordinates: Tensor, z: Tensor, intrinsics: Tensor) -> Tensor:
     coordinates = homogenize_points(coordinates)
-    ray_directions = einsum(intrinsics.inverse(), coordinates, "... i j, ... j -> ... i")
+    ray_directions = einsum(kernels.small_inverse(intrinsics), coordinates, "... i j, ... j -> ... i")
     return ray_directions * z[..., None]
 
 
@@ -67,7 +68,7 @@ def _edge_midpoints(device) -> Tensor:
 
 def get_fov(intrinsics: Tensor) -> Tensor:
     """(reference projection.py:233-247) fov from K^-1 applied to the edge midpoints."""
-    intrinsics_inv = torch.linalg.inv_ex(intrinsics)[0]
+    intrinsics_inv = kernels.small_inverse(intrinsics)
     mids = _edge_midpoints(intrinsics.device)
 
     def process_vector(i):

@@ -16,12 +16,28 @@ def _f32(t: torch.Tensor) -> torch.Tensor:
     return t.contiguous()
 
 
+def small_inverse(x: torch.Tensor) -> torch.Tensor:
+    """Inverse of [..., d, d] (d = 2, 3, 4) camera matrices. Device tensors: one HIP launch
+    (tsplat_small_inverse) instead of rocsolver's getrf/getri chain. Host tensors (camera setup
+    from host data, e.g. the CPU oracle path or dataset prep) use torch.linalg on the host."""
+    if not x.is_cuda:
+        return torch.linalg.inv_ex(x)[0]
+    lib = _lib.load()
+    d = x.shape[-1]
+    xf = _f32(x)
+    out = torch.empty_like(xf)
+    n = xf.numel() // (d * d)
+    _lib.check(lib.tsplat_small_inverse(_lib.ptr(xf), _lib.ptr(out), n, d, _lib.stream_ptr(x.device)),
+               "tsplat_small_inverse")
+    return out.to(x.dtype) if x.dtype != torch.float32 else out
+
+
 def pack_cameras(intr: torch.Tensor, pose: torch.Tensor) -> torch.Tensor:
     """[N, 30] = K^-1, K, R, t per (v b) camera (the inputs of calculate_grid,
     reference depth_predictor_trans.py:36-49, with K^-1 taken by torch.inverse as there)."""
     intr = intr.float()
     return torch.cat(
-        [torch.linalg.inv_ex(intr)[0].reshape(-1, 9), intr.reshape(-1, 9), pose[:, :3, :3].reshape(-1, 9).float(),
+        [small_inverse(intr).reshape(-1, 9), intr.reshape(-1, 9), pose[:, :3, :3].reshape(-1, 9).float(),
          pose[:, :3, 3].float()], dim=1).contiguous()
 
 
@@ -127,8 +143,8 @@ def adapter_cameras(extrinsics: torch.Tensor, intrinsics: torch.Tensor, image_sh
     h, w = image_shape
     ext = extrinsics.reshape(-1, 4, 4).float()
     k = intrinsics.reshape(-1, 3, 3).float()
-    kinv = torch.linalg.inv_ex(k)[0]
-    k2inv = torch.linalg.inv_ex(k[:, :2, :2])[0]
+    kinv = small_inverse(k)
+    k2inv = small_inverse(k[:, :2, :2].contiguous())
     pix = torch.stack([torch.full_like(k[:, 0, 0], 1.0 / w), torch.full_like(k[:, 0, 0], 1.0 / h)], -1)
     mult = 0.1 * (k2inv @ pix[..., None])[..., 0].sum(-1)
     return torch.cat([ext[:, :3, :3].reshape(-1, 9), ext[:, :3, 3], kinv.reshape(-1, 9), mult[:, None]], 1).contiguous()

@@ -14,6 +14,7 @@ from math import isqrt
 import torch
 from torch import Tensor
 
+from ... import kernels
 from ... import _lib
 from ...geometry.projection import get_fov
 
@@ -75,7 +76,7 @@ def prepare_cameras(
     tan_fov_x = (0.5 * fov_x).tan()
     tan_fov_y = (0.5 * fov_y).tan()
     projection_matrix = get_projection_matrix(near, far, fov_x, fov_y).transpose(1, 2)
-    view_matrix = torch.linalg.inv_ex(extrinsics)[0].transpose(1, 2)
+    view_matrix = kernels.small_inverse(extrinsics).transpose(1, 2)
     full_projection = view_matrix @ projection_matrix
     v = extrinsics.shape[0]
     return RasterCameras(

@@ -47,7 +47,7 @@ class GaussianAdapter(nn.Module):
                                         opacity_exponent, gaussians_per_pixel)
 
     def get_scale_multiplier(self, intrinsics, pixel_size, multiplier: float = 0.1):
-        xy_multipliers = multiplier * einsum(intrinsics[..., :2, :2].inverse(), pixel_size, "... i j, j -> ... i")
+        xy_multipliers = multiplier * einsum(kernels.small_inverse(intrinsics[..., :2, :2].contiguous()), pixel_size, "... i j, j -> ... i")
         return xy_multipliers.sum(dim=-1)
 
     @property

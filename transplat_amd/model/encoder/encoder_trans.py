@@ -18,6 +18,7 @@ import torch.nn.functional as F
 from einops import rearrange
 from torch import nn
 
+from ... import kernels
 from ..depth_anything.dpt import DepthAnythingV2
 from ..types import Gaussians
 from .backbone.backbone_multiview import BackboneMultiview
@@ -124,7 +125,7 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
             intr_curr[:, :, 1, :] *= float(h)
             camk = torch.eye(4, device=device).view(1, 1, 4, 4).repeat(b, v, 1, 1).float()
             camk[:, :, :3, :3] = intr_curr
-            img2world = torch.matmul(context["extrinsics"].clone().detach(), torch.linalg.inv_ex(camk)[0])
+            img2world = torch.matmul(context["extrinsics"].clone().detach(), kernels.small_inverse(camk))
 
         with bench("encoder_2_backbone"), self._dense():
             trans_features, cnn_features = self.backbone(context["image"], attn_splits=self.cfg.multiview_trans_attn_split,

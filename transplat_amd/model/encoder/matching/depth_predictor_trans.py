@@ -12,6 +12,7 @@ import torch.nn.functional as F
 from einops import rearrange, repeat
 from torch import nn
 
+from .... import kernels
 from ...utils.cam_param_encoder import cam_param_encoder
 from ...utils.uv_transformer import UVTransformer
 from .ldm_unet import UNetModel, run_sequential
@@ -31,14 +32,14 @@ def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, nu
         # features[:, cur_view_order] as a roll (list indexing is a host copy: not graph-capturable)
         feat_lists.append(rearrange(torch.roll(features, -idx, dims=1), "b v ... -> (v b) ..."))
         if v > 2:
-            cur = [torch.linalg.inv_ex(extrinsics[:, v1].clone().detach())[0] @ extrinsics[:, v0].clone().detach()
+            cur = [kernels.small_inverse(extrinsics[:, v1].clone().detach()) @ extrinsics[:, v0].clone().detach()
                    for v0, v1 in zip(init_view_order, cur_view_order)]
             pose_curr_lists.append(torch.cat(cur, dim=0))
     if v == 2:
         pose_ref = extrinsics[:, 0].clone().detach()
         pose_tgt = extrinsics[:, 1].clone().detach()
-        pose = torch.linalg.inv_ex(pose_tgt)[0] @ pose_ref
-        pose_curr_lists = [torch.cat((pose, torch.linalg.inv_ex(pose)[0]), dim=0)]
+        pose = kernels.small_inverse(pose_tgt) @ pose_ref
+        pose_curr_lists = [torch.cat((pose, kernels.small_inverse(pose)), dim=0)]
     intr_curr = intrinsics[:, :, :3, :3].clone().detach()
     intr_curr[:, :, 0, :] *= float(w)
     intr_curr[:, :, 1, :] *= float(h)
@@ -113,7 +114,7 @@ class DepthPredictorTrans(nn.Module):
             camk = torch.eye(4, device=intr_curr.device).view(1, 4, 4).repeat(intr_curr.shape[0], 1, 1).float()
             camk[:, :3, :3] = intr_curr
             c2w = rearrange(extrinsics.clone().detach(), "b v ... -> (v b) ...", b=b, v=v)
-            img2world = torch.matmul(c2w, torch.linalg.inv_ex(camk)[0]).reshape(-1, 16)
+            img2world = torch.matmul(c2w, kernels.small_inverse(camk)).reshape(-1, 16)
         pos_feature = self.cam_param_encoder(dino_feature, img2world)  # [(v b), C, h, w]
         # (b v)-ordered channel-last query positions: the reference's bev_pos after its permutes
         bev_pos = rearrange(pos_feature, "(v b) c h w -> (b v) (h w) c", v=v, b=b)
