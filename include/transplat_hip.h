@@ -159,7 +159,10 @@ int tsplat_sh_rotation_fwd(const float* rotations, const double* basis, float* o
 
 /* GroupNorm over NCHW fp32 with the producing convolution's bias, the following activation and
  * the residual add fused: y = act(group_norm(x + pre_bias[c]) * gamma + beta) [+ residual],
- * act 0 none, 1 SiLU, 2 GELU (erf); pre_bias and residual may be NULL.
+ * act 0 none, 1 SiLU, 2 GELU (erf), 3 ReLU, where with a residual 3 also applies ReLU after the
+ * add (y = relu(residual + relu(norm)), the UniMatch ResidualBlock ending with InstanceNorm =
+ * GroupNorm(groups = C), reference src/model/encoder/backbone/unimatch/backbone.py ResidualBlock);
+ * pre_bias and residual may be NULL.
  * Replaces the U-Net / refine-head chains GroupNorm32 -> SiLU (-> + skip) and GroupNorm -> GELU
  * (reference src/model/encoder/matching/ldm_unet/unet.py:177-370, util.py:189-208,
  * depth_predictor_trans.py:142-206; torch.nn.functional.group_norm semantics: biased variance,

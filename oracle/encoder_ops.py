@@ -248,9 +248,19 @@ def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", 
         y = torch.nn.functional.silu(y)
     elif act == "gelu":
         y = torch.nn.functional.gelu(y)
+    elif act == "relu":
+        y = torch.relu(y)
     if residual is not None:
         y = residual.float() + y
+        if act == "relu":  # UniMatch ResidualBlock: relu(x + relu(norm(conv(y))))
+            y = torch.relu(y)
     return y
+
+
+def instance_norm(x, eps: float, act: str = "none", residual=None):
+    """nn.InstanceNorm2d (affine=False) [-> ReLU] [-> relu(residual + .)] (reference
+    src/model/encoder/backbone/unimatch/backbone.py ResidualBlock / CNNEncoder)."""
+    return group_norm(x, x.shape[1], None, None, eps, act, residual)
 
 
 def sh_rotation(rotations, d_sh: int):
@@ -289,4 +299,4 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
 
 
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
-                       "sh_rotation", "fused_linear", "attention_merge")
+                       "sh_rotation", "fused_linear", "attention_merge", "instance_norm")

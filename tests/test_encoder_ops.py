@@ -317,3 +317,23 @@ def test_small_inverse_kernel(device, d):
     out = K.small_inverse(a.to(device)).cpu().double()
     rel = ((out - ref).abs().amax((-2, -1)) / ref.abs().amax((-2, -1))).max().item()
     assert rel < 1e-5, rel
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,act,res", [((2, 64, 128, 128), "relu", False), ((2, 96, 64, 64), "relu", True),
+                                           ((2, 128, 64, 64), "none", False), ((1, 3, 7, 9), "relu", True)])
+def test_instance_norm_kernel(device, shape, act, res):
+    """InstanceNorm2d (+ ReLU, + the ResidualBlock's relu(x + .)) through the GroupNorm kernel with
+    one group per channel vs torch's instance_norm on the CPU."""
+    from transplat_amd import kernels as K
+
+    x = seeded(shape, 51) * 2.0 + 0.5
+    r = seeded(shape, 52) if res else None
+    ref = torch.nn.functional.instance_norm(x, eps=1e-5)
+    if act == "relu":
+        ref = torch.relu(ref)
+    if res:
+        ref = torch.relu(r + ref)
+    np.testing.assert_allclose(E.instance_norm(x, 1e-5, act, r).numpy(), ref.numpy(), atol=1e-5)
+    out = K.instance_norm(x.to(device), 1e-5, act, r.to(device) if res else None).cpu()
+    assert (out - ref).abs().max().item() < 2e-5

@@ -15,6 +15,23 @@ ap.add_argument("--dense-dtype", default="fp32")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 model = build_model(dev, args.dense_dtype)
+# module ranges, so every op can be attributed to the innermost module that launched it
+_open = {}
+
+
+def _pre(mod, *_):
+    rf = torch.profiler.record_function("mod::" + type(mod).__name__)
+    rf.__enter__()
+    _open.setdefault(id(mod), []).append(rf)
+
+
+def _post(mod, *_):
+    _open[id(mod)].pop().__exit__(None, None, None)
+
+
+for _m in model.modules():
+    _m.register_forward_pre_hook(_pre)
+    _m.register_forward_hook(_post)
 data = S.make_batch(args.batch, image_shape=(256, 256), device=dev)
 with torch.no_grad():
     for _ in range(3):
@@ -31,8 +48,12 @@ for ev in prof.events():
     dt = getattr(ev, "self_device_time_total", 0) or getattr(ev, "self_cuda_time_total", 0)
     if not dt or ev.device_type != torch.autograd.DeviceType.CPU:
         continue
-    frames = [f for f in (ev.stack or []) if "transplat_amd" in f]
-    where = frames[0].split("transplat_amd/")[-1] if frames else "?"
+    par, chain = ev.cpu_parent, []
+    while par is not None and len(chain) < 2:
+        if par.name.startswith("mod::"):
+            chain.append(par.name[5:])
+        par = par.cpu_parent
+    where = "/".join(reversed(chain)) if chain else "?"
     a = agg[(ev.name, where)]
     a[0] += 1
     a[1] += dt

@@ -93,8 +93,13 @@ template <int ACT>
 __device__ __forceinline__ float activate(float v) {
     if (ACT == 1) return v / (1.0f + expf(-v));                     // SiLU
     if (ACT == 2) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));  // GELU (erf)
+    if (ACT == 3) return fmaxf(v, 0.0f);                             // ReLU
     return v;
 }
+
+// after the residual add: ACT 3 is the UniMatch ResidualBlock ending relu(x + relu(norm(y)))
+template <int ACT>
+__device__ __forceinline__ float post_residual(float v) { return ACT == 3 ? fmaxf(v, 0.0f) : v; }
 
 template <bool VEC, int ACT, bool RES>
 __global__ void __launch_bounds__(kThreads)
@@ -144,10 +149,10 @@ apply_kernel(const float* __restrict__ x, const float* __restrict__ pb, const fl
                 v.w = activate<ACT>(v.w * sc + sh);
                 if (RES) {
                     const float4 r = *reinterpret_cast<const float4*>(res + base + i);
-                    v.x += r.x;
-                    v.y += r.y;
-                    v.z += r.z;
-                    v.w += r.w;
+                    v.x = post_residual<ACT>(v.x + r.x);
+                    v.y = post_residual<ACT>(v.y + r.y);
+                    v.z = post_residual<ACT>(v.z + r.z);
+                    v.w = post_residual<ACT>(v.w + r.w);
                 }
                 *reinterpret_cast<float4*>(y + base + i) = v;
             }
@@ -157,7 +162,7 @@ apply_kernel(const float* __restrict__ x, const float* __restrict__ pb, const fl
             const int c = g * cpg + (int)((start + i) / HW);
             const float sc = rstd * gamma[c];
             float v = activate<ACT>((x[base + i] + (pb ? pb[c] : 0.f)) * sc + (beta[c] - sc * mean));
-            if (RES) v += res[base + i];
+            if (RES) v = post_residual<ACT>(v + res[base + i]);
             y[base + i] = v;
         }
     }
@@ -181,7 +186,7 @@ extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, cons
                                      void* stream_) {
     using namespace tsplat::gn;
     if (!x || !gamma || !beta || !y || !workspace) return TSPLAT_EINVAL;
-    if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups || act < 0 || act > 2 ||
+    if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups || act < 0 || act > 3 ||
         hw > INT32_MAX)
         return TSPLAT_EINVAL;
     const int cpg = c / groups;
@@ -208,7 +213,8 @@ extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, cons
     switch (act) {                       \
         case 0: TSPLAT_GN_APPLY(V, 0, R); break; \
         case 1: TSPLAT_GN_APPLY(V, 1, R); break; \
-        default: TSPLAT_GN_APPLY(V, 2, R); break; \
+        case 2: TSPLAT_GN_APPLY(V, 2, R); break; \
+        default: TSPLAT_GN_APPLY(V, 3, R); break; \
     }
     if (vec) {
         if (residual) { TSPLAT_GN_ACT(true, true) } else { TSPLAT_GN_ACT(true, false) }

@@ -150,7 +150,19 @@ def adapter_cameras(extrinsics: torch.Tensor, intrinsics: torch.Tensor, image_sh
     return torch.cat([ext[:, :3, :3].reshape(-1, 9), ext[:, :3, 3], kinv.reshape(-1, 9), mult[:, None]], 1).contiguous()
 
 
-_ACTS = {"none": 0, "silu": 1, "gelu": 2}
+_ACTS = {"none": 0, "silu": 1, "gelu": 2, "relu": 3}
+_AFFINE_ID: dict = {}
+
+
+def instance_norm(x, eps: float, act: str = "none", residual=None):
+    """InstanceNorm2d (affine=False, instance statistics) as GroupNorm with one group per channel
+    (tsplat_group_norm_fwd), with "relu" and the ResidualBlock ending relu(residual + relu(norm))."""
+    c = x.shape[1]
+    key = (c, x.device)
+    if key not in _AFFINE_ID:
+        _AFFINE_ID[key] = (torch.ones(c, device=x.device), torch.zeros(c, device=x.device))
+    w, b = _AFFINE_ID[key]
+    return group_norm(x, c, w, b, eps, act, residual)
 
 
 def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None, pre_bias=None):

@@ -11,6 +11,8 @@ import math
 import torch
 from torch import nn
 
+from .... import kernels
+
 
 class ResidualBlock(nn.Module):
     def __init__(self, in_planes, planes, norm_layer=nn.InstanceNorm2d, stride=1, dilation=1):
@@ -29,6 +31,12 @@ class ResidualBlock(nn.Module):
             self.downsample = nn.Sequential(nn.Conv2d(in_planes, planes, kernel_size=1, stride=stride), self.norm3)
 
     def forward(self, x):
+        if isinstance(self.norm1, nn.InstanceNorm2d) and not self.norm1.affine:
+            # InstanceNorm + ReLU (+ residual + ReLU) as one GroupNorm-kernel launch each
+            y = kernels.instance_norm(self.conv1(x), self.norm1.eps, "relu")
+            if self.downsample is not None:
+                x = kernels.instance_norm(self.downsample[0](x), self.norm3.eps)
+            return kernels.instance_norm(self.conv2(y), self.norm2.eps, "relu", residual=x)
         y = self.relu(self.norm1(self.conv1(x)))
         y = self.relu(self.norm2(self.conv2(y)))
         if self.downsample is not None:
@@ -62,7 +70,10 @@ class CNNEncoder(nn.Module):
         return nn.Sequential(layer1, layer2)
 
     def forward(self, x):
-        x = self.relu1(self.norm1(self.conv1(x)))
+        if isinstance(self.norm1, nn.InstanceNorm2d) and not self.norm1.affine:
+            x = kernels.instance_norm(self.conv1(x), self.norm1.eps, "relu")
+        else:
+            x = self.relu1(self.norm1(self.conv1(x)))
         x = self.layer3(self.layer2(self.layer1(x)))
         return [self.conv2(x)]
 
