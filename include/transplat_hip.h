@@ -174,6 +174,14 @@ int tsplat_group_norm_fwd(const float* x, const float* pre_bias, const float* ga
                           float* y, void* workspace, int32_t n, int32_t c, int64_t hw, int32_t groups,
                           float eps, int32_t act, void* stream);
 
+/* Convolution epilogue without a norm: y = act(x + bias[c]) [+ residual] over [n, c, hw] fp32
+ * (act as above; 3 with a residual = relu(residual + relu(.))), hw % 4 == 0, 16-B aligned; y may
+ * alias x. Replaces the bias add_ + activation (+ residual add) passes after a MIOpen convolution
+ * (reference depth_predictor_trans.py:151-206 conv -> GELU heads, depth_anything_v2/util/blocks.py
+ * ResidualConvUnit relu -> conv -> relu -> conv -> + x). bias may be NULL. */
+int tsplat_bias_act_fwd(const float* x, const float* bias, const float* residual, float* y, int32_t n, int32_t c,
+                        int64_t hw, int32_t act, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Gaussian adapter (encoder stage 5 + GaussianAdapter.forward, reference
  * src/model/encoder/encoder_trans.py:294-353, common/gaussian_adapter.py:48-96), one pass:

@@ -257,6 +257,20 @@ def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", 
     return y
 
 
+def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
+    """conv -> (GELU | ReLU) [-> + residual (-> ReLU)] as the reference module chains compute it."""
+    y = conv(x)
+    if act == "gelu":
+        y = torch.nn.functional.gelu(y)
+    elif act == "relu":
+        y = torch.relu(y)
+    if residual is not None:
+        y = y + residual
+        if act == "relu":
+            y = torch.relu(y)
+    return y
+
+
 def instance_norm(x, eps: float, act: str = "none", residual=None):
     """nn.InstanceNorm2d (affine=False) [-> ReLU] [-> relu(residual + .)] (reference
     src/model/encoder/backbone/unimatch/backbone.py ResidualBlock / CNNEncoder)."""
@@ -299,4 +313,5 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
 
 
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
-                       "sh_rotation", "fused_linear", "attention_merge", "instance_norm")
+                       "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
+                       "conv_bias_act")

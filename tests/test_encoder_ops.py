@@ -337,3 +337,20 @@ def test_instance_norm_kernel(device, shape, act, res):
     np.testing.assert_allclose(E.instance_norm(x, 1e-5, act, r).numpy(), ref.numpy(), atol=1e-5)
     out = K.instance_norm(x.to(device), 1e-5, act, r.to(device) if res else None).cpu()
     assert (out - ref).abs().max().item() < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,cout,hw,act,res", [(163, 168, 64, "gelu", False), (168, 84, 64, "none", False),
+                                                 (64, 64, 37, "relu", False), (64, 64, 36, "none", True)])
+def test_conv_bias_act(device, cin, cout, hw, act, res):
+    """Bias-free MIOpen convolution + tsplat_bias_act_fwd (bias, GELU / ReLU, skip add in one pass)
+    vs the module chain on the CPU (37x37: odd plane size takes the module path)."""
+    from transplat_amd import kernels as K
+
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(cin, cout, 3, 1, 1)
+    x = seeded((2, cin, hw, hw), 61)
+    r = seeded((2, cout, hw, hw), 62) if res else None
+    ref = E.conv_bias_act(conv, x, act, r)
+    out = K.conv_bias_act(conv.to(device), x.to(device), act, r.to(device) if res else None).cpu()
+    assert (out - ref).abs().max().item() < 2e-3 * max(1.0, ref.abs().max().item())

@@ -212,7 +212,7 @@ def test_depth_predictor_gpu(device, nv):
 
 
 # ------------------------------------------------------------------ Depth-Anything-V2 ViT-B
-def test_depth_anything_cpu():
+def test_depth_anything_cpu(cpu_ops):
     from transplat_amd.model.depth_anything.dpt import DepthAnythingV2
 
     g = np.load(GOLD / "depth_anything.npz")

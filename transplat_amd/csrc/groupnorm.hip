@@ -227,3 +227,60 @@ extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, cons
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Convolution epilogue without normalisation: y = post(act(x + bias[c]) (+ residual)) over NCHW,
+// one pass instead of PyTorch's bias add_ + activation (+ add) passes after a MIOpen convolution.
+namespace tsplat {
+namespace gn {
+
+template <int ACT, bool RES>
+__global__ void __launch_bounds__(kThreads)
+bias_act_kernel(const float* __restrict__ x, const float* __restrict__ bias, const float* __restrict__ res,
+                float* __restrict__ y, int n4, int hw4, int C) {
+    const int i = blockIdx.x * kThreads + threadIdx.x;  // 32-bit index math (n4 < 2^31 checked)
+    if (i >= n4) return;
+    const int c = (i / hw4) % C;
+    const float b = bias ? bias[c] : 0.f;
+    float4 v = reinterpret_cast<const float4*>(x)[i];
+    v.x = activate<ACT>(v.x + b);
+    v.y = activate<ACT>(v.y + b);
+    v.z = activate<ACT>(v.z + b);
+    v.w = activate<ACT>(v.w + b);
+    if (RES) {
+        const float4 r = reinterpret_cast<const float4*>(res)[i];
+        v.x = post_residual<ACT>(v.x + r.x);
+        v.y = post_residual<ACT>(v.y + r.y);
+        v.z = post_residual<ACT>(v.z + r.z);
+        v.w = post_residual<ACT>(v.w + r.w);
+    }
+    reinterpret_cast<float4*>(y)[i] = v;
+}
+
+}  // namespace gn
+}  // namespace tsplat
+
+extern "C" int tsplat_bias_act_fwd(const float* x, const float* bias, const float* residual, float* y, int32_t n,
+                                   int32_t c, int64_t hw, int32_t act, void* stream_) {
+    using namespace tsplat::gn;
+    if (!x || !y || n <= 0 || c <= 0 || hw <= 0 || hw % 4 || act < 0 || act > 3) return TSPLAT_EINVAL;
+    if ((uintptr_t)x % 16 || (uintptr_t)y % 16 || (residual && (uintptr_t)residual % 16)) return TSPLAT_EINVAL;
+    const int64_t n4 = (int64_t)n * c * hw / 4;
+    if (n4 > INT32_MAX) return TSPLAT_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    const dim3 grid((unsigned)((n4 + kThreads - 1) / kThreads));
+#define TSPLAT_BA(A, R) \
+    hipLaunchKernelGGL((bias_act_kernel<A, R>), grid, dim3(kThreads), 0, stream, x, bias, residual, y, (int)n4, (int)(hw / 4), c)
+#define TSPLAT_BA_ACT(R)                   \
+    switch (act) {                         \
+        case 0: TSPLAT_BA(0, R); break;    \
+        case 1: TSPLAT_BA(1, R); break;    \
+        case 2: TSPLAT_BA(2, R); break;    \
+        default: TSPLAT_BA(3, R); break;   \
+    }
+    if (residual) { TSPLAT_BA_ACT(true) } else { TSPLAT_BA_ACT(false) }
+#undef TSPLAT_BA_ACT
+#undef TSPLAT_BA
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

@@ -5,6 +5,8 @@ requires device tensors and the in-tree HIP library; there is no fallback path.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -152,6 +154,45 @@ def adapter_cameras(extrinsics: torch.Tensor, intrinsics: torch.Tensor, image_sh
 
 _ACTS = {"none": 0, "silu": 1, "gelu": 2, "relu": 3}
 _AFFINE_ID: dict = {}
+
+
+_NO_CONV_EPI = os.environ.get("TSPLAT_NO_CONV_EPI", "")  # A/B timing knob only: "all" or a site name
+
+
+def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
+    """conv(x) + bias -> act [-> + residual (-> relu for "relu")] with the bias, activation and
+    residual in ONE pass after the bias-free MIOpen convolution (tsplat_bias_act_fwd). Under bf16
+    autocast (config C3's dense layers) or for outputs the kernel's float4 layout cannot take, the
+    module's own forward and PyTorch activations run instead (dense-layer glue, same math).
+    Used on the depth predictor's full-resolution conv -> GELU -> conv heads (+0.4 % e2e); on the
+    DPT ResidualConvUnits the bias-free convolutions measured 3 % slower end to end (A/B with
+    TSPLAT_NO_CONV_EPI=<site>), so those keep the module path."""
+    import torch.nn.functional as F
+
+    if not x.is_cuda:
+        raise RuntimeError("transplat HIP ops need device tensors (no CPU path)")
+    fused = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32 and _NO_CONV_EPI not in ("all", site)
+    if fused:
+        y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+        fused = (y.shape[-1] * y.shape[-2]) % 4 == 0 and y.is_contiguous()
+    if not fused:
+        y = conv(x)
+        if act == "gelu":
+            y = F.gelu(y)
+        elif act == "relu":
+            y = torch.relu(y)
+        if residual is not None:
+            y = y + residual
+            if act == "relu":
+                y = torch.relu(y)
+        return y
+    lib = _lib.load()
+    n, c = y.shape[:2]
+    res = _f32(residual) if residual is not None else None
+    rc = lib.tsplat_bias_act_fwd(_lib.ptr(y), _lib.ptr(conv.bias), _lib.ptr(res), _lib.ptr(y), n, c,
+                                 y.shape[-1] * y.shape[-2], _ACTS[act], _lib.stream_ptr(y.device))
+    _lib.check(rc, "tsplat_bias_act_fwd")
+    return y
 
 
 def instance_norm(x, eps: float, act: str = "none", residual=None):

@@ -8,6 +8,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+
 from .dinov2 import DINOv2
 
 

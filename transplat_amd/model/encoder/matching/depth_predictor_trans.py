@@ -18,6 +18,14 @@ from ...utils.uv_transformer import UVTransformer
 from .ldm_unet import UNetModel, run_sequential
 
 
+def _conv_gelu_conv(seq: nn.Sequential, x):
+    """Sequential(Conv2d, GELU, Conv2d) head with each conv's bias (and the GELU) applied in one
+    pass after the bias-free convolution (kernels.conv_bias_act)."""
+    if not (len(seq) == 3 and isinstance(seq[1], nn.GELU) and seq[1].approximate == "none"):
+        return seq(x)
+    return kernels.conv_bias_act(seq[2], kernels.conv_bias_act(seq[0], x, "gelu", site="head"), site="head")
+
+
 @torch.autocast("cuda", enabled=False)
 def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, num_samples):
     """(reference :59-109) per-view features, pixel intrinsics, relative poses and disparity
@@ -173,7 +181,7 @@ class DepthPredictorTrans(nn.Module):
 
         raw_correlation = (run_sequential(self.corr_refine_net, raw_correlation_in)
                            + self.regressor_residual(raw_correlation_in))
-        pdf = F.softmax(self.depth_head_lowres(raw_correlation), dim=1)
+        pdf = F.softmax(_conv_gelu_conv(self.depth_head_lowres, raw_correlation), dim=1)
         coarse_disps = (disp_candi_curr * pdf).sum(dim=1, keepdim=True)
         pdf_max = torch.max(pdf, dim=1, keepdim=True)[0]
         pdf_max = F.interpolate(pdf_max, scale_factor=self.upscale_factor)
@@ -185,9 +193,10 @@ class DepthPredictorTrans(nn.Module):
         refine_out = run_sequential(self.refine_unet, torch.cat((extra_info["images"], da_depth, proj_feature, fullres_disps,
                                                  pdf_max), dim=1))
 
-        raw_gaussians = self.to_gaussians(torch.cat([refine_out, extra_info["images"], proj_feat_in_fullres], dim=1))
+        raw_gaussians = _conv_gelu_conv(self.to_gaussians,
+                                        torch.cat([refine_out, extra_info["images"], proj_feat_in_fullres], dim=1))
         raw_gaussians = rearrange(raw_gaussians, "(v b) c h w -> b v (h w) c", v=v, b=b)
-        delta_disps, raw_densities = self.to_disparity(refine_out).split(gaussians_per_pixel, dim=1)
+        delta_disps, raw_densities = _conv_gelu_conv(self.to_disparity, refine_out).split(gaussians_per_pixel, dim=1)
         densities = repeat(F.sigmoid(raw_densities), "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
         fine_disps = (fullres_disps + delta_disps).clamp(1.0 / rearrange(far, "b v -> (v b) () () ()"),
                                                          1.0 / rearrange(near, "b v -> (v b) () () ()"))
