@@ -27,12 +27,11 @@ timeout -k 10 300 python bench.py --workload raster --steps 20 --warmup 3 > $OUT
 tail -1 $OUT/bench_raster.log | cut -c1-200
 cd /tmp && export TMPDIR=/tmp
 step prof
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof_e2e_fp32_b1 -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_e2e_fp32_b1.log 2>&1 || exit 1
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof_c3 -o run --output-format csv -- python3 $R/bench.py --batch 8 --dense-dtype bf16 --steps 5 --warmup 2 --no-cpu-baseline > $OUT/prof_c3.log 2>&1 || exit 1
+# (rocprof passes without MIOpen's algorithm search, so its trial kernels do not pollute the per-step
+# stats; the hand-written kernels are the same launches as in the bench)
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof_e2e_fp32_b1 -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-conv-search > $OUT/prof_e2e_fp32_b1.log 2>&1 || exit 1
+timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof_c3 -o run --output-format csv -- python3 $R/bench.py --batch 8 --dense-dtype bf16 --steps 5 --warmup 2 --no-cpu-baseline --no-conv-search > $OUT/prof_c3.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_raster -o run --output-format csv -- python3 $R/bench.py --workload raster --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_raster.log 2>&1 || exit 1
 step pmc
-for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 500 rocprofv3 --pmc $C -d $OUT/pmc_e2e_$C -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 1 --no-graph --no-cpu-baseline > $OUT/pmc_e2e_$C.log 2>&1 || exit 1
-  timeout -k 10 500 rocprofv3 --pmc $C -d $OUT/pmc_c3_$C -o run --output-format csv -- python3 $R/bench.py --batch 8 --dense-dtype bf16 --steps 2 --warmup 1 --no-graph --no-cpu-baseline > $OUT/pmc_c3_$C.log 2>&1 || exit 1
-done
+cd $R && bash tools/pmc_round.sh || exit 1
 echo done
