@@ -268,6 +268,14 @@ int tsplat_linear_f32_attn_merge_fwd(const float* partials, int32_t batch, int32
  * cuda_splatting.py:93-96), Gauss-Jordan with partial pivoting, one thread per matrix. */
 int tsplat_small_inverse(const float* in, float* out, int32_t n, int32_t dim, void* stream);
 
+/* Dense multi-head self-attention of the DINOv2 ViT-B encoder (exact fp32 MFMA), replacing
+ * scaled_dot_product_attention + its permute / transpose copies in Attention.forward (reference
+ * src/depth_anything_v2/dinov2_layers/attention.py): qkv [batch, tokens, 3, heads, head_dim] (the
+ * qkv Linear's output as it is), out [batch, tokens, heads, head_dim] = softmax(q k^T * scale) v.
+ * head_dim must be 64. */
+int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, int32_t tokens, int32_t heads,
+                       int32_t head_dim, float scale, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -271,6 +271,16 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
     return y
 
 
+def mha(qkv, heads: int, scale: float):
+    """DINOv2 Attention core (reference dinov2_layers/attention.py): reshape to heads, softmax
+    attention (torch SDPA math), back to [B, N, heads * head_dim]."""
+    b, n, c3 = qkv.shape
+    d = c3 // (3 * heads)
+    q, k, v = qkv.reshape(b, n, 3, heads, d).permute(2, 0, 3, 1, 4)
+    x = torch.nn.functional.scaled_dot_product_attention(q, k, v, scale=scale)
+    return x.transpose(1, 2).reshape(b, n, heads * d)
+
+
 def instance_norm(x, eps: float, act: str = "none", residual=None):
     """nn.InstanceNorm2d (affine=False) [-> ReLU] [-> relu(residual + .)] (reference
     src/model/encoder/backbone/unimatch/backbone.py ResidualBlock / CNNEncoder)."""
@@ -314,4 +324,4 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
 
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
-                       "conv_bias_act")
+                       "conv_bias_act", "mha")

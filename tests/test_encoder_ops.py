@@ -354,3 +354,17 @@ def test_conv_bias_act(device, cin, cout, hw, act, res):
     ref = E.conv_bias_act(conv, x, act, r)
     out = K.conv_bias_act(conv.to(device), x.to(device), act, r.to(device) if res else None).cpu()
     assert (out - ref).abs().max().item() < 2e-3 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("b,n,heads", [(2, 325, 12), (1, 37, 12), (3, 5, 2), (1, 1025, 4)])
+def test_mha_kernel(device, b, n, heads):
+    """DINOv2 multi-head attention (tsplat_mha_f32_fwd, straight from the qkv layout) vs torch SDPA
+    math on the CPU; N = 325 is the 256x256 token count, N = 5 leaves a wave without keys."""
+    from transplat_amd import kernels as K
+
+    qkv = seeded((b, n, 3 * heads * 64), 71) * 2.0
+    ref = E.mha(qkv, heads, 64 ** -0.5)
+    out = K.mha(qkv.to(device), heads, 64 ** -0.5).cpu()
+    assert out.shape == (b, n, heads * 64)
+    assert (out - ref).abs().max().item() < 5e-5  # fp32, different summation order over up to 1025 keys

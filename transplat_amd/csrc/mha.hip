@@ -1,0 +1,207 @@
+// Dense multi-head self-attention of the Depth-Anything-V2 ViT-B encoder (DINOv2) on gfx950,
+// exact fp32 MFMA.
+//
+// Semantics: reference src/depth_anything_v2/dinov2_layers/attention.py Attention.forward,
+//   qkv = x Wqkv^T + b  -> [B, N, 3, H, 64];  out = softmax(q k^T * scale) v  -> [B, N, H, 64]
+// (torch.nn.functional.scaled_dot_product_attention, no mask, no dropout). The kernel reads q, k, v
+// straight from the qkv projection's output and writes the [B, N, H * 64] layout the output
+// projection consumes, so the permute / transpose copies around SDPA disappear.
+//
+// Shape at 256x256 input: 2 images x 12 heads, N = 325 tokens (1 + 18 x 18), head dim 64:
+// 0.65 GFLOP per call. Mapping: one workgroup = 4 waves on the same 32 queries of one (image,
+// head); wave w walks the w-th quarter of the keys in 32-key tiles with no LDS and no barrier
+// (each lane loads its own key row for S^T = K Q^T and one 128-B V segment per k-step for
+// O^T += V^T P^T, the next tile prefetched into registers), and the four (max, sum, O) partials are
+// merged once through LDS. 24 x 11 query blocks = 264 workgroups, ~1 wave per SIMD.
+#include "common.h"
+#include "prof.h"
+
+namespace tsplat {
+namespace mha {
+
+constexpr int kD = 64;   // head dim
+constexpr int kQW = 32;  // queries per workgroup (one MFMA tile)
+constexpr int kKT = 32;  // keys per tile
+constexpr int kThreads = 256;
+constexpr float kLog2e = 1.4426950408889634f;
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float halves_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halves_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+struct Tile {
+    floatx4 k[8];  // this lane's key row, dims 32 h .. 32 h + 31
+    float v[32];   // V[key 8u + 4h + j][32 dt + c] for (u, j, dt): index (u * 4 + j) * 2 + dt
+};
+
+__global__ void __launch_bounds__(kThreads)
+mha_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, int H, float scale) {
+    __shared__ float sO[4][2][16][64];
+    __shared__ float sML[4][2][kQW];
+
+    const int qblk = blockIdx.x, bh = blockIdx.y;
+    const int b = bh / H, head = bh - b * H;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const size_t tok = (size_t)3 * H * kD;  // floats per token row of qkv
+    const float* base = qkv + (size_t)b * N * tok + (size_t)head * kD;
+    const float* qb = base;
+    const float* kb = base + (size_t)H * kD;
+    const float* vb = base + (size_t)2 * H * kD;
+
+    // keys of this wave: a quarter of N, in 32-key tiles (the last tile masked past N)
+    const int per = (N + 3) / 4;
+    const int k_lo = wid * per, k_hi = min(N, k_lo + per);
+    const int q = qblk * kQW + c;
+    const bool qvalid = q < N;
+
+    float qr[32];
+    {
+        const float qs = scale * kLog2e;
+        const floatx4* src = reinterpret_cast<const floatx4*>(qb + (size_t)(qvalid ? q : 0) * tok + 32 * h);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const floatx4 t = src[i];
+            qr[4 * i] = t.x * qs;
+            qr[4 * i + 1] = t.y * qs;
+            qr[4 * i + 2] = t.z * qs;
+            qr[4 * i + 3] = t.w * qs;
+        }
+    }
+    auto load_tile = [&](int k0, Tile& t) {
+        const int kr = min(k0 + c, N - 1);  // clamped row; masked below
+        const floatx4* ks = reinterpret_cast<const floatx4*>(kb + (size_t)kr * tok + 32 * h);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t.k[i] = ks[i];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int vr = min(k0 + 8 * u + 4 * h + j, N - 1);
+                const float* vs = vb + (size_t)vr * tok + c;
+                t.v[(u * 4 + j) * 2] = vs[0];
+                t.v[(u * 4 + j) * 2 + 1] = vs[32];
+            }
+    };
+
+    floatx16 o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    Tile cur, nxt;
+    if (k_lo < k_hi) load_tile(k_lo, cur);
+    for (int k0 = k_lo; k0 < k_hi; k0 += kKT) {
+        const bool has_next = k0 + kKT < k_hi;
+        if (has_next) load_tile(k0 + kKT, nxt);
+        // S^T[key 8(r >> 2) + 4h + (r & 3)][query c]; k-step t contracts dims {t, 32 + t}
+        floatx16 s;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            s = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.k[i].x, qr[4 * i + 0], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.k[i].y, qr[4 * i + 1], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.k[i].z, qr[4 * i + 2], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.k[i].w, qr[4 * i + 3], s, 0, 0, 0);
+        }
+        // keys past this wave's range score -inf (their exp is exactly 0)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (k0 + 8 * (r >> 2) + 4 * h + (r & 3) >= k_hi) s[r] = -INFINITY;
+        float bmax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[r]);
+        bmax = halves_max(bmax);
+        const float m_new = fmaxf(m_run, bmax);
+        if (__any(m_new > m_run)) {
+            const float corr = __builtin_amdgcn_exp2f(m_run - m_new);
+            l_run *= corr;
+            o[0] *= corr;
+            o[1] *= corr;
+            m_run = m_new;
+        }
+        float bsum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float e = __builtin_amdgcn_exp2f(s[r] - m_run);
+            s[r] = e;
+            bsum += e;
+        }
+        l_run += halves_sum(bsum);
+        // O^T[d = 32 dt + 8(r >> 2) + 4h + (r & 3)][query c] += V^T P^T, k-step (u, j) contracts keys
+        // {8u + j, 8u + 4 + j} (lane halves): B = the S^T register 4u + j itself
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.v[(u * 4 + j) * 2], s[4 * u + j], o[0], 0, 0, 0);
+                o[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.v[(u * 4 + j) * 2 + 1], s[4 * u + j], o[1], 0, 0, 0);
+            }
+        if (has_next) cur = nxt;
+    }
+
+    // merge the four key quarters: waves 0 and 1 finish d tiles 0 and 1
+    if (h == 0) {
+        sML[wid][0][c] = m_run;
+        sML[wid][1][c] = l_run;
+    }
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sO[wid][dt][r][lane] = o[dt][r];
+    __syncthreads();
+    if (wid >= 2 || !qvalid) return;
+    float mw[4], M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        mw[w] = sML[w][0][c];
+        M = fmaxf(M, mw[w]);
+    }
+    float a[4], L = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        a[w] = mw[w] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw[w] - M);
+        L += a[w] * sML[w][1][c];
+    }
+    const float inv = 1.0f / L;
+    float acc[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) t += a[w] * sO[w][wid][r][lane];
+        acc[r] = t * inv;
+    }
+    // out[b][q][head][d], d = 32 wid + 8u + 4h + (0..3) in acc[4u .. 4u + 3]
+    float* dst = out + (((size_t)b * N + q) * H + head) * kD + 32 * wid + 4 * h;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        *reinterpret_cast<floatx4*>(dst + 8 * u) = (floatx4){acc[4 * u], acc[4 * u + 1], acc[4 * u + 2], acc[4 * u + 3]};
+}
+
+}  // namespace mha
+}  // namespace tsplat
+
+extern "C" int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, int32_t tokens, int32_t heads,
+                                  int32_t head_dim, float scale, void* stream_) {
+    using namespace tsplat::mha;
+    if (!qkv || !out || batch <= 0 || tokens <= 0 || heads <= 0 || head_dim != kD) return TSPLAT_EINVAL;
+    if ((int64_t)batch * heads > 65535) return TSPLAT_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(tsplat::prof::kMha, stream);
+    hipLaunchKernelGGL(mha_f32_kernel, dim3((tokens + kQW - 1) / kQW, batch * heads), dim3(kThreads), 0, stream, qkv,
+                       out, tokens, heads, scale);
+    TSPLAT_PROF_END(tsplat::prof::kMha, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

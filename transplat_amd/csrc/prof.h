@@ -21,7 +21,8 @@ enum KernelId : int {
     kGroupNorm = 10,  // both launches of tsplat_group_norm_fwd
     kUvCrossTable = 11,
     kLinear = 12,     // tsplat_linear_f32_fwd
-    kNumKernels = 13,
+    kMha = 13,        // tsplat_mha_f32_fwd
+    kNumKernels = 14,
 };
 
 int active();                 // kernel id being timed (0 = off)

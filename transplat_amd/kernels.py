@@ -306,6 +306,19 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     return out
 
 
+def mha(qkv, heads: int, scale: float):
+    """Multi-head self-attention from the qkv projection output [B, N, 3 * heads * 64] ->
+    [B, N, heads * 64] (tsplat_mha_f32_fwd; no permute copies)."""
+    lib = _lib.load()
+    b, n, c3 = qkv.shape
+    d = c3 // (3 * heads)
+    x = _f32(qkv)
+    out = torch.empty((b, n, heads * d), dtype=torch.float32, device=qkv.device)
+    _lib.check(lib.tsplat_mha_f32_fwd(_lib.ptr(x), _lib.ptr(out), b, n, heads, d, float(scale),
+                                      _lib.stream_ptr(qkv.device)), "tsplat_mha_f32_fwd")
+    return out
+
+
 def sh_rotation(rotations, d_sh: int):
     """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
     wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""

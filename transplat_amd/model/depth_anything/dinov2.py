@@ -14,6 +14,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from ... import kernels
+
 
 class PatchEmbed(nn.Module):
     def __init__(self, img_size=224, patch_size=16, in_chans=3, embed_dim=768):
@@ -61,6 +63,9 @@ class Attention(nn.Module):
 
     def forward(self, x):
         b, n, c = x.shape
+        if x.dtype == torch.float32 and c // self.num_heads == 64 and not torch.is_autocast_enabled(x.device.type):
+            # exact-fp32 MFMA attention straight from the qkv projection's layout
+            return self.proj(kernels.mha(self.qkv(x), self.num_heads, self.scale))
         qkv = self.qkv(x).reshape(b, n, 3, self.num_heads, c // self.num_heads).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
         x = F.scaled_dot_product_attention(q, k, v, scale=self.scale)
