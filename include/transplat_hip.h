@@ -182,6 +182,13 @@ int tsplat_group_norm_fwd(const float* x, const float* pre_bias, const float* ga
 int tsplat_bias_act_fwd(const float* x, const float* bias, const float* residual, float* y, int32_t n, int32_t c,
                         int64_t hw, int32_t act, void* stream);
 
+/* Pre-norm residual step of the DINOv2 blocks (reference dinov2_layers/block.py Block.forward:
+ * x = x + ls(sublayer(norm(x)))): x_out = x + ls * y, n_out = LayerNorm(x_out; ln_w, ln_b, ln_eps)
+ * with the NEXT sub-layer's norm, over rows of dim 256 / 512 / 768 / 1024 fp32. y may be NULL
+ * (plain LayerNorm of x, x_out unused), ls may be NULL (no LayerScale). */
+int tsplat_residual_ln_fwd(const float* x, const float* y, const float* ls, const float* ln_w, const float* ln_b,
+                           float ln_eps, float* x_out, float* n_out, int32_t rows, int32_t dim, void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Gaussian adapter (encoder stage 5 + GaussianAdapter.forward, reference
  * src/model/encoder/encoder_trans.py:294-353, common/gaussian_adapter.py:48-96), one pass:

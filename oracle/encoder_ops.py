@@ -281,6 +281,13 @@ def mha(qkv, heads: int, scale: float):
     return x.transpose(1, 2).reshape(b, n, heads * d)
 
 
+def residual_ln(x, y, ls, norm):
+    """DINOv2 pre-norm residual step: x' = x + ls * y (LayerScale), LayerNorm(x') with the next norm."""
+    if y is not None:
+        x = x + (ls * y if ls is not None else y)
+    return x, torch.nn.functional.layer_norm(x, (x.shape[-1],), norm.weight, norm.bias, norm.eps)
+
+
 def instance_norm(x, eps: float, act: str = "none", residual=None):
     """nn.InstanceNorm2d (affine=False) [-> ReLU] [-> relu(residual + .)] (reference
     src/model/encoder/backbone/unimatch/backbone.py ResidualBlock / CNNEncoder)."""
@@ -324,4 +331,4 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
 
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
-                       "conv_bias_act", "mha")
+                       "conv_bias_act", "mha", "residual_ln")

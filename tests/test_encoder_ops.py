@@ -368,3 +368,23 @@ def test_mha_kernel(device, b, n, heads):
     out = K.mha(qkv.to(device), heads, 64 ** -0.5).cpu()
     assert out.shape == (b, n, heads * 64)
     assert (out - ref).abs().max().item() < 5e-5  # fp32, different summation order over up to 1025 keys
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,dim,with_y,with_ls", [(650, 768, True, True), (650, 768, False, False),
+                                                     (7, 256, True, False), (33, 1024, True, True)])
+def test_residual_ln_kernel(device, rows, dim, with_y, with_ls):
+    """DINOv2 pre-norm residual step (x + ls * y, LayerNorm) in one launch vs the CPU restatement."""
+    from transplat_amd import kernels as K
+
+    norm = torch.nn.LayerNorm(dim, eps=1e-6)
+    with torch.no_grad():
+        norm.weight.copy_(seeded((dim,), 81) * 0.1 + 1.0)
+        norm.bias.copy_(seeded((dim,), 82) * 0.1)
+    x, y = seeded((rows, dim), 83) * 3.0, seeded((rows, dim), 84) if with_y else None
+    ls = seeded((dim,), 85) if with_ls else None
+    rx, rn = E.residual_ln(x, y, ls, norm)
+    d = lambda t: t.to(device) if t is not None else None
+    ox, on = K.residual_ln(d(x), d(y), d(ls), norm.to(device))
+    assert (ox.cpu() - rx).abs().max().item() < 1e-5
+    assert (on.cpu() - rn).abs().max().item() < 2e-5

@@ -284,3 +284,85 @@ extern "C" int tsplat_bias_act_fwd(const float* x, const float* bias, const floa
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Pre-norm transformer residual step of the DINOv2 blocks: x' = x + ls * y (LayerScale residual),
+// n = LayerNorm(x') with the NEXT sub-layer's norm, one pass over the row (one wave per row).
+namespace tsplat {
+namespace gn {
+
+template <int V4>  // float4s per lane (dim = 256 V4)
+__global__ void __launch_bounds__(kThreads)
+residual_ln_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ ls,
+                   const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ x_out,
+                   float* __restrict__ n_out, int rows, float eps) {
+    const int row = blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    constexpr int D = 256 * V4;
+    const size_t off = (size_t)row * D;
+    float4 v[V4];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < V4; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        v[k] = *reinterpret_cast<const float4*>(x + off + c);
+        if (y) {
+            const float4 t = *reinterpret_cast<const float4*>(y + off + c);
+            float4 g = make_float4(1.f, 1.f, 1.f, 1.f);
+            if (ls) g = *reinterpret_cast<const float4*>(ls + c);
+            v[k].x += g.x * t.x;
+            v[k].y += g.y * t.y;
+            v[k].z += g.z * t.z;
+            v[k].w += g.w * t.w;
+        }
+        s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float mean = s * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < V4; ++k) {
+        const float a = v[k].x - mean, bb = v[k].y - mean, cc = v[k].z - mean, d = v[k].w - mean;
+        q += (a * a + bb * bb) + (cc * cc + d * d);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) q += __shfl_xor(q, o);
+    const float rstd = rsqrtf(q * (1.0f / D) + eps);
+#pragma unroll
+    for (int k = 0; k < V4; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        if (x_out) *reinterpret_cast<float4*>(x_out + off + c) = v[k];
+        const float4 g = *reinterpret_cast<const float4*>(w + c), bt = *reinterpret_cast<const float4*>(b + c);
+        *reinterpret_cast<float4*>(n_out + off + c) =
+            make_float4((v[k].x - mean) * rstd * g.x + bt.x, (v[k].y - mean) * rstd * g.y + bt.y,
+                        (v[k].z - mean) * rstd * g.z + bt.z, (v[k].w - mean) * rstd * g.w + bt.w);
+    }
+}
+
+}  // namespace gn
+}  // namespace tsplat
+
+extern "C" int tsplat_residual_ln_fwd(const float* x, const float* y, const float* ls, const float* ln_w,
+                                      const float* ln_b, float ln_eps, float* x_out, float* n_out, int32_t rows,
+                                      int32_t dim, void* stream_) {
+    using namespace tsplat::gn;
+    if (!x || !ln_w || !ln_b || !n_out || rows <= 0 || (ls && !y)) return TSPLAT_EINVAL;
+    if (y && !x_out) return TSPLAT_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    const dim3 grid((rows + kThreads / kWave - 1) / (kThreads / kWave));
+#define TSPLAT_RLN(V)                                                                                   \
+    hipLaunchKernelGGL(residual_ln_kernel<V>, grid, dim3(kThreads), 0, stream, x, y, ls, ln_w, ln_b, x_out, \
+                       n_out, rows, ln_eps)
+    switch (dim) {
+        case 256: TSPLAT_RLN(1); break;
+        case 512: TSPLAT_RLN(2); break;
+        case 768: TSPLAT_RLN(3); break;
+        case 1024: TSPLAT_RLN(4); break;
+        default: return TSPLAT_EINVAL;
+    }
+#undef TSPLAT_RLN
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

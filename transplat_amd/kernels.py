@@ -306,6 +306,24 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     return out
 
 
+def residual_ln(x, y, ls, norm):
+    """(x + ls * y, LayerNorm(x + ls * y)) in one pass (tsplat_residual_ln_fwd); y None: (x, LN(x)).
+    norm: an nn.LayerNorm (weight, bias, eps); ls: LayerScale gamma or None."""
+    lib = _lib.load()
+    d = x.shape[-1]
+    xf = _f32(x)
+    rows = xf.numel() // d
+    yf = _f32(y) if y is not None else None
+    x_out = torch.empty_like(xf) if y is not None else xf
+    n_out = torch.empty_like(xf)
+    rc = lib.tsplat_residual_ln_fwd(_lib.ptr(xf), _lib.ptr(yf), _lib.ptr(_f32(ls)) if ls is not None else None,
+                                    _lib.ptr(_f32(norm.weight)), _lib.ptr(_f32(norm.bias)), float(norm.eps),
+                                    _lib.ptr(x_out) if y is not None else None, _lib.ptr(n_out), rows, d,
+                                    _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_residual_ln_fwd")
+    return x_out, n_out
+
+
 def mha(qkv, heads: int, scale: float):
     """Multi-head self-attention from the qkv projection output [B, N, 3 * heads * 64] ->
     [B, N, heads * 64] (tsplat_mha_f32_fwd; no permute copies)."""

@@ -153,16 +153,42 @@ class DinoVisionTransformer(nn.Module):
         x = torch.cat((self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x), dim=1)
         return x + self.interpolate_pos_encoding(x, w, h).to(x.dtype)
 
+    def _fused_ok(self, x) -> bool:
+        return (x.dtype == torch.float32 and not torch.is_autocast_enabled(x.device.type)
+                and x.shape[-1] in (256, 512, 768, 1024)
+                and all(isinstance(m, (LayerScale, nn.Identity)) for b in self.blocks for m in (b.ls1, b.ls2)))
+
+    def _blocks_fused(self, x, take, norm: bool):
+        """The block chain with every pre-norm residual step x = x + ls(y), h = norm_next(x) as ONE
+        kernel (kernels.residual_ln) instead of mul + add + LayerNorm launches; same math."""
+        gamma = lambda m: m.gamma if isinstance(m, LayerScale) else None
+        blocks = self.blocks
+        _, h = kernels.residual_ln(x, None, None, blocks[0].norm1)
+        outputs = []
+        for i, blk in enumerate(blocks):
+            x, h2 = kernels.residual_ln(x, blk.attn(h), gamma(blk.ls1), blk.norm2)
+            last = i + 1 == len(blocks)
+            x, h = kernels.residual_ln(x, blk.mlp(h2), gamma(blk.ls2), self.norm if last else blocks[i + 1].norm1)
+            if i in take:
+                if not norm:
+                    outputs.append(x)
+                else:  # the last block's step already produced self.norm(x)
+                    outputs.append(h if last else kernels.residual_ln(x, None, None, self.norm)[1])
+        return outputs
+
     def get_intermediate_layers(self, x, n=4, reshape=False, return_class_token=False, norm=True):
         x = self.prepare_tokens(x)
         take = range(len(self.blocks) - n, len(self.blocks)) if isinstance(n, int) else n
-        outputs = []
-        for i, blk in enumerate(self.blocks):
-            x = blk(x)
-            if i in take:
-                outputs.append(x)
-        if norm:
-            outputs = [self.norm(o) for o in outputs]
+        if self._fused_ok(x):
+            outputs = self._blocks_fused(x, take, norm)
+        else:
+            outputs = []
+            for i, blk in enumerate(self.blocks):
+                x = blk(x)
+                if i in take:
+                    outputs.append(x)
+            if norm:
+                outputs = [self.norm(o) for o in outputs]
         class_tokens = [o[:, 0] for o in outputs]
         outputs = [o[:, 1:] for o in outputs]
         if return_class_token:
