@@ -105,6 +105,15 @@ int tsplat_raster_fwd(const tsplat_raster_desc* desc,
                       void* workspace, int32_t* status, void* stream);
 
 
+/* Per-view camera constants of render_cuda (reference cuda_splatting.py:56-96 with get_fov and
+ * get_projection_matrix) from extrinsics [V, 4, 4] (c2w), normalised intrinsics [V, 3, 3], near
+ * and far [V], bg [V, 3] (bg_per_view) or [3]: writes the viewmat / projmat / campos / tanfov / bg
+ * / scale arrays tsplat_raster_fwd takes (one thread per view; scale_invariant as render_cuda). */
+int tsplat_raster_cameras(const float* extrinsics, const float* intrinsics, const float* near, const float* far,
+                          const float* bg, int32_t bg_per_view, int32_t scale_invariant, int32_t num_views,
+                          float* viewmat, float* projmat, float* campos, float* tanfov, float* bg_out, float* scale,
+                          void* stream);
+
 /* ------------------------------------------------------------------------------------------
  * Depth-candidate correlation (cost volume), all fp32, channel-last features.
  * Queries are (b v)-ordered: n = 2*b + v (the UVTransformerEncoder layout, utils/encoder.py:44);

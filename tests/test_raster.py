@@ -264,3 +264,28 @@ def test_raster_dtu_stress_parity(device):
     cams = _target_cams(S.make_batch(1, num_context=3, num_target=1, image_shape=hw), hw)
     color, radii, color_ref, radii_ref, counts = _run_both(g, cams, hw, 1, 3, device)
     _assert_parity(color, radii, color_ref, radii_ref)
+
+
+@pytest.mark.gpu
+def test_raster_cameras_kernel_matches_host_math(device):
+    """tsplat_raster_cameras (one launch) vs prepare_cameras' torch math on the host, for the
+    synthetic target cameras and randomised poses / intrinsics / near-far."""
+    from transplat_amd.model.decoder.hip_splatting import prepare_cameras
+
+    t = S.make_batch(2, image_shape=(256, 256))["target"]
+    ext = t["extrinsics"].reshape(-1, 4, 4)
+    g = torch.Generator().manual_seed(5)
+    ext[:, :3, 3] += torch.randn(ext.shape[0], 3, generator=g)
+    intr = t["intrinsics"].reshape(-1, 3, 3).clone()
+    intr[:, 0, 0] *= 1.0 + 0.2 * torch.rand(intr.shape[0], generator=g)
+    near = t["near"].reshape(-1) * (1.0 + torch.rand(ext.shape[0], generator=g))
+    far = t["far"].reshape(-1)
+    bg = torch.rand(ext.shape[0], 3, generator=g)
+    for inv in (True, False):
+        ref = prepare_cameras(ext, intr, near, far, bg, scale_invariant=inv)
+        out = prepare_cameras(ext.to(device), intr.to(device), near.to(device), far.to(device), bg.to(device),
+                              scale_invariant=inv)
+        for f in ref.__dataclass_fields__:
+            a, b = getattr(out, f).cpu(), getattr(ref, f)
+            assert a.shape == b.shape, f
+            assert (a - b).abs().max().item() <= 1e-5 * max(1.0, b.abs().max().item()), f

@@ -62,7 +62,21 @@ def prepare_cameras(
     background_color: Tensor,
     scale_invariant: bool = True,
 ) -> RasterCameras:
-    """Camera math of render_cuda (cuda_splatting.py:73-96) for V = (b v) flattened views."""
+    """Camera math of render_cuda (cuda_splatting.py:73-96) for V = (b v) flattened views. Device
+    tensors: one launch (tsplat_raster_cameras); host tensors (the oracle / CPU-baseline callers)
+    take the same math on torch ops."""
+    if extrinsics.is_cuda:
+        lib = _lib.load()
+        v = extrinsics.shape[0]
+        dev = extrinsics.device
+        f = lambda t: t.float().contiguous()
+        ext, intr, nr, fr, bg = f(extrinsics), f(intrinsics), f(near), f(far), f(background_color)
+        out = [torch.empty((v, n), dtype=torch.float32, device=dev) for n in (16, 16, 3, 2, 3, 2)]
+        rc = lib.tsplat_raster_cameras(_lib.ptr(ext), _lib.ptr(intr), _lib.ptr(nr), _lib.ptr(fr), _lib.ptr(bg),
+                                       int(bg.dim() == 2), int(scale_invariant), v, *(_lib.ptr(t) for t in out),
+                                       _lib.stream_ptr(dev))
+        _lib.check(rc, "tsplat_raster_cameras")
+        return RasterCameras(*out)
     extrinsics = extrinsics.float()
     if scale_invariant:
         scale = 1 / near
