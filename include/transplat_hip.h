@@ -105,6 +105,11 @@ int tsplat_raster_fwd(const tsplat_raster_desc* desc,
                       void* workspace, int32_t* status, void* stream);
 
 
+/* Depth-candidate softmax head (reference depth_predictor_trans.py:170-180): logits [n, depths, hw]
+ * (NCHW), disp [n, depths] -> coarse [n, hw] = sum_d disp softmax_d, pdf_max [n, hw] = max_d softmax_d. */
+int tsplat_depth_softmax_fwd(const float* logits, const float* disp, float* coarse, float* pdf_max, int32_t n,
+                             int32_t depths, int32_t hw, void* stream);
+
 /* Per-view camera constants of render_cuda (reference cuda_splatting.py:56-96 with get_fov and
  * get_projection_matrix) from extrinsics [V, 4, 4] (c2w), normalised intrinsics [V, 3, 3], near
  * and far [V], bg [V, 3] (bg_per_view) or [3]: writes the viewmat / projmat / campos / tanfov / bg
@@ -261,7 +266,9 @@ int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void* v, void* 
  *   variance, rsqrt(var + ln_eps), ln_gamma / ln_beta [128]); 4 + residual [M, N];
  *   8 split: column block j of 128 is written to out + j * split_stride as its own [M, 128]
  *   matrix (not with 4); 32 GELU of the INPUT: exact-erf GELU applied to [x1 | x2] as it is
- *   loaded (the producing layer's activation; N must be 128). Epilogues applied in that order.
+ *   loaded (the producing layer's activation; N must be 128); 128 ReLU of the input (same rule);
+ *   64 with 4: the residual is added BEFORE the LayerNorm (post-norm layers: LN(x W^T + b + r)).
+ *   Epilogues applied in that order.
  * ---------------------------------------------------------------------------------------- */
 int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x2, int32_t k2, const float* w,
                           const float* bias, const float* ln_gamma, const float* ln_beta, float ln_eps,

@@ -281,6 +281,15 @@ def mha(qkv, heads: int, scale: float):
     return x.transpose(1, 2).reshape(b, n, heads * d)
 
 
+def depth_softmax(logits, disp):
+    """reference depth_predictor_trans.py:170-180: pdf = softmax over depths, coarse disparity =
+    sum(disp * pdf), pdf_max = max(pdf)."""
+    pdf = torch.nn.functional.softmax(logits, dim=1)
+    n, d = logits.shape[:2]
+    coarse = (disp.reshape(n, d, 1, 1) * pdf).sum(dim=1, keepdim=True)
+    return coarse, torch.max(pdf, dim=1, keepdim=True)[0]
+
+
 def residual_ln(x, y, ls, norm):
     """DINOv2 pre-norm residual step: x' = x + ls * y (LayerScale), LayerNorm(x') with the next norm."""
     if y is not None:
@@ -304,18 +313,23 @@ def sh_rotation(rotations, d_sh: int):
 
 # kernels.<name> -> oracle.<name>: what a CPU run of the module glue swaps in (tests, bench cpu leg)
 def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, residual=None, split: bool = False,
-                 gelu_in: bool = False):
+                 gelu_in: bool = False, relu_in: bool = False, res_pre_ln: bool = False):
     """CPU restatement of kernels.fused_linear: the reference TransformerLayer's chain
-    (multiview_transformer.py:327-407) torch.cat -> nn.Linear -> nn.GELU -> nn.LayerNorm -> + x."""
+    (multiview_transformer.py:327-407) torch.cat -> nn.Linear -> nn.GELU -> nn.LayerNorm -> + x, and
+    the UV encoder layers' post-norm form LN(Linear(x) + identity) (utils/encoder.py:131-209)."""
     x = torch.cat([x1, x2], dim=-1) if x2 is not None else x1
     if gelu_in:
         x = torch.nn.functional.gelu(x)
+    if relu_in:
+        x = torch.relu(x)
     y = torch.nn.functional.linear(x, weight, bias)
     if gelu:
         y = torch.nn.functional.gelu(y)
+    if residual is not None and res_pre_ln:
+        y = y + residual
     if ln is not None:
         y = torch.nn.functional.layer_norm(y, (y.shape[-1],), ln[0], ln[1], ln[2])
-    if residual is not None:
+    if residual is not None and not res_pre_ln:
         y = residual + y
     if split:
         return [t.contiguous() for t in y.split(128, dim=-1)]
@@ -331,4 +345,4 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
 
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
-                       "conv_bias_act", "mha", "residual_ln")
+                       "conv_bias_act", "mha", "residual_ln", "depth_softmax")

@@ -388,3 +388,34 @@ def test_residual_ln_kernel(device, rows, dim, with_y, with_ls):
     ox, on = K.residual_ln(d(x), d(y), d(ls), norm.to(device))
     assert (ox.cpu() - rx).abs().max().item() < 1e-5
     assert (on.cpu() - rn).abs().max().item() < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,relu_in", [(128, False), (256, True)])
+def test_fused_linear_post_norm(device, k, relu_in):
+    """UV encoder post-norm form LN(x W^T + b + identity) (+ ReLU on the FFN hidden input)."""
+    from transplat_amd import kernels as K
+
+    m = 2 * 4096
+    x = seeded((m, k), 91)
+    w = seeded((128, k), 92) / math.sqrt(k)
+    b = seeded((128,), 93)
+    r = seeded((m, 128), 94)
+    lnp = (seeded((128,), 95) * 0.1 + 1.0, seeded((128,), 96) * 0.1, 1e-5)
+    ref = E.fused_linear(x, w, bias=b, ln=lnp, residual=r, relu_in=relu_in, res_pre_ln=True)
+    d = lambda t: t.to(device)
+    out = K.fused_linear(d(x), d(w), bias=d(b), ln=(d(lnp[0]), d(lnp[1]), lnp[2]), residual=d(r), relu_in=relu_in,
+                         res_pre_ln=True).cpu()
+    assert (out - ref).abs().max().item() < 2e-4
+
+
+@pytest.mark.gpu
+def test_depth_softmax_kernel(device):
+    """Depth-candidate softmax head (expected disparity + max pdf) vs the CPU restatement."""
+    from transplat_amd import kernels as K
+
+    logits = seeded((2, 128, 64, 64), 97) * 4.0
+    disp = torch.linspace(0.01, 1.0, 128).repeat(2, 1).reshape(2, 128, 1, 1)
+    rc, rm = E.depth_softmax(logits, disp)
+    oc, om = K.depth_softmax(logits.to(device), disp.to(device))
+    assert (oc.cpu() - rc).abs().max().item() < 1e-6 and (om.cpu() - rm).abs().max().item() < 1e-6

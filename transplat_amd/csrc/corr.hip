@@ -368,3 +368,45 @@ extern "C" int tsplat_msda_fwd(const float* value, const float* loc, const float
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Depth-candidate softmax head (reference depth_predictor_trans.py:170-180):
+//   pdf = softmax(logits, dim = depth);  coarse = sum_d disp[d] * pdf[d];  pdf_max = max_d pdf[d]
+// one thread per pixel over the D channel planes of [N, D, H*W] (coalesced across pixels); the
+// [N, D, H, W] pdf is never written (nothing else reads it).
+namespace tsplat {
+namespace corr {
+
+__global__ void __launch_bounds__(kThreads)
+depth_softmax_kernel(const float* __restrict__ logits, const float* __restrict__ disp, float* __restrict__ coarse,
+                     float* __restrict__ pmax, int D, int HW) {
+    const int p = blockIdx.x * kThreads + threadIdx.x, n = blockIdx.y;
+    if (p >= HW) return;
+    const float* l = logits + (size_t)n * D * HW + p;
+    const float* dv = disp + (size_t)n * D;
+    float m = -INFINITY;
+    for (int d = 0; d < D; ++d) m = fmaxf(m, l[(size_t)d * HW]);
+    float s = 0.f, w = 0.f;
+    for (int d = 0; d < D; ++d) {
+        const float e = expf(l[(size_t)d * HW] - m);
+        s += e;
+        w += e * dv[d];
+    }
+    coarse[(size_t)n * HW + p] = w / s;
+    pmax[(size_t)n * HW + p] = 1.0f / s;  // = exp(m - m) / s, the largest pdf entry
+}
+
+}  // namespace corr
+}  // namespace tsplat
+
+extern "C" int tsplat_depth_softmax_fwd(const float* logits, const float* disp, float* coarse, float* pdf_max,
+                                        int32_t n, int32_t depths, int32_t hw, void* stream_) {
+    using namespace tsplat::corr;
+    if (!logits || !disp || !coarse || !pdf_max || n <= 0 || depths <= 0 || hw <= 0 || n > 65535)
+        return TSPLAT_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    hipLaunchKernelGGL(depth_softmax_kernel, dim3((hw + kThreads - 1) / kThreads, n), dim3(kThreads), 0, stream,
+                       logits, disp, coarse, pdf_max, depths, hw);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

@@ -28,7 +28,11 @@ constexpr int kBN = 128;  // columns per workgroup
 constexpr int kBK = 64;   // K chunk
 constexpr int kThreads = 512;  // 8 waves: two per SIMD
 
-enum Flags : int { kGelu = 1, kLayerNorm = 2, kResidual = 4, kSplit = 8, kBias = 16, kGeluIn = 32 };
+enum Flags : int {
+    kGelu = 1, kLayerNorm = 2, kResidual = 4, kSplit = 8, kBias = 16, kGeluIn = 32,
+    kResPreLN = 64,  // with kResidual: the residual is added BEFORE the LayerNorm (post-norm layers)
+    kReluIn = 128,   // ReLU applied to X as it is staged (the producing FFN layer's activation)
+};
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
@@ -143,13 +147,15 @@ __device__ __forceinline__ void stage_load(const Args& a, int m0, int n0, int K,
 }
 
 template <int BM>
-__device__ __forceinline__ void stage_store(float* sX, float* sW, int tid, const Stage<BM>& st, bool gelu_in) {
+__device__ __forceinline__ void stage_store(float* sX, float* sW, int tid, const Stage<BM>& st, bool gelu_in,
+                                            bool relu_in) {
     const int srow = tid >> 4, sq = tid & 15;
 #pragma unroll
     for (int i = 0; i < BM / 32; ++i) {
         const int r = srow + 32 * i;
         floatx4 x = st.x[i];
         if (gelu_in) x = (floatx4){gelu_erf(x.x), gelu_erf(x.y), gelu_erf(x.z), gelu_erf(x.w)};
+        if (relu_in) x = (floatx4){fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f)};
         *reinterpret_cast<floatx4*>(&sX[r * kBK + ((sq ^ (r & 15)) * 4)]) = x;
     }
 #pragma unroll
@@ -209,6 +215,7 @@ linear_f32_kernel(Args a) {
     const int q0 = BM == 64 ? 0 : 4 * sel;            // first 16-B unit of the wave's k-steps
     constexpr int NQ = BM == 64 ? 8 : 4;
     const bool gelu_in = a.flags & kGeluIn;  // GELU of the producing layer applied to X on its way to LDS
+    const bool relu_in = a.flags & kReluIn;
 
     floatx16 acc;
 #pragma unroll
@@ -224,20 +231,20 @@ linear_f32_kernel(Args a) {
     }
     stage_load<BM, ATTN>(a, m0, n0, K, 0, tid, s0, ar);
     if (nchunks > 1) stage_load<BM, ATTN>(a, m0, n0, K, 1, tid, s1, ar);
-    stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in);
+    stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in, relu_in);
     __syncthreads();
     for (int ck = 0; ck < nchunks; ck += 2) {
         // even chunk ck (buffer 0); s1 holds chunk ck + 1, s0 is free
         if (ck + 2 < nchunks) stage_load<BM, ATTN>(a, m0, n0, K, ck + 2, tid, s0, ar);
         chunk_mfma<NQ>(sX[0], sW[0], wrow, xr, h, q0, acc);
         if (ck + 1 >= nchunks) break;
-        stage_store<BM>(sX[1], sW[1], tid, s1, gelu_in);
+        stage_store<BM>(sX[1], sW[1], tid, s1, gelu_in, relu_in);
         __syncthreads();
         // odd chunk ck + 1 (buffer 1); s0 holds chunk ck + 2, s1 is free
         if (ck + 3 < nchunks) stage_load<BM, ATTN>(a, m0, n0, K, ck + 3, tid, s1, ar);
         chunk_mfma<NQ>(sX[1], sW[1], wrow, xr, h, q0, acc);
         if (ck + 2 >= nchunks) break;
-        stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in);
+        stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in, relu_in);
         __syncthreads();
     }
     __syncthreads();  // every wave is done with the LDS tiles
@@ -273,6 +280,17 @@ linear_f32_kernel(Args a) {
     if (a.flags & kGelu) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) y[r] = gelu_erf(y[r]);
+    }
+    if ((a.flags & kResidual) && (a.flags & kResPreLN) && m < a.M) {
+        const float* rr = a.res + (size_t)m * a.N + nb;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const floatx4 r = *reinterpret_cast<const floatx4*>(rr + 8 * u);
+            y[4 * u] += r.x;
+            y[4 * u + 1] += r.y;
+            y[4 * u + 2] += r.z;
+            y[4 * u + 3] += r.w;
+        }
     }
     if (a.flags & kLayerNorm) {  // N == 128: the workgroup holds whole rows
         float s = 0.f;
@@ -314,7 +332,7 @@ linear_f32_kernel(Args a) {
         dst = a.out + (size_t)m * a.N;
         col0 = nb;
     }
-    const float* res = (a.flags & kResidual) ? a.res + (size_t)m * a.N : nullptr;
+    const float* res = ((a.flags & kResidual) && !(a.flags & kResPreLN)) ? a.res + (size_t)m * a.N : nullptr;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         floatx4 o = {y[4 * u], y[4 * u + 1], y[4 * u + 2], y[4 * u + 3]};
@@ -335,7 +353,8 @@ extern "C" int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x
     using namespace tsplat::linear;
     if (!x1 || !w || !out || M <= 0 || N <= 0 || k1 <= 0 || k2 < 0) return TSPLAT_EINVAL;
     if (k1 % kBK || k2 % kBK || N % kBN || (k2 > 0 && !x2)) return TSPLAT_EINVAL;
-    if ((flags & kGeluIn) && N != kBN) return TSPLAT_EINVAL;  // each X element staged exactly once
+    if ((flags & (kGeluIn | kReluIn)) && N != kBN) return TSPLAT_EINVAL;  // each X element staged once
+    if ((flags & kResPreLN) && !(flags & kResidual)) return TSPLAT_EINVAL;
     if ((flags & kBias) && !bias) return TSPLAT_EINVAL;
     if ((flags & kLayerNorm) && (N != kBN || !ln_gamma || !ln_beta)) return TSPLAT_EINVAL;
     if ((flags & kResidual) && (!residual || (flags & kSplit))) return TSPLAT_EINVAL;

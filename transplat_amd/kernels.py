@@ -228,13 +228,15 @@ def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", 
 
 
 _LIN_GELU, _LIN_LN, _LIN_RES, _LIN_SPLIT, _LIN_BIAS, _LIN_GELU_IN = 1, 2, 4, 8, 16, 32
+_LIN_RES_PRE_LN, _LIN_RELU_IN = 64, 128
 
 
 def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, residual=None, split: bool = False,
-                 gelu_in: bool = False):
+                 gelu_in: bool = False, relu_in: bool = False, res_pre_ln: bool = False):
     """epilogue([x1 | x2] weight^T) in one exact-fp32 MFMA launch (tsplat_linear_f32_fwd):
     (+ bias) -> (exact GELU) -> (LayerNorm with ln = (gamma, beta, eps), N = 128) -> (+ residual);
-    gelu_in applies exact GELU to the input first (the producing layer's activation, N = 128).
+    gelu_in / relu_in apply exact GELU / ReLU to the input first (the producing layer's activation,
+    N = 128); res_pre_ln adds the residual before the LayerNorm (post-norm: LN(y + residual)).
     x1 [..., k1], x2 [..., k2] (concatenated along the last axis without materialising it);
     split=True returns the N / 128 column blocks as separate contiguous [..., 128] tensors."""
     lib = _lib.load()
@@ -250,7 +252,8 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     if b is not None and b.shape[0] != m:
         raise ValueError("x1 and x2 row counts differ")
     flags = (_LIN_GELU if gelu else 0) | (_LIN_LN if ln is not None else 0) | (_LIN_BIAS if bias is not None else 0)
-    flags |= _LIN_GELU_IN if gelu_in else 0
+    flags |= (_LIN_GELU_IN if gelu_in else 0) | (_LIN_RELU_IN if relu_in else 0)
+    flags |= _LIN_RES_PRE_LN if res_pre_ln and residual is not None else 0
     res = None
     if residual is not None:
         res = _f32(residual).reshape(m, n)
@@ -322,6 +325,20 @@ def residual_ln(x, y, ls, norm):
                                     _lib.stream_ptr(x.device))
     _lib.check(rc, "tsplat_residual_ln_fwd")
     return x_out, n_out
+
+
+def depth_softmax(logits, disp):
+    """(coarse disparity, max pdf) of softmax(logits, dim=1) over the depth candidates:
+    logits [N, D, H, W], disp [N, D(, 1, 1)] -> two [N, 1, H, W] maps (tsplat_depth_softmax_fwd)."""
+    lib = _lib.load()
+    n, d, h, w = logits.shape
+    lf = _f32(logits)
+    df = _f32(disp.reshape(n, d))
+    coarse = torch.empty((n, 1, h, w), dtype=torch.float32, device=logits.device)
+    pmax = torch.empty_like(coarse)
+    _lib.check(lib.tsplat_depth_softmax_fwd(_lib.ptr(lf), _lib.ptr(df), _lib.ptr(coarse), _lib.ptr(pmax), n, d,
+                                            h * w, _lib.stream_ptr(logits.device)), "tsplat_depth_softmax_fwd")
+    return coarse, pmax
 
 
 def mha(qkv, heads: int, scale: float):

@@ -181,9 +181,13 @@ class DepthPredictorTrans(nn.Module):
 
         raw_correlation = (run_sequential(self.corr_refine_net, raw_correlation_in)
                            + self.regressor_residual(raw_correlation_in))
-        pdf = F.softmax(_conv_gelu_conv(self.depth_head_lowres, raw_correlation), dim=1)
-        coarse_disps = (disp_candi_curr * pdf).sum(dim=1, keepdim=True)
-        pdf_max = torch.max(pdf, dim=1, keepdim=True)[0]
+        logits = _conv_gelu_conv(self.depth_head_lowres, raw_correlation)
+        if logits.dtype == torch.float32:  # softmax, expected disparity and max in one pass
+            coarse_disps, pdf_max = kernels.depth_softmax(logits, disp_candi_curr)
+        else:
+            pdf = F.softmax(logits, dim=1)
+            coarse_disps = (disp_candi_curr * pdf).sum(dim=1, keepdim=True)
+            pdf_max = torch.max(pdf, dim=1, keepdim=True)[0]
         pdf_max = F.interpolate(pdf_max, scale_factor=self.upscale_factor)
         fullres_disps = F.interpolate(coarse_disps, scale_factor=self.upscale_factor, mode="bilinear",
                                       align_corners=True)

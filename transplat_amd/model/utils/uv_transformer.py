@@ -43,8 +43,8 @@ class UVSelfAttention(nn.Module):
         self.value_proj = nn.Linear(embed_dims, embed_dims)
         self.output_proj = nn.Linear(embed_dims, embed_dims)
 
-    def forward(self, query, value, query_pos, ref_2d, bev_h: int, bev_w: int):
-        identity = query
+    def core(self, query, value, query_pos, ref_2d, bev_h: int, bev_w: int):
+        """The sampled values before output_proj (forward = output_proj(core) + identity)."""
         if query_pos is not None:
             query = query + query_pos
         bsv, nq, _ = query.shape
@@ -53,8 +53,11 @@ class UVSelfAttention(nn.Module):
         weights = self.attention_weights(query).view(bsv, nq, self.num_points).softmax(-1)
         # offset / (W, H) per coordinate (the reference divides by the spatial-shape tensor)
         loc = ref_2d[:, :, None, :] + torch.stack((offsets[..., 0] / bev_w, offsets[..., 1] / bev_h), -1)
-        out = kernels.msda(value, loc, weights, bev_h, bev_w)
-        return self.dropout(self.output_proj(out)) + identity
+        return kernels.msda(value, loc, weights, bev_h, bev_w)
+
+    def forward(self, query, value, query_pos, ref_2d, bev_h: int, bev_w: int):
+        out = self.core(query, value, query_pos, ref_2d, bev_h, bev_w)
+        return self.dropout(self.output_proj(out)) + query
 
 
 class UVCrossAttention(nn.Module):
@@ -76,15 +79,17 @@ class UVCrossAttention(nn.Module):
         self.value_proj = nn.Linear(embed_dims, embed_dims)
         self.output_proj = nn.Linear(embed_dims, embed_dims)
 
-    def forward(self, query, key_cl, value_cl, cameras, bev_h: int, bev_w: int):
-        identity = query
-        b = key_cl.shape[0]
+    def core(self, query, key_cl, value_cl, cameras, bev_h: int, bev_w: int):
+        """The correlation before output_proj (forward = output_proj(core) + identity)."""
         value = self.value_proj(value_cl)  # per view; the kernel reads the other view (the flip)
         offsets = self.sampling_offsets(query)
         logits = self.attention_weights(query)
         intr, pose, disp = cameras
-        out = kernels.uv_cross(value, key_cl, intr, pose, disp, offsets, logits, bev_h, bev_w)
-        return self.dropout(self.output_proj(out)) + identity
+        return kernels.uv_cross(value, key_cl, intr, pose, disp, offsets, logits, bev_h, bev_w)
+
+    def forward(self, query, key_cl, value_cl, cameras, bev_h: int, bev_w: int):
+        out = self.core(query, key_cl, value_cl, cameras, bev_h, bev_w)
+        return self.dropout(self.output_proj(out)) + query
 
 
 class UVCoarseAttention(nn.Module):
@@ -153,9 +158,34 @@ class UVTransformerEncoderLayer(nn.Module):
     def forward(self, query, key_cl, bev_pos, ref_2d, cameras, bev_h, bev_w):
         if self.mode == "coarse":
             return self.attentions[0](query, key_cl, cameras, bev_h, bev_w)
+        if self._fused_ok(query):
+            return self._fine_fused(query, key_cl, bev_pos, ref_2d, cameras, bev_h, bev_w)
         query = self.norms[0](self.attentions[0](query, query, bev_pos, ref_2d, bev_h, bev_w))
         query = self.norms[1](self.attentions[1](query, key_cl, key_cl, cameras, bev_h, bev_w))
         return self.norms[2](self.ffns[0](query, None))
+
+    def _fused_ok(self, query) -> bool:
+        ffn = self.ffns[0]
+        return (query.dtype == torch.float32 and not torch.is_autocast_enabled(query.device.type)
+                and self.embed_dims == 128 and len(ffn.layers) == 3 and ffn.feedforward_channels % 128 == 0)
+
+    def _fine_fused(self, query, key_cl, bev_pos, ref_2d, cameras, bev_h, bev_w):
+        """Fine layer with each output projection + bias + identity + LayerNorm (and the FFN's
+        second Linear with its ReLU-on-load) as one kernels.fused_linear launch; same math as the
+        module chain (dropout is the identity at test time)."""
+        K = kernels
+        sa, ca, ffn = self.attentions[0], self.attentions[1], self.ffns[0]
+        ln = lambda m: (m.weight, m.bias, m.eps)
+        out = sa.core(query, query, bev_pos, ref_2d, bev_h, bev_w)
+        query = K.fused_linear(out, sa.output_proj.weight, bias=sa.output_proj.bias, ln=ln(self.norms[0]),
+                               residual=query, res_pre_ln=True)
+        out = ca.core(query, key_cl, key_cl, cameras, bev_h, bev_w)
+        query = K.fused_linear(out, ca.output_proj.weight, bias=ca.output_proj.bias, ln=ln(self.norms[1]),
+                               residual=query, res_pre_ln=True)
+        fc1, fc2 = ffn.layers[0][0], ffn.layers[1]
+        hidden = K.fused_linear(query, fc1.weight, bias=fc1.bias)
+        return K.fused_linear(hidden, fc2.weight, bias=fc2.bias, ln=ln(self.norms[2]), residual=query,
+                              res_pre_ln=True, relu_in=True)
 
 
 class UVTransformerEncoder(nn.Module):
