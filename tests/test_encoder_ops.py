@@ -182,7 +182,9 @@ def test_gaussian_adapter_kernel(device):
     ((2, 128, 64, 64), 8, "silu", False, False), ((2, 32, 256, 256), 8, "silu", True, True),
     ((2, 128, 16, 16), 8, "none", True, False), ((2, 32, 64, 64), 4, "gelu", False, True),
     ((3, 12, 5, 7), 4, "silu", True, True),  # odd HW: scalar path
-    ((2, 128, 4096), 8, "none", False, True)])
+    ((2, 128, 4096), 8, "none", False, True),
+    ((2, 128, 64, 64), 32, "silu", True, True), ((2, 64, 32, 32), 32, "gelu", False, True),  # single launch
+    ((2, 96, 40, 40), 32, "silu", True, False)])
 def test_group_norm_kernel(device, shape, groups, act, res, pb):
     """GroupNorm (+ folded conv bias, + SiLU/GELU, + residual) vs torch on CPU."""
     from transplat_amd import kernels as K

@@ -1,4 +1,5 @@
-// GroupNorm (+ activation, + residual) over NCHW fp32, two launches.
+// GroupNorm (+ activation, + residual) over NCHW fp32: one launch when a group fits one
+// workgroup's registers (<= 16,384 elements), else two.
 //
 // Replaces the GroupNorm -> SiLU/GELU (-> residual add) chains of the depth predictor's U-Nets
 // and refine heads (reference src/model/encoder/matching/ldm_unet/{unet.py:177-370, util.py:
@@ -168,6 +169,85 @@ apply_kernel(const float* __restrict__ x, const float* __restrict__ pb, const fl
     }
 }
 
+// Single-launch form for groups of at most 512 * NPT elements: one 512-thread workgroup per
+// (sample, group) holds the group in registers (NPT floats per thread), reduces the mean and then
+// the centred sum of squares (two exact block reductions, no partials), and writes
+// act(norm) (+ residual) -- one read and one write of x, one launch instead of two.
+constexpr int kFusedThreads = 512;
+
+__device__ __forceinline__ float block_sum512(float v, float* red) {
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();  // red may still be read from the previous reduction
+    if ((threadIdx.x & (kWave - 1)) == 0) red[w] = v;
+    __syncthreads();
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kFusedThreads / kWave; ++i) t += red[i];
+    return t;
+}
+
+template <int NPT, int ACT, bool RES>
+__global__ void __launch_bounds__(kFusedThreads)
+fused_kernel(const float* __restrict__ x, const float* __restrict__ pb, const float* __restrict__ gamma,
+             const float* __restrict__ beta, const float* __restrict__ res, float* __restrict__ y, int L, int HW,
+             int cpg, int G, float eps) {
+    __shared__ float red[kFusedThreads / kWave];
+    const int seg = blockIdx.x, tid = threadIdx.x;
+    const int g = seg % G;
+    const int64_t base = (int64_t)seg * L;
+    float4 v[NPT / 4];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NPT / 4; ++k) {
+        const int i = (k * kFusedThreads + tid) * 4;  // HW % 4 == 0: one channel per float4
+        if (i < L) {
+            v[k] = *reinterpret_cast<const float4*>(x + base + i);
+            if (pb) {
+                const float b = pb[g * cpg + i / HW];
+                v[k].x += b;
+                v[k].y += b;
+                v[k].z += b;
+                v[k].w += b;
+            }
+            s += (v[k].x + v[k].y) + (v[k].z + v[k].w);
+        }
+    }
+    const float mean = block_sum512(s, red) / (float)L;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NPT / 4; ++k) {
+        const int i = (k * kFusedThreads + tid) * 4;
+        if (i < L) {
+            const float a = v[k].x - mean, b = v[k].y - mean, c = v[k].z - mean, d = v[k].w - mean;
+            q += (a * a + b * b) + (c * c + d * d);
+        }
+    }
+    const float rstd = rsqrtf(block_sum512(q, red) / (float)L + eps);
+#pragma unroll
+    for (int k = 0; k < NPT / 4; ++k) {
+        const int i = (k * kFusedThreads + tid) * 4;
+        if (i < L) {
+            const int c = g * cpg + i / HW;
+            const float sc = rstd * gamma[c], sh = beta[c] - sc * mean;
+            float4 o;
+            o.x = activate<ACT>(v[k].x * sc + sh);
+            o.y = activate<ACT>(v[k].y * sc + sh);
+            o.z = activate<ACT>(v[k].z * sc + sh);
+            o.w = activate<ACT>(v[k].w * sc + sh);
+            if (RES) {
+                const float4 r = *reinterpret_cast<const float4*>(res + base + i);
+                o.x = post_residual<ACT>(o.x + r.x);
+                o.y = post_residual<ACT>(o.y + r.y);
+                o.z = post_residual<ACT>(o.z + r.z);
+                o.w = post_residual<ACT>(o.w + r.w);
+            }
+            *reinterpret_cast<float4*>(y + base + i) = o;
+        }
+    }
+}
+
 }  // namespace gn
 }  // namespace tsplat
 
@@ -197,6 +277,35 @@ extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, cons
     const dim3 grid((unsigned)S, (unsigned)(n * groups));
     const bool vec = (hw % 4 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
                      (!residual || (uintptr_t)residual % 16 == 0);
+    if (vec && L <= (int64_t)kFusedThreads * 32 && x != y) {
+        // the whole group fits one workgroup's registers: single launch
+        const int npt = L <= kFusedThreads * 4 ? 4 : L <= kFusedThreads * 8 ? 8 : L <= kFusedThreads * 16 ? 16 : 32;
+        TSPLAT_PROF_BEGIN(prof::kGroupNorm, stream);
+#define TSPLAT_GN_F(N, A, R)                                                                                  \
+    hipLaunchKernelGGL((fused_kernel<N, A, R>), dim3((unsigned)(n * groups)), dim3(kFusedThreads), 0, stream, x, \
+                       pre_bias, gamma, beta, residual, y, (int)L, (int)hw, cpg, groups, eps)
+#define TSPLAT_GN_FA(N, R)                   \
+    switch (act) {                           \
+        case 0: TSPLAT_GN_F(N, 0, R); break; \
+        case 1: TSPLAT_GN_F(N, 1, R); break; \
+        case 2: TSPLAT_GN_F(N, 2, R); break; \
+        default: TSPLAT_GN_F(N, 3, R); break; \
+    }
+#define TSPLAT_GN_FN(N)                                                       \
+    if (residual) { TSPLAT_GN_FA(N, true) } else { TSPLAT_GN_FA(N, false) }
+        switch (npt) {
+            case 4: TSPLAT_GN_FN(4); break;
+            case 8: TSPLAT_GN_FN(8); break;
+            case 16: TSPLAT_GN_FN(16); break;
+            default: TSPLAT_GN_FN(32); break;
+        }
+#undef TSPLAT_GN_FN
+#undef TSPLAT_GN_FA
+#undef TSPLAT_GN_F
+        TSPLAT_PROF_END(prof::kGroupNorm, stream);
+        TSPLAT_CHECK_LAUNCH();
+        return TSPLAT_OK;
+    }
     float2* part = (float2*)workspace;
     TSPLAT_PROF_BEGIN(prof::kGroupNorm, stream);
     if (vec)
