@@ -241,11 +241,14 @@ int tsplat_win_attn_fwd(const float* q, const float* k, const float* v, float* o
  * prologue: tsplat_win_attn_split() returns the key split the 128-query kernel uses for the shape
  * (> 1: split, 1: none, 0: another kernel serves it); tsplat_win_attn_partials_fwd runs only the
  * main kernel and leaves the partials (unnormalised O, max in natural log, sum) in workspace
- * (tsplat_win_attn_workspace_bytes bytes), for tsplat_linear_f32_attn_merge_fwd. */
+ * (tsplat_win_attn_workspace_bytes bytes), for tsplat_linear_f32_attn_merge_fwd. Query batch b
+ * attends to the keys / values of batch (b + key_batch_shift) % batch: with the two views stacked
+ * [v0; v1], shift = batch / 2 is the reference's cross-view pairing (batch_features,
+ * multiview_transformer.py:495-515) without building the swapped copy. */
 int32_t tsplat_win_attn_split(int32_t batch, int32_t height, int32_t width, int32_t key_views, int32_t splits);
 int tsplat_win_attn_partials_fwd(const float* q, const float* k, const float* v, void* workspace, int32_t batch,
                                  int32_t height, int32_t width, int32_t channels, int32_t key_views,
-                                 int32_t splits, int32_t with_shift, void* stream);
+                                 int32_t splits, int32_t with_shift, int32_t key_batch_shift, void* stream);
 
 /* bf16 variant (config C3): q, k, v, out are bf16 (raw 16-bit storage), same layouts and
  * semantics; bf16 MFMA with fp32 accumulation and an fp32 softmax (P rounded to bf16 for the

@@ -336,9 +336,13 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     return y
 
 
-def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, merge_weight, ln, residual=None):
+def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, merge_weight, ln, residual=None,
+                    kv_shift: int = 0):
     """CPU restatement of kernels.attention_merge: window attention, merge Linear, LayerNorm,
-    optional residual (reference multiview_transformer.py:327-407)."""
+    optional residual (reference multiview_transformer.py:327-407); kv_shift pairs query batch i
+    with key batch (i + kv_shift) % B (batch_features' view swap, :495-515)."""
+    if kv_shift:
+        k, v = torch.roll(k, -kv_shift, dims=0), torch.roll(v, -kv_shift, dims=0)
     msg = window_attention(q, k, v, h, w, num_splits, with_shift)
     return fused_linear(msg, merge_weight, ln=ln, residual=residual)
 

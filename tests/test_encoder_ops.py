@@ -276,9 +276,11 @@ def test_fused_linear_kernel(device, m, k1, k2, n, gelu, ln, res, split, bias, g
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hw,m,shift,b,res", [(64, 1, True, 2, True), (64, 1, False, 2, False), (64, 2, True, 3, True),
-                                              (32, 1, True, 2, False), (64, 1, True, 8, True)])
-def test_attention_merge_kernel(device, hw, m, shift, b, res):
+@pytest.mark.parametrize("hw,m,shift,b,res,kvs", [(64, 1, True, 2, True, 0), (64, 1, False, 2, False, 0),
+                                                  (64, 2, True, 3, True, 0), (32, 1, True, 2, False, 0),
+                                                  (64, 1, True, 8, True, 0), (64, 1, True, 2, True, 1),
+                                                  (64, 1, False, 4, False, 2), (64, 1, True, 8, False, 4)])
+def test_attention_merge_kernel(device, hw, m, shift, b, res, kvs):
     """Window attention + merge Linear + LayerNorm (+ residual) with the split-key combine folded
     into the merge kernel (tsplat_win_attn_partials_fwd + tsplat_linear_f32_attn_merge_fwd; key
     splits 4 / 8 here, b = 8 takes the unsplit path) vs the CPU restatement."""
@@ -293,9 +295,10 @@ def test_attention_merge_kernel(device, hw, m, shift, b, res):
     r = seeded((b, hw * hw, 128), 47) if res else None
     ks = int(_lib.load().tsplat_win_attn_split(b, hw, hw, m, 2))
     assert (ks > 1) == (b < 8)
-    ref = E.attention_merge(q, k, v, hw, hw, 2, shift, wm, ln, residual=r)
+    ref = E.attention_merge(q, k, v, hw, hw, 2, shift, wm, ln, residual=r, kv_shift=kvs)
     d = lambda t: t.to(device) if t is not None else None
-    out = K.attention_merge(d(q), d(k), d(v), hw, hw, 2, shift, d(wm), (d(ln[0]), d(ln[1]), ln[2]), residual=d(r))
+    out = K.attention_merge(d(q), d(k), d(v), hw, hw, 2, shift, d(wm), (d(ln[0]), d(ln[1]), ln[2]), residual=d(r),
+                            kv_shift=kvs)
     err = (out.cpu() - ref).abs().max().item()
     assert err < 1e-3, err
 

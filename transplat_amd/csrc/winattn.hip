@@ -92,6 +92,7 @@ struct Params {
     int shift_h, shift_w;           // roll of the shifted layer: half a window per axis
     int ksplit, keys_per_split;     // key range [s * keys_per_split, (s+1) * keys_per_split)
     int wh, ww, ww_log2;            // window rows / columns; log2(ww), or -1 if not a power of 2
+    int kv_shift, nbatch;           // keys / values of query batch b come from batch (b + kv_shift) % nbatch
     float scale;
 };
 
@@ -205,8 +206,9 @@ win_attn_f32_kernel(Params p, const float* __restrict__ q, const float* __restri
     const int g = lane >> 4, ql = lane & 15;
     const size_t HW = (size_t)p.H * p.W;
     const float* qb = q + (size_t)b * HW * kC;
-    const float* kb = k + (size_t)b * p.m * HW * kC;
-    const float* vb = v + (size_t)b * p.m * HW * kC;
+    const int bkv = p.kv_shift ? (b + p.kv_shift) % p.nbatch : b;
+    const float* kb = k + (size_t)bkv * p.m * HW * kC;
+    const float* vb = v + (size_t)bkv * p.m * HW * kC;
 
     // this lane's query and its 32 channels [32g, 32g+32)
     const int tq = qblk * kBQ + wid * 16 + ql;
@@ -447,8 +449,9 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
     const int c = lane & 31, h = lane >> 5;
     const size_t HW = (size_t)p.H * p.W;
     const float* qb = q + (size_t)b * HW * kC;
-    const float* kb = k + (size_t)b * p.m * HW * kC;
-    const float* vb = v + (size_t)b * p.m * HW * kC;
+    const int bkv = p.kv_shift ? (b + p.kv_shift) % p.nbatch : b;
+    const float* kb = k + (size_t)bkv * p.m * HW * kC;
+    const float* vb = v + (size_t)bkv * p.m * HW * kC;
 
     // staging: thread = (key row tid & 63, 32-channel quarter tid >> 6)
     const int grow = tid & 63, gpart = tid >> 6;
@@ -673,8 +676,9 @@ win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __r
     const int c = lane & 31, h = lane >> 5;
     const size_t HW = (size_t)p.H * p.W;
     const float* qb = q + (size_t)b * HW * kC;
-    const float* kb = k + (size_t)b * p.m * HW * kC;
-    const float* vb = v + (size_t)b * p.m * HW * kC;
+    const int bkv = p.kv_shift ? (b + p.kv_shift) % p.nbatch : b;
+    const float* kb = k + (size_t)bkv * p.m * HW * kC;
+    const float* vb = v + (size_t)bkv * p.m * HW * kC;
 
     const int tq = qblk * 64 + qg * 32 + c;
     const int qpix = win_pixel(p, wi, tq);
@@ -930,8 +934,9 @@ win_attn_f32_quad_kernel(Params p, const float* __restrict__ q, const float* __r
     const int c = lane & 31, h = lane >> 5;
     const size_t HW = (size_t)p.H * p.W;
     const float* qb = q + (size_t)b * HW * kC;
-    const float* kb = k + (size_t)b * p.m * HW * kC;
-    const float* vb = v + (size_t)b * p.m * HW * kC;
+    const int bkv = p.kv_shift ? (b + p.kv_shift) % p.nbatch : b;
+    const float* kb = k + (size_t)bkv * p.m * HW * kC;
+    const float* vb = v + (size_t)bkv * p.m * HW * kC;
     float* sK = smem + wid * kQuadWave;
     float* sV = sK + kQT * kC;
     int* sReg = reinterpret_cast<int*>(sV + kQT * kVRow);
@@ -1404,6 +1409,8 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     p.wh = height / splits;
     p.ww = width / splits;
     p.ww_log2 = (p.ww & (p.ww - 1)) == 0 ? __builtin_ctz(p.ww) : -1;
+    p.kv_shift = 0;
+    p.nbatch = batch;
     if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
     if (p.L % kBQ || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
@@ -1471,9 +1478,11 @@ extern "C" int32_t tsplat_win_attn_split(int32_t batch, int32_t height, int32_t 
 // tsplat_linear_f32_attn_merge_fwd). Only for shapes where tsplat_win_attn_split() > 1.
 extern "C" int tsplat_win_attn_partials_fwd(const float* q, const float* k, const float* v, void* workspace,
                                             int32_t batch, int32_t height, int32_t width, int32_t channels,
-                                            int32_t key_views, int32_t splits, int32_t with_shift, void* stream_) {
+                                            int32_t key_views, int32_t splits, int32_t with_shift,
+                                            int32_t key_batch_shift, void* stream_) {
     using namespace tsplat::winattn;
     if (!q || !k || !v || !workspace || channels != kC) return TSPLAT_EINVAL;
+    if (key_batch_shift < 0 || key_batch_shift >= batch) return TSPLAT_EINVAL;
     const int ks = tsplat_win_attn_split(batch, height, width, key_views, splits);
     if (ks <= 1) return TSPLAT_EINVAL;
     Params p;
@@ -1488,10 +1497,13 @@ extern "C" int tsplat_win_attn_partials_fwd(const float* q, const float* k, cons
     p.wh = height / splits;
     p.ww = width / splits;
     p.ww_log2 = (p.ww & (p.ww - 1)) == 0 ? __builtin_ctz(p.ww) : -1;
+    p.kv_shift = 0;
+    p.nbatch = batch;
     if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
     p.ksplit = ks;
     p.keys_per_split = p.L * p.m / p.ksplit;
+    p.kv_shift = key_batch_shift;
     const size_t n = (size_t)batch * splits * splits * p.ksplit * p.L;
     Partials part{(float*)workspace, nullptr, nullptr};
     part.m = part.o + n * kC;
@@ -1537,6 +1549,8 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     p.wh = height / splits;
     p.ww = width / splits;
     p.ww_log2 = (p.ww & (p.ww - 1)) == 0 ? __builtin_ctz(p.ww) : -1;
+    p.kv_shift = 0;
+    p.nbatch = batch;
     if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
     if (p.L % kBQ3 || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);

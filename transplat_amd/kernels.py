@@ -274,25 +274,29 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     return out.reshape(*lead, n)
 
 
-def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, merge_weight, ln, residual=None):
+def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, merge_weight, ln, residual=None,
+                    kv_shift: int = 0):
     """norm(window_attention(q, k, v) merge_weight^T) [+ residual] for the fp32 transformer layer.
     Where the attention kernel splits the keys (b = 1 at 64x64), the combine of its partials runs
     in the merge kernel's operand staging (tsplat_win_attn_partials_fwd +
     tsplat_linear_f32_attn_merge_fwd: no combine launch, no [B, L, 128] attention output);
-    otherwise window_attention + fused_linear."""
+    otherwise window_attention + fused_linear. kv_shift: query batch i attends to the keys /
+    values of batch (i + kv_shift) % B (the two-view cross pairing without a swapped copy)."""
     lib = _lib.load()
     b, l, c = q.shape
     m = 1 if k.dim() == 3 else k.shape[1]
     fp32 = q.dtype == k.dtype == v.dtype == torch.float32
     ks = int(lib.tsplat_win_attn_split(b, h, w, m, num_splits)) if fp32 and c == 128 else 0
     if ks <= 1:
+        if kv_shift:
+            k, v = torch.roll(k, -kv_shift, dims=0), torch.roll(v, -kv_shift, dims=0)
         msg = window_attention(q, k, v, h, w, num_splits, with_shift)
         return fused_linear(msg, merge_weight, ln=ln, residual=residual)
     q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
     ws = torch.empty(int(lib.tsplat_win_attn_workspace_bytes(b, h, w, m, num_splits)), dtype=torch.uint8,
                      device=q.device)
     rc = lib.tsplat_win_attn_partials_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(ws), b, h, w, c, m,
-                                          num_splits, int(with_shift), _lib.stream_ptr(q.device))
+                                          num_splits, int(with_shift), int(kv_shift), _lib.stream_ptr(q.device))
     _lib.check(rc, "tsplat_win_attn_partials_fwd")
     n = merge_weight.shape[0]
     out = torch.empty((b, l, n), dtype=torch.float32, device=q.device)

@@ -52,9 +52,11 @@ class TransformerLayer(nn.Module):
             cache[names] = hit
         return hit[1]
 
-    def _forward_fused(self, source, target, height, width, attn_num_splits):
+    def _forward_fused(self, source, target, height, width, attn_num_splits, kv_shift: int = 0):
         """fp32 path: 4-5 kernels.fused_linear launches (exact fp32 MFMA, epilogues fused) around
-        the attention kernel instead of ~12 PyTorch launches; same math as forward() below."""
+        the attention kernel instead of ~12 PyTorch launches; same math as forward() below.
+        kv_shift > 0: `target` is NOT view-swapped; query batch i reads the keys / values of its
+        batch (i + kv_shift) % B (the swap is index arithmetic in the attention kernel)."""
         K = kernels
         if target is source:
             query, key, value = K.fused_linear(source, self._cat_weights(("q_proj", "k_proj", "v_proj")), split=True)
@@ -64,9 +66,9 @@ class TransformerLayer(nn.Module):
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
         if self.no_ffn:
             return K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
-                                     self.merge.weight, ln1, residual=source)
+                                     self.merge.weight, ln1, residual=source, kv_shift=kv_shift)
         message = K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
-                                    self.merge.weight, ln1)
+                                    self.merge.weight, ln1, kv_shift=kv_shift)
         # mlp[0] is the one large plain GEMM of the layer (8192 x 256 x 1024 at b = 1): hipBLASLt
         # runs it at 103 TF, above this build's kernel (66 TF); its GELU moves into mlp[2]'s load
         hidden = self.mlp[0](torch.cat([source, message], dim=-1))
@@ -106,6 +108,14 @@ class TransformerBlock(nn.Module):
         source = self.self_attn(source, source, height=height, width=width, attn_num_splits=attn_num_splits)
         return self.cross_attn_ffn(source, target, height=height, width=width, attn_num_splits=attn_num_splits)
 
+    def forward_pair(self, x, height, width, attn_num_splits, kv_shift: int):
+        """Two views stacked [v0; v1] in x (fp32 fused path): self attention, then cross attention
+        against the other view as a key-batch shift instead of a swapped copy."""
+        # the cross layer's keys / values come from the block INPUT (reference batch_features runs
+        # between blocks, :624-628), its queries from the self-attention output
+        y = self.self_attn._forward_fused(x, x, height, width, attn_num_splits)
+        return self.cross_attn_ffn._forward_fused(y, x, height, width, attn_num_splits, kv_shift=kv_shift)
+
 
 def batch_features(features):
     """(reference :495-515) queries [N*B, ...] and the other N-1 views [N*B, N-1, ...]."""
@@ -142,6 +152,14 @@ class MultiViewFeatureTransformer(nn.Module):
         num_views = len(multi_view_features)
         if not attn_num_splits or attn_num_splits <= 1:
             raise NotImplementedError("TranSplat runs split-window attention (multiview_trans_attn_split=2)")
+        if (num_views == 2 and c == 128 and multi_view_features[0].dtype == torch.float32
+                and not torch.is_autocast_enabled(multi_view_features[0].device.type)):
+            # two views: batch_features' concat0 after each block is the block output itself and
+            # concat1 its view swap, so the layers pair query batch i with key batch (i + b) % 2b
+            x = torch.cat(multi_view_features, dim=0).reshape(2 * b, c, -1).permute(0, 2, 1).contiguous()
+            for layer in self.layers:
+                x = layer.forward_pair(x, h, w, attn_num_splits, kv_shift=b)
+            return [f.view(b, h, w, c).permute(0, 3, 1, 2).contiguous() for f in x.chunk(chunks=2, dim=0)]
         concat0, concat1 = batch_features(multi_view_features)
         concat0 = concat0.reshape(num_views * b, c, -1).permute(0, 2, 1)  # [N*B, HW, C]
         concat1 = concat1.reshape(num_views * b, num_views - 1, c, -1).permute(0, 1, 3, 2)  # [N*B, N-1, HW, C]
