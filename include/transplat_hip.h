@@ -213,13 +213,15 @@ int tsplat_residual_ln_fwd(const float* x, const float* y, const float* ls, cons
  *   sh_rot [batch*views, d_sh, d_sh] block-diagonal real-SH rotation of c2w R (e3nn wigner_D);
  *   outputs means [batch, views*H*W, 3], cov [.., 3, 3], harmonics [.., 3, d_sh], opacities [..];
  *   opacity = 0.5 (1 - (1 - pdf)^e + pdf^(1/e)) / gaussians_per_pixel (map_pdf_to_opacity).
+ *   raw_nchw != 0: raw is the head's output map [views * batch, raw_ch, H*W] as the convolution
+ *   wrote it ((v b) order, channel stride H*W), read in place instead of its [b, v, HW, c] copy.
  * ---------------------------------------------------------------------------------------- */
 int tsplat_gaussian_adapter_fwd(const float* raw, const float* depths, const float* densities,
                                 const float* cams, const float* sh_rot, float* means, float* cov,
                                 float* harmonics, float* opacities, int32_t batch, int32_t views,
                                 int32_t height, int32_t width, int32_t raw_ch, int32_t d_sh,
                                 float scale_min, float scale_max, float opacity_exponent,
-                                int32_t gaussians_per_pixel, void* stream);
+                                int32_t gaussians_per_pixel, int32_t raw_nchw, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Shifted-window attention of the multi-view transformer (exact fp32 MFMA):

@@ -163,12 +163,20 @@ def test_oracle_adapter_shapes_and_identity_rotation():
 
 
 @pytest.mark.gpu
-def test_gaussian_adapter_kernel(device):
+@pytest.mark.parametrize("layout", ["bvhwc", "head_nchw"])
+def test_gaussian_adapter_kernel(device, layout):
+    from einops import rearrange
     from transplat_amd import kernels as K
 
     raw, depths, dens, ext, intr = _adapter_inputs()
     ref = E.gaussian_adapter(raw, depths, dens, ext, intr, (24, 32), 0.5, 15.0, 2.0)
-    out = K.gaussian_adapter(*(t.to(device) for t in (raw, depths, dens, ext, intr)), (24, 32), 0.5, 15.0, 2.0)
+    raw_d = raw.to(device)
+    if layout == "head_nchw":
+        # the depth head's output map [(v b), c, h, w] and the view the encoder hands the adapter
+        head = rearrange(raw_d, "b v (h w) c -> (v b) c h w", h=24).contiguous()
+        raw_d = rearrange(head, "(v b) c h w -> b v (h w) c", b=2)
+        assert not raw_d.is_contiguous()
+    out = K.gaussian_adapter(raw_d, *(t.to(device) for t in (depths, dens, ext, intr)), (24, 32), 0.5, 15.0, 2.0)
     for name, r, o in zip(("means", "cov", "harmonics", "opacity"), ref, out):
         o = o.cpu()
         # per-element relative error, floored at 1e-3 of the tensor's scale (covariances are

@@ -55,7 +55,7 @@ SIGNATURES = {
     "tsplat_group_norm_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, ctypes.c_int64, _I32]),
     "tsplat_group_norm_fwd": (ctypes.c_int, [_P] * 7 + [_I32, _I32, ctypes.c_int64, _I32, ctypes.c_float, _I32, _P]),
     "tsplat_sh_rotation_fwd": (ctypes.c_int, [_P] * 3 + [_I32] * 2 + [_P]),
-    "tsplat_gaussian_adapter_fwd": (ctypes.c_int, [_P] * 9 + [_I32] * 6 + [ctypes.c_float] * 3 + [_I32, _P]),
+    "tsplat_gaussian_adapter_fwd": (ctypes.c_int, [_P] * 9 + [_I32] * 6 + [ctypes.c_float] * 3 + [_I32, _I32, _P]),
     "tsplat_win_attn_split": (_I32, [_I32] * 5),
     "tsplat_depth_softmax_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 3 + [_P]),
     "tsplat_raster_cameras": (ctypes.c_int, [_P] * 5 + [_I32] * 3 + [_P] * 7),

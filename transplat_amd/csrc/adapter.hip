@@ -21,6 +21,7 @@ constexpr int kMaxSh = 25;
 struct Params {
     int B, V, H, W, R, dsh;
     float smin, smax, op_exp, inv_gpp;
+    int nchw;  // raw is the head's [(v b), R, H*W] map (channel stride H*W) instead of [b, v, HW, R]
 };
 
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
@@ -39,7 +40,9 @@ adapter_kernel(Params p, const float* __restrict__ raw, const float* __restrict_
     if (pix >= hw) return;
     const int b = bv / p.V, v = bv - b * p.V;
     const float* c = cams + (size_t)bv * 22;
-    const float* r = raw + ((size_t)bv * hw + pix) * p.R;
+    // channel k of this pixel's raw vector is r[k * cs]
+    const size_t cs = p.nchw ? (size_t)hw : 1;
+    const float* r = p.nchw ? raw + (size_t)(v * p.B + b) * p.R * hw + pix : raw + ((size_t)bv * hw + pix) * p.R;
     const size_t gi = (size_t)b * p.V * hw + (size_t)v * hw + pix;  // output index (b, v*HW + pix)
     const float depth = depths[(size_t)bv * hw + pix];
 
@@ -47,7 +50,7 @@ adapter_kernel(Params p, const float* __restrict__ raw, const float* __restrict_
     const int py = pix / p.W, px = pix - py * p.W;
     const float fw = (float)p.W, fh = (float)p.H;
     const float x = ((float)px + 0.5f) / fw + (sigmoidf(r[0]) - 0.5f) * (1.0f / fw);
-    const float y = ((float)py + 0.5f) / fh + (sigmoidf(r[1]) - 0.5f) * (1.0f / fh);
+    const float y = ((float)py + 0.5f) / fh + (sigmoidf(r[cs]) - 0.5f) * (1.0f / fh);
     const float* ki = c + 12;
     float d0 = ki[0] * x + ki[1] * y + ki[2];
     float d1 = ki[3] * x + ki[4] * y + ki[5];
@@ -66,8 +69,8 @@ adapter_kernel(Params p, const float* __restrict__ raw, const float* __restrict_
     const float mult = c[21];
     float s[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) s[i] = (p.smin + (p.smax - p.smin) * sigmoidf(r[2 + i])) * depth * mult;
-    float qi = r[5], qj = r[6], qk = r[7], qr = r[8];
+    for (int i = 0; i < 3; ++i) s[i] = (p.smin + (p.smax - p.smin) * sigmoidf(r[(2 + i) * cs])) * depth * mult;
+    float qi = r[5 * cs], qj = r[6 * cs], qk = r[7 * cs], qr = r[8 * cs];
     const float qn = sqrtf(qi * qi + qj * qj + qk * qk + qr * qr) + 1e-8f;
     qi /= qn; qj /= qn; qk /= qn; qr /= qn;
     const float two_s = 2.0f / (qi * qi + qj * qj + qk * qk + qr * qr + 1e-8f);
@@ -94,12 +97,12 @@ adapter_kernel(Params p, const float* __restrict__ raw, const float* __restrict_
 #pragma unroll
     for (int ch = 0; ch < 3; ++ch) {
         float sh[DSH];
-        const float* rs = r + 9 + ch * DSH;
+        const float* rs = r + (9 + ch * DSH) * cs;
 #pragma unroll
         for (int k = 0; k < DSH; ++k) {
             const int l = k < 1 ? 0 : (k < 4 ? 1 : (k < 9 ? 2 : (k < 16 ? 3 : 4)));
             const float mask = l == 0 ? 1.0f : (l == 1 ? 0.025f : (l == 2 ? 0.00625f : (l == 3 ? 0.0015625f : 0.000390625f)));
-            sh[k] = rs[k] * mask;
+            sh[k] = rs[k * cs] * mask;
         }
 #pragma unroll
         for (int ll = 0; ll * ll < DSH; ++ll) {
@@ -131,7 +134,7 @@ extern "C" int tsplat_gaussian_adapter_fwd(const float* raw, const float* depths
                                            int32_t views, int32_t height, int32_t width, int32_t raw_ch,
                                            int32_t d_sh, float scale_min, float scale_max,
                                            float opacity_exponent, int32_t gaussians_per_pixel,
-                                           void* stream_) {
+                                           int32_t raw_nchw, void* stream_) {
     using namespace tsplat::adapter;
     if (!raw || !depths || !densities || !cams || !sh_rot || !means || !cov || !harmonics || !opacities)
         return TSPLAT_EINVAL;
@@ -139,7 +142,7 @@ extern "C" int tsplat_gaussian_adapter_fwd(const float* raw, const float* depths
         raw_ch != 9 + 3 * d_sh || gaussians_per_pixel != 1 || opacity_exponent <= 0.f)
         return TSPLAT_EINVAL;
     Params p{batch, views, height, width, raw_ch, d_sh, scale_min, scale_max, opacity_exponent,
-             1.0f / (float)gaussians_per_pixel};
+             1.0f / (float)gaussians_per_pixel, raw_nchw ? 1 : 0};
     hipStream_t stream = (hipStream_t)stream_;
     dim3 grid(ceil_div(height * width, kThreads), batch * views);
 #define TSPLAT_ADAPTER_LAUNCH(N)                                                                     \

@@ -382,7 +382,11 @@ def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape
     b, v, hw, r = raw.shape
     d_sh = (r - 9) // 3
     h, w = image_shape
-    raw, depths, densities = _f32(raw), _f32(depths), _f32(densities)
+    # the head's "(v b) c h w -> b v (h w) c" view of its NCHW output map is read in place
+    nchw = raw.dtype == torch.float32 and raw.stride() == (r * hw, b * r * hw, 1, hw)
+    if not nchw:
+        raw = _f32(raw)
+    depths, densities = _f32(depths), _f32(densities)
     cams = adapter_cameras(extrinsics, intrinsics, image_shape)
     shrot = sh_rotation(extrinsics.reshape(-1, 4, 4)[:, :3, :3], d_sh)
     dev = raw.device
@@ -394,6 +398,6 @@ def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape
     rc = lib.tsplat_gaussian_adapter_fwd(
         _lib.ptr(raw), _lib.ptr(depths), _lib.ptr(densities), _lib.ptr(cams), _lib.ptr(shrot), _lib.ptr(means),
         _lib.ptr(cov), _lib.ptr(harm), _lib.ptr(opac), b, v, h, w, r, d_sh, float(scale_min), float(scale_max),
-        float(opacity_exponent), int(gaussians_per_pixel), _lib.stream_ptr(dev))
+        float(opacity_exponent), int(gaussians_per_pixel), int(nchw), _lib.stream_ptr(dev))
     _lib.check(rc, "tsplat_gaussian_adapter_fwd")
     return means, cov, harm, opac
