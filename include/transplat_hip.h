@@ -304,6 +304,19 @@ int tsplat_small_inverse(const float* in, float* out, int32_t n, int32_t dim, vo
 int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, int32_t tokens, int32_t heads,
                        int32_t head_dim, float scale, void* stream);
 
+/* Direct convolution of the depth predictor U-Nets' low-resolution levels (exact fp32 MFMA),
+ * replacing MIOpen for nn.Conv2d in reference src/model/encoder/matching/ldm_unet/unet.py (ResBlock
+ * in/out convs unet.py:212-250 and 1x1 skip unet.py:258-266, Downsample unet.py:140-170, Upsample
+ * unet.py:105-137): y [batch, c_out, hout, wout] = conv(x, w, bias, stride, padding = ksize / 2)
+ * with x = cat([x1 (c1 channels), x2 (c2 channels, may be 0)], dim 1) [batch, c1 + c2, height, width]
+ * read in place, nearest-upsampled 2x first when upsample = 1. ksize 1 or 3, stride 1 or 2 (not
+ * with upsample), c1 and c2 even. w_packed is the weight [c_out, cin, k, k] laid out as
+ * [ceil(c_out / 32)][k * k][cin / 2][2][32] (zero rows past c_out); bias may be null. ksplit
+ * (1..16) waves share one 32 x 32 output tile. */
+int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* w_packed,
+                          const float* bias, float* y, int32_t batch, int32_t height, int32_t width, int32_t c_out,
+                          int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -271,6 +271,24 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
     return y
 
 
+def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsample: bool = False) -> bool:
+    """Every 2-D convolution the direct kernel takes (so CPU model runs exercise its call sites)."""
+    k = weight.shape[-1]
+    pad = padding[0] if isinstance(padding, (tuple, list)) else (padding if padding is not None else k // 2)
+    return (x.dim() == 4 and k in (1, 3) and stride in (1, 2) and not (upsample and stride != 1) and pad == k // 2
+            and weight.shape[1] == x.shape[1] + c2 and x.shape[1] % 2 == 0 and c2 % 2 == 0)
+
+
+def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: bool = False):
+    """nn.Conv2d(padding = k // 2) of cat([x1, x2], 1), nearest-upsampled 2x first if upsample:
+    the reference ldm_unet chains ResBlock(cat([h, skip])) (unet.py:1096-1100), Upsample
+    (unet.py:128-137: F.interpolate(nearest) -> conv), Downsample (unet.py:160-170)."""
+    x = x1 if x2 is None else torch.cat([x1, x2], dim=1)
+    if upsample:
+        x = torch.nn.functional.interpolate(x, scale_factor=2, mode="nearest")
+    return torch.nn.functional.conv2d(x, weight, bias, stride, weight.shape[-1] // 2)
+
+
 def mha(qkv, heads: int, scale: float):
     """DINOv2 Attention core (reference dinov2_layers/attention.py): reshape to heads, softmax
     attention (torch SDPA math), back to [B, N, heads * head_dim]."""
@@ -349,4 +367,5 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
 
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
-                       "conv_bias_act", "mha", "residual_ln", "depth_softmax")
+                       "conv_bias_act", "mha", "residual_ln", "depth_softmax", "conv2d_direct_ok",
+                       "conv2d_direct")

@@ -61,6 +61,7 @@ SIGNATURES = {
     "tsplat_raster_cameras": (ctypes.c_int, [_P] * 5 + [_I32] * 3 + [_P] * 7),
     "tsplat_small_inverse": (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     "tsplat_mha_f32_fwd": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, ctypes.c_float, _P]),
+    "tsplat_conv2d_f32_fwd": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _P, _P] + [_I32] * 8 + [_P]),
     "tsplat_residual_ln_fwd": (ctypes.c_int, [_P] * 5 + [ctypes.c_float, _P, _P, _I32, _I32, _P]),
     "tsplat_bias_act_fwd": (ctypes.c_int, [_P] * 4 + [_I32, _I32, ctypes.c_int64, _I32, _P]),
     "tsplat_win_attn_partials_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 8 + [_P]),
@@ -119,7 +120,7 @@ def stream_ptr(device: torch.device | None = None) -> int:
 
 PROF_IDS = {"raster_preprocess": 1, "raster_scan": 2, "raster_scatter": 3, "raster_render": 4,
             "uv_coarse": 5, "uv_cross": 6, "msda": 7, "win_attn": 8, "raster": 9,
-            "group_norm": 10, "uv_cross_table": 11, "linear": 12, "mha": 13}
+            "group_norm": 10, "uv_cross_table": 11, "linear": 12, "mha": 13, "conv": 14}
 
 
 def prof_enable(name: str | None) -> None:

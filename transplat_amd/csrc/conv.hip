@@ -1,0 +1,201 @@
+// Direct 3x3 / 1x1 convolution for the depth predictor U-Nets' low-resolution levels on gfx950,
+// exact fp32 MFMA.
+//
+// Semantics: torch.nn.functional.conv2d(x, w, bias, stride, padding = k // 2) on NCHW fp32 (the
+// reference's nn.Conv2d layers in src/model/encoder/matching/ldm_unet/unet.py: ResBlock in/out
+// convolutions unet.py:212-250, Downsample unet.py:140-170, Upsample unet.py:105-137, the ResBlock
+// 1x1 skip unet.py:258-266), with two extensions that remove the glue around them:
+//   * two input sources: x = cat([x1, x2], dim=1) read in place (the output blocks' skip concat);
+//   * upsample = 1: x is first nearest-upsampled 2x (Upsample's F.interpolate) -- read in place.
+//
+// Why not MIOpen here: at 16^2..64^2 with 32..256 channels the fp32 convolutions are latency
+// bound; MIOpen's NCHW kernels take 13-30 us each (~1.1 ms of the step over 56 launches), while
+// the arithmetic is 9-600 MFLOP. This kernel spreads one 32 (cout) x 32 (pixel) output tile over
+// `ksplit` waves of one workgroup (the reduction split over input-channel pairs), so even a 16^2
+// layer fills hundreds of SIMDs.
+//
+// Implicit GEMM: D[co][px] = sum_k W[co][k] X[k][px], k = (tap, ci), one v_mfma_f32_32x32x2_f32
+// per (tap, ci pair): A = the packed weights (one coalesced 256-B load per k-step, layout
+// [co_tile][tap][ci/2][2][32], built once on the host), B = the input gathered at the tap's shifted
+// pixel (32 consecutive pixels per lane half -> 128-B segments; padding lanes read a valid address
+// and select 0). Each wave walks ci pairs w, w + ksplit, ... one batch (all 9 taps of 1-2 pairs, or
+// 8-16 pairs of a 1x1) at a time with the next batch's loads in flight; the ksplit partial tiles are
+// summed through LDS, the bias added, and the tile stored (lanes = consecutive pixels).
+#include "common.h"
+#include "prof.h"
+
+namespace tsplat {
+namespace conv {
+
+constexpr int kMaxWaves = 16;
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+struct Args {
+    const float* x1;
+    const float* x2;
+    const float* wp;    // packed weights [cot][taps][cin/2][2][32]
+    const float* bias;  // [cout] or null
+    float* y;           // [n, cout, hout, wout]
+    int c1, c2, cout, n;
+    int hin, win;       // stored input size
+    int hv, wv;         // virtual input size (2x when upsampling)
+    int hout, wout;
+    int npx;            // n * hout * wout
+};
+
+// G = ci pairs per batch (all their taps): the loads of one batch are in flight while the previous
+// batch's G * T MFMAs run, so a wave's time is ~ (its batches) x (memory latency) for these small
+// layers -- larger G, fewer round trips.
+template <int KS, int S, int UP, int G>
+__global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
+    extern __shared__ float sred[];  // [ksplit][16][64]
+    constexpr int T = KS * KS, PAD = KS / 2;
+    constexpr int B = G * T;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, ksplit = blockDim.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const int cot = blockIdx.y;
+    const int hwo = p.hout * p.wout, hwi = p.hin * p.win;
+    const int px = blockIdx.x * 32 + c;
+    const int pxc = min(px, p.npx - 1);
+    const int nb = pxc / hwo, pix = pxc - nb * hwo;
+    const int oy = pix / p.wout, ox = pix - oy * p.wout;
+    const int cp_all = (p.c1 + p.c2) >> 1, cp1 = p.c1 >> 1;
+
+    // per-tap input offset of this lane's pixel (0 = a valid address, masked, for padding)
+    int off[T];
+    unsigned vmask = 0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int ky = t / KS, kx = t - ky * KS;
+        const int iy = oy * S + ky - PAD, ix = ox * S + kx - PAD;
+        const bool v = px < p.npx && iy >= 0 && iy < p.hv && ix >= 0 && ix < p.wv;
+        off[t] = v ? (UP ? (iy >> 1) * p.win + (ix >> 1) : iy * p.win + ix) : 0;
+        vmask |= (unsigned)v << t;
+    }
+    const size_t wtap = (size_t)cp_all * 64;  // packed-weight stride between taps
+    const float* wbase = p.wp + (size_t)cot * T * wtap + lane;
+    // channel 2 cp + h of the concatenated input for this lane's image
+    auto chan = [&](int cp) -> const float* {
+        return cp < cp1 ? p.x1 + ((size_t)nb * p.c1 + 2 * cp + h) * hwi
+                        : p.x2 + ((size_t)nb * p.c2 + 2 * (cp - cp1) + h) * hwi;
+    };
+    // this wave's ci pairs: w, w + ksplit, ... in batches of G
+    const int ncp = cp_all > w ? (cp_all - w + ksplit - 1) / ksplit : 0;
+    const int nbatch = (ncp + G - 1) / G;
+    auto load = [&](int bi, float* a, float* b) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int i = bi * G + g;
+            const bool ok = i < ncp;
+            const int cp = w + (ok ? i : 0) * ksplit;
+            const float* src = chan(cp);
+            const float* wq = wbase + (size_t)cp * 64;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const float av = wq[t * wtap];
+                const float bv = src[off[t]];
+                a[g * T + t] = ok ? av : 0.f;
+                b[g * T + t] = ok && ((vmask >> t) & 1) ? bv : 0.f;
+            }
+        }
+    };
+
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    float ca[B], cb[B], na[B], nbv[B];
+    if (nbatch > 0) load(0, ca, cb);
+#pragma unroll 1
+    for (int bi = 0; bi < nbatch; ++bi) {
+        const bool more = bi + 1 < nbatch;
+        if (more) load(bi + 1, na, nbv);
+#pragma unroll
+        for (int k = 0; k < B; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[k], cb[k], acc, 0, 0, 0);
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < B; ++k) {
+                ca[k] = na[k];
+                cb[k] = nbv[k];
+            }
+        }
+    }
+
+    // sum the ksplit partial tiles
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sred[(w * 16 + r) * 64 + lane] = acc[r];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
+        const int r = idx >> 6, l = idx & 63;
+        float s = 0.f;
+        for (int k = 0; k < ksplit; ++k) s += sred[(k * 16 + r) * 64 + l];
+        const int co = cot * 32 + 8 * (r >> 2) + 4 * (l >> 5) + (r & 3);
+        const int q = blockIdx.x * 32 + (l & 31);
+        if (co >= p.cout || q >= p.npx) continue;
+        if (p.bias) s += p.bias[co];
+        const int qn = q / hwo, qp = q - qn * hwo;
+        p.y[((size_t)qn * p.cout + co) * hwo + qp] = s;
+    }
+}
+
+}  // namespace conv
+}  // namespace tsplat
+
+extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* w_packed,
+                                     const float* bias, float* y, int32_t batch, int32_t height, int32_t width,
+                                     int32_t c_out, int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit,
+                                     void* stream_) {
+    using namespace tsplat::conv;
+    if (!x1 || !w_packed || !y || batch <= 0 || height <= 0 || width <= 0 || c_out <= 0) return TSPLAT_EINVAL;
+    if (c1 <= 0 || (c1 & 1) || c2 < 0 || (c2 & 1) || (c2 > 0 && !x2)) return TSPLAT_EINVAL;
+    if (!(ksize == 1 || ksize == 3) || !(stride == 1 || stride == 2) || !(upsample == 0 || upsample == 1))
+        return TSPLAT_EINVAL;
+    if (ksplit < 1 || ksplit > kMaxWaves) return TSPLAT_EINVAL;
+    Args p{};
+    p.x1 = x1;
+    p.x2 = x2;
+    p.wp = w_packed;
+    p.bias = bias;
+    p.y = y;
+    p.c1 = c1;
+    p.c2 = c2;
+    p.cout = c_out;
+    p.n = batch;
+    p.hin = height;
+    p.win = width;
+    p.hv = upsample ? 2 * height : height;
+    p.wv = upsample ? 2 * width : width;
+    const int pad = ksize / 2;
+    p.hout = (p.hv + 2 * pad - ksize) / stride + 1;
+    p.wout = (p.wv + 2 * pad - ksize) / stride + 1;
+    if (p.hout <= 0 || p.wout <= 0) return TSPLAT_EINVAL;
+    const int64_t npx = (int64_t)batch * p.hout * p.wout;
+    const int64_t in_elems = (int64_t)batch * (c1 > c2 ? c1 : c2) * height * width;
+    if (npx >= (1ll << 31) || in_elems >= (1ll << 31)) return TSPLAT_EINVAL;
+    p.npx = (int)npx;
+    hipStream_t stream = (hipStream_t)stream_;
+    const dim3 grid((unsigned)((npx + 31) / 32), (unsigned)((c_out + 31) / 32));
+    const dim3 block(64 * ksplit);
+    const size_t lds = (size_t)ksplit * 16 * 64 * sizeof(float);
+    TSPLAT_PROF_BEGIN(tsplat::prof::kConv, stream);
+#define TSPLAT_CONV_LAUNCH(KS, S, UP, G) \
+    hipLaunchKernelGGL((conv_f32_kernel<KS, S, UP, G>), grid, block, lds, stream, p)
+    // ci pairs per batch: 2 (3x3) / 16 (1x1) once a wave has that many, else 1 / 8
+    const int per_wave = ((c1 + c2) / 2 + ksplit - 1) / ksplit;
+    const bool wide = per_wave >= (ksize == 3 ? 2 : 16);
+    if (ksize == 3 && stride == 1 && !upsample) {
+        if (wide) TSPLAT_CONV_LAUNCH(3, 1, 0, 2); else TSPLAT_CONV_LAUNCH(3, 1, 0, 1);
+    } else if (ksize == 3 && stride == 2 && !upsample) {
+        if (wide) TSPLAT_CONV_LAUNCH(3, 2, 0, 2); else TSPLAT_CONV_LAUNCH(3, 2, 0, 1);
+    } else if (ksize == 3 && stride == 1 && upsample) {
+        if (wide) TSPLAT_CONV_LAUNCH(3, 1, 1, 2); else TSPLAT_CONV_LAUNCH(3, 1, 1, 1);
+    } else if (ksize == 1 && stride == 1 && !upsample) {
+        if (wide) TSPLAT_CONV_LAUNCH(1, 1, 0, 16); else TSPLAT_CONV_LAUNCH(1, 1, 0, 8);
+    } else {
+        return TSPLAT_EINVAL;
+    }
+#undef TSPLAT_CONV_LAUNCH
+    TSPLAT_PROF_END(tsplat::prof::kConv, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

@@ -22,7 +22,8 @@ enum KernelId : int {
     kUvCrossTable = 11,
     kLinear = 12,     // tsplat_linear_f32_fwd
     kMha = 13,        // tsplat_mha_f32_fwd
-    kNumKernels = 14,
+    kConv = 14,       // tsplat_conv2d_f32_fwd
+    kNumKernels = 15,
 };
 
 int active();                 // kernel id being timed (0 = off)

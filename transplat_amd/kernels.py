@@ -6,6 +6,7 @@ requires device tensors and the in-tree HIP library; there is no fallback path.
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -356,6 +357,93 @@ def mha(qkv, heads: int, scale: float):
     _lib.check(lib.tsplat_mha_f32_fwd(_lib.ptr(x), _lib.ptr(out), b, n, heads, d, float(scale),
                                       _lib.stream_ptr(qkv.device)), "tsplat_mha_f32_fwd")
     return out
+
+
+# packed weights per weight tensor: id -> (weakref, version, packed); a hit needs the same live
+# tensor (never a new tensor at a recycled address or id) at an unchanged version
+_CONV_PACKED: dict = {}
+# Which convolutions go to tsplat_conv2d_f32_fwd: "auto" (the latency-bound ones, see
+# conv2d_direct_ok), "off" (always MIOpen), "all" (every shape the kernel takes; tests / A/B)
+_CONV_MODE = os.environ.get("TSPLAT_CONV", "auto")
+_CONV_MAX_FLOP = 1.5e9  # above this MIOpen's kernels are as fast or faster (tools/bench_conv.py)
+
+
+def conv_pack_weight(weight):
+    """[cout, cin, k, k] -> [ceil(cout / 32), k * k, cin / 2, 2, 32] (zero-padded couts), cached per
+    weight tensor version: the A-operand order of tsplat_conv2d_f32_fwd."""
+    hit = _CONV_PACKED.get(id(weight))
+    if hit is not None and hit[0]() is weight and hit[1] == weight._version:
+        return hit[2]
+    co, ci, k, _ = weight.shape
+    cot = (co + 31) // 32
+    w = torch.zeros((cot * 32, ci, k * k), dtype=torch.float32, device=weight.device)
+    w[:co] = weight.detach().float().reshape(co, ci, k * k)
+    packed = w.reshape(cot, 32, ci // 2, 2, k * k).permute(0, 4, 2, 3, 1).contiguous()
+    if len(_CONV_PACKED) > 512:
+        for k in [k for k, v in _CONV_PACKED.items() if v[0]() is None]:
+            del _CONV_PACKED[k]
+    _CONV_PACKED[id(weight)] = (weakref.ref(weight), weight._version, packed)
+    return packed
+
+
+def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsample: bool = False) -> bool:
+    """True when tsplat_conv2d_f32_fwd takes this convolution and (mode "auto") it is a
+    latency-bound one where the direct kernel beats MIOpen."""
+    if _CONV_MODE == "off" or not x.is_cuda or torch.is_autocast_enabled("cuda"):
+        return False
+    if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4:
+        return False
+    co, ci, k, k2 = weight.shape
+    if k != k2 or k not in (1, 3) or stride not in (1, 2) or (upsample and stride != 1):
+        return False
+    pad = padding if padding is not None else k // 2
+    if isinstance(pad, (tuple, list)):
+        if len(set(pad)) != 1:
+            return False
+        pad = pad[0]
+    c1 = x.shape[1]
+    if pad != k // 2 or ci != c1 + c2 or c1 % 2 or c2 % 2:
+        return False
+    if _CONV_MODE == "all":
+        return True
+    h, w = x.shape[2] * (2 if upsample else 1), x.shape[3] * (2 if upsample else 1)
+    npx = x.shape[0] * (h // stride) * (w // stride)
+    flop = 2.0 * npx * co * ci * k * k
+    # a 3x3 with few output tiles and a long reduction runs on few CUs (one 16-wave workgroup
+    # per tile): MIOpen is as fast there (bench_conv.py: 2 x 256 -> 128 at 16^2)
+    tiles = ((npx + 31) // 32) * ((co + 31) // 32)
+    return flop <= _CONV_MAX_FLOP and (k == 1 or tiles >= 128 or ci <= 128)
+
+
+def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: bool = False):
+    """conv2d(cat([x1, x2], 1) (nearest-upsampled 2x if upsample), weight, bias, stride,
+    padding = k // 2) in one exact-fp32 MFMA launch (tsplat_conv2d_f32_fwd), NCHW fp32."""
+    lib = _lib.load()
+    n, c1, h, w = x1.shape
+    a = _f32(x1)
+    b = _f32(x2) if x2 is not None else None
+    c2 = b.shape[1] if b is not None else 0
+    if b is not None and (b.shape[0] != n or b.shape[2:] != x1.shape[2:]):
+        raise ValueError(f"x2 {tuple(b.shape)} does not match x1 {tuple(x1.shape)}")
+    co, ci, k, _ = weight.shape
+    if ci != c1 + c2:
+        raise ValueError(f"weight {tuple(weight.shape)} does not match {c1} + {c2} input channels")
+    hv, wv = (2 * h, 2 * w) if upsample else (h, w)
+    hout, wout = (hv + 2 * (k // 2) - k) // stride + 1, (wv + 2 * (k // 2) - k) // stride + 1
+    y = torch.empty((n, co, hout, wout), dtype=torch.float32, device=x1.device)
+    # waves per 32 x 32 tile: the ci pairs split over up to 16 waves (>= 2 pairs of a 3x3, >= 16 of a
+    # 1x1 each) while the grid stays <= 4096 waves
+    tiles = ((n * hout * wout + 31) // 32) * ((co + 31) // 32)
+    pairs = ci // 2
+    ksplit = 16
+    while ksplit > 1 and (tiles * ksplit > 4096 or pairs < (2 if k == 3 else 16) * ksplit):
+        ksplit //= 2
+    pb = _f32(bias) if bias is not None else None
+    rc = lib.tsplat_conv2d_f32_fwd(_lib.ptr(a), c1, _lib.ptr(b), c2, _lib.ptr(conv_pack_weight(weight)),
+                                   _lib.ptr(pb), _lib.ptr(y), n, h, w, co, k, stride, int(upsample), ksplit,
+                                   _lib.stream_ptr(x1.device))
+    _lib.check(rc, "tsplat_conv2d_f32_fwd")
+    return y
 
 
 def sh_rotation(rotations, d_sh: int):

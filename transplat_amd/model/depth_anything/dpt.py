@@ -4,12 +4,20 @@ as the reference forward does; parameter names match (`depth_head.{projects,resi
 scratch.{layer*_rn,refinenet*,output_conv*}}`)."""
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
 
 from .dinov2 import DINOv2
+
+# The token maps enter the DPT as channels-last views (permute of [B, N, C]); the whole conv chain
+# then runs MIOpen's NHWC kernels, measured ~4% faster end-to-end than an NCHW copy up front. The
+# conv weights are laid out channels-last once (first forward) so torch stops re-laying them out
+# on every call.
+_DPT_CL_WEIGHTS = os.environ.get("TSPLAT_DPT_CL_WEIGHTS", "1") != "0"
 
 
 class ResidualConvUnit(nn.Module):
@@ -92,7 +100,15 @@ class DPTHead(nn.Module):
             nn.Conv2d(32, 1, kernel_size=1, stride=1, padding=0), nn.ReLU(True), nn.Identity())
         self.scratch = s
 
+    def _channels_last_weights(self):
+        for m in self.modules():
+            if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)) and m.weight.dim() == 4:
+                m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
+        self._cl_done = True
+
     def forward(self, out_features, patch_h, patch_w):
+        if _DPT_CL_WEIGHTS and not getattr(self, "_cl_done", False) and out_features[0][0].is_cuda:
+            self._channels_last_weights()
         out = []
         for i, x in enumerate(out_features):
             x = x[0]

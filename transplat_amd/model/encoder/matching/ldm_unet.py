@@ -5,7 +5,9 @@ Only the configuration the depth predictor instantiates is built: postnorm ResBl
 down/up-sampling, legacy QKV attention at the requested resolutions with views folded into the
 token axis, middle block = ResBlock, Identity, ResBlock. Module indices and parameter names
 follow the reference (`input_blocks.{i}.{j}`, `middle_block.{0,2}`, `output_blocks.{i}.{j}`,
-`out.{0,1}`) so checkpoint keys load. Convolutions and GEMMs run on MIOpen / hipBLASLt; every
+`out.{0,1}`) so checkpoint keys load. The latency-bound low-resolution convolutions run as a direct
+fp32 MFMA kernel reading the skip concat / nearest upsample in place (kernels.conv2d_direct), the
+rest and the GEMMs on MIOpen / hipBLASLt; every
 GroupNorm runs as one fused gfx950 kernel pair together with the activation and residual add
 that follow it in the reference's module chain (kernels.group_norm).
 """
@@ -30,18 +32,34 @@ def gn_act(norm: nn.GroupNorm, x, act: str = "none", residual=None, pre_bias=Non
     return y.type(x.dtype)
 
 
-def conv_nobias(conv: nn.Module, x):
-    """The convolution without its bias (the following fused GroupNorm adds it)."""
+def conv(conv: nn.Module, x, x2=None, upsample: bool = False, bias: bool = True):
+    """conv(cat([x, x2], 1) (nearest-upsampled 2x if upsample)) [+ bias]. The latency-bound 2-D
+    convolutions of the low-resolution levels run as one direct fp32 MFMA kernel that reads the
+    concat / upsample in place (kernels.conv2d_direct); the rest materialise them and run MIOpen."""
+    b = conv.bias if bias else None
+    if isinstance(conv, nn.Conv2d) and conv.dilation == (1, 1) and conv.groups == 1 and conv.stride[0] == conv.stride[1]:
+        c2 = x2.shape[1] if x2 is not None else 0
+        if kernels.conv2d_direct_ok(x, conv.weight, conv.stride[0], conv.padding, c2=c2, upsample=upsample):
+            return kernels.conv2d_direct(x, conv.weight, b, conv.stride[0], x2=x2, upsample=upsample)
+    if x2 is not None:
+        x = torch.cat([x, x2], dim=1)
+    if upsample:
+        x = F.interpolate(x, scale_factor=2, mode="nearest")
     if isinstance(conv, nn.Conv2d):
-        return F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
-    return F.conv1d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+        return F.conv2d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
+    return F.conv1d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
-def conv_gn_act(conv: nn.Module, norm: nn.GroupNorm, x, act: str = "none", residual=None):
+def conv_nobias(conv_mod: nn.Module, x, x2=None):
+    """The convolution without its bias (the following fused GroupNorm adds it)."""
+    return conv(conv_mod, x, x2, bias=False)
+
+
+def conv_gn_act(conv_mod: nn.Module, norm: nn.GroupNorm, x, act: str = "none", residual=None, x2=None):
     """conv -> GroupNorm -> act (-> + residual) with the conv bias folded into the norm kernel."""
-    if conv.bias is None:
-        return gn_act(norm, conv(x), act, residual)
-    return gn_act(norm, conv_nobias(conv, x), act, residual, pre_bias=conv.bias)
+    if conv_mod.bias is None:
+        return gn_act(norm, conv(conv_mod, x, x2), act, residual)
+    return gn_act(norm, conv_nobias(conv_mod, x, x2), act, residual, pre_bias=conv_mod.bias)
 
 
 def run_sequential(seq: nn.Sequential, x):
@@ -98,10 +116,16 @@ class ResBlock(nn.Module):
         self.skip_connection = (nn.Identity() if self.out_channels == channels
                                 else nn.Conv2d(channels, self.out_channels, 1))
 
-    def forward(self, x):
-        # skip + SiLU(GN(conv(SiLU(GN(conv(x)))))): both GN + SiLU pairs and the residual fused
-        h = conv_gn_act(self.in_layers[0], self.in_layers[1], x, "silu")
-        return conv_gn_act(self.out_layers[0], self.out_layers[1], h, "silu", residual=self.skip_connection(x))
+    def forward(self, x, x2=None):
+        # skip + SiLU(GN(conv(SiLU(GN(conv(x)))))): both GN + SiLU pairs and the residual fused;
+        # x2: the output blocks' skip input, x = cat([x, x2], 1) without materialising the concat
+        # where the convolutions read it in place
+        h = conv_gn_act(self.in_layers[0], self.in_layers[1], x, "silu", x2=x2)
+        if isinstance(self.skip_connection, nn.Identity):
+            skip = x if x2 is None else torch.cat([x, x2], dim=1)
+        else:
+            skip = conv(self.skip_connection, x, x2)
+        return conv_gn_act(self.out_layers[0], self.out_layers[1], h, "silu", residual=skip)
 
 
 class QKVAttentionLegacy(nn.Module):
@@ -156,7 +180,7 @@ class Downsample(nn.Module):
         self.op = nn.Conv2d(channels, out_channels or channels, 3, stride=2, padding=1)
 
     def forward(self, x):
-        return self.op(x)
+        return conv(self.op, x)
 
 
 class Upsample(nn.Module):
@@ -166,7 +190,7 @@ class Upsample(nn.Module):
         self.conv = nn.Conv2d(channels, out_channels or channels, 3, padding=1)
 
     def forward(self, x):
-        return self.conv(F.interpolate(x, scale_factor=2, mode="nearest"))
+        return conv(self.conv, x, upsample=True)
 
 
 class UNetModel(nn.Module):
@@ -221,5 +245,9 @@ class UNetModel(nn.Module):
             hs.append(h)
         h = self.middle_block(h)
         for module in self.output_blocks:
-            h = module(torch.cat([h, hs.pop()], dim=1))
+            # ResBlock(cat([h, skip])): the concat is read in place by its convolutions
+            mods = list(module)
+            h = mods[0](h, hs.pop())
+            for m in mods[1:]:
+                h = m(h)
         return run_sequential(self.out, h)
