@@ -317,6 +317,15 @@ int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x2, int32_t 
                           const float* bias, float* y, int32_t batch, int32_t height, int32_t width, int32_t c_out,
                           int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit, void* stream);
 
+/* Channels-last form of tsplat_conv2d_f32_fwd for the Depth-Anything DPT head (reference
+ * src/depth_anything_v2/util/blocks.py ResidualConvUnit / FeatureFusionBlock.out_conv), whose conv
+ * chain runs on channels-last maps: x [batch, height, width, c_in], y and residual
+ * [batch, height, width, c_out]; stride 1, padding ksize / 2; y = conv(relu_in ? relu(x) : x) (+ bias)
+ * (+ residual). Same packed weights and ksplit as tsplat_conv2d_f32_fwd. */
+int tsplat_conv2d_f32_nhwc_fwd(const float* x, int32_t c_in, const float* w_packed, const float* bias,
+                               const float* residual, float* y, int32_t batch, int32_t height, int32_t width,
+                               int32_t c_out, int32_t ksize, int32_t relu_in, int32_t ksplit, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -289,6 +289,17 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
     return torch.nn.functional.conv2d(x, weight, bias, stride, weight.shape[-1] // 2)
 
 
+def conv2d_nhwc_ok(x, weight) -> bool:
+    """Every stride-1 conv the channels-last kernel takes (CPU model runs exercise its sites)."""
+    return x.dim() == 4 and weight.shape[-1] in (1, 3) and x.shape[1] % 2 == 0 and x.shape[1] > 1
+
+
+def conv2d_nhwc(x, weight, bias=None, residual=None, relu_in: bool = False):
+    """DPT ResidualConvUnit step (reference util/blocks.py:73-99): conv(relu(x)) + bias (+ residual)."""
+    y = torch.nn.functional.conv2d(torch.relu(x) if relu_in else x, weight, bias, 1, weight.shape[-1] // 2)
+    return y if residual is None else y + residual
+
+
 def mha(qkv, heads: int, scale: float):
     """DINOv2 Attention core (reference dinov2_layers/attention.py): reshape to heads, softmax
     attention (torch SDPA math), back to [B, N, heads * head_dim]."""
@@ -368,4 +379,4 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
                        "conv_bias_act", "mha", "residual_ln", "depth_softmax", "conv2d_direct_ok",
-                       "conv2d_direct")
+                       "conv2d_direct", "conv2d_nhwc_ok", "conv2d_nhwc")

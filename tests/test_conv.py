@@ -66,3 +66,26 @@ def test_conv2d_direct_weight_cache_tracks_updates(device):
     wt.mul_(2.0)
     y1 = K.conv2d_direct(x, wt)
     torch.testing.assert_close(y1, 2 * y0, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,c,h,w,cout,k,relu,res,bias", [
+    (2, 128, 9, 9, 128, 3, True, False, True), (2, 128, 18, 18, 128, 3, True, True, True),
+    (2, 128, 36, 36, 128, 3, False, True, False), (2, 128, 18, 18, 128, 1, False, False, True),
+    (1, 6, 5, 7, 40, 3, True, True, True)])
+def test_conv2d_nhwc_kernel(device, n, c, h, w, cout, k, relu, res, bias):
+    """Channels-last variant (DPT ResidualConvUnit: ReLU on load, bias, residual) vs the oracle."""
+    from transplat_amd import kernels as K
+
+    x = seeded((n, c, h, w), 31)
+    wt = seeded((cout, c, k, k), 32) * (1.0 / c ** 0.5)
+    b = seeded((cout,), 33) if bias else None
+    r = seeded((n, cout, h, w), 34) if res else None
+    ref = E.conv2d_nhwc(x, wt, b, residual=r, relu_in=relu)
+    cl = lambda t: t.to(device).contiguous(memory_format=torch.channels_last)  # noqa: E731
+    assert K.conv2d_nhwc_ok(cl(x), wt.to(device)) or c < 8
+    out = K.conv2d_nhwc(cl(x), wt.to(device), b.to(device) if b is not None else None,
+                        residual=cl(r) if r is not None else None, relu_in=relu)
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    err = (out.cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-5, err

@@ -163,18 +163,18 @@ def test_oracle_adapter_shapes_and_identity_rotation():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", ["bvhwc", "head_nchw"])
-def test_gaussian_adapter_kernel(device, layout):
+@pytest.mark.parametrize("layout,b", [("bvhwc", 2), ("head_nchw", 2), ("head_nchw", 1)])
+def test_gaussian_adapter_kernel(device, layout, b):
     from einops import rearrange
     from transplat_amd import kernels as K
 
-    raw, depths, dens, ext, intr = _adapter_inputs()
+    raw, depths, dens, ext, intr = _adapter_inputs(b=b)
     ref = E.gaussian_adapter(raw, depths, dens, ext, intr, (24, 32), 0.5, 15.0, 2.0)
     raw_d = raw.to(device)
     if layout == "head_nchw":
         # the depth head's output map [(v b), c, h, w] and the view the encoder hands the adapter
         head = rearrange(raw_d, "b v (h w) c -> (v b) c h w", h=24).contiguous()
-        raw_d = rearrange(head, "(v b) c h w -> b v (h w) c", b=2)
+        raw_d = rearrange(head, "(v b) c h w -> b v (h w) c", b=b)
         assert not raw_d.is_contiguous()
     out = K.gaussian_adapter(raw_d, *(t.to(device) for t in (depths, dens, ext, intr)), (24, 32), 0.5, 15.0, 2.0)
     for name, r, o in zip(("means", "cov", "harmonics", "opacity"), ref, out):

@@ -36,7 +36,8 @@ struct Args {
     const float* x2;
     const float* wp;    // packed weights [cot][taps][cin/2][2][32]
     const float* bias;  // [cout] or null
-    float* y;           // [n, cout, hout, wout]
+    const float* res;   // residual added to the output (y's layout) or null
+    float* y;           // [n, cout, hout, wout] (NHWC: [n, hout, wout, cout])
     int c1, c2, cout, n;
     int hin, win;       // stored input size
     int hv, wv;         // virtual input size (2x when upsampling)
@@ -47,7 +48,10 @@ struct Args {
 // G = ci pairs per batch (all their taps): the loads of one batch are in flight while the previous
 // batch's G * T MFMAs run, so a wave's time is ~ (its batches) x (memory latency) for these small
 // layers -- larger G, fewer round trips.
-template <int KS, int S, int UP, int G>
+// NHWC: input / output / residual channels-last ([n, h, w, c]; one source, no upsample) -- the DPT
+// head's conv chain runs channels-last. RELU: ReLU applied to the input on load (the DPT
+// ResidualConvUnit's activation before each convolution).
+template <int KS, int S, int UP, int G, bool NHWC, bool RELU>
 __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
     extern __shared__ float sred[];  // [ksplit][16][64]
     constexpr int T = KS * KS, PAD = KS / 2;
@@ -70,13 +74,17 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
         const int ky = t / KS, kx = t - ky * KS;
         const int iy = oy * S + ky - PAD, ix = ox * S + kx - PAD;
         const bool v = px < p.npx && iy >= 0 && iy < p.hv && ix >= 0 && ix < p.wv;
-        off[t] = v ? (UP ? (iy >> 1) * p.win + (ix >> 1) : iy * p.win + ix) : 0;
+        if (NHWC)
+            off[t] = v ? (nb * hwi + iy * p.win + ix) * p.c1 : 0;
+        else
+            off[t] = v ? (UP ? (iy >> 1) * p.win + (ix >> 1) : iy * p.win + ix) : 0;
         vmask |= (unsigned)v << t;
     }
     const size_t wtap = (size_t)cp_all * 64;  // packed-weight stride between taps
     const float* wbase = p.wp + (size_t)cot * T * wtap + lane;
     // channel 2 cp + h of the concatenated input for this lane's image
     auto chan = [&](int cp) -> const float* {
+        if (NHWC) return p.x1 + 2 * cp + h;
         return cp < cp1 ? p.x1 + ((size_t)nb * p.c1 + 2 * cp + h) * hwi
                         : p.x2 + ((size_t)nb * p.c2 + 2 * (cp - cp1) + h) * hwi;
     };
@@ -94,7 +102,7 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
 #pragma unroll
             for (int t = 0; t < T; ++t) {
                 const float av = wq[t * wtap];
-                const float bv = src[off[t]];
+                const float bv = RELU ? fmaxf(src[off[t]], 0.f) : src[off[t]];
                 a[g * T + t] = ok ? av : 0.f;
                 b[g * T + t] = ok && ((vmask >> t) & 1) ? bv : 0.f;
             }
@@ -126,15 +134,31 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
     for (int r = 0; r < 16; ++r) sred[(w * 16 + r) * 64 + lane] = acc[r];
     __syncthreads();
     for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
-        const int r = idx >> 6, l = idx & 63;
+        // NCHW: consecutive threads -> consecutive pixels; NHWC: -> consecutive output channels
+        int r, l;
+        if (NHWC) {
+            const int col = idx & 31, pl = idx >> 5;
+            r = ((col >> 3) << 2) | (col & 3);
+            l = ((col >> 2) & 1) * 32 + pl;
+        } else {
+            r = idx >> 6;
+            l = idx & 63;
+        }
         float s = 0.f;
         for (int k = 0; k < ksplit; ++k) s += sred[(k * 16 + r) * 64 + l];
         const int co = cot * 32 + 8 * (r >> 2) + 4 * (l >> 5) + (r & 3);
         const int q = blockIdx.x * 32 + (l & 31);
         if (co >= p.cout || q >= p.npx) continue;
         if (p.bias) s += p.bias[co];
-        const int qn = q / hwo, qp = q - qn * hwo;
-        p.y[((size_t)qn * p.cout + co) * hwo + qp] = s;
+        size_t o;
+        if (NHWC) {
+            o = (size_t)q * p.cout + co;
+        } else {
+            const int qn = q / hwo, qp = q - qn * hwo;
+            o = ((size_t)qn * p.cout + co) * hwo + qp;
+        }
+        if (p.res) s += p.res[o];
+        p.y[o] = s;
     }
 }
 
@@ -179,7 +203,7 @@ extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x
     const size_t lds = (size_t)ksplit * 16 * 64 * sizeof(float);
     TSPLAT_PROF_BEGIN(tsplat::prof::kConv, stream);
 #define TSPLAT_CONV_LAUNCH(KS, S, UP, G) \
-    hipLaunchKernelGGL((conv_f32_kernel<KS, S, UP, G>), grid, block, lds, stream, p)
+    hipLaunchKernelGGL((conv_f32_kernel<KS, S, UP, G, false, false>), grid, block, lds, stream, p)
     // ci pairs per batch: 2 (3x3) / 16 (1x1) once a wave has that many, else 1 / 8
     const int per_wave = ((c1 + c2) / 2 + ksplit - 1) / ksplit;
     const bool wide = per_wave >= (ksize == 3 ? 2 : 16);
@@ -193,6 +217,56 @@ extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x
         if (wide) TSPLAT_CONV_LAUNCH(1, 1, 0, 16); else TSPLAT_CONV_LAUNCH(1, 1, 0, 8);
     } else {
         return TSPLAT_EINVAL;
+    }
+#undef TSPLAT_CONV_LAUNCH
+    TSPLAT_PROF_END(tsplat::prof::kConv, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_conv2d_f32_nhwc_fwd(const float* x, int32_t c_in, const float* w_packed, const float* bias,
+                                          const float* residual, float* y, int32_t batch, int32_t height,
+                                          int32_t width, int32_t c_out, int32_t ksize, int32_t relu_in,
+                                          int32_t ksplit, void* stream_) {
+    using namespace tsplat::conv;
+    if (!x || !w_packed || !y || batch <= 0 || height <= 0 || width <= 0 || c_out <= 0) return TSPLAT_EINVAL;
+    if (c_in <= 0 || (c_in & 1) || !(ksize == 1 || ksize == 3) || ksplit < 1 || ksplit > kMaxWaves)
+        return TSPLAT_EINVAL;
+    const int64_t elems = (int64_t)batch * height * width * (c_in > c_out ? c_in : c_out);
+    if (elems >= (1ll << 31)) return TSPLAT_EINVAL;
+    Args p{};
+    p.x1 = x;
+    p.wp = w_packed;
+    p.bias = bias;
+    p.res = residual;
+    p.y = y;
+    p.c1 = c_in;
+    p.cout = c_out;
+    p.n = batch;
+    p.hin = p.hv = p.hout = height;
+    p.win = p.wv = p.wout = width;
+    p.npx = batch * height * width;
+    hipStream_t stream = (hipStream_t)stream_;
+    const dim3 grid((unsigned)((p.npx + 31) / 32), (unsigned)((c_out + 31) / 32));
+    const dim3 block(64 * ksplit);
+    const size_t lds = (size_t)ksplit * 16 * 64 * sizeof(float);
+    const int per_wave = (c_in / 2 + ksplit - 1) / ksplit;
+    const bool wide = per_wave >= (ksize == 3 ? 2 : 16);
+    TSPLAT_PROF_BEGIN(tsplat::prof::kConv, stream);
+#define TSPLAT_CONV_LAUNCH(KS, G, RELU) \
+    hipLaunchKernelGGL((conv_f32_kernel<KS, 1, 0, G, true, RELU>), grid, block, lds, stream, p)
+    if (ksize == 3) {
+        if (relu_in) {
+            if (wide) TSPLAT_CONV_LAUNCH(3, 2, true); else TSPLAT_CONV_LAUNCH(3, 1, true);
+        } else {
+            if (wide) TSPLAT_CONV_LAUNCH(3, 2, false); else TSPLAT_CONV_LAUNCH(3, 1, false);
+        }
+    } else {
+        if (relu_in) {
+            if (wide) TSPLAT_CONV_LAUNCH(1, 16, true); else TSPLAT_CONV_LAUNCH(1, 8, true);
+        } else {
+            if (wide) TSPLAT_CONV_LAUNCH(1, 16, false); else TSPLAT_CONV_LAUNCH(1, 8, false);
+        }
     }
 #undef TSPLAT_CONV_LAUNCH
     TSPLAT_PROF_END(tsplat::prof::kConv, stream);

@@ -446,6 +446,40 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
     return y
 
 
+def conv2d_nhwc_ok(x, weight) -> bool:
+    """True when tsplat_conv2d_f32_nhwc_fwd takes conv(x, weight) (stride 1, padding k // 2) on the
+    channels-last map x and (mode "auto") it is latency-bound (same rule as conv2d_direct_ok)."""
+    if x.dim() != 4 or not x.is_contiguous(memory_format=torch.channels_last) or x.shape[1] == 1:
+        return False
+    return conv2d_direct_ok(x, weight, 1, weight.shape[-1] // 2)
+
+
+def conv2d_nhwc(x, weight, bias=None, residual=None, relu_in: bool = False):
+    """conv2d(relu(x) if relu_in else x, weight, bias, 1, k // 2) (+ residual) on channels-last
+    fp32 maps, one exact-fp32 MFMA launch (tsplat_conv2d_f32_nhwc_fwd); returns channels-last."""
+    lib = _lib.load()
+    n, c, h, w = x.shape
+    co, ci, k, _ = weight.shape
+    if ci != c or not x.is_contiguous(memory_format=torch.channels_last) or x.dtype != torch.float32:
+        raise ValueError("conv2d_nhwc needs a channels-last fp32 input matching the weight")
+    y = torch.empty((n, co, h, w), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    res = None
+    if residual is not None:
+        res = residual.float().contiguous(memory_format=torch.channels_last)
+        if res.shape != y.shape:
+            raise ValueError(f"residual {tuple(res.shape)} != output {tuple(y.shape)}")
+    tiles = ((n * h * w + 31) // 32) * ((co + 31) // 32)
+    ksplit = 16
+    while ksplit > 1 and (tiles * ksplit > 4096 or c // 2 < (2 if k == 3 else 16) * ksplit):
+        ksplit //= 2
+    pb = _f32(bias) if bias is not None else None
+    rc = lib.tsplat_conv2d_f32_nhwc_fwd(_lib.ptr(x), c, _lib.ptr(conv_pack_weight(weight)), _lib.ptr(pb),
+                                        _lib.ptr(res), _lib.ptr(y), n, h, w, co, k, int(relu_in), ksplit,
+                                        _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_conv2d_f32_nhwc_fwd")
+    return y
+
+
 def sh_rotation(rotations, d_sh: int):
     """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
     wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""
@@ -471,7 +505,9 @@ def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape
     d_sh = (r - 9) // 3
     h, w = image_shape
     # the head's "(v b) c h w -> b v (h w) c" view of its NCHW output map is read in place
-    nchw = raw.dtype == torch.float32 and raw.stride() == (r * hw, b * r * hw, 1, hw)
+    # (strides of size-1 dimensions are arbitrary: compared only where the size is > 1)
+    nchw = raw.dtype == torch.float32 and all(
+        n == 1 or st == want for n, st, want in zip(raw.shape, raw.stride(), (r * hw, b * r * hw, 1, hw)))
     if not nchw:
         raw = _f32(raw)
     depths, densities = _f32(depths), _f32(densities)

@@ -11,6 +11,7 @@ import torch.nn.functional as F
 from torch import nn
 
 
+from ... import kernels
 from .dinov2 import DINOv2
 
 # The token maps enter the DPT as channels-last views (permute of [B, N, C]); the whole conv chain
@@ -18,6 +19,12 @@ from .dinov2 import DINOv2
 # conv weights are laid out channels-last once (first forward) so torch stops re-laying them out
 # on every call.
 _DPT_CL_WEIGHTS = os.environ.get("TSPLAT_DPT_CL_WEIGHTS", "1") != "0"
+# Opt-in: "1" runs the latency-bound DPT convolutions (ResidualConvUnits <= 36^2, out_convs) as the
+# channels-last direct kernel (kernels.conv2d_nhwc, ReLU / bias / residual fused), "rcu" only the
+# units. Measured 2.0 % ("1") and 1.3 % ("rcu") SLOWER end to end than MIOpen's NHWC kernels: the
+# kernel's pixel-per-lane B gathers touch 32 cache lines per load on a channels-last map. Default
+# "0" (MIOpen) until the operand is staged through LDS.
+_DPT_DIRECT = os.environ.get("TSPLAT_DPT_DIRECT", "0")
 
 
 class ResidualConvUnit(nn.Module):
@@ -32,6 +39,12 @@ class ResidualConvUnit(nn.Module):
         self.activation = activation
 
     def forward(self, x):
+        if (_DPT_DIRECT != "0" and not self.bn and isinstance(self.activation, nn.ReLU)
+                and kernels.conv2d_nhwc_ok(x, self.conv1.weight)):
+            # latency-bound levels (<= 36^2): ReLU-on-load, bias and the residual fused into the
+            # channels-last direct convolution, two launches for the unit
+            out = kernels.conv2d_nhwc(x, self.conv1.weight, self.conv1.bias, relu_in=True)
+            return kernels.conv2d_nhwc(out, self.conv2.weight, self.conv2.bias, residual=x, relu_in=True)
         out = self.conv1(self.activation(x))
         if self.bn:
             out = self.bn1(out)
@@ -62,6 +75,8 @@ class FeatureFusionBlock(nn.Module):
         else:
             modifier = {"size": size}
         output = F.interpolate(output, **modifier, mode="bilinear", align_corners=self.align_corners)
+        if _DPT_DIRECT == "1" and kernels.conv2d_nhwc_ok(output, self.out_conv.weight):
+            return kernels.conv2d_nhwc(output, self.out_conv.weight, self.out_conv.bias)
         return self.out_conv(output)
 
 

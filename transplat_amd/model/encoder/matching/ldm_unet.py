@@ -32,15 +32,22 @@ def gn_act(norm: nn.GroupNorm, x, act: str = "none", residual=None, pre_bias=Non
     return y.type(x.dtype)
 
 
+def _direct(conv: nn.Module, x, x2=None, upsample: bool = False) -> bool:
+    """Whether conv(cat([x, x2])) runs as the direct kernel (kernels.conv2d_direct_ok)."""
+    if not (isinstance(conv, nn.Conv2d) and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.stride[0] == conv.stride[1]):
+        return False
+    c2 = x2.shape[1] if x2 is not None else 0
+    return kernels.conv2d_direct_ok(x, conv.weight, conv.stride[0], conv.padding, c2=c2, upsample=upsample)
+
+
 def conv(conv: nn.Module, x, x2=None, upsample: bool = False, bias: bool = True):
     """conv(cat([x, x2], 1) (nearest-upsampled 2x if upsample)) [+ bias]. The latency-bound 2-D
     convolutions of the low-resolution levels run as one direct fp32 MFMA kernel that reads the
     concat / upsample in place (kernels.conv2d_direct); the rest materialise them and run MIOpen."""
     b = conv.bias if bias else None
-    if isinstance(conv, nn.Conv2d) and conv.dilation == (1, 1) and conv.groups == 1 and conv.stride[0] == conv.stride[1]:
-        c2 = x2.shape[1] if x2 is not None else 0
-        if kernels.conv2d_direct_ok(x, conv.weight, conv.stride[0], conv.padding, c2=c2, upsample=upsample):
-            return kernels.conv2d_direct(x, conv.weight, b, conv.stride[0], x2=x2, upsample=upsample)
+    if _direct(conv, x, x2, upsample):
+        return kernels.conv2d_direct(x, conv.weight, b, conv.stride[0], x2=x2, upsample=upsample)
     if x2 is not None:
         x = torch.cat([x, x2], dim=1)
     if upsample:
@@ -120,6 +127,8 @@ class ResBlock(nn.Module):
         # skip + SiLU(GN(conv(SiLU(GN(conv(x)))))): both GN + SiLU pairs and the residual fused;
         # x2: the output blocks' skip input, x = cat([x, x2], 1) without materialising the concat
         # where the convolutions read it in place
+        if x2 is not None and not _direct(self.in_layers[0], x, x2):
+            x, x2 = torch.cat([x, x2], dim=1), None  # materialised once for both convolutions
         h = conv_gn_act(self.in_layers[0], self.in_layers[1], x, "silu", x2=x2)
         if isinstance(self.skip_connection, nn.Identity):
             skip = x if x2 is None else torch.cat([x, x2], dim=1)
