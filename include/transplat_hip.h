@@ -326,6 +326,13 @@ int tsplat_conv2d_f32_nhwc_fwd(const float* x, int32_t c_in, const float* w_pack
                                const float* residual, float* y, int32_t batch, int32_t height, int32_t width,
                                int32_t c_out, int32_t ksize, int32_t relu_in, int32_t ksplit, void* stream);
 
+/* y [n, c, height * scale, width * scale] = act(bilinear_upsample(x) + bias[c]) with
+ * align_corners = True (reference depth_predictor_trans.py upsampler: Conv2d -> Upsample(bilinear,
+ * align_corners=True) -> GELU, with the conv's bias moved past the interpolation); x [n, c, height,
+ * width] NCHW fp32, bias may be null; act 0 none, 2 GELU (erf), 3 ReLU; width * scale % 4 == 0. */
+int tsplat_upsample_bilinear_act_fwd(const float* x, const float* bias, float* y, int32_t n, int32_t c,
+                                     int32_t height, int32_t width, int32_t scale, int32_t act, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

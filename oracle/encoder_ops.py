@@ -300,6 +300,15 @@ def conv2d_nhwc(x, weight, bias=None, residual=None, relu_in: bool = False):
     return y if residual is None else y + residual
 
 
+def upsample_bilinear_act(x, scale: int, bias=None, act: str = "none"):
+    """depth predictor upsampler tail (reference depth_predictor_trans.py): conv bias -> bilinear
+    upsample (align_corners=True) -> activation, in the reference's order."""
+    if bias is not None:
+        x = x + bias.reshape(1, -1, 1, 1)
+    y = torch.nn.functional.interpolate(x, scale_factor=scale, mode="bilinear", align_corners=True)
+    return {"none": y, "gelu": torch.nn.functional.gelu(y), "relu": torch.relu(y)}[act]
+
+
 def mha(qkv, heads: int, scale: float):
     """DINOv2 Attention core (reference dinov2_layers/attention.py): reshape to heads, softmax
     attention (torch SDPA math), back to [B, N, heads * head_dim]."""
@@ -379,4 +388,5 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
                        "conv_bias_act", "mha", "residual_ln", "depth_softmax", "conv2d_direct_ok",
-                       "conv2d_direct", "conv2d_nhwc_ok", "conv2d_nhwc")
+                       "conv2d_direct", "conv2d_nhwc_ok", "conv2d_nhwc",
+                       "upsample_bilinear_act")

@@ -432,3 +432,20 @@ def test_depth_softmax_kernel(device):
     rc, rm = E.depth_softmax(logits, disp)
     oc, om = K.depth_softmax(logits.to(device), disp.to(device))
     assert (oc.cpu() - rc).abs().max().item() < 1e-6 and (om.cpu() - rm).abs().max().item() < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,scale,act,bias", [((2, 128, 64, 64), 4, "gelu", True), ((1, 3, 5, 7), 4, "none", False),
+                                                   ((2, 8, 16, 16), 2, "relu", True)])
+def test_upsample_bilinear_act_kernel(device, shape, scale, act, bias):
+    """Depth predictor upsampler tail (bias -> bilinear align_corners -> GELU) vs the oracle."""
+    from transplat_amd import kernels as K
+
+    x = seeded(shape, 71)
+    b = seeded((shape[1],), 72) if bias else None
+    ref = E.upsample_bilinear_act(x, scale, b, act)
+    out = K.upsample_bilinear_act(x.to(device), scale, b.to(device) if b is not None else None, act).cpu()
+    # rounding-level: the source coordinate o (in - 1) / (out - 1) is an fp32 value up to 63 (ulp
+    # 3.8e-6), so a one-ulp different rounding moves an interpolation weight by ~4e-6; the bias is
+    # added after the interpolation (exact in real arithmetic)
+    assert (out - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())

@@ -480,6 +480,20 @@ def conv2d_nhwc(x, weight, bias=None, residual=None, relu_in: bool = False):
     return y
 
 
+def upsample_bilinear_act(x, scale: int, bias=None, act: str = "none"):
+    """act(interpolate(x, scale_factor=scale, mode="bilinear", align_corners=True) + bias[c]) in one
+    pass (tsplat_upsample_bilinear_act_fwd), NCHW fp32."""
+    lib = _lib.load()
+    n, c, h, w = x.shape
+    xf = _f32(x)
+    y = torch.empty((n, c, h * scale, w * scale), dtype=torch.float32, device=x.device)
+    rc = lib.tsplat_upsample_bilinear_act_fwd(_lib.ptr(xf), _lib.ptr(_f32(bias) if bias is not None else None),
+                                              _lib.ptr(y), n, c, h, w, int(scale), _ACTS[act],
+                                              _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_upsample_bilinear_act_fwd")
+    return y
+
+
 def sh_rotation(rotations, d_sh: int):
     """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
     wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""

@@ -18,6 +18,19 @@ from ...utils.uv_transformer import UVTransformer
 from .ldm_unet import UNetModel, run_sequential
 
 
+def _conv_upsample_gelu(seq: nn.Sequential, x):
+    """Sequential(Conv2d, Upsample(bilinear, align_corners=True), GELU): the bias-free convolution,
+    then interpolation + bias + GELU in one pass over the full-resolution map
+    (kernels.upsample_bilinear_act) instead of bias add, interpolation and GELU kernels."""
+    conv, up, act = seq
+    if (x.dtype != torch.float32 or torch.is_autocast_enabled("cuda") or not isinstance(act, nn.GELU)
+            or act.approximate != "none" or up.mode != "bilinear" or not up.align_corners
+            or float(up.scale_factor) != int(up.scale_factor)):
+        return seq(x)
+    y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+    return kernels.upsample_bilinear_act(y, int(up.scale_factor), conv.bias, "gelu")
+
+
 def _conv_gelu_conv(seq: nn.Sequential, x):
     """Sequential(Conv2d, GELU, Conv2d) head with each conv's bias (and the GELU) applied in one
     pass after the bias-free convolution (kernels.conv_bias_act)."""
@@ -192,7 +205,7 @@ class DepthPredictorTrans(nn.Module):
         fullres_disps = F.interpolate(coarse_disps, scale_factor=self.upscale_factor, mode="bilinear",
                                       align_corners=True)
 
-        proj_feat_in_fullres = self.upsampler(torch.cat((feat01, cnn_features), dim=1))
+        proj_feat_in_fullres = _conv_upsample_gelu(self.upsampler, torch.cat((feat01, cnn_features), dim=1))
         proj_feature = self.proj_feature(proj_feat_in_fullres)
         refine_out = run_sequential(self.refine_unet, torch.cat((extra_info["images"], da_depth, proj_feature, fullres_disps,
                                                  pdf_max), dim=1))
