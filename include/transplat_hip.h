@@ -304,6 +304,16 @@ int tsplat_small_inverse(const float* in, float* out, int32_t n, int32_t dim, vo
 int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, int32_t tokens, int32_t heads,
                        int32_t head_dim, float scale, void* stream);
 
+/* Legacy channels-first QKV attention of the depth predictor U-Nets (exact fp32 MFMA), replacing
+ * QKVAttentionLegacy.forward (reference src/model/encoder/matching/ldm_unet/unet.py:510-552) with
+ * use_cross_view_self_attn folding the views into the tokens: qkv [views * batch, 3 * heads * 32,
+ * tokens_per_view] ((v b) order, per head rows q | k | v), out [views * batch, heads * 32,
+ * tokens_per_view] = softmax over all views' tokens of q.k * scale, times v. views = 1 for plain
+ * self-attention. head_dim must be 32; scale multiplies the dot product (the reference's
+ * (q / ch^(1/4)).(k / ch^(1/4)) is scale = ch^(-1/2)). */
+int tsplat_qkv_attention_cf_fwd(const float* qkv, float* out, int32_t batch, int32_t heads, int32_t views,
+                                int32_t tokens_per_view, int32_t head_dim, float scale, void* stream);
+
 /* Direct convolution of the depth predictor U-Nets' low-resolution levels (exact fp32 MFMA),
  * replacing MIOpen for nn.Conv2d in reference src/model/encoder/matching/ldm_unet/unet.py (ResBlock
  * in/out convs unet.py:212-250 and 1x1 skip unet.py:258-266, Downsample unet.py:140-170, Upsample

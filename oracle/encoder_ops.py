@@ -309,6 +309,23 @@ def upsample_bilinear_act(x, scale: int, bias=None, act: str = "none"):
     return {"none": y, "gelu": torch.nn.functional.gelu(y), "relu": torch.relu(y)}[act]
 
 
+def qkv_attention_cf(qkv, heads: int, views: int = 1):
+    """reference ldm_unet/unet.py QKVAttentionLegacy.forward (:510-552), with
+    use_cross_view_self_attn when views > 1: "(v b) n t -> b n (v t)", heads split before q/k/v,
+    softmax((q s)^T (k s)) v with s = ch^(-1/4), back to "(v b) n t"."""
+    from einops import rearrange
+
+    if views > 1:
+        qkv = rearrange(qkv, "(v b) n t -> b n (v t)", v=views)
+    bs, width, length = qkv.shape
+    ch = width // (3 * heads)
+    q, k, v = qkv.reshape(bs * heads, ch * 3, length).split(ch, dim=1)
+    scale = 1 / math.sqrt(math.sqrt(ch))
+    weight = torch.softmax(torch.einsum("bct,bcs->bts", q * scale, k * scale).float(), dim=-1)
+    a = torch.einsum("bts,bcs->bct", weight, v).reshape(bs, -1, length)
+    return rearrange(a, "b n (v t) -> (v b) n t", v=views) if views > 1 else a
+
+
 def mha(qkv, heads: int, scale: float):
     """DINOv2 Attention core (reference dinov2_layers/attention.py): reshape to heads, softmax
     attention (torch SDPA math), back to [B, N, heads * head_dim]."""
@@ -389,4 +406,4 @@ KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gau
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
                        "conv_bias_act", "mha", "residual_ln", "depth_softmax", "conv2d_direct_ok",
                        "conv2d_direct", "conv2d_nhwc_ok", "conv2d_nhwc",
-                       "upsample_bilinear_act")
+                       "upsample_bilinear_act", "qkv_attention_cf")

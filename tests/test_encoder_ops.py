@@ -449,3 +449,15 @@ def test_upsample_bilinear_act_kernel(device, shape, scale, act, bias):
     # 3.8e-6), so a one-ulp different rounding moves an interpolation weight by ~4e-6; the bias is
     # added after the interpolation (exact in real arithmetic)
     assert (out - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("vb,heads,views,t", [(2, 4, 2, 256), (2, 1, 2, 256), (3, 2, 1, 100), (4, 1, 2, 37)])
+def test_qkv_attention_cf_kernel(device, vb, heads, views, t):
+    """U-Net legacy QKV attention (head dim 32, views folded into the tokens) vs the oracle."""
+    from transplat_amd import kernels as K
+
+    qkv = seeded((vb, 3 * heads * 32, t), 81) * 2.0
+    ref = E.qkv_attention_cf(qkv, heads, views)
+    out = K.qkv_attention_cf(qkv.to(device), heads, views).cpu()
+    assert (out - ref).abs().max().item() < 5e-5

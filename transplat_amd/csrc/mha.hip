@@ -189,6 +189,138 @@ mha_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, in
         *reinterpret_cast<floatx4*>(dst + 8 * u) = (floatx4){acc[4 * u], acc[4 * u + 1], acc[4 * u + 2], acc[4 * u + 3]};
 }
 
+// ---------------------------------------------------------------------------------------------
+// Channels-first legacy QKV attention of the depth predictor U-Nets (head dim 32).
+//
+// Semantics: reference src/model/encoder/matching/ldm_unet/unet.py QKVAttentionLegacy.forward:
+// per (batch, head), rows q | k | v (channels-first), out = einsum("bts,bcs->bct",
+// softmax((q * s)^T (k * s)), v) with s = 32^(-1/4) (applied once to the dot product here:
+// s^2 = 1/sqrt(32)). use_cross_view_self_attn folds the V views into the token axis
+// ("(v b) n t -> b n (v t)"): the kernel reads qkv [(v b), 3 * heads * 32, t] and writes out
+// [(v b), heads * 32, t] in that layout directly (token T' = view * t + i), so the two rearrange
+// copies disappear.
+// At 16^2 x 2 views T = 512; 1 or 4 heads: latency-bound, so one workgroup = 8 waves on 32
+// queries, each wave walking an eighth of the keys (no LDS, no barrier in the loop; channels-first
+// rows make the K / Q operand loads coalesced across lanes and each lane's V run contiguous), the
+// eight (max, sum, O) partials merged once through LDS.
+constexpr int kCfD = 32;
+constexpr int kCfWaves = 8;
+
+__global__ void __launch_bounds__(kCfWaves * 64)
+mha_cf32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int B, int H, int tl, int T, float scale) {
+    __shared__ float sO[kCfWaves][16][64];
+    __shared__ float sML[kCfWaves][2][kQW];
+
+    const int qblk = blockIdx.x, bh = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const int b = bh / H, head = bh - b * H;
+    // element (row, token) of this (batch, head): view = token / tl
+    const size_t vstride = (size_t)B * 3 * H * kCfD * tl;  // between views
+    const float* base = qkv + ((size_t)b * 3 * H + (size_t)head * 3) * kCfD * tl;
+    auto at = [&](int row, int tok) -> const float* {
+        const int vw = tok / tl;
+        return base + vw * vstride + (size_t)row * tl + (tok - vw * tl);
+    };
+
+    const int per = (T + kCfWaves - 1) / kCfWaves;
+    const int k_lo = min(T, wid * per), k_hi = min(T, k_lo + per);
+    const int q = qblk * kQW + c;
+    const bool qvalid = q < T;
+
+    // k-step t contracts dims {t, 16 + t}: this lane holds dim 16 h + t
+    float qr[16];
+    {
+        const float qs = scale * kLog2e;
+        const int qc = qvalid ? q : 0;
+        const float* qp = at(16 * h, qc);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) qr[t] = qp[(size_t)t * tl] * qs;
+    }
+    floatx16 o;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    for (int k0 = k_lo; k0 < k_hi; k0 += kKT) {
+        // S^T[key 8(r >> 2) + 4h + (r & 3)][query c] = sum_d K[d][key] Q[d][query]
+        const int kr = min(k0 + c, T - 1);
+        float kv[16];
+        const float* kp = at(kCfD + 16 * h, kr);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) kv[t] = kp[(size_t)t * tl];
+        // V[d = c][keys k0 + 8u + 4h + j], j = 0..3 (clamped past T)
+        float vv[16];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vv[u * 4 + j] = *at(2 * kCfD + c, min(k0 + 8 * u + 4 * h + j, T - 1));
+        floatx16 s;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+        for (int t = 0; t < 16; ++t) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[t], qr[t], s, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+            if (k0 + 8 * (r >> 2) + 4 * h + (r & 3) >= k_hi) s[r] = -INFINITY;
+        float bmax = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[r]);
+        bmax = halves_max(bmax);
+        const float m_new = fmaxf(m_run, bmax);
+        if (__any(m_new > m_run)) {
+            const float corr = __builtin_amdgcn_exp2f(m_run - m_new);
+            l_run *= corr;
+            o *= corr;
+            m_run = m_new;
+        }
+        float bsum = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float e = __builtin_amdgcn_exp2f(s[r] - m_run);
+            s[r] = e;
+            bsum += e;
+        }
+        l_run += halves_sum(bsum);
+        // O^T[d = 8(r >> 2) + 4h + (r & 3)][query c] += V^T P^T; k-step (u, j): keys {8u + j, 8u + 4 + j}
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o = __builtin_amdgcn_mfma_f32_32x32x2f32(vv[u * 4 + j], s[4 * u + j], o, 0, 0, 0);
+    }
+
+    if (h == 0) {
+        sML[wid][0][c] = m_run;
+        sML[wid][1][c] = l_run;
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sO[wid][r][lane] = o[r];
+    __syncthreads();
+    // wave w finishes registers r = 2w, 2w + 1 of the merged tile
+    if (!qvalid) return;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < kCfWaves; ++w) M = fmaxf(M, sML[w][0][c]);
+    float a[kCfWaves], L = 0.f;
+#pragma unroll
+    for (int w = 0; w < kCfWaves; ++w) {
+        const float mw = sML[w][0][c];
+        a[w] = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - M);
+        L += a[w] * sML[w][1][c];
+    }
+    const float inv = 1.0f / L;
+    const int vw = q / tl;
+    float* dst = out + (((size_t)vw * B + b) * H + head) * kCfD * tl + (q - vw * tl);
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+        const int r = 2 * wid + rr;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < kCfWaves; ++w) t += a[w] * sO[w][r][lane];
+        const int d = 8 * (r >> 2) + 4 * h + (r & 3);
+        dst[(size_t)d * tl] = t * inv;
+    }
+}
+
 }  // namespace mha
 }  // namespace tsplat
 
@@ -201,6 +333,23 @@ extern "C" int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, i
     TSPLAT_PROF_BEGIN(tsplat::prof::kMha, stream);
     hipLaunchKernelGGL(mha_f32_kernel, dim3((tokens + kQW - 1) / kQW, batch * heads), dim3(kThreads), 0, stream, qkv,
                        out, tokens, heads, scale);
+    TSPLAT_PROF_END(tsplat::prof::kMha, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_qkv_attention_cf_fwd(const float* qkv, float* out, int32_t batch, int32_t heads,
+                                           int32_t views, int32_t tokens_per_view, int32_t head_dim, float scale,
+                                           void* stream_) {
+    using namespace tsplat::mha;
+    if (!qkv || !out || batch <= 0 || heads <= 0 || views <= 0 || tokens_per_view <= 0 || head_dim != kCfD)
+        return TSPLAT_EINVAL;
+    if ((int64_t)batch * heads > 65535 || (int64_t)views * tokens_per_view >= (1 << 30)) return TSPLAT_EINVAL;
+    const int tokens = views * tokens_per_view;
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(tsplat::prof::kMha, stream);
+    hipLaunchKernelGGL(mha_cf32_kernel, dim3((tokens + kQW - 1) / kQW, batch * heads), dim3(kCfWaves * 64), 0, stream,
+                       qkv, out, batch, heads, tokens_per_view, tokens, scale);
     TSPLAT_PROF_END(tsplat::prof::kMha, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

@@ -494,6 +494,23 @@ def upsample_bilinear_act(x, scale: int, bias=None, act: str = "none"):
     return y
 
 
+def qkv_attention_cf(qkv, heads: int, views: int = 1):
+    """QKVAttentionLegacy (head dim 32, views folded into the tokens when views > 1):
+    qkv [(v b), 3 * heads * 32, t] -> [(v b), heads * 32, t] in one launch
+    (tsplat_qkv_attention_cf_fwd; no rearrange copies)."""
+    lib = _lib.load()
+    vb, width, t = qkv.shape
+    ch = width // (3 * heads)
+    if vb % views or ch * 3 * heads != width:
+        raise ValueError(f"qkv {tuple(qkv.shape)} does not split into {views} views x {heads} heads")
+    x = _f32(qkv)
+    out = torch.empty((vb, heads * ch, t), dtype=torch.float32, device=qkv.device)
+    rc = lib.tsplat_qkv_attention_cf_fwd(_lib.ptr(x), _lib.ptr(out), vb // views, heads, views, t, ch,
+                                         float(ch ** -0.5), _lib.stream_ptr(qkv.device))
+    _lib.check(rc, "tsplat_qkv_attention_cf_fwd")
+    return out
+
+
 def sh_rotation(rotations, d_sh: int):
     """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
     wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""

@@ -148,6 +148,11 @@ class QKVAttentionLegacy(nn.Module):
         self.use_cross_view_self_attn = use_cross_view_self_attn
 
     def forward(self, qkv):
+        width = qkv.shape[1]
+        if (qkv.dtype == torch.float32 and width // (3 * self.n_heads) == 32
+                and not torch.is_autocast_enabled("cuda")):
+            # one kernel reading / writing the (v b) layout in place (kernels.qkv_attention_cf)
+            return kernels.qkv_attention_cf(qkv, self.n_heads, self.n_frames if self.use_cross_view_self_attn else 1)
         if self.use_cross_view_self_attn:
             qkv = rearrange(qkv, "(v b) n t -> b n (v t)", v=self.n_frames)
         bs, width, length = qkv.shape
