@@ -273,6 +273,8 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
 
 def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsample: bool = False) -> bool:
     """Every 2-D convolution the direct kernel takes (so CPU model runs exercise its call sites)."""
+    if weight.dim() == 3:
+        weight = weight.unsqueeze(-1)
     k = weight.shape[-1]
     pad = padding[0] if isinstance(padding, (tuple, list)) else (padding if padding is not None else k // 2)
     return (x.dim() == 4 and k in (1, 3) and stride in (1, 2) and not (upsample and stride != 1) and pad == k // 2
@@ -284,6 +286,8 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
     the reference ldm_unet chains ResBlock(cat([h, skip])) (unet.py:1096-1100), Upsample
     (unet.py:128-137: F.interpolate(nearest) -> conv), Downsample (unet.py:160-170)."""
     x = x1 if x2 is None else torch.cat([x1, x2], dim=1)
+    if weight.dim() == 3:
+        weight = weight.unsqueeze(-1)
     if upsample:
         x = torch.nn.functional.interpolate(x, scale_factor=2, mode="nearest")
     return torch.nn.functional.conv2d(x, weight, bias, stride, weight.shape[-1] // 2)

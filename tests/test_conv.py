@@ -89,3 +89,17 @@ def test_conv2d_nhwc_kernel(device, n, c, h, w, cout, k, relu, res, bias):
     assert out.is_contiguous(memory_format=torch.channels_last)
     err = (out.cpu() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 2e-5, err
+
+
+@pytest.mark.gpu
+def test_conv1d_k1_through_direct_kernel(device):
+    """The U-Net attention blocks' Conv1d(k=1) (qkv, proj_out) run as the 1x1 direct conv on [n, c, t, 1]."""
+    from transplat_amd import kernels as K
+
+    x = seeded((2, 128, 256), 41)
+    wt, b = seeded((384, 128, 1), 42) * 0.1, seeded((384,), 43)
+    ref = torch.nn.functional.conv1d(x, wt, b)
+    xd = x.to(device).unsqueeze(-1)
+    assert K.conv2d_direct_ok(xd, wt.to(device))
+    out = K.conv2d_direct(xd, wt.to(device), b.to(device)).squeeze(-1).cpu()
+    assert (out - ref).abs().max().item() < 2e-5 * ref.abs().max().item()

@@ -374,7 +374,7 @@ def conv_pack_weight(weight):
     hit = _CONV_PACKED.get(id(weight))
     if hit is not None and hit[0]() is weight and hit[1] == weight._version:
         return hit[2]
-    co, ci, k, _ = weight.shape
+    co, ci, k = weight.shape[:3]  # a Conv1d weight [cout, cin, 1] packs as the 1x1 it is
     cot = (co + 31) // 32
     w = torch.zeros((cot * 32, ci, k * k), dtype=torch.float32, device=weight.device)
     w[:co] = weight.detach().float().reshape(co, ci, k * k)
@@ -393,6 +393,10 @@ def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsa
         return False
     if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4:
         return False
+    if weight.dim() == 3:  # Conv1d, kernel 1, on x viewed as [n, c, t, 1]
+        if weight.shape[-1] != 1:
+            return False
+        weight = weight.unsqueeze(-1)
     co, ci, k, k2 = weight.shape
     if k != k2 or k not in (1, 3) or stride not in (1, 2) or (upsample and stride != 1):
         return False
@@ -425,7 +429,7 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
     c2 = b.shape[1] if b is not None else 0
     if b is not None and (b.shape[0] != n or b.shape[2:] != x1.shape[2:]):
         raise ValueError(f"x2 {tuple(b.shape)} does not match x1 {tuple(x1.shape)}")
-    co, ci, k, _ = weight.shape
+    co, ci, k = weight.shape[:3]
     if ci != c1 + c2:
         raise ValueError(f"weight {tuple(weight.shape)} does not match {c1} + {c2} input channels")
     hv, wv = (2 * h, 2 * w) if upsample else (h, w)

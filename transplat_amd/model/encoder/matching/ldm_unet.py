@@ -48,6 +48,11 @@ def conv(conv: nn.Module, x, x2=None, upsample: bool = False, bias: bool = True)
     b = conv.bias if bias else None
     if _direct(conv, x, x2, upsample):
         return kernels.conv2d_direct(x, conv.weight, b, conv.stride[0], x2=x2, upsample=upsample)
+    if (isinstance(conv, nn.Conv1d) and x2 is None and not upsample and conv.kernel_size == (1,)
+            and conv.stride == (1,) and conv.groups == 1 and x.dim() == 3
+            and kernels.conv2d_direct_ok(x.unsqueeze(-1), conv.weight)):
+        # the attention blocks' qkv / proj_out: a 1x1 over [n, c, t] viewed as [n, c, t, 1]
+        return kernels.conv2d_direct(x.unsqueeze(-1), conv.weight, b).squeeze(-1)
     if x2 is not None:
         x = torch.cat([x, x2], dim=1)
     if upsample:
@@ -183,7 +188,7 @@ class AttentionBlock(nn.Module):
     def forward(self, x):
         b, c, *spatial = x.shape
         x = x.reshape(b, c, -1)
-        h = self.attention(self.qkv(x))
+        h = self.attention(conv(self.qkv, x))
         return conv_gn_act(self.proj_out, self.norm, h, residual=x).reshape(b, c, *spatial)
 
 
