@@ -8,6 +8,9 @@ OUT=$R/gpurun_out/final
 mkdir -p $OUT
 export PYTHONPATH=$R
 step() { echo "== $1"; }
+# part: "all" (default), "bench" (tests .. raster bench) or "prof" (rocprof passes + PMC)
+PART=${1:-all}
+if [ "$PART" != "prof" ]; then
 step tests
 timeout -k 10 900 python -m pytest tests -m gpu -q > $OUT/pytest_gpu.log 2>&1; rc=$?; tail -2 $OUT/pytest_gpu.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
@@ -25,6 +28,8 @@ tail -1 $OUT/bench_fp32_b8.log | cut -c1-200
 step raster
 timeout -k 10 300 python bench.py --workload raster --steps 20 --warmup 3 > $OUT/bench_raster.log 2>&1 || exit 1
 tail -1 $OUT/bench_raster.log | cut -c1-200
+fi
+[ "$PART" = "bench" ] && { echo done; exit 0; }
 cd /tmp && export TMPDIR=/tmp
 step prof
 # (rocprof passes without MIOpen's algorithm search, so its trial kernels do not pollute the per-step
@@ -32,6 +37,8 @@ step prof
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof_e2e_fp32_b1 -o run --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-conv-search > $OUT/prof_e2e_fp32_b1.log 2>&1 || exit 1
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof_c3 -o run --output-format csv -- python3 $R/bench.py --batch 8 --dense-dtype bf16 --steps 5 --warmup 2 --no-cpu-baseline --no-conv-search > $OUT/prof_c3.log 2>&1 || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_raster -o run --output-format csv -- python3 $R/bench.py --workload raster --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_raster.log 2>&1 || exit 1
+if [ "${NO_PMC:-0}" != "1" ]; then
 step pmc
 cd $R && bash tools/pmc_round.sh || exit 1
+fi
 echo done
