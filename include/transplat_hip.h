@@ -196,6 +196,14 @@ int tsplat_group_norm_fwd(const float* x, const float* pre_bias, const float* ga
 int tsplat_bias_act_fwd(const float* x, const float* bias, const float* residual, float* y, int32_t n, int32_t c,
                         int64_t hw, int32_t act, void* stream);
 
+/* Channels-last conv epilogue: y [rows, c] = act(x + bias[c]) (+ res1) (+ res2), NHWC maps with
+ * c % 4 == 0, 16-byte aligned; act 0 none, 2 GELU (erf), 3 ReLU (before the residuals). The
+ * Depth-Anything DPT ResidualConvUnit / FeatureFusionBlock (reference
+ * src/depth_anything_v2/util/blocks.py:73-150) after bias-free MIOpen convolutions: conv1 -> bias +
+ * ReLU, conv2 -> bias + unit residual (+ the fusion block's skip). x may equal y. */
+int tsplat_bias_act_nhwc_fwd(const float* x, const float* bias, const float* res1, const float* res2, float* y,
+                             int64_t rows, int32_t c, int32_t act, void* stream);
+
 /* Pre-norm residual step of the DINOv2 blocks (reference dinov2_layers/block.py Block.forward:
  * x = x + ls(sublayer(norm(x)))): x_out = x + ls * y, n_out = LayerNorm(x_out; ln_w, ln_b, ln_eps)
  * with the NEXT sub-layer's norm, over rows of dim 256 / 512 / 768 / 1024 fp32. y may be NULL

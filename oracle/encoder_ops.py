@@ -330,6 +330,17 @@ def qkv_attention_cf(qkv, heads: int, views: int = 1):
     return rearrange(a, "b n (v t) -> (v b) n t", v=views) if views > 1 else a
 
 
+def conv_nhwc_epilogue(conv, x, act: str = "none", res1=None, res2=None):
+    """DPT unit chains (reference util/blocks.py): act(conv(x)) (+ res1) (+ res2)."""
+    y = conv(x)
+    y = {"none": y, "relu": torch.relu(y), "gelu": torch.nn.functional.gelu(y)}[act]
+    if res1 is not None:
+        y = y + res1
+    if res2 is not None:
+        y = y + res2
+    return y
+
+
 def mha(qkv, heads: int, scale: float):
     """DINOv2 Attention core (reference dinov2_layers/attention.py): reshape to heads, softmax
     attention (torch SDPA math), back to [B, N, heads * head_dim]."""
@@ -410,4 +421,5 @@ KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gau
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
                        "conv_bias_act", "mha", "residual_ln", "depth_softmax", "conv2d_direct_ok",
                        "conv2d_direct", "conv2d_nhwc_ok", "conv2d_nhwc",
-                       "upsample_bilinear_act", "qkv_attention_cf")
+                       "upsample_bilinear_act", "qkv_attention_cf",
+                       "conv_nhwc_epilogue")

@@ -103,3 +103,25 @@ def test_conv1d_k1_through_direct_kernel(device):
     assert K.conv2d_direct_ok(xd, wt.to(device))
     out = K.conv2d_direct(xd, wt.to(device), b.to(device)).squeeze(-1).cpu()
     assert (out - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("act,nres", [("relu", 0), ("none", 1), ("none", 2), ("gelu", 1)])
+def test_conv_nhwc_epilogue(device, act, nres):
+    """Bias-free MIOpen conv on channels-last maps + tsplat_bias_act_nhwc_fwd (bias, act, residuals)
+    vs the module chain (DPT ResidualConvUnit / FeatureFusionBlock)."""
+    from transplat_amd import kernels as K
+
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(128, 128, 3, padding=1)
+    x = seeded((2, 128, 18, 18), 51)
+    rs = [seeded((2, 128, 18, 18), 52 + i) for i in range(nres)] + [None] * (2 - nres)
+    with torch.no_grad():
+        ref = E.conv_nhwc_epilogue(conv, x, act, *rs)
+        cd = conv.to(device)
+        cd.weight.data = cd.weight.data.contiguous(memory_format=torch.channels_last)
+        cl = lambda t: t.to(device).contiguous(memory_format=torch.channels_last) if t is not None else None  # noqa
+        out = K.conv_nhwc_epilogue(cd, cl(x), act, *[cl(r) for r in rs])
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    err = (out.cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, err

@@ -67,6 +67,7 @@ SIGNATURES = {
     "tsplat_conv2d_f32_nhwc_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P] + [_I32] * 7 + [_P]),
     "tsplat_residual_ln_fwd": (ctypes.c_int, [_P] * 5 + [ctypes.c_float, _P, _P, _I32, _I32, _P]),
     "tsplat_bias_act_fwd": (ctypes.c_int, [_P] * 4 + [_I32, _I32, ctypes.c_int64, _I32, _P]),
+    "tsplat_bias_act_nhwc_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int64, _I32, _I32, _P]),
     "tsplat_win_attn_partials_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 8 + [_P]),
     "tsplat_linear_f32_attn_merge_fwd": (ctypes.c_int, [_P] + [_I32] * 6 + [_P] * 3 + [ctypes.c_float, _P, _P, _I32,
                                                                                        _I32, _P]),

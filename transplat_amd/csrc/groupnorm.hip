@@ -395,6 +395,79 @@ extern "C" int tsplat_bias_act_fwd(const float* x, const float* bias, const floa
 }
 
 // ---------------------------------------------------------------------------------------------
+// Channels-last form: y = act(x + bias[c]) (+ res1) (+ res2) over [rows, C] (NHWC maps, C % 4 == 0)
+// -- the epilogues of the DPT head's bias-free MIOpen convolutions (ResidualConvUnit: bias + ReLU
+// after conv1; bias + the unit's residual (+ the fusion block's skip) after conv2).
+namespace tsplat {
+namespace gn {
+
+template <int ACT, int NRES>
+__global__ void __launch_bounds__(kThreads)
+bias_act_nhwc_kernel(const float* __restrict__ x, const float* __restrict__ bias, const float* __restrict__ r1,
+                     const float* __restrict__ r2, float* __restrict__ y, int n4, int c4) {
+    const int i = blockIdx.x * kThreads + threadIdx.x;
+    if (i >= n4) return;
+    float4 v = reinterpret_cast<const float4*>(x)[i];
+    if (bias) {
+        const float4 b = reinterpret_cast<const float4*>(bias)[i % c4];
+        v.x += b.x;
+        v.y += b.y;
+        v.z += b.z;
+        v.w += b.w;
+    }
+    v.x = activate<ACT>(v.x);
+    v.y = activate<ACT>(v.y);
+    v.z = activate<ACT>(v.z);
+    v.w = activate<ACT>(v.w);
+    if (NRES >= 1) {
+        const float4 r = reinterpret_cast<const float4*>(r1)[i];
+        v.x += r.x;
+        v.y += r.y;
+        v.z += r.z;
+        v.w += r.w;
+    }
+    if (NRES >= 2) {
+        const float4 r = reinterpret_cast<const float4*>(r2)[i];
+        v.x += r.x;
+        v.y += r.y;
+        v.z += r.z;
+        v.w += r.w;
+    }
+    reinterpret_cast<float4*>(y)[i] = v;
+}
+
+}  // namespace gn
+}  // namespace tsplat
+
+extern "C" int tsplat_bias_act_nhwc_fwd(const float* x, const float* bias, const float* res1, const float* res2,
+                                        float* y, int64_t rows, int32_t c, int32_t act, void* stream_) {
+    using namespace tsplat::gn;
+    if (!x || !y || rows <= 0 || c <= 0 || c % 4 || !(act == 0 || act == 2 || act == 3)) return TSPLAT_EINVAL;
+    if (res2 && !res1) return TSPLAT_EINVAL;
+    if ((uintptr_t)x % 16 || (uintptr_t)y % 16 || (bias && (uintptr_t)bias % 16) || (res1 && (uintptr_t)res1 % 16) ||
+        (res2 && (uintptr_t)res2 % 16))
+        return TSPLAT_EINVAL;
+    const int64_t n4 = rows * c / 4;
+    if (n4 > INT32_MAX) return TSPLAT_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    const dim3 grid((unsigned)((n4 + kThreads - 1) / kThreads));
+    const int nres = res2 ? 2 : (res1 ? 1 : 0);
+#define TSPLAT_BAN(A, R) \
+    hipLaunchKernelGGL((bias_act_nhwc_kernel<A, R>), grid, dim3(kThreads), 0, stream, x, bias, res1, res2, y, (int)n4, c / 4)
+#define TSPLAT_BAN_R(A)                  \
+    switch (nres) {                      \
+        case 0: TSPLAT_BAN(A, 0); break; \
+        case 1: TSPLAT_BAN(A, 1); break; \
+        default: TSPLAT_BAN(A, 2); break; \
+    }
+    if (act == 0) { TSPLAT_BAN_R(0) } else if (act == 2) { TSPLAT_BAN_R(2) } else { TSPLAT_BAN_R(3) }
+#undef TSPLAT_BAN_R
+#undef TSPLAT_BAN
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
 // Pre-norm transformer residual step of the DINOv2 blocks: x' = x + ls * y (LayerScale residual),
 // n = LayerNorm(x') with the NEXT sub-layer's norm, one pass over the row (one wave per row).
 namespace tsplat {

@@ -515,6 +515,27 @@ def qkv_attention_cf(qkv, heads: int, views: int = 1):
     return out
 
 
+def conv_nhwc_epilogue(conv, x, act: str = "none", res1=None, res2=None):
+    """act(conv(x) + bias) (+ res1) (+ res2) on channels-last fp32 maps: the bias-free MIOpen
+    convolution, then bias, activation and residuals in one pass (tsplat_bias_act_nhwc_fwd)."""
+    import torch.nn.functional as F
+
+    y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+    cl = torch.channels_last
+    if not y.is_contiguous(memory_format=cl):
+        y = y.contiguous(memory_format=cl)
+    rs = [r.contiguous(memory_format=cl) if r is not None else None for r in (res1, res2)]
+    for r in rs:
+        if r is not None and (r.shape != y.shape or r.dtype != torch.float32):
+            raise ValueError(f"residual {tuple(r.shape)} does not match the output {tuple(y.shape)}")
+    lib = _lib.load()
+    rc = lib.tsplat_bias_act_nhwc_fwd(_lib.ptr(y), _lib.ptr(conv.bias), _lib.ptr(rs[0]), _lib.ptr(rs[1]),
+                                      _lib.ptr(y), y.numel() // y.shape[1], y.shape[1], _ACTS[act],
+                                      _lib.stream_ptr(y.device))
+    _lib.check(rc, "tsplat_bias_act_nhwc_fwd")
+    return y
+
+
 def sh_rotation(rotations, d_sh: int):
     """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
     wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""

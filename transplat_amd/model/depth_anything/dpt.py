@@ -25,6 +25,8 @@ _DPT_CL_WEIGHTS = os.environ.get("TSPLAT_DPT_CL_WEIGHTS", "1") != "0"
 # kernel's pixel-per-lane B gathers touch 32 cache lines per load on a channels-last map. Default
 # "0" (MIOpen) until the operand is staged through LDS.
 _DPT_DIRECT = os.environ.get("TSPLAT_DPT_DIRECT", "0")
+# conv epilogues (bias + ReLU, bias + residuals) fused after the MIOpen convolutions; "0" = A/B off
+_DPT_EPI = os.environ.get("TSPLAT_DPT_EPI", "1") != "0"
 
 
 class ResidualConvUnit(nn.Module):
@@ -38,20 +40,32 @@ class ResidualConvUnit(nn.Module):
             self.bn2 = nn.BatchNorm2d(features)
         self.activation = activation
 
-    def forward(self, x):
+    def _epilogue_ok(self, x) -> bool:
+        return (_DPT_EPI and not self.bn and isinstance(self.activation, nn.ReLU) and x.dtype == torch.float32
+                and self.conv1.weight.dtype == torch.float32 and x.shape[1] % 4 == 0
+                and not torch.is_autocast_enabled("cuda"))
+
+    def forward(self, x, skip=None):
+        """out(x) + x (+ skip: the FeatureFusionBlock's other input, added in the same pass)."""
+        if _DPT_DIRECT == "0" and self._epilogue_ok(x):
+            # bias-free MIOpen convs with bias + ReLU / bias + residual(s) fused after each:
+            # 3 glue launches per unit instead of 5 (6 with the fusion block's add)
+            out = kernels.conv_nhwc_epilogue(self.conv1, self.activation(x), "relu")
+            return kernels.conv_nhwc_epilogue(self.conv2, out, "none", x, skip)
         if (_DPT_DIRECT != "0" and not self.bn and isinstance(self.activation, nn.ReLU)
                 and kernels.conv2d_nhwc_ok(x, self.conv1.weight)):
             # latency-bound levels (<= 36^2): ReLU-on-load, bias and the residual fused into the
             # channels-last direct convolution, two launches for the unit
             out = kernels.conv2d_nhwc(x, self.conv1.weight, self.conv1.bias, relu_in=True)
-            return kernels.conv2d_nhwc(out, self.conv2.weight, self.conv2.bias, residual=x, relu_in=True)
+            y = kernels.conv2d_nhwc(out, self.conv2.weight, self.conv2.bias, residual=x, relu_in=True)
+            return y if skip is None else skip + y
         out = self.conv1(self.activation(x))
         if self.bn:
             out = self.bn1(out)
         out = self.conv2(self.activation(out))
         if self.bn:
             out = self.bn2(out)
-        return out + x
+        return out + x if skip is None else skip + (out + x)
 
 
 class FeatureFusionBlock(nn.Module):
@@ -66,7 +80,7 @@ class FeatureFusionBlock(nn.Module):
     def forward(self, *xs, size=None):
         output = xs[0]
         if len(xs) == 2:
-            output = output + self.resConfUnit1(xs[1])
+            output = self.resConfUnit1(xs[1], skip=output)  # xs[0] + unit(xs[1])
         output = self.resConfUnit2(output)
         if size is None and self.size is None:
             modifier = {"scale_factor": 2}
@@ -141,7 +155,13 @@ class DPTHead(nn.Module):
         out_feature = final_out.clone().detach()
         final_out = F.interpolate(final_out, (int(patch_h * 14), int(patch_w * 14)), mode="bilinear",
                                   align_corners=True)
-        return s.output_conv2(final_out), out_feature
+        oc = s.output_conv2
+        if (_DPT_EPI and final_out.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")
+                and final_out.is_cuda and final_out.is_contiguous(memory_format=torch.channels_last)):
+            # conv -> ReLU as conv + (bias, ReLU) epilogue; the 1-channel tail stays on the modules
+            h = kernels.conv_nhwc_epilogue(oc[0], final_out, "relu")
+            return oc[4](oc[3](oc[2](h))), out_feature
+        return oc(final_out), out_feature
 
 
 class DepthAnythingV2(nn.Module):
