@@ -106,7 +106,8 @@ int tsplat_raster_fwd(const tsplat_raster_desc* desc,
 
 
 /* Depth-candidate softmax head (reference depth_predictor_trans.py:170-180): logits [n, depths, hw]
- * (NCHW), disp [n, depths] -> coarse [n, hw] = sum_d disp softmax_d, pdf_max [n, hw] = max_d softmax_d. */
+ * (NCHW), disp [n, depths] -> coarse [n, hw] = sum_d disp softmax_d, pdf_max [n, hw] = max_d softmax_d;
+ * depths <= 256. */
 int tsplat_depth_softmax_fwd(const float* logits, const float* disp, float* coarse, float* pdf_max, int32_t n,
                              int32_t depths, int32_t hw, void* stream);
 

@@ -423,15 +423,17 @@ def test_fused_linear_post_norm(device, k, relu_in):
 
 
 @pytest.mark.gpu
-def test_depth_softmax_kernel(device):
+@pytest.mark.parametrize("n,d,h,w", [(2, 128, 64, 64), (1, 37, 9, 11), (3, 256, 8, 8)])
+def test_depth_softmax_kernel(device, n, d, h, w):
     """Depth-candidate softmax head (expected disparity + max pdf) vs the CPU restatement."""
     from transplat_amd import kernels as K
 
-    logits = seeded((2, 128, 64, 64), 97) * 4.0
-    disp = torch.linspace(0.01, 1.0, 128).repeat(2, 1).reshape(2, 128, 1, 1)
+    logits = seeded((n, d, h, w), 97) * 4.0
+    disp = torch.linspace(0.01, 1.0, d).repeat(n, 1).reshape(n, d, 1, 1)
     rc, rm = E.depth_softmax(logits, disp)
     oc, om = K.depth_softmax(logits.to(device), disp.to(device))
-    assert (oc.cpu() - rc).abs().max().item() < 1e-6 and (om.cpu() - rm).abs().max().item() < 1e-6
+    # 2e-6 on O(1) values: the kernel merges 8 depth slices' sums with an exp(m_slice - M) rescale
+    assert (oc.cpu() - rc).abs().max().item() < 2e-6 and (om.cpu() - rm).abs().max().item() < 2e-6
 
 
 @pytest.mark.gpu

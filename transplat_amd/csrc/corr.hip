@@ -377,23 +377,56 @@ extern "C" int tsplat_msda_fwd(const float* value, const float* loc, const float
 namespace tsplat {
 namespace corr {
 
-__global__ void __launch_bounds__(kThreads)
+// 256 threads = 32 pixels x 8 depth slices (lanes of a wave: consecutive pixels of one slice, so
+// every load is a 128-B row segment); each thread keeps its slice's logits in registers, the 8
+// slices' (max, sum, weighted sum) merge through LDS. 256 workgroups at 64^2 x 2 instead of 32
+// one-pixel-per-thread workgroups walking all 128 depths serially (58 us -> a few us).
+constexpr int kSmPix = 32, kSmSlices = 8, kSmMaxPer = 32;
+
+__global__ void __launch_bounds__(kSmPix * kSmSlices)
 depth_softmax_kernel(const float* __restrict__ logits, const float* __restrict__ disp, float* __restrict__ coarse,
                      float* __restrict__ pmax, int D, int HW) {
-    const int p = blockIdx.x * kThreads + threadIdx.x, n = blockIdx.y;
-    if (p >= HW) return;
-    const float* l = logits + (size_t)n * D * HW + p;
+    __shared__ float sm[3][kSmSlices][kSmPix];
+    const int pl = threadIdx.x % kSmPix, sl = threadIdx.x / kSmPix;
+    const int p = blockIdx.x * kSmPix + pl, n = blockIdx.y;
+    const int per = (D + kSmSlices - 1) / kSmSlices;
+    const int d0 = sl * per, d1 = min(D, d0 + per);
+    const int pc = min(p, HW - 1);
+    const float* l = logits + (size_t)n * D * HW + pc;
     const float* dv = disp + (size_t)n * D;
+    float v[kSmMaxPer];
+#pragma unroll
+    for (int k = 0; k < kSmMaxPer; ++k) v[k] = (k < d1 - d0) ? l[(size_t)(d0 + k) * HW] : -INFINITY;
     float m = -INFINITY;
-    for (int d = 0; d < D; ++d) m = fmaxf(m, l[(size_t)d * HW]);
+#pragma unroll
+    for (int k = 0; k < kSmMaxPer; ++k) m = fmaxf(m, v[k]);
     float s = 0.f, w = 0.f;
-    for (int d = 0; d < D; ++d) {
-        const float e = expf(l[(size_t)d * HW] - m);
-        s += e;
-        w += e * dv[d];
+#pragma unroll
+    for (int k = 0; k < kSmMaxPer; ++k) {
+        if (k < d1 - d0) {
+            const float e = expf(v[k] - m);
+            s += e;
+            w += e * dv[d0 + k];
+        }
     }
-    coarse[(size_t)n * HW + p] = w / s;
-    pmax[(size_t)n * HW + p] = 1.0f / s;  // = exp(m - m) / s, the largest pdf entry
+    sm[0][sl][pl] = m;
+    sm[1][sl][pl] = s;
+    sm[2][sl][pl] = w;
+    __syncthreads();
+    if (sl != 0 || p >= HW) return;
+    float M = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < kSmSlices; ++k) M = fmaxf(M, sm[0][k][pl]);
+    float S = 0.f, W = 0.f;
+#pragma unroll
+    for (int k = 0; k < kSmSlices; ++k) {
+        const float mk = sm[0][k][pl];
+        const float a = mk == -INFINITY ? 0.f : expf(mk - M);
+        S += a * sm[1][k][pl];
+        W += a * sm[2][k][pl];
+    }
+    coarse[(size_t)n * HW + p] = W / S;
+    pmax[(size_t)n * HW + p] = 1.0f / S;  // = exp(M - M) / S, the largest pdf entry
 }
 
 }  // namespace corr
@@ -404,8 +437,9 @@ extern "C" int tsplat_depth_softmax_fwd(const float* logits, const float* disp, 
     using namespace tsplat::corr;
     if (!logits || !disp || !coarse || !pdf_max || n <= 0 || depths <= 0 || hw <= 0 || n > 65535)
         return TSPLAT_EINVAL;
+    if (depths > kSmSlices * kSmMaxPer) return TSPLAT_EINVAL;
     hipStream_t stream = (hipStream_t)stream_;
-    hipLaunchKernelGGL(depth_softmax_kernel, dim3((hw + kThreads - 1) / kThreads, n), dim3(kThreads), 0, stream,
+    hipLaunchKernelGGL(depth_softmax_kernel, dim3((hw + kSmPix - 1) / kSmPix, n), dim3(kSmPix * kSmSlices), 0, stream,
                        logits, disp, coarse, pdf_max, depths, hw);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

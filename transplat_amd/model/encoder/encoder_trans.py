@@ -143,8 +143,11 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
             da_depth, out_feature = self.da_model(da_images)
             da_depth = F.interpolate(da_depth[None].float(), (h, w), mode="bilinear", align_corners=True)
             da_depth = da_depth.view(b, v, 1, h, w).flatten(2)
-            da_max = torch.max(da_depth, dim=-1, keepdim=True)[0]
-            da_min = torch.min(da_depth, dim=-1, keepdim=True)[0]
+            # per-view min / max in two aminmax stages (rows of w, then the h row results): the
+            # single-row reductions ran on 2 workgroups each (~20 us apiece); exact either way
+            lo, hi = torch.aminmax(da_depth.view(b, v, h, w), dim=-1)
+            da_min = lo.amin(dim=-1, keepdim=True)
+            da_max = hi.amax(dim=-1, keepdim=True)
             da_depth = ((da_depth - da_min) / (da_max - da_min)).reshape(b, v, 1, h, w)
         dino_feature = out_feature.float().view(b, v, *out_feature.shape[1:])
 
