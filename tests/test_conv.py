@@ -27,6 +27,8 @@ CASES = [
     (1, 6, 4, 9, 13, 40, 3, 1, False, True),          # ragged: odd sizes, cout % 32 != 0, tiny cin
     (1, 6, 0, 9, 13, 40, 3, 2, False, True),
     (3, 2, 0, 5, 7, 1, 3, 1, True, True),
+    (2, 128, 0, 32, 32, 128, 3, 2, False, True),      # single-shot (4 ci pairs per wave) stride 2
+    (1, 96, 0, 12, 12, 64, 3, 1, False, True),        # single-shot with 3 pairs per wave
 ]
 
 

@@ -112,6 +112,14 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    if constexpr (G == 4) {
+        // single-shot form (host guarantees <= 4 ci pairs per wave): all 36 k-steps' loads in one
+        // round trip, no second buffer
+        float ca[B], cb[B];
+        load(0, ca, cb);
+#pragma unroll
+        for (int k = 0; k < B; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[k], cb[k], acc, 0, 0, 0);
+    } else {
     float ca[B], cb[B], na[B], nbv[B];
     if (nbatch > 0) load(0, ca, cb);
 #pragma unroll 1
@@ -127,6 +135,7 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
                 cb[k] = nbv[k];
             }
         }
+    }
     }
 
     // sum the ksplit partial tiles
@@ -204,15 +213,17 @@ extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x
     TSPLAT_PROF_BEGIN(tsplat::prof::kConv, stream);
 #define TSPLAT_CONV_LAUNCH(KS, S, UP, G) \
     hipLaunchKernelGGL((conv_f32_kernel<KS, S, UP, G, false, false>), grid, block, lds, stream, p)
-    // ci pairs per batch: 2 (3x3) / 16 (1x1) once a wave has that many, else 1 / 8
+    // ci pairs per batch: 3x3 -> all of a wave's pairs in one shot when it has 3-4, else 2 (or 1);
+    // 1x1 -> 16 once a wave has that many, else 8
     const int per_wave = ((c1 + c2) / 2 + ksplit - 1) / ksplit;
     const bool wide = per_wave >= (ksize == 3 ? 2 : 16);
+    const bool one = ksize == 3 && per_wave >= 3 && per_wave <= 4;
     if (ksize == 3 && stride == 1 && !upsample) {
-        if (wide) TSPLAT_CONV_LAUNCH(3, 1, 0, 2); else TSPLAT_CONV_LAUNCH(3, 1, 0, 1);
+        if (one) TSPLAT_CONV_LAUNCH(3, 1, 0, 4); else if (wide) TSPLAT_CONV_LAUNCH(3, 1, 0, 2); else TSPLAT_CONV_LAUNCH(3, 1, 0, 1);
     } else if (ksize == 3 && stride == 2 && !upsample) {
-        if (wide) TSPLAT_CONV_LAUNCH(3, 2, 0, 2); else TSPLAT_CONV_LAUNCH(3, 2, 0, 1);
+        if (one) TSPLAT_CONV_LAUNCH(3, 2, 0, 4); else if (wide) TSPLAT_CONV_LAUNCH(3, 2, 0, 2); else TSPLAT_CONV_LAUNCH(3, 2, 0, 1);
     } else if (ksize == 3 && stride == 1 && upsample) {
-        if (wide) TSPLAT_CONV_LAUNCH(3, 1, 1, 2); else TSPLAT_CONV_LAUNCH(3, 1, 1, 1);
+        if (one) TSPLAT_CONV_LAUNCH(3, 1, 1, 4); else if (wide) TSPLAT_CONV_LAUNCH(3, 1, 1, 2); else TSPLAT_CONV_LAUNCH(3, 1, 1, 1);
     } else if (ksize == 1 && stride == 1 && !upsample) {
         if (wide) TSPLAT_CONV_LAUNCH(1, 1, 0, 16); else TSPLAT_CONV_LAUNCH(1, 1, 0, 8);
     } else {

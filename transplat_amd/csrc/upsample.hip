@@ -24,15 +24,16 @@ __device__ __forceinline__ float act(float v) {
 template <int ACT>
 __global__ void __launch_bounds__(256) bilinear_ac_kernel(const float* __restrict__ x, const float* __restrict__ bias,
                                                           float* __restrict__ y, int c, int h, int w, int ho, int wo,
-                                                          float rh, float rw, long total4) {
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+                                                          float rh, float rw, int total4) {
+    // 32-bit index math (total4 < 2^31 checked on the host): 64-bit divisions cost ~100 VALU ops
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= total4) return;
     const int wo4 = wo >> 2;
-    const int ox0 = (int)(i % wo4) * 4;
-    const long rowi = i / wo4;
-    const int oy = (int)(rowi % ho);
-    const long nc = rowi / ho;
-    const float* src = x + nc * (long)h * w;
+    const int rowi = i / wo4;
+    const int ox0 = (i - rowi * wo4) * 4;
+    const int nc = rowi / ho;
+    const int oy = rowi - nc * ho;
+    const float* src = x + (size_t)nc * h * w;
     const float b = bias ? bias[nc % c] : 0.f;
     const float hr = rh * (float)oy;
     const int h0 = (int)hr;
@@ -50,7 +51,7 @@ __global__ void __launch_bounds__(256) bilinear_ac_kernel(const float* __restric
         const float v = l0 * (m0 * r0[w0] + m1 * r0[w1]) + l1 * (m0 * r1[w0] + m1 * r1[w1]);
         out[j] = act<ACT>(v + b);
     }
-    *reinterpret_cast<float4*>(y + rowi * wo + ox0) = make_float4(out[0], out[1], out[2], out[3]);
+    *reinterpret_cast<float4*>(y + (size_t)rowi * wo + ox0) = make_float4(out[0], out[1], out[2], out[3]);
 }
 
 }  // namespace upsample
@@ -63,7 +64,9 @@ extern "C" int tsplat_upsample_bilinear_act_fwd(const float* x, const float* bia
     if (!x || !y || n <= 0 || c <= 0 || height <= 0 || width <= 0 || scale < 1) return TSPLAT_EINVAL;
     const int ho = height * scale, wo = width * scale;
     if (wo % 4) return TSPLAT_EINVAL;
-    const long total4 = (long)n * c * ho * (wo / 4);
+    const int64_t total4_64 = (int64_t)n * c * ho * (wo / 4);
+    if (total4_64 >= (1ll << 31)) return TSPLAT_EINVAL;
+    const int total4 = (int)total4_64;
     // align_corners = True scale, as torch computes it in float: (in - 1) / (out - 1)
     const float rh = ho > 1 ? (float)(height - 1) / (float)(ho - 1) : 0.f;
     const float rw = wo > 1 ? (float)(width - 1) / (float)(wo - 1) : 0.f;
