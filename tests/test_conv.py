@@ -127,3 +127,18 @@ def test_conv_nhwc_epilogue(device, act, nres):
     assert out.is_contiguous(memory_format=torch.channels_last)
     err = (out.cpu() - ref).abs().max().item() / ref.abs().max().item()
     assert err < 1e-5, err
+
+
+@pytest.mark.gpu
+def test_patch_embed_gemm_matches_conv(device):
+    """DINOv2 PatchEmbed's fp32 device path (unfold + one GEMM) vs the stride-14 convolution."""
+    from transplat_amd.model.depth_anything.dinov2 import PatchEmbed
+
+    torch.manual_seed(0)
+    pe = PatchEmbed(img_size=252, patch_size=14, in_chans=3, embed_dim=768)
+    x = seeded((2, 3, 252, 252), 61)
+    with torch.no_grad():
+        ref = pe.proj(x).flatten(2).transpose(1, 2)
+        out = pe.to(device)(x.to(device)).cpu()
+    assert out.shape == ref.shape
+    assert (out - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
