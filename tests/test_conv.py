@@ -142,3 +142,21 @@ def test_patch_embed_gemm_matches_conv(device):
         out = pe.to(device)(x.to(device)).cpu()
     assert out.shape == ref.shape
     assert (out - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
+
+
+@pytest.mark.gpu
+def test_unet_full_res_1x1_gemm_path(device, monkeypatch):
+    """The U-Net's 1x1 convolutions that the direct kernel does not take run as a batched GEMM
+    (ldm_unet.conv): same result as the convolution, with and without bias."""
+    from transplat_amd import kernels as K
+    from transplat_amd.model.encoder.matching import ldm_unet as U
+
+    monkeypatch.setattr(K, "_CONV_MODE", "off")
+    x = seeded((2, 64, 64, 64), 71)
+    for bias in (True, False):
+        torch.manual_seed(0)
+        conv = torch.nn.Conv2d(64, 32, 1, bias=bias)
+        with torch.no_grad():
+            ref = conv(x)
+            out = U.conv(conv.to(device), x.to(device)).cpu()
+        assert (out - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
