@@ -91,20 +91,25 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
     // this wave's ci pairs: w, w + ksplit, ... in batches of G
     const int ncp = cp_all > w ? (cp_all - w + ksplit - 1) / ksplit : 0;
     const int nbatch = (ncp + G - 1) / G;
+    // (called only when ncp > 0) every load is issued unconditionally from a clamped, valid
+    // address and masked afterwards: a conditional load would become a branch with its own
+    // s_waitcnt, serialising the batch's round trips
     auto load = [&](int bi, float* a, float* b) {
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             const int i = bi * G + g;
             const bool ok = i < ncp;
-            const int cp = w + (ok ? i : 0) * ksplit;
+            const int cp = w + min(i, ncp - 1) * ksplit;
             const float* src = chan(cp);
             const float* wq = wbase + (size_t)cp * 64;
 #pragma unroll
             for (int t = 0; t < T; ++t) {
                 const float av = wq[t * wtap];
                 const float bv = RELU ? fmaxf(src[off[t]], 0.f) : src[off[t]];
-                a[g * T + t] = ok ? av : 0.f;
-                b[g * T + t] = ok && ((vmask >> t) & 1) ? bv : 0.f;
+                // masks as multipliers (exact: x * 1 = x, finite x * 0 = 0), so the loaded values
+                // are always used and the compiler cannot sink the loads into branches
+                a[g * T + t] = av * (ok ? 1.f : 0.f);
+                b[g * T + t] = bv * (ok && ((vmask >> t) & 1) ? 1.f : 0.f);
             }
         }
     };
@@ -112,30 +117,42 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    if constexpr (G == 4) {
-        // single-shot form (host guarantees <= 4 ci pairs per wave): all 36 k-steps' loads in one
-        // round trip, no second buffer
-        float ca[B], cb[B];
-        load(0, ca, cb);
-#pragma unroll
-        for (int k = 0; k < B; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[k], cb[k], acc, 0, 0, 0);
-    } else {
-    float ca[B], cb[B], na[B], nbv[B];
-    if (nbatch > 0) load(0, ca, cb);
+    if constexpr (KS == 3) {
+        // 3x3: one batch = G ci pairs x 9 taps, all of its loads issued before its MFMAs (one memory
+        // round trip per batch); single-buffered so the 1024-thread workgroup stays within 128 VGPRs
+        // (G = 4 is launched only when a wave has <= 4 pairs: one batch, no loop-carried state, so
+        // the 72 operand registers fit next to the accumulator without spilling)
+        const int nb = G == 4 ? min(nbatch, 1) : nbatch;
 #pragma unroll 1
-    for (int bi = 0; bi < nbatch; ++bi) {
-        const bool more = bi + 1 < nbatch;
-        if (more) load(bi + 1, na, nbv);
+        for (int bi = 0; bi < nb; ++bi) {
+            float ca[B], cb[B];
+            load(bi, ca, cb);
+            // keep the loads ahead of the MFMAs: left alone, the scheduler issues each load just before
+            // its MFMA (a vmcnt(0) wait per k-step) to save registers
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int k = 0; k < B; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[k], cb[k], acc, 0, 0, 0);
-        if (more) {
+            for (int k = 0; k < B; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[k], cb[k], acc, 0, 0, 0);
+        }
+    } else {
+        // 1x1: 8-16 pairs per batch, the next batch's loads in flight during this batch's MFMAs
+        float ca[B], cb[B], na[B], nbv[B];
+        if (nbatch > 0) load(0, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 1
+        for (int bi = 0; bi < nbatch; ++bi) {
+            const bool more = bi + 1 < nbatch;
+            if (more) load(bi + 1, na, nbv);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int k = 0; k < B; ++k) {
-                ca[k] = na[k];
-                cb[k] = nbv[k];
+            for (int k = 0; k < B; ++k) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ca[k], cb[k], acc, 0, 0, 0);
+            if (more) {
+#pragma unroll
+                for (int k = 0; k < B; ++k) {
+                    ca[k] = na[k];
+                    cb[k] = nbv[k];
+                }
             }
         }
-    }
     }
 
     // sum the ksplit partial tiles
@@ -213,7 +230,7 @@ extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x
     TSPLAT_PROF_BEGIN(tsplat::prof::kConv, stream);
 #define TSPLAT_CONV_LAUNCH(KS, S, UP, G) \
     hipLaunchKernelGGL((conv_f32_kernel<KS, S, UP, G, false, false>), grid, block, lds, stream, p)
-    // ci pairs per batch: 3x3 -> all of a wave's pairs in one shot when it has 3-4, else 2 (or 1);
+    // ci pairs per batch: 3x3 -> all of a wave's 3-4 pairs in one batch, else 2 (1 if it has 1);
     // 1x1 -> 16 once a wave has that many, else 8
     const int per_wave = ((c1 + c2) / 2 + ksplit - 1) / ksplit;
     const bool wide = per_wave >= (ksize == 3 ? 2 : 16);

@@ -365,6 +365,7 @@ _CONV_PACKED: dict = {}
 # Which convolutions go to tsplat_conv2d_f32_fwd: "auto" (the latency-bound ones, see
 # conv2d_direct_ok), "off" (always MIOpen), "all" (every shape the kernel takes; tests / A/B)
 _CONV_MODE = os.environ.get("TSPLAT_CONV", "auto")
+_CONV_KSPLIT = int(os.environ.get("TSPLAT_CONV_KSPLIT", "0"))  # tuning override (tools/bench_conv.py)
 _CONV_MAX_FLOP = 1.5e9  # above this MIOpen's kernels are as fast or faster (tools/bench_conv.py)
 
 
@@ -442,6 +443,7 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
     ksplit = 16
     while ksplit > 1 and (tiles * ksplit > 4096 or pairs < (2 if k == 3 else 16) * ksplit):
         ksplit //= 2
+    ksplit = _CONV_KSPLIT or ksplit
     pb = _f32(bias) if bias is not None else None
     rc = lib.tsplat_conv2d_f32_fwd(_lib.ptr(a), c1, _lib.ptr(b), c2, _lib.ptr(conv_pack_weight(weight)),
                                    _lib.ptr(pb), _lib.ptr(y), n, h, w, co, k, stride, int(upsample), ksplit,
