@@ -241,19 +241,25 @@ mha_cf32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int B, i
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[r] = 0.f;
     float m_run = -INFINITY, l_run = 0.f;
-    for (int k0 = k_lo; k0 < k_hi; k0 += kKT) {
-        // S^T[key 8(r >> 2) + 4h + (r & 3)][query c] = sum_d K[d][key] Q[d][query]
+    // this lane's K column (16 dims) and V row segment (16 keys) of a 32-key tile, the next tile's
+    // loads issued before the current tile's MFMAs (a scheduling barrier keeps them there)
+    auto load_tile = [&](int k0, float* kv, float* vv) {
         const int kr = min(k0 + c, T - 1);
-        float kv[16];
         const float* kp = at(kCfD + 16 * h, kr);
 #pragma unroll
         for (int t = 0; t < 16; ++t) kv[t] = kp[(size_t)t * tl];
-        // V[d = c][keys k0 + 8u + 4h + j], j = 0..3 (clamped past T)
-        float vv[16];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int j = 0; j < 4; ++j) vv[u * 4 + j] = *at(2 * kCfD + c, min(k0 + 8 * u + 4 * h + j, T - 1));
+    };
+    float kv[16], vv[16], nk[16], nv[16];
+    if (k_lo < k_hi) load_tile(k_lo, kv, vv);
+    for (int k0 = k_lo; k0 < k_hi; k0 += kKT) {
+        const bool has_next = k0 + kKT < k_hi;
+        if (has_next) load_tile(k0 + kKT, nk, nv);
+        __builtin_amdgcn_sched_barrier(0);
+        // S^T[key 8(r >> 2) + 4h + (r & 3)][query c] = sum_d K[d][key] Q[d][query]
         floatx16 s;
 #pragma unroll
         for (int r = 0; r < 16; ++r) s[r] = 0.f;
@@ -286,6 +292,13 @@ mha_cf32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int B, i
         for (int u = 0; u < 4; ++u)
 #pragma unroll
             for (int j = 0; j < 4; ++j) o = __builtin_amdgcn_mfma_f32_32x32x2f32(vv[u * 4 + j], s[4 * u + j], o, 0, 0, 0);
+        if (has_next) {
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                kv[t] = nk[t];
+                vv[t] = nv[t];
+            }
+        }
     }
 
     if (h == 0) {
