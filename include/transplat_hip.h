@@ -352,6 +352,12 @@ int tsplat_conv2d_f32_nhwc_fwd(const float* x, int32_t c_in, const float* w_pack
 int tsplat_upsample_bilinear_act_fwd(const float* x, const float* bias, float* y, int32_t n, int32_t c,
                                      int32_t height, int32_t width, int32_t scale, int32_t act, void* stream);
 
+/* Channels-last bilinear resize with align_corners = True to any output size (the DPT head's
+ * F.interpolate calls, reference src/depth_anything_v2/util/blocks.py FeatureFusionBlock.forward and
+ * dpt.py DPTHead.forward): x [n, height, width, c], y [n, out_height, out_width, c], c % 4 == 0. */
+int tsplat_resize_bilinear_nhwc_fwd(const float* x, float* y, int32_t n, int32_t height, int32_t width, int32_t c,
+                                    int32_t out_height, int32_t out_width, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

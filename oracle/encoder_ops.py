@@ -341,6 +341,11 @@ def conv_nhwc_epilogue(conv, x, act: str = "none", res1=None, res2=None):
     return y
 
 
+def resize_bilinear_nhwc(x, size):
+    """reference DPT interpolations: F.interpolate(bilinear, align_corners=True)."""
+    return torch.nn.functional.interpolate(x, size=tuple(int(v) for v in size), mode="bilinear", align_corners=True)
+
+
 def mha(qkv, heads: int, scale: float):
     """DINOv2 Attention core (reference dinov2_layers/attention.py): reshape to heads, softmax
     attention (torch SDPA math), back to [B, N, heads * head_dim]."""
@@ -422,4 +427,4 @@ KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gau
                        "conv_bias_act", "mha", "residual_ln", "depth_softmax", "conv2d_direct_ok",
                        "conv2d_direct", "conv2d_nhwc_ok", "conv2d_nhwc",
                        "upsample_bilinear_act", "qkv_attention_cf",
-                       "conv_nhwc_epilogue")
+                       "conv_nhwc_epilogue", "resize_bilinear_nhwc")

@@ -463,3 +463,18 @@ def test_qkv_attention_cf_kernel(device, vb, heads, views, t):
     ref = E.qkv_attention_cf(qkv, heads, views)
     out = K.qkv_attention_cf(qkv.to(device), heads, views).cpu()
     assert (out - ref).abs().max().item() < 5e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,size", [((2, 128, 9, 9), (18, 18)), ((2, 128, 72, 72), (144, 144)),
+                                        ((2, 64, 144, 144), (252, 252)), ((1, 4, 5, 3), (7, 11))])
+def test_resize_bilinear_nhwc_kernel(device, shape, size):
+    """DPT channels-last bilinear resizes (align_corners) vs the oracle (torch interpolate on CPU)."""
+    from transplat_amd import kernels as K
+
+    x = seeded(shape, 91)
+    ref = E.resize_bilinear_nhwc(x, size)
+    out = K.resize_bilinear_nhwc(x.to(device).contiguous(memory_format=torch.channels_last), size)
+    assert out.is_contiguous(memory_format=torch.channels_last)
+    # fp32 source-coordinate rounding (see the upsample test): 1e-5 of the map's scale
+    assert (out.cpu() - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())

@@ -54,6 +54,35 @@ __global__ void __launch_bounds__(256) bilinear_ac_kernel(const float* __restric
     *reinterpret_cast<float4*>(y + (size_t)rowi * wo + ox0) = make_float4(out[0], out[1], out[2], out[3]);
 }
 
+// Channels-last bilinear resize (align_corners = True, any output size): the DPT head's
+// FeatureFusionBlock / final interpolations on its channels-last maps (reference
+// src/depth_anything_v2/util/blocks.py FeatureFusionBlock.forward, dpt.py DPTHead.forward). One
+// thread = one output pixel x 4 channels (float4 loads / stores along C).
+__global__ void __launch_bounds__(256) bilinear_ac_nhwc_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                               int h, int w, int c4, int ho, int wo, float rh,
+                                                               float rw, int total) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int cc = i % c4;
+    const int pix = i / c4;
+    const int ox = pix % wo;
+    const int t = pix / wo;
+    const int oy = t % ho, n = t / ho;
+    const float hr = rh * (float)oy, wr = rw * (float)ox;
+    const int h0 = (int)hr, w0 = (int)wr;
+    const int h1 = h0 + (h0 < h - 1 ? 1 : 0), w1 = w0 + (w0 < w - 1 ? 1 : 0);
+    const float l1 = hr - (float)h0, l0 = 1.f - l1, m1 = wr - (float)w0, m0 = 1.f - m1;
+    const float4* src = reinterpret_cast<const float4*>(x) + (size_t)n * h * w * c4 + cc;
+    const float4 a = src[((size_t)h0 * w + w0) * c4], b = src[((size_t)h0 * w + w1) * c4];
+    const float4 cq = src[((size_t)h1 * w + w0) * c4], d = src[((size_t)h1 * w + w1) * c4];
+    float4 o;
+    o.x = l0 * (m0 * a.x + m1 * b.x) + l1 * (m0 * cq.x + m1 * d.x);
+    o.y = l0 * (m0 * a.y + m1 * b.y) + l1 * (m0 * cq.y + m1 * d.y);
+    o.z = l0 * (m0 * a.z + m1 * b.z) + l1 * (m0 * cq.z + m1 * d.z);
+    o.w = l0 * (m0 * a.w + m1 * b.w) + l1 * (m0 * cq.w + m1 * d.w);
+    reinterpret_cast<float4*>(y)[i] = o;
+}
+
 }  // namespace upsample
 }  // namespace tsplat
 
@@ -78,6 +107,24 @@ extern "C" int tsplat_upsample_bilinear_act_fwd(const float* x, const float* bia
         case 3: hipLaunchKernelGGL(bilinear_ac_kernel<3>, grid, block, 0, stream, x, bias, y, c, height, width, ho, wo, rh, rw, total4); break;
         default: return TSPLAT_EINVAL;
     }
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_resize_bilinear_nhwc_fwd(const float* x, float* y, int32_t n, int32_t height, int32_t width,
+                                               int32_t c, int32_t out_height, int32_t out_width, void* stream_) {
+    using namespace tsplat::upsample;
+    if (!x || !y || n <= 0 || height <= 0 || width <= 0 || c <= 0 || c % 4 || out_height <= 0 || out_width <= 0)
+        return TSPLAT_EINVAL;
+    if ((uintptr_t)x % 16 || (uintptr_t)y % 16) return TSPLAT_EINVAL;
+    const int64_t total64 = (int64_t)n * out_height * out_width * (c / 4);
+    if (total64 >= (1ll << 31) || (int64_t)n * height * width * c >= (1ll << 31)) return TSPLAT_EINVAL;
+    const int total = (int)total64;
+    const float rh = out_height > 1 ? (float)(height - 1) / (float)(out_height - 1) : 0.f;
+    const float rw = out_width > 1 ? (float)(width - 1) / (float)(out_width - 1) : 0.f;
+    hipStream_t stream = (hipStream_t)stream_;
+    hipLaunchKernelGGL(bilinear_ac_nhwc_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, y,
+                       height, width, c / 4, out_height, out_width, rh, rw, total);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }

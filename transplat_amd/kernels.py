@@ -538,6 +538,20 @@ def conv_nhwc_epilogue(conv, x, act: str = "none", res1=None, res2=None):
     return y
 
 
+def resize_bilinear_nhwc(x, size):
+    """F.interpolate(x, size, mode="bilinear", align_corners=True) of a channels-last fp32 map in one
+    launch (tsplat_resize_bilinear_nhwc_fwd); returns channels-last."""
+    n, c, h, w = x.shape
+    ho, wo = int(size[0]), int(size[1])
+    if x.dtype != torch.float32 or not x.is_contiguous(memory_format=torch.channels_last) or c % 4:
+        raise ValueError("resize_bilinear_nhwc needs a channels-last fp32 map with C % 4 == 0")
+    y = torch.empty((n, c, ho, wo), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    lib = _lib.load()
+    rc = lib.tsplat_resize_bilinear_nhwc_fwd(_lib.ptr(x), _lib.ptr(y), n, h, w, c, ho, wo, _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_resize_bilinear_nhwc_fwd")
+    return y
+
+
 def sh_rotation(rotations, d_sh: int):
     """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
     wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""

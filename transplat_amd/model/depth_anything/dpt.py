@@ -29,6 +29,21 @@ _DPT_DIRECT = os.environ.get("TSPLAT_DPT_DIRECT", "0")
 _DPT_EPI = os.environ.get("TSPLAT_DPT_EPI", "1") != "0"
 
 
+def _resize(x, modifier: dict, align_corners: bool):
+    """F.interpolate(x, **modifier, mode="bilinear", align_corners=...); the channels-last fp32 maps
+    of the head go through one kernel (kernels.resize_bilinear_nhwc) instead of torch's NHWC
+    interpolation kernel."""
+    if (_DPT_EPI and align_corners and x.is_cuda and x.dtype == torch.float32 and x.shape[1] % 4 == 0
+            and x.is_contiguous(memory_format=torch.channels_last) and not torch.is_autocast_enabled("cuda")):
+        if "size" in modifier:
+            size = modifier["size"]
+        else:
+            sf = modifier["scale_factor"]
+            size = (int(x.shape[-2] * sf), int(x.shape[-1] * sf))
+        return kernels.resize_bilinear_nhwc(x, size)
+    return F.interpolate(x, **modifier, mode="bilinear", align_corners=align_corners)
+
+
 class ResidualConvUnit(nn.Module):
     def __init__(self, features, activation, bn):
         super().__init__()
@@ -88,7 +103,7 @@ class FeatureFusionBlock(nn.Module):
             modifier = {"size": self.size}
         else:
             modifier = {"size": size}
-        output = F.interpolate(output, **modifier, mode="bilinear", align_corners=self.align_corners)
+        output = _resize(output, modifier, self.align_corners)
         if _DPT_DIRECT == "1" and kernels.conv2d_nhwc_ok(output, self.out_conv.weight):
             return kernels.conv2d_nhwc(output, self.out_conv.weight, self.out_conv.bias)
         return self.out_conv(output)
@@ -153,8 +168,7 @@ class DPTHead(nn.Module):
         path_1 = s.refinenet1(path_2, layer_1_rn)
         final_out = s.output_conv1(path_1)
         out_feature = final_out.clone().detach()
-        final_out = F.interpolate(final_out, (int(patch_h * 14), int(patch_w * 14)), mode="bilinear",
-                                  align_corners=True)
+        final_out = _resize(final_out, {"size": (int(patch_h * 14), int(patch_w * 14))}, True)
         oc = s.output_conv2
         if (_DPT_EPI and final_out.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")
                 and final_out.is_cuda and final_out.is_contiguous(memory_format=torch.channels_last)):
