@@ -414,10 +414,9 @@ def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsa
     h, w = x.shape[2] * (2 if upsample else 1), x.shape[3] * (2 if upsample else 1)
     npx = x.shape[0] * (h // stride) * (w // stride)
     flop = 2.0 * npx * co * ci * k * k
-    # a 3x3 with few output tiles and a long reduction runs on few CUs (one 16-wave workgroup
-    # per tile): MIOpen is as fast there (bench_conv.py: 2 x 256 -> 128 at 16^2)
-    tiles = ((npx + 31) // 32) * ((co + 31) // 32)
-    return flop <= _CONV_MAX_FLOP and (k == 1 or tiles >= 128 or ci <= 128)
+    # (since the batch loads are scheduled ahead of the MFMAs, the few-tile / long-reduction 3x3s
+    # -- 2 x 256 -> 128 at 16^2 -- also beat MIOpen: 23.5 vs 25.7 us, bench_conv.py)
+    return flop <= _CONV_MAX_FLOP
 
 
 def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: bool = False):
