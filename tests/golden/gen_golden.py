@@ -94,12 +94,65 @@ def install_shims(ref: Path):
 
     torch.cuda.synchronize = lambda *a, **k: None
 
+    # e3nn (absent, unpinned): the build's restatement of matrix_to_angles / wigner_D, so the
+    # adapter fixtures pin A1-A3 exactly and isolate A4 (SH rotation) to that restatement
+    from transplat_amd.misc import sh_rotation as shr
+
+    e3nn = types.ModuleType("e3nn")
+    o3 = types.ModuleType("e3nn.o3")
+    o3.matrix_to_angles = shr.matrix_to_angles
+    o3.wigner_D = shr.wigner_d
+    e3nn.o3 = o3
+    sys.modules.update({"e3nn": e3nn, "e3nn.o3": o3})
+    # omegaconf (absent): src/global_cfg.py only imports DictConfig for an annotation
+    oc = types.ModuleType("omegaconf")
+    oc.DictConfig = dict
+    sys.modules["omegaconf"] = oc
+    install_raster_stub()
+
     sys.path.insert(0, str(ref))
     for name in ("src", "src.model", "src.model.encoder", "src.model.encoder.backbone",
-                 "src.depth_anything_v2"):
+                 "src.depth_anything_v2", "src.dataset", "src.dataset.shims", "src.model.decoder"):
         m = types.ModuleType(name)
         m.__path__ = [str(ref / name.replace(".", "/"))]
         sys.modules[name] = m
+
+
+RASTER_CALLS: list = []
+
+
+def install_raster_stub():
+    """`diff_gaussian_rasterization` (un-vendored CUDA fork) replaced by a RECORDING stub: the
+    reference `render_cuda` (cuda_splatting.py:56-136) runs unchanged and every per-view call
+    stores the GaussianRasterizationSettings and the tensors it hands the rasterizer. The stub
+    renders nothing (zeros): only the call-site conventions are pinned this way."""
+    m = types.ModuleType("diff_gaussian_rasterization")
+
+    class GaussianRasterizationSettings:
+        def __init__(self, **kw):
+            self.__dict__.update(kw)
+
+    class GaussianRasterizer:
+        def __init__(self, raster_settings):
+            self.raster_settings = raster_settings
+
+        def __call__(self, means3D, means2D, shs=None, colors_precomp=None, opacities=None, scales=None,
+                     rotations=None, cov3D_precomp=None):
+            s = self.raster_settings
+            t = lambda x: x.detach().clone().float()
+            RASTER_CALLS.append({
+                "H": s.image_height, "W": s.image_width, "tanfovx": s.tanfovx, "tanfovy": s.tanfovy,
+                "bg": t(s.bg), "scale_modifier": s.scale_modifier, "viewmatrix": t(s.viewmatrix),
+                "projmatrix": t(s.projmatrix), "sh_degree": s.sh_degree, "campos": t(s.campos),
+                "prefiltered": s.prefiltered, "means3D": t(means3D), "shs": t(shs), "opacities": t(opacities),
+                "cov3D_precomp": t(cov3D_precomp), "colors_precomp_is_none": colors_precomp is None,
+            })
+            return (torch.zeros(3, s.image_height, s.image_width),
+                    torch.zeros(means3D.shape[0], dtype=torch.int32))
+
+    m.GaussianRasterizationSettings = GaussianRasterizationSettings
+    m.GaussianRasterizer = GaussianRasterizer
+    sys.modules["diff_gaussian_rasterization"] = m
 
 
 def imp(name):
@@ -351,8 +404,172 @@ def gen_state_dict_keys():
     print(f"wrote state_dict_keys.json: {len(keys)} tensors")
 
 
+def decoder_case():
+    """Decoder inputs for the call-site fixture: 2 scenes x 512 Gaussians (degree-4 SH), 3 target
+    views each on a non-square 72 x 120 image (partial tiles), per-view near != 1 and far,
+    fx != fy, principal point != 0.5, background != 0. Also used by tests/test_decoder_golden.py
+    (the test reads the stored inputs, never regenerates them)."""
+    from transplat_amd import synthetic as S
+
+    g = S.make_gaussians(2, image_shape=(16, 16))  # G = 2 views x 16 x 16 = 512 per scene
+    ext = S.target_extrinsics(S.context_extrinsics(2), (0.25, 0.5, 0.75)).expand(2, 3, 4, 4).clone()
+    ext[1, :, :3, 3] += torch.tensor([0.1, -0.05, 0.2])
+    intr = torch.tensor([[0.9, 0.0, 0.45], [0.0, 1.2, 0.55], [0.0, 0.0, 1.0]]).expand(2, 3, 3, 3).clone()
+    intr[1, :, 0, 0] = 1.1
+    near = torch.tensor([[0.5, 0.7, 1.0], [2.0, 1.5, 1.0]])
+    far = torch.tensor([[50.0, 60.0, 70.0], [80.0, 90.0, 100.0]])
+    bg = torch.tensor([0.1, 0.2, 0.3])
+    return dict(means=g["means"], covariances=g["covariances"], harmonics=g["harmonics"],
+                opacities=g["opacities"], extrinsics=ext, intrinsics=intr, near=near, far=far, bg=bg,
+                image_shape=np.array([72, 120]))
+
+
+def _calls_to_arrays(calls, prefix):
+    out = {}
+    for key in ("viewmatrix", "projmatrix", "campos", "bg", "means3D", "shs", "opacities", "cov3D_precomp"):
+        out[f"{prefix}{key}"] = torch.stack([c[key] for c in calls])
+    for key in ("tanfovx", "tanfovy", "scale_modifier", "sh_degree", "H", "W"):
+        out[f"{prefix}{key}"] = np.array([c[key] for c in calls])
+    out[f"{prefix}prefiltered"] = np.array([c["prefiltered"] for c in calls])
+    out[f"{prefix}colors_precomp_is_none"] = np.array([c["colors_precomp_is_none"] for c in calls])
+    return out
+
+
+def gen_decoder_calls():
+    """What the reference decoder hands its rasterizer: DecoderSplattingCUDA.forward's repeat +
+    render_cuda (decoder_splatting_cuda.py:41-73, cuda_splatting.py:56-136) and the depth path
+    (decoder_splatting_cuda.py:77-95 -> render_depth_cuda, cuda_splatting.py:375-417), recorded
+    per view by the diff_gaussian_rasterization stub."""
+    from einops import rearrange, repeat
+
+    cs = imp("src.model.decoder.cuda_splatting")
+    c = decoder_case()
+    b, v = c["extrinsics"].shape[:2]
+    h, w = (int(x) for x in c["image_shape"])
+    flat = lambda t: rearrange(t, "b v ... -> (b v) ...")
+    RASTER_CALLS.clear()
+    with torch.no_grad():
+        cs.render_cuda(flat(c["extrinsics"]), flat(c["intrinsics"]), flat(c["near"]), flat(c["far"]), (h, w),
+                       repeat(c["bg"], "c -> (b v) c", b=b, v=v),
+                       repeat(c["means"], "b g xyz -> (b v) g xyz", v=v),
+                       repeat(c["covariances"], "b g i j -> (b v) g i j", v=v),
+                       repeat(c["harmonics"], "b g c d_sh -> (b v) g c d_sh", v=v),
+                       repeat(c["opacities"], "b g -> (b v) g", v=v))
+    out = _calls_to_arrays(RASTER_CALLS, "color_")
+    for mode in ("depth", "disparity", "relative_disparity", "log"):
+        RASTER_CALLS.clear()
+        with torch.no_grad():
+            cs.render_depth_cuda(flat(c["extrinsics"]), flat(c["intrinsics"]), flat(c["near"]), flat(c["far"]),
+                                 (h, w), repeat(c["means"], "b g xyz -> (b v) g xyz", v=v),
+                                 repeat(c["covariances"], "b g i j -> (b v) g i j", v=v),
+                                 repeat(c["opacities"], "b g -> (b v) g", v=v), mode=mode)
+        rec = _calls_to_arrays(RASTER_CALLS, "")
+        out[f"{mode}_shs"] = rec["shs"]
+        out[f"{mode}_bg"] = rec["bg"]
+        out[f"{mode}_sh_degree"] = rec["sh_degree"]
+    save("decoder_calls", **{f"in_{k}": t for k, t in c.items()}, **out)
+
+
+class _Stub(torch.nn.Module):
+    def __init__(self, fn):
+        super().__init__()
+        self.fn = fn
+
+    def forward(self, *a, **k):
+        return self.fn(*a, **k)
+
+
+def _reference_encoder(num_views=2):
+    """Reference EncoderTrans (encoder_trans.py:74-137) built under the harness: global cfg set to
+    a test-mode namespace, and its DA-V2 checkpoint load (`torch.load('checkpoints/...')`,
+    absent offline) answered with a freshly built model's state_dict; canonical weights follow."""
+    from types import SimpleNamespace as NS
+
+    gc = imp("src.global_cfg")
+    gc.cfg = NS(mode="test", dataset=NS(view_sampler=NS(num_context_views=num_views)))
+    bbm = imp("src.model.encoder.backbone.backbone_multiview")
+    sys.modules["src.model.encoder.backbone"].BackboneMultiview = bbm.BackboneMultiview
+    et = imp("src.model.encoder.encoder_trans")
+    ga = imp("src.model.encoder.common.gaussian_adapter")
+    dpt = imp("src.depth_anything_v2.dpt")
+    cfg = NS(name="trans", d_feature=128, num_depth_candidates=128, num_surfaces=1, visualizer=None,
+             gaussian_adapter=ga.GaussianAdapterCfg(gaussian_scale_min=0.5, gaussian_scale_max=15.0, sh_degree=4),
+             opacity_mapping=et.OpacityMappingCfg(initial=0.0, final=0.0, warm_up=1), gaussians_per_pixel=1,
+             unimatch_weights_path=None, downscale_factor=4, shim_patch_size=4, multiview_trans_attn_split=2,
+             costvolume_unet_feat_dim=128, costvolume_unet_channel_mult=[1, 1, 1], costvolume_unet_attn_res=[4],
+             depth_unet_feat_dim=32, depth_unet_attn_res=[16], depth_unet_channel_mult=[1, 1, 1, 1, 1],
+             wo_depth_refine=False, wo_cost_volume=False, wo_cost_volume_refine=False)
+    sd = dpt.DepthAnythingV2(encoder="vitb", features=128, out_channels=[96, 192, 384, 768]).state_dict()
+    real_load = torch.load
+    torch.load = lambda *a, **k: sd
+    try:
+        enc = et.EncoderTrans(cfg)
+    finally:
+        torch.load = real_load
+    return enc
+
+
+def adapter_case():
+    """Stage-5 inputs: 2 scenes x 2 views of a non-square 24 x 32 map, rotated cameras (yaw,
+    pitch, roll) so the SH rotation is non-trivial, fx != fy, principal point != 0.5."""
+    from transplat_amd import synthetic as S
+
+    b, v, h, w = 2, 2, 24, 32
+    ctx = S.make_batch(b, image_shape=(h, w))["context"]
+    ext = ctx["extrinsics"].clone()
+    ang = seeded((b, v, 3), 1004, 0.6)
+    for i in range(b):
+        for j in range(v):
+            a, bb, c = ang[i, j].tolist()
+            rz = torch.tensor([[np.cos(a), -np.sin(a), 0], [np.sin(a), np.cos(a), 0], [0, 0, 1]])
+            ry = torch.tensor([[np.cos(bb), 0, np.sin(bb)], [0, 1, 0], [-np.sin(bb), 0, np.cos(bb)]])
+            rx = torch.tensor([[1, 0, 0], [0, np.cos(c), -np.sin(c)], [0, np.sin(c), np.cos(c)]])
+            ext[i, j, :3, :3] = (rz @ ry @ rx).float() @ ext[i, j, :3, :3]
+    intr = ctx["intrinsics"].clone()
+    intr[..., 0, 0], intr[..., 1, 1], intr[..., 0, 2], intr[..., 1, 2] = 0.95, 1.15, 0.47, 0.52
+    ctx.update(extrinsics=ext, intrinsics=intr)
+    raw = seeded((b, v, h * w, 84), 1001)
+    depths = 1.0 + 19.0 * seeded((b, v, h * w, 1, 1), 1002, kind="rand")
+    dens = seeded((b, v, h * w, 1, 1), 1003, kind="rand")
+    return ctx, raw, depths, dens
+
+
+def gen_adapter():
+    """Encoder stage 5 + GaussianAdapter.forward (encoder_trans.py:294-353,
+    gaussian_adapter.py:48-96) run by the reference EncoderTrans.forward with its backbone /
+    DA-V2 / depth predictor replaced by stubs that return the seeded stage-4 outputs."""
+    enc = _reference_encoder().eval()
+    ctx, raw, depths, dens = adapter_case()
+    b, v, _, h, w = ctx["image"].shape
+    enc.backbone = _Stub(lambda *a, **k: (torch.zeros(b * v, 128, h // 4, w // 4),) * 2)
+    enc.da_model = _Stub(lambda x: (torch.rand(x.shape[0], 18, 18), torch.zeros(x.shape[0], 64, 4, 4)))
+    enc.depth_predictor = _Stub(lambda *a, **k: (depths, dens, raw))
+    with torch.no_grad():
+        gs = enc(ctx, global_step=0, deterministic=True)
+    save("adapter", extrinsics=ctx["extrinsics"], intrinsics=ctx["intrinsics"], means=gs.means,
+         covariances=gs.covariances, harmonics=gs.harmonics, opacities=gs.opacities)
+
+
+def gen_encoder():
+    """The whole reference EncoderTrans.forward at 256 x 256 (b = 1, V = 2) with canonical weights:
+    backbone, DA-V2 ViT-B + DPT, depth predictor, adapter (SH rotation via the e3nn restatement).
+    Large outputs are pinned by a row sample."""
+    from transplat_amd import synthetic as S
+
+    enc = canonical_init(_reference_encoder(), seed=61).eval()
+    ctx = S.make_batch(1, image_shape=(256, 256))["context"]
+    with torch.no_grad():
+        gs = enc(ctx, global_step=0, deterministic=True)
+    idx, means = subset_rows(gs.means[0], 2048, 11)
+    save("encoder_256", idx=idx, means=means, covariances=gs.covariances[0][idx], harmonics=gs.harmonics[0][idx],
+         opacities=gs.opacities[0][idx])
+
+
 ALL = {
     "state_dict_keys": gen_state_dict_keys,
+    "decoder_calls": gen_decoder_calls,
+    "adapter": gen_adapter,
+    "encoder": gen_encoder,
     "win_attn": gen_window_attention,
     "mvt": gen_mvt,
     "backbone": gen_backbone,

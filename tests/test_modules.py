@@ -240,3 +240,21 @@ def test_encoder_state_dict_matches_reference_keys():
     ref = json.loads((GOLD / "state_dict_keys.json").read_text())
     mine = {k: list(v.shape) for k, v in EncoderTrans(EncoderTransCfg()).state_dict().items()}
     assert mine == ref
+
+
+@pytest.mark.gpu
+def test_depth_anything_gpu(device):
+    """DA-V2 ViT-B + DPT on the gfx950 path with its default settings (patch-embed GEMM,
+    tsplat_mha_f32_fwd attention, tsplat_residual_ln_fwd, channels-last DPT weights, NHWC conv
+    epilogues and bilinear resizes) against the reference golden (reference dpt.py:177-184)."""
+    from transplat_amd.model.depth_anything.dpt import DepthAnythingV2
+
+    g = np.load(GOLD / "depth_anything.npz")
+    m = canonical_init(DepthAnythingV2(encoder="vitb", features=128, out_channels=[96, 192, 384, 768]),
+                       seed=51).eval().to(device)
+    with torch.no_grad():
+        depth, feat = m(seeded((1, 3, 252, 252), 701).to(device))
+    depth, feat = depth.float().cpu(), feat.float().cpu()
+    assert list(feat.shape) == list(g["feat_shape"])
+    _close(depth, g["depth"], 1e-3)
+    _close(feat.reshape(-1)[torch.tensor(g["feat_idx"])], g["feat_vals"], 1e-3)

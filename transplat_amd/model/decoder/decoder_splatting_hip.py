@@ -25,6 +25,24 @@ class DecoderSplattingHIPCfg:
     check_overflow: bool = True  # sync after each call to surface capacity overflow
 
 
+def depth_fake_color(extrinsics: Tensor, means: Tensor, near: Tensor, far: Tensor,
+                     mode: DepthRenderingMode = "depth") -> Tensor:
+    """Per-view fake colour of the depth render (reference cuda_splatting.py:388-401):
+    extrinsics [V, 4, 4] c2w, means [V, G, 3], near / far [V] -> [V, G]. The "log" mode keeps the
+    reference's minimum(near).maximum(far) order."""
+    cam = torch.einsum("bij,bgj->bgi", extrinsics.inverse(), torch.cat([means, torch.ones_like(means[..., :1])], -1))
+    fake = cam[..., 2]
+    if mode == "disparity":
+        fake = 1 / fake
+    elif mode == "relative_disparity":
+        eps = 1e-10  # depth_to_relative_disparity (reference matching/conversions.py:18-28)
+        disp_near, disp_far = 1 / (near[:, None] + eps), 1 / (far[:, None] + eps)
+        fake = 1 - (1 / (fake + eps) - disp_far) / (disp_near - disp_far + eps)
+    elif mode == "log":
+        fake = fake.minimum(near[:, None]).maximum(far[:, None]).log()
+    return fake
+
+
 class DecoderSplattingHIP(Decoder[DecoderSplattingHIPCfg]):
     background_color: Tensor
 
@@ -85,18 +103,9 @@ class DecoderSplattingHIP(Decoder[DecoderSplattingHIPCfg]):
         b, v, _, _ = extrinsics.shape
         ext = rearrange(extrinsics, "b v i j -> (b v) i j")
         means = repeat(gaussians.means, "b g xyz -> (b v) g xyz", v=v)
-        cam_pts = torch.einsum("bij,bgj->bgi", ext.inverse(), torch.cat([means, torch.ones_like(means[..., :1])], -1))
-        fake = cam_pts[..., 2]
         nr = rearrange(near, "b v -> (b v)")
         fr = rearrange(far, "b v -> (b v)")
-        if mode == "disparity":
-            fake = 1 / fake
-        elif mode == "relative_disparity":
-            eps = 1e-10  # depth_to_relative_disparity (reference matching/conversions.py:18-28)
-            disp_near, disp_far = 1 / (nr[:, None] + eps), 1 / (fr[:, None] + eps)
-            fake = 1 - (1 / (fake + eps) - disp_far) / (disp_near - disp_far + eps)
-        elif mode == "log":
-            fake = fake.minimum(nr[:, None]).maximum(fr[:, None]).log()
+        fake = depth_fake_color(ext, means, nr, fr, mode)
         cams = prepare_cameras(ext, rearrange(intrinsics, "b v i j -> (b v) i j"), nr, fr,
                                torch.zeros((b * v, 3), device=ext.device))
         color, _ = rasterize(

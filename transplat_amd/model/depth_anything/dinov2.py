@@ -2,8 +2,9 @@
 dinov2_layers/*): patch 14, LayerScale blocks, bicubic position-embedding interpolation with the
 0.1 offset, `get_intermediate_layers` with the final LayerNorm. Parameter names follow the
 reference (`pretrained.{cls_token,pos_embed,mask_token,patch_embed.proj,blocks.{i}.{norm1,attn.
-{qkv,proj},ls1.gamma,norm2,mlp.{fc1,fc2},ls2.gamma},norm}`). Attention runs through PyTorch SDPA
-(aotriton / CK flash attention on gfx950) instead of xformers.
+{qkv,proj},ls1.gamma,norm2,mlp.{fc1,fc2},ls2.gamma},norm}`). On the GPU, attention runs the
+hand-written exact-fp32 MFMA kernel tsplat_mha_f32_fwd (kernels.mha) instead of xformers, and the
+pre-norm residual steps run tsplat_residual_ln_fwd.
 """
 from __future__ import annotations
 
