@@ -100,10 +100,15 @@ def test_window_attention_kernel_large_logits(device):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hw,b", [(16, 1), (32, 2)])
-def test_uv_coarse_kernel(device, hw, b):
+@pytest.mark.parametrize("hw,b,variant", [(16, 1, "dedup"), (32, 2, "dedup"), (64, 1, "dedup"), (64, 2, "dedup"),
+                                          (16, 1, "direct"), (64, 1, "direct")])
+def test_uv_coarse_kernel(device, monkeypatch, hw, b, variant):
+    """Corner-deduplicated coarse correlation (default) and the sample-then-dot kernel
+    (TSPLAT_UV_COARSE_DIRECT=1), incl. the production 64 x 64 map at b = 1 and 2."""
     from transplat_amd import kernels as K
 
+    if variant == "direct":
+        monkeypatch.setenv("TSPLAT_UV_COARSE_DIRECT", "1")
     intr, pose, disp = _cams(b, hw)
     feat = seeded((b, 2, hw * hw, 128), 31)
     ref = E.uv_coarse(feat, intr, pose, disp, hw, hw)

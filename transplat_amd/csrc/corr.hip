@@ -18,6 +18,8 @@
 #include "common.h"
 #include "prof.h"
 
+#include <cstdlib>
+
 namespace tsplat {
 namespace corr {
 
@@ -149,6 +151,189 @@ uv_coarse_kernel(Geo g, const float* __restrict__ feat, const float* __restrict_
             if ((int)threadIdx.x < cnt) out[((size_t)n * HW + p) * g.D + base + threadIdx.x] = s_out[threadIdx.x];
             __syncthreads();
         }
+    }
+}
+
+// ---- coarse, corner-deduplicated: corr(p, d) = sum_corner w_corner <F_other[corner], key_p> / sqrt(C)
+// The D samples of a pixel lie on its epipolar segment in the other view and are uniform in
+// disparity, so consecutive samples sit ~0.5 px apart and their bilinear corners repeat: at the
+// production shape 512 corner reads (128 depths x 4) per pixel touch only ~130 distinct feature
+// rows. One wave per query pixel:
+//   1. each lane places S = D / 64 samples and marks their valid corners in a per-wave LDS bitmap
+//      over the other view's H*W pixels (ds_or);
+//   2. a wave scan of the bitmap's popcounts ranks the distinct corners and lists them;
+//   3. each distinct corner's 128-wide dot with the own feature is computed ONCE (4 lanes per
+//      corner, 32 channels = one 128-B line per lane, two xor-shuffles) into LDS;
+//   4. each lane combines its samples' 4 weighted corner dots (rank = prefix + popcount below).
+// On-chip feature traffic drops from 2 KB to ~0.5 KB per (pixel, depth) pair's share; the sum
+// order differs from the sample-then-dot form only by rounding (tests hold 1e-4 absolute).
+constexpr int kDedupWaves = 4;
+constexpr int kDedupMaxS = 4;  // D <= 256
+
+template <int S>
+__global__ void __launch_bounds__(kDedupWaves * 64)
+uv_coarse_dedup_kernel(Geo g, int nw, const float* __restrict__ feat, const float* __restrict__ cams,
+                       const float* __restrict__ disp, float* __restrict__ out, int diag) {
+    extern __shared__ unsigned smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = blockIdx.y;
+    const int HW = g.H * g.W;
+    const int p = blockIdx.x * kDedupWaves + wave;
+    const bool active = p < HW;
+    unsigned* bm = smem + (size_t)wave * (2 * nw + 8 * g.D);
+    unsigned* pre = bm + nw;
+    int* list = reinterpret_cast<int*>(pre + nw);
+    float* dots = reinterpret_cast<float*>(list + 4 * g.D);
+    // own feature (the dot operand: 8 lanes per corner, lane `sub` holds channels i*32 + sub*4 .. +3)
+    // and this lane's disparities are loaded first: their latency overlaps sampling and ranking
+    const int sub = lane & 7;
+    const int pc = active ? p : 0;
+    float4 key[4];
+    {
+        const float4* own = reinterpret_cast<const float4*>(feat + ((size_t)n * HW + pc) * kC) + sub;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) key[i] = own[8 * i];
+    }
+    const float* c = cam_ptr(cams, g, n);
+    const int b = n >> 1, v = n & 1;
+    const float* dsp = disp + (size_t)(v * g.B + b) * g.D;
+    float dv[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) dv[s] = dsp[min(lane + 64 * s, g.D - 1)];
+    for (int i = lane; i < nw; i += 64) bm[i] = 0u;
+    __syncthreads();
+
+    // 1. samples -> bilinear corners (mmcv zero padding), marked in the bitmap. A corner that the
+    //    previous depth sample (lane - 1, or lane 63 of the previous slice) also touches is not
+    //    re-marked: consecutive samples share most corners, and same-word LDS atomics serialise.
+    int cidx[S][4];
+    float cw[S][4];
+    const float fw = (float)g.W, fh = (float)g.H;
+    float ray[3];
+    pixel_ray(c, (float)(pc % g.W), (float)(pc / g.W), ray);
+    int prev_cell = -1;  // previous sample's (y0 * W + x0) + (W + 1) offset code, -1 = none
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int d = lane + 64 * s;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            cidx[s][k] = -1;
+            cw[s][k] = 0.f;
+        }
+        int y0 = 0, x0 = 0, cell = -1;
+        if (active && d < g.D) {
+            float rx, ry;
+            sample_ref(c, g, ray, dv[s], rx, ry);
+            const float xim = rx * fw - 0.5f, yim = ry * fh - 0.5f;
+            if (yim > -1.0f && xim > -1.0f && yim < fh && xim < fw) {
+                const float fy = floorf(yim), fx = floorf(xim);
+                y0 = (int)fy;
+                x0 = (int)fx;
+                const int y1 = y0 + 1, x1 = x0 + 1;
+                const float ly = yim - fy, lx = xim - fx, hy = 1.0f - ly, hx = 1.0f - lx;
+                if (y0 >= 0 && x0 >= 0) { cidx[s][0] = y0 * g.W + x0; cw[s][0] = hy * hx; }
+                if (y0 >= 0 && x1 <= g.W - 1) { cidx[s][1] = y0 * g.W + x1; cw[s][1] = hy * lx; }
+                if (y1 <= g.H - 1 && x0 >= 0) { cidx[s][2] = y1 * g.W + x0; cw[s][2] = ly * hx; }
+                if (y1 <= g.H - 1 && x1 <= g.W - 1) { cidx[s][3] = y1 * g.W + x1; cw[s][3] = ly * lx; }
+                cell = (y0 + 1) * (g.W + 2) + (x0 + 1);  // y0, x0 >= -1
+            }
+        }
+        // the previous depth sample's cell: lane - 1 of this slice, lane 63 of the previous one
+        int pcell = __shfl_up(cell, 1, 64);
+        const int last = __shfl(cell, 63, 64);
+        if (lane == 0) pcell = prev_cell;
+        prev_cell = last;
+        const int py0 = pcell >= 0 ? pcell / (g.W + 2) - 1 : -100, px0 = pcell >= 0 ? pcell % (g.W + 2) - 1 : -100;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int ci = cidx[s][k];
+            if (ci < 0) continue;
+            const int yy = y0 + (k >> 1), xx = x0 + (k & 1);
+            const bool seen = yy >= py0 && yy <= py0 + 1 && xx >= px0 && xx <= px0 + 1;
+            if (!seen) atomicOr(&bm[ci >> 5], 1u << (ci & 31));
+        }
+    }
+    __syncthreads();
+    if (diag == 1) { if (active) out[((size_t)n * HW + p) * g.D + lane] = (float)bm[lane] + key[0].x; return; }
+
+    // 2. rank the distinct corners. Lane l tests word w0 + (l >> 5), bit l & 31; only non-empty
+    //    words are visited (a uniform loop over the ballot of non-empty words).
+    int total = 0;
+    for (int wb = 0; wb < nw; wb += 64) {
+        const int wl = wb + lane;
+        const unsigned mine = wl < nw ? bm[wl] : 0u;
+        unsigned long long nz = __ballot(mine != 0u);
+        while (nz) {
+            const int w = wb + __ffsll((long long)nz) - 1;
+            nz &= nz - 1ull;
+            const unsigned bits = bm[w];
+            const int l = lane & 31;
+            if (lane < 32) {
+                if ((bits >> l) & 1u) list[total + __popc(bits & ((1u << l) - 1u))] = w * 32 + l;
+                if (lane == 0) pre[w] = (unsigned)total;
+            }
+            total += __popc(bits);
+        }
+    }
+    __syncthreads();
+    if (diag == 2) { if (active) out[((size_t)n * HW + p) * g.D + lane] = (float)list[lane] + key[0].x; return; }
+
+    // 3. one dot per distinct corner: 8 lanes per corner (each load instruction covers a full
+    //    128-B line of 8 rows), 8 corners per pass, the next pass's rows in flight
+    if (active) {
+        const float4* other = reinterpret_cast<const float4*>(feat + (size_t)(n ^ 1) * HW * kC) + sub;
+        const int jend = (total + 7) & ~7;  // same trip count for every lane (shuffles)
+        auto load = [&](int jj, float4* x) {
+            const float4* row = other + (size_t)(jj < total ? list[jj] : 0) * (kC / 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = row[8 * i];
+        };
+        auto dot = [&](int jj, const float4* x) {
+            float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a0 += x[i].x * key[i].x;
+                a1 += x[i].y * key[i].y;
+                a0 += x[i].z * key[i].z;
+                a1 += x[i].w * key[i].w;
+            }
+            float acc = a0 + a1;
+            acc += __shfl_xor(acc, 1, 8);
+            acc += __shfl_xor(acc, 2, 8);
+            acc += __shfl_xor(acc, 4, 8);
+            if (jj < total && sub == 0) dots[jj] = acc;
+        };
+        float4 xa[4], xb[4];
+        int j = lane >> 3;
+        if (j < jend) load(j, xa);
+        for (; j < jend; j += 16) {
+            if (j + 8 < jend) load(j + 8, xb);
+            dot(j, xa);
+            if (j + 16 < jend) load(j + 16, xa);
+            if (j + 8 < jend) dot(j + 8, xb);
+        }
+    }
+    __syncthreads();
+    if (diag == 3) { if (active) out[((size_t)n * HW + p) * g.D + lane] = dots[lane]; return; }
+    if (!active) return;
+
+    // 4. each sample = its corners' weighted dots (rank = word prefix + popcount below the bit)
+    const float inv_sqrt_c = 1.0f / sqrtf((float)kC);
+    float* o = out + ((size_t)n * HW + p) * g.D;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int d = lane + 64 * s;
+        if (d >= g.D) continue;
+        float val = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int ci = cidx[s][k];
+            if (ci < 0) continue;
+            const unsigned wd = bm[ci >> 5];
+            const int rank = (int)pre[ci >> 5] + __popc(wd & ((1u << (ci & 31)) - 1u));
+            val += cw[s][k] * dots[rank];
+        }
+        o[d] = val * inv_sqrt_c;
     }
 }
 
@@ -307,9 +492,26 @@ extern "C" int tsplat_uv_coarse_fwd(const float* feat, const float* cams, const 
         return TSPLAT_EINVAL;
     Geo g{batch, height, width, depths};
     hipStream_t stream = (hipStream_t)stream_;
+    const int hw = height * width;
+    const int nw = (hw + 31) / 32;
+    const size_t lds = (size_t)kDedupWaves * (2 * nw + 8 * depths) * sizeof(unsigned);
+    const int S = (depths + 63) / 64;
     TSPLAT_PROF_BEGIN(prof::kUvCoarse, stream);
-    hipLaunchKernelGGL(uv_coarse_kernel, dim3(height * width, 2 * batch), dim3(kThreads), 0, stream,
-                       g, feat, cams, disp, out);
+    const char* denv = getenv("TSPLAT_CORR_DIAG");  // diagnostic builds: stop after phase 1 / 2 / 3
+    const int diag = denv ? atoi(denv) : 0;
+    const char* env = getenv("TSPLAT_UV_COARSE_DIRECT");  // A/B switch: the sample-then-dot kernel
+    if (S <= kDedupMaxS && lds <= 64 * 1024 && !(env && env[0] == '1')) {
+        const dim3 grid(ceil_div(hw, kDedupWaves), 2 * batch), block(kDedupWaves * 64);
+        switch (S) {
+            case 1: hipLaunchKernelGGL(uv_coarse_dedup_kernel<1>, grid, block, lds, stream, g, nw, feat, cams, disp, out, diag); break;
+            case 2: hipLaunchKernelGGL(uv_coarse_dedup_kernel<2>, grid, block, lds, stream, g, nw, feat, cams, disp, out, diag); break;
+            case 3: hipLaunchKernelGGL(uv_coarse_dedup_kernel<3>, grid, block, lds, stream, g, nw, feat, cams, disp, out, diag); break;
+            default: hipLaunchKernelGGL(uv_coarse_dedup_kernel<4>, grid, block, lds, stream, g, nw, feat, cams, disp, out, diag); break;
+        }
+    } else {
+        hipLaunchKernelGGL(uv_coarse_kernel, dim3(hw, 2 * batch), dim3(kThreads), 0, stream, g, feat, cams, disp,
+                           out);
+    }
     TSPLAT_PROF_END(prof::kUvCoarse, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
