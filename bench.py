@@ -70,6 +70,29 @@ def init_dist():
     return world, rank, local
 
 
+def timed_steps(step, steps: int, world: int, sync, device) -> float:
+    """EXACTLY `steps` calls of `step` bracketed by sync + barrier on both sides; the MAX of the
+    ranks' wall times (every rank returns the same value). `sync` waits for the device
+    (torch.cuda.synchronize on the GPU). The only collectives are the barriers and this one
+    all-reduce of a scalar (RCCL on GPUs, gloo in the CPU tests)."""
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def raster_bytes_per_view(g: int, d_sh: int, h: int, w: int) -> int:
     # means 12 + cov 24 (upper triangle of the 3x3) + SH 3*d_sh*4 + opacity 4, image 3*4 per pixel
     return g * (12 + 24 + 3 * d_sh * 4 + 4) + h * w * 12
@@ -141,9 +164,21 @@ def e2e_roofline_info(kernel: str, batch: int, dense_dtype: str = "fp32") -> dic
     raise ValueError(kernel)
 
 
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
 def cpu_baseline_e2e(model, seconds: float):
     """The same test_step on the host: the build's modules with the oracle's CPU restatements in
-    place of the HIP kernels and the C oracle rasterizer (kind 'port'), on >= 1 scene."""
+    place of the HIP kernels and the C oracle rasterizer (kind 'port'), on >= 1 scene. Torch and the
+    rasterizer's OpenMP both use torch.get_num_threads() threads (the process's CPU share: 16 on
+    the GPU box, where OMP_NUM_THREADS is set by the pool)."""
     import copy
 
     from oracle import encoder_ops as E
@@ -156,6 +191,8 @@ def cpu_baseline_e2e(model, seconds: float):
     for n in saved:
         setattr(kernels, n, getattr(E, n))
     threads = torch.get_num_threads()
+    oracle_raster.set_threads(threads)
+    t_raster = 0.0
     try:
         enc = copy.deepcopy(model.encoder).float().cpu()
         enc.cfg.dense_dtype = "fp32"
@@ -166,7 +203,9 @@ def cpu_baseline_e2e(model, seconds: float):
                 g = enc(batch["context"], 0, deterministic=True)
             t = batch["target"]
             cams = prepare_cameras(t["extrinsics"][0], t["intrinsics"][0], t["near"][0], t["far"][0], torch.zeros(3, 3))
+            tr = time.perf_counter()
             oracle_raster.render(g.means, g.covariances, g.harmonics, g.opacities, cams, (256, 256), 3, 3)
+            t_raster += time.perf_counter() - tr
             n_views += 3
             el = time.perf_counter() - t0
             if el >= seconds:
@@ -178,33 +217,46 @@ def cpu_baseline_e2e(model, seconds: float):
         "value": n_views / el, "unit": "views/s", "cores": threads, "kind": "port",
         "sample": f"{n_views // 3} scene(s) x 3 views, 256x256: the build's encoder modules on CPU (torch, "
                   f"{threads} threads) with oracle/encoder_ops.py restatements for the HIP kernels + "
-                  f"oracle/raster_ref.c (1 thread), {el:.1f} s, nproc={os.cpu_count()}",
+                  f"oracle/raster_ref.c (OpenMP, {threads} threads; raster {t_raster / n_views * 1e3:.0f} ms/view), "
+                  f"{el:.1f} s, host {cpu_model()}, nproc={os.cpu_count()}",
     }
 
 
 def cpu_baseline_raster(cpu_inputs, seconds: float):
-    """Oracle C rasterizer (scalar, 1 thread) on as many views as fit `seconds` (>= 1)."""
+    """Oracle C rasterizer on as many views as fit `seconds` (>= 1), with OpenMP over tiles at
+    torch.get_num_threads() threads; a single-thread pass on a quarter of the budget is reported
+    beside it."""
     from oracle import raster as oracle_raster
 
     g, cams, hw, vps = cpu_inputs
     one = {k: t[:1] for k, t in g.items()}
-    n_views, t0 = 0, time.perf_counter()
-    while True:
-        i = n_views % vps
-        sub = type(cams)(*(getattr(cams, f)[i : i + 1] for f in cams.__dataclass_fields__))
-        oracle_raster.render(one["means"], one["covariances"], one["harmonics"], one["opacities"], sub, hw, 1,
-                             min(3, int(round(one["harmonics"].shape[-1] ** 0.5)) - 1))
-        n_views += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
+    deg = min(3, int(round(one["harmonics"].shape[-1] ** 0.5)) - 1)
+
+    def run(budget):
+        n_views, t0 = 0, time.perf_counter()
+        while True:
+            i = n_views % vps
+            sub = type(cams)(*(getattr(cams, f)[i : i + 1] for f in cams.__dataclass_fields__))
+            oracle_raster.render(one["means"], one["covariances"], one["harmonics"], one["opacities"], sub, hw, 1, deg)
+            n_views += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return n_views, el
+
+    threads = torch.get_num_threads()
+    oracle_raster.set_threads(1)
+    n1, el1 = run(seconds / 4)
+    oracle_raster.set_threads(threads)
+    n_views, el = run(seconds)
     return {
         "value": n_views / el,
         "unit": "views/s",
-        "cores": 1,
+        "cores": threads,
         "kind": "port",
-        "sample": f"{n_views} views of one synthetic 256x256 scene (G=131072) through oracle/raster_ref.c, "
-                  f"{el:.1f} s, host {platform.processor() or platform.machine()}, nproc={os.cpu_count()}",
+        "value_1thread": n1 / el1,
+        "sample": f"{n_views} views of one synthetic 256x256 scene (G=131072) through oracle/raster_ref.c "
+                  f"(OpenMP over Gaussians / tiles, {threads} threads; 1 thread: {n1 / el1:.2f} views/s), "
+                  f"{el:.1f} s, host {cpu_model()}, nproc={os.cpu_count()}",
     }
 
 
@@ -233,21 +285,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device if dist.get_backend() == "nccl" else "cpu", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_steps(step, args.steps, world, torch.cuda.synchronize, device)
     from transplat_amd.model.decoder.hip_splatting import check_status
 
     check_status(device)  # any capacity overflow during the timed steps invalidates the run

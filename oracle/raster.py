@@ -30,8 +30,19 @@ def load():
         f = lib.tsplat_ref_raster_view
         f.restype = ctypes.c_long
         f.argtypes = [ctypes.c_int] * 5 + [ctypes.c_void_p] * 12
+        lib.tsplat_ref_set_threads.argtypes = [ctypes.c_int]
+        lib.tsplat_ref_set_threads.restype = None
+        lib.tsplat_ref_max_threads.restype = ctypes.c_int
         _lib = lib
     return _lib
+
+
+def set_threads(n: int) -> int:
+    """OpenMP threads of the C rasterizer (images are bit-identical for any count); returns the
+    count in effect."""
+    lib = load()
+    lib.tsplat_ref_set_threads(int(n))
+    return int(lib.tsplat_ref_max_threads())
 
 
 def _p(a: np.ndarray):

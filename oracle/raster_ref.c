@@ -29,6 +29,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define TILE 16
 
@@ -138,6 +141,24 @@ static int cmp_u64(const void* a, const void* b) {
  * campos[3], tanfov[2], bg[3], scale[2] = (s, s*s). Outputs out_color[3*H*W], out_radii[G].
  * Returns the number of (gaussian, tile) instances, or -1 on allocation failure.
  */
+/* OpenMP over Gaussians (preprocess) and tiles (sort, blend): every thread writes disjoint
+ * outputs, so the image is bit-identical for any thread count. n <= 0 leaves the default. */
+void tsplat_ref_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}
+
+int tsplat_ref_max_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
 long tsplat_ref_raster_view(int G, int H, int W, int M, int deg, const float* means,
                             const float* cov, const float* shs, const float* opacity,
                             const float* vm, const float* pm, const float* campos,
@@ -150,6 +171,7 @@ long tsplat_ref_raster_view(int G, int H, int W, int M, int deg, const float* me
     long* counts = (long*)calloc((size_t)T + 1, sizeof(long));
     if (!rec || !counts) return -1;
 
+#pragma omp parallel for schedule(static)
     for (int g = 0; g < G; ++g) {
         int radius = 0;
         out_radii[g] = 0;
@@ -216,6 +238,12 @@ long tsplat_ref_raster_view(int G, int H, int W, int M, int deg, const float* me
         q->b = rgb[2];
         q->depth = vz;
         out_radii[g] = radius;
+    }
+    /* per-tile counts (serial: cheap, and keeps the parallel preprocess free of shared writes) */
+    for (int g = 0; g < G; ++g) {
+        if (out_radii[g] <= 0) continue;
+        int x0, y0, x1, y1;
+        get_rect(rec[g].px, rec[g].py, out_radii[g], tiles_x, tiles_y, &x0, &y0, &x1, &y1);
         for (int yy = y0; yy < y1; ++yy)
             for (int xx = x0; xx < x1; ++xx) counts[yy * tiles_x + xx]++;
     }
@@ -242,9 +270,11 @@ long tsplat_ref_raster_view(int G, int H, int W, int M, int deg, const float* me
                 keys[offs[t] + cur[t]++] = key;
             }
     }
+#pragma omp parallel for schedule(dynamic)
     for (int t = 0; t < T; ++t) qsort(keys + offs[t], (size_t)(offs[t + 1] - offs[t]), 8, cmp_u64);
 
     const size_t hwn = (size_t)H * W;
+#pragma omp parallel for schedule(dynamic)
     for (int t = 0; t < T; ++t) {
         const int tx = t % tiles_x, ty = t / tiles_x;
         for (int ly = 0; ly < TILE; ++ly)

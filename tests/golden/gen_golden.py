@@ -11,7 +11,15 @@ package __init__ files are not executed) and import shims for packages absent fr
     mmcv 2.1.0 (grid_sample bilinear, zeros padding, align_corners=False);
   * `jaxtyping`: annotation-only stub;  `cv2`, `torchvision.transforms`: import-only stubs
     (used by DepthAnythingV2.image2tensor, never on the forward path);
-  * `torch.cuda.synchronize` = no-op (called unconditionally by the reference).
+  * `torch.cuda.synchronize` = no-op (called unconditionally by the reference);
+  * `e3nn.o3`: the build's restatement of matrix_to_angles / wigner_D (e3nn absent, unpinned), so
+    the adapter / encoder fixtures pin everything but the SH rotation to the reference itself;
+  * `omegaconf`: DictConfig only (src/global_cfg.py annotation); the global cfg is set to a
+    test-mode namespace, and EncoderTrans's DA-V2 checkpoint load is answered with a freshly built
+    model's state_dict (canonical weights are filled in afterwards);
+  * `diff_gaussian_rasterization` and `plyfile`: RECORDING stubs (the CUDA rasterizer fork and the
+    PLY writer are absent): the reference decoder / export code runs unchanged and what it hands
+    them (settings, tensors, the vertex array) is stored.
 Reference modules are imported by path from --ref and the script refuses to run without it, so
 no reference source or bytecode is written into the repo: only inputs' seeds and the outputs
 (as .npz data) are committed next to this script.
@@ -109,6 +117,7 @@ def install_shims(ref: Path):
     oc.DictConfig = dict
     sys.modules["omegaconf"] = oc
     install_raster_stub()
+    install_plyfile_stub()
 
     sys.path.insert(0, str(ref))
     for name in ("src", "src.model", "src.model.encoder", "src.model.encoder.backbone",
@@ -119,6 +128,29 @@ def install_shims(ref: Path):
 
 
 RASTER_CALLS: list = []
+PLY_ELEMENTS: list = []
+
+
+def install_plyfile_stub():
+    """`plyfile` (absent) replaced by a recording stub: PlyElement.describe keeps the structured
+    vertex array the reference export builds; PlyData.write writes nothing."""
+    m = types.ModuleType("plyfile")
+
+    class PlyElement:
+        @staticmethod
+        def describe(elements, name):
+            PLY_ELEMENTS.append((name, elements.copy()))
+            return name
+
+    class PlyData:
+        def __init__(self, elements):
+            self.elements = elements
+
+        def write(self, path):
+            pass
+
+    m.PlyElement, m.PlyData = PlyElement, PlyData
+    sys.modules["plyfile"] = m
 
 
 def install_raster_stub():
@@ -565,8 +597,34 @@ def gen_encoder():
          opacities=gs.opacities[0][idx])
 
 
+def gen_ply():
+    """Reference export_ply (src/model/ply_export.py:26-92) on 256 seeded Gaussians; the vertex
+    array it hands PlyElement.describe is stored field by field."""
+    pe = imp("src.model.ply_export")
+    g = 256
+    ext = torch.eye(4)
+    ang = seeded((3,), 1101, 0.5)
+    from scipy.spatial.transform import Rotation as Rot
+
+    ext[:3, :3] = torch.tensor(Rot.from_rotvec(ang.numpy()).as_matrix(), dtype=torch.float32)
+    ext[:3, 3] = seeded((3,), 1102)
+    means = seeded((g, 3), 1103, 3.0)
+    scales = seeded((g, 3), 1104, kind="rand") * 0.2 + 0.01
+    rots = seeded((g, 4), 1105)
+    rots = rots / rots.norm(dim=-1, keepdim=True)
+    harm = seeded((g, 3, 25), 1106)
+    opac = seeded((g,), 1107, kind="rand")
+    PLY_ELEMENTS.clear()
+    pe.export_ply(ext, means, scales, rots, harm, opac, Path("/tmp/unused.ply"))
+    name, el = PLY_ELEMENTS[0]
+    assert name == "vertex"
+    save("ply_export", extrinsics=ext, means=means, scales=scales, rotations=rots, harmonics=harm,
+         opacities=opac, names=np.array(el.dtype.names), **{f"v_{n}": el[n] for n in el.dtype.names})
+
+
 ALL = {
     "state_dict_keys": gen_state_dict_keys,
+    "ply": gen_ply,
     "decoder_calls": gen_decoder_calls,
     "adapter": gen_adapter,
     "encoder": gen_encoder,

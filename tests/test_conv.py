@@ -41,6 +41,26 @@ def test_oracle_conv2d_direct_matches_cat_and_interpolate():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("k", [3, 1])
+def test_conv2d_direct_nonfinite_corner(device, k):
+    """Zero-padding semantics with a non-finite input: an Inf at pixel (0, 0) reaches exactly the
+    outputs whose receptive field holds it (as torch's conv2d); the kernel's masked padding taps
+    (clamped loads of that same pixel) contribute +0, not Inf * 0 = NaN, everywhere else."""
+    from transplat_amd import kernels as K
+
+    x = seeded((1, 32, 16, 16), 21)
+    x[0, 3, 0, 0] = float("inf")
+    wt = seeded((32, 32, k, k), 22) * (1.0 / 32**0.5)
+    ref = E.conv2d_direct(x, wt, None, 1)
+    out = K.conv2d_direct(x.to(device), wt.to(device), None, 1).cpu()
+    fin = torch.isfinite(ref)
+    assert (~fin).any() and fin.any()
+    assert torch.equal(torch.isfinite(out), fin)
+    err = (out[fin] - ref[fin]).abs().max().item() / ref[fin].abs().max().item()
+    assert err < 2e-5, err
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,c1,c2,h,w,cout,k,stride,up,has_bias", CASES)
 def test_conv2d_direct_kernel(device, n, c1, c2, h, w, cout, k, stride, up, has_bias):
     from transplat_amd import kernels as K

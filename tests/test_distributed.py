@@ -93,3 +93,41 @@ def test_evaluate_cli_small_index(device):
     summary = json.loads(out.stdout.strip().splitlines()[-1])
     assert summary["scenes"] == 2 and summary["views"] == 6
     assert summary["psnr"] == summary["psnr"]  # finite
+
+
+def _bench_worker(rank, world, port, out):
+    """bench.py's N > 1 timing path (timed_steps) on gloo: rank r's step sleeps (r + 1) x 20 ms, so
+    the max-over-ranks time must be rank 1's and both ranks must report it."""
+    import sys
+    import time
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    calls = []
+
+    def step():
+        calls.append(1)
+        time.sleep(0.02 * (rank + 1))
+
+    el = bench.timed_steps(step, 5, world, lambda: None, torch.device("cpu"))
+    out.put((rank, len(calls), el))
+    dist.destroy_process_group()
+
+
+def test_bench_timed_steps_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [5, 5]  # exactly `steps` calls per rank
+    assert res[0][2] == res[1][2]  # every rank reports the max
+    assert 0.2 <= res[1][2] < 0.6  # rank 1: 5 x 40 ms

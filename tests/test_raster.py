@@ -138,6 +138,22 @@ def _target_cams(batch, hw, bg=None):
     return prepare_cameras(ext, K, t["near"].reshape(-1), t["far"].reshape(-1), bgv)
 
 
+def test_oracle_thread_count_invariant():
+    """The OpenMP oracle (the CPU baseline) renders bit-identical images for any thread count."""
+    hw = (64, 64)
+    g = S.make_gaussians(1, image_shape=hw)
+    cams = _target_cams(S.make_batch(1, image_shape=hw), hw)
+    args = (g["means"], g["covariances"], g["harmonics"], g["opacities"], cams, hw, 3, 3)
+    before = oracle_raster.set_threads(1)
+    try:
+        c1, r1, n1 = oracle_raster.render(*args)
+        oracle_raster.set_threads(4)
+        c4, r4, n4 = oracle_raster.render(*args)
+    finally:
+        oracle_raster.set_threads(before)
+    assert np.array_equal(c1, c4) and np.array_equal(r1, r4) and n1 == n4
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("deg", [3, 4, 0])
 def test_raster_small_scene_parity(device, deg):

@@ -3,10 +3,13 @@ transformer's shape at 256x256 input). Prints average µs per call (HIP events) 
 Variants via env TSPLAT_WINATTN / TSPLAT_WINATTN_KSPLIT (see csrc/winattn.hip)."""
 import argparse
 import os
+import sys
+from pathlib import Path
 
 import torch
 
-from transplat_amd import _lib, kernels
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+from transplat_amd import _lib, kernels  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=2)

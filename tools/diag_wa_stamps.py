@@ -1,6 +1,6 @@
 """Segment shares of the key-pair window-attention loop from a TSPLAT_WA_STAMP diagnostic build.
 
-    bash tools/build_ablation.sh && (stamp build: see tools/_stamp_build.sh)
+    bash tools/build_ablation.sh && (stamp build: see tools/stamp_build.sh)
     TSPLAT_LIB=build/abl/lib_stamp.so TSPLAT_WINATTN=pair TSPLAT_WINATTN_KSPLIT=2 python tools/diag_wa_stamps.py --batch 16
 
 Per-wave s_memtime sums (100 MHz... counted in s_memtime units) per segment, averaged over waves."""

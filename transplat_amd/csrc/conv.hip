@@ -106,10 +106,13 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
             for (int t = 0; t < T; ++t) {
                 const float av = wq[t * wtap];
                 const float bv = RELU ? fmaxf(src[off[t]], 0.f) : src[off[t]];
-                // masks as multipliers (exact: x * 1 = x, finite x * 0 = 0), so the loaded values
-                // are always used and the compiler cannot sink the loads into branches
-                a[g * T + t] = av * (ok ? 1.f : 0.f);
-                b[g * T + t] = bv * (ok && ((vmask >> t) & 1) ? 1.f : 0.f);
+                // masks applied to the bits (an AND with 0 or ~0: exactly +0 for a masked operand even
+                // when the clamped address holds an Inf / NaN, where a multiply by 0 would give NaN),
+                // so the loaded values are always used and the loads cannot sink into branches
+                const unsigned ma = ok ? ~0u : 0u;
+                const unsigned mb = (ok && ((vmask >> t) & 1)) ? ~0u : 0u;
+                a[g * T + t] = __uint_as_float(__float_as_uint(av) & ma);
+                b[g * T + t] = __uint_as_float(__float_as_uint(bv) & mb);
             }
         }
     };

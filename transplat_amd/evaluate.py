@@ -65,6 +65,14 @@ def gather_results(local: list[SceneResult], device: torch.device, world: int) -
     return sorted(out, key=lambda r: r.scene_idx)
 
 
+def _raster_status(device: torch.device) -> None:
+    """Raise if any rasterizer call on `device` exceeded its instance capacity (the eval model is
+    built with check_overflow=False so its step can be a replayed hipGraph; the flag is sticky)."""
+    from .model.decoder.hip_splatting import check_status
+
+    check_status(device)
+
+
 def evaluate(step: Callable[[dict], torch.Tensor], scenes: list, make_batch: Callable[[int, object], dict],
              device: torch.device, rank: int = 0, world: int = 1) -> list[SceneResult]:
     """`make_batch(scene_idx, entry)` -> batch dict (b = 1); `step(batch)` -> color [1, V, 3, H, W]."""
@@ -75,6 +83,7 @@ def evaluate(step: Callable[[dict], torch.Tensor], scenes: list, make_batch: Cal
         color = step(batch)
         if device.type == "cuda":
             torch.cuda.synchronize(device)
+            _raster_status(device)  # a capacity overflow must not become a silent wrong-image PSNR
         dt = time.perf_counter() - t0
         gt = batch["target"]["image"][0].to(color.device)
         psnr = compute_psnr(gt, color[0]).mean().item()
@@ -97,6 +106,7 @@ def evaluate_stream(step: Callable[[dict], torch.Tensor], examples, device: torc
         color = step(batch)
         if device.type == "cuda":
             torch.cuda.synchronize(device)
+            _raster_status(device)  # a capacity overflow must not become a silent wrong-image PSNR
         dt = time.perf_counter() - t0
         psnr = compute_psnr(batch["target"]["image"][0], color[0]).mean().item()
         local.append(SceneResult(idx, psnr, int(color.shape[1]), dt))

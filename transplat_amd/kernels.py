@@ -175,7 +175,10 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
     fused = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32 and _NO_CONV_EPI not in ("all", site)
     if fused:
         y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
-        fused = (y.shape[-1] * y.shape[-2]) % 4 == 0 and y.is_contiguous()
+        # the kernel indexes the residual with y's NCHW layout: a broadcastable residual ([C, 1, 1],
+        # a batch-1 map) takes the module path, where `y + residual` broadcasts
+        fused = ((y.shape[-1] * y.shape[-2]) % 4 == 0 and y.is_contiguous()
+                 and (residual is None or tuple(residual.shape) == tuple(y.shape)))
     if not fused:
         y = conv(x)
         if act == "gelu":
