@@ -258,6 +258,28 @@ def test_window_attention_bf16_kernel(device, hw, m, shift, b):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shift,b", [(False, 2), (True, 2), (True, 16)])
+def test_window_attention_bf16_growing_scores(device, shift, b):
+    """Scores that grow along the key order (keys scaled up to 4x, queries 3x) so the running max
+    keeps moving past the bf16 kernel's deferred-rescale threshold on later key tiles (random O(1)
+    scores would only take the branch on the first tile); b = 2 runs the split-key partials path,
+    b = 16 the single-pass one."""
+    from transplat_amd import kernels as K
+
+    hw = 64
+    q = (seeded((b, hw * hw, 128), 94) * 3.0).bfloat16()
+    # in-window key position t of pixel (y, x) is (y % 32) * 32 + x % 32: scale by it
+    ys, xs = torch.meshgrid(torch.arange(hw), torch.arange(hw), indexing="ij")
+    t = ((ys % 32) * 32 + xs % 32).reshape(-1).float() / 1024.0
+    k = (seeded((b, hw * hw, 128), 95) * (0.25 + 3.75 * t)[None, :, None]).bfloat16()
+    v = seeded(k.shape, 96).bfloat16()
+    ref = E.window_attention(q.float(), k.float(), v.float(), hw, hw, 2, shift)
+    out = K.window_attention(q.to(device), k.to(device), v.to(device), hw, hw, 2, shift)
+    err = (out.float().cpu() - ref).abs().max().item()
+    assert err < 1.5e-2 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("m,k1,k2,n,gelu,ln,res,split,bias,gin", [
     (8192, 128, 0, 384, False, False, False, True, False, False),    # self-attention q | k | v
     (8192, 128, 0, 128, False, True, True, False, False, False),     # merge + norm1 + residual

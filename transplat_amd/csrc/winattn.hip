@@ -37,6 +37,12 @@ namespace winattn {
 #define TSPLAT_WA_ABL 0
 #endif
 constexpr int kAbl = TSPLAT_WA_ABL;
+// TSPLAT_WA2_ABL (diagnostic builds only): removes one phase of the bf16 v2 loop -- 1 softmax,
+// 2 PV MFMAs, 3 QK MFMAs, 4 next-tile gather + staging (results are wrong in such a build)
+#ifndef TSPLAT_WA2_ABL
+#define TSPLAT_WA2_ABL 0
+#endif
+constexpr int kAbl2 = TSPLAT_WA2_ABL;
 
 // TSPLAT_WA_STAMP (diagnostic builds only): per-wave s_memtime sums of the key-pair kernel's loop
 // segments, read back with tsplat_diag_wa_stamps(); shares are meaningful, the build's time is not
@@ -1328,6 +1334,245 @@ win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __res
     }
 }
 
+// ============================================================================================
+// bf16 v2 (default for bf16): the same operand maps as win_attn_bf16_kernel, re-cut for the
+// VALU budget beside 2.5 PF of matrix cores (one 32x32x16 MFMA = 32 cycles, of which 24 are free
+// for vector issue):
+//   * K / V / mask tiles double-buffered in LDS, one barrier per key tile (the next tile's rows,
+//     loaded during this tile, are written to the other buffer after this tile's MFMAs);
+//   * V stays row-major in LDS (16-B writes, the XOR image (b) of cdna_hip_programming.md T10) and
+//     the PV A operand V^T[d][keys] comes from ds_read_b64_tr_b16: two transposed reads per
+//     fragment instead of 16 two-byte transposing writes + shuffles per staged row;
+//   * softmax in the log2 domain on the raw scores: one max3 tree, then exp2(fma(s, c, -m)) with
+//     c = log2(e) / sqrt(C) -- no separate scale, subtract and log2(e) multiplies;
+//   * deferred rescale (T13): the running max m moves only when a tile's max exceeds it by more
+//     than kThr (log2 units), a wave-uniform branch, so P <= 2^kThr in bf16 (same relative
+//     precision) and the 64-register O rescale and l update are skipped on almost every tile;
+//   * the shifted-window mask rides on the QK^T MFMA: one extra k = 16 step per 32-key subtile
+//     with A = kMaskBonus at the key's region slot (one-hot, from LDS) and B = 1 at the query's
+//     region slot (registers), which adds kMaskBonus to every same-region score. Softmax is
+//     invariant to a per-query shift, so this equals the reference's -100 on different-region
+//     pairs up to the bonus's bf16 rounding: different-region weights are e^(-99.7) instead of
+//     e^(-100) relative -- both below fp32's normal range, i.e. zero for the output.
+// ============================================================================================
+constexpr float kThr = 8.0f;             // deferred-rescale threshold (log2 units): P <= 256
+constexpr float kMaskBonus = 1128.0f;    // bf16-exact; x 1/sqrt(128) = 99.7 (reference: 100)
+
+// byte offset of 16-B chunk ch (0..15) of row r in a [rows][128 x bf16] tile, image (b) of T10:
+// conflict-free for ds_read_b128 row reads and ds_read_b64_tr_b16 transposed reads alike
+__device__ __forceinline__ int vimg_off(int r, int ch) {
+    return 256 * r + 16 * (ch ^ (((r & 3) << 2) | ((r >> 2) & 3)));
+}
+
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+
+// v_max3_f32 as written: fmaxf() on MFMA results makes the compiler insert canonicalising
+// v_max_f32 x, x first (scores are finite products, no signalling NaNs to quieten)
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__global__ void __launch_bounds__(kThreads, 2)
+win_attn_bf16_v2_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                        const __bf16* __restrict__ v, __bf16* __restrict__ out, Partials part) {
+    // double-buffered K / V / mask tiles: one barrier per key tile
+    __shared__ __attribute__((aligned(16))) __bf16 sKb[2][kBK * kC];
+    __shared__ __attribute__((aligned(16))) unsigned char sVb[2][kBK * kC * 2];
+    __shared__ __attribute__((aligned(16))) bf16x8 sMaskAb[2][kBK][2];  // one-hot key-region fragments
+
+    int qblk, wi, bz;
+    xcd_block_coords(qblk, wi, bz);
+    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const size_t HW = (size_t)p.H * p.W;
+    const int kvb = (b + p.kv_shift) % p.nbatch;
+    const __bf16* qb = q + (size_t)b * HW * kC;
+    const __bf16* kb = k + (size_t)kvb * p.m * HW * kC;
+    const __bf16* vb = v + (size_t)kvb * p.m * HW * kC;
+    const float cl2 = p.scale * kLog2e;
+
+    const int tq = qblk * kBQ3 + wid * kQW + c;
+    const int qpix = win_pixel(p, wi, tq);
+    bf16x8 qf[8];
+    {
+        const bf16x8* src = reinterpret_cast<const bf16x8*>(qb + (size_t)qpix * kC + 8 * h);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qf[i] = src[2 * i];
+    }
+    // mask B operand: B[k = 8h + j][query c] = 1 at the query's region slot
+    bf16x8 qmask;
+    {
+        const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qmask[j] = (__bf16)(qreg == 8 * h + j ? 1.0f : 0.0f);
+    }
+    floatx16 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    // gather: thread = (key row grow, 32-channel quarter gpart); the next tile's rows are loaded
+    // into registers right after this tile's barrier and written to LDS after the end-of-tile
+    // barrier (issue early / write late)
+    const int grow = tid & 63, gpart = tid >> 6;
+    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
+    bf16x8 kv[4], vv[4];
+    int kreg = 0;
+    auto gather = [&](int k0) {
+        const int j = k0 + grow;
+        const int tk = j / p.m, vi = j - tk * p.m;
+        const int kpix = win_pixel(p, wi, tk);
+        const bf16x8* ksrc = reinterpret_cast<const bf16x8*>(kb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
+        const bf16x8* vsrc = reinterpret_cast<const bf16x8*>(vb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            kv[i] = ksrc[i];
+            vv[i] = vsrc[i];
+        }
+        kreg = p.shift ? win_region(p, wi, j % p.L) : 0;
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int chunk = 4 * gpart + i;
+            *reinterpret_cast<bf16x8*>(&sKb[buf][grow * kC + ((chunk ^ (grow & 15)) * 8)]) = kv[i];
+            *reinterpret_cast<bf16x8*>(&sVb[buf][vimg_off(grow, chunk)]) = vv[i];
+        }
+        if (p.shift && gpart < 2) {
+            bf16x8 a;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = (__bf16)(kreg == 8 * gpart + j ? kMaskBonus : 0.0f);
+            sMaskAb[buf][grow][gpart] = a;
+        }
+    };
+    gather(kbeg);
+    stage(0);
+    __syncthreads();
+    if (kbeg + kBK < kend) gather(kbeg + kBK);
+    for (int k0 = kbeg, buf = 0; k0 < kend; k0 += kBK, buf ^= 1) {
+        const __bf16* sK = sKb[buf];
+        const unsigned char* sV = sVb[buf];
+        const bf16x8(*sMaskA)[2] = sMaskAb[buf];
+
+        // ---- S^T = K Q^T (+ the mask step), raw scores
+        floatx16 s[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[0][r] = s[1][r] = 0.f;
+        {
+            bf16x8 kk[2][8];
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int row = 32 * sub + c, chunk = 2 * i + h;
+                    kk[sub][i] = *reinterpret_cast<const bf16x8*>(&sK[row * kC + ((chunk ^ (row & 15)) * 8)]);
+                }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (kAbl2 == 3) {
+                    s[0][i] += (float)kk[0][i][0];
+                    s[1][i] += (float)kk[1][i][0];
+                    continue;
+                }
+                s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk[0][i], qf[i], s[0], 0, 0, 0);
+                s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk[1][i], qf[i], s[1], 0, 0, 0);
+            }
+            if (p.shift) {
+                s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sMaskA[c][h], qmask, s[0], 0, 0, 0);
+                s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sMaskA[32 + c][h], qmask, s[1], 0, 0, 0);
+            }
+        }
+        // ---- online softmax (fp32, log2 domain), deferred rescale
+        if (kAbl2 != 1) {
+        float bmax = max3_raw(s[0][0], s[1][0], s[0][1]);
+        bmax = max3_raw(bmax, s[1][1], s[0][2]);
+#pragma unroll
+        for (int r = 2; r < 15; ++r) bmax = max3_raw(bmax, s[1][r], s[0][r + 1]);
+        bmax = fmaxf(bmax, s[1][15]);
+        const float bm2 = halves_max(bmax) * cl2;
+        if (__any(bm2 > m_run + kThr)) {
+            const float m_new = fmaxf(m_run, bm2);
+            const float corr = fast_exp2(m_run - m_new);
+            l_run *= corr;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+            m_run = m_new;
+        }
+        float bsum = 0.f;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = fast_exp2(fmaf(s[sub][r], cl2, -m_run));
+                s[sub][r] = e;
+                bsum += e;
+            }
+        l_run += halves_sum(bsum);
+        }
+
+        // ---- O^T += V^T P^T: 4 k-steps of 16 keys; A = V^T by transposed LDS reads
+#pragma unroll
+        for (int ksx = 0; ksx < 4; ++ksx) {
+            const int sub = ksx >> 1, st = ksx & 1;
+            bf16x8 pf;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) pf[e] = (__bf16)s[sub][8 * st + e];
+            // group g = lane >> 4 reads the 4-key x 16-d block rows r0.., cols 32 dt + 16 (g & 1);
+            // lane 4qq + pp of the group supplies row r0 + qq, chunk c0 + (pp >> 1), half pp & 1
+            const int gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+            const int r0 = 16 * ksx + 4 * h + qq;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const int c0 = 4 * dt + 2 * ((lane >> 4) & 1) + (pp >> 1);
+                const shortx4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) shortx4*)(sV + vimg_off(r0, c0) + 8 * (pp & 1)));
+                const shortx4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (__attribute__((address_space(3))) shortx4*)(sV + vimg_off(r0 + 8, c0) + 8 * (pp & 1)));
+                typedef short shortx8 __attribute__((ext_vector_type(8)));
+                const shortx8 vs = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                if (kAbl2 == 2) { o[dt][0] += (float)pf[0] + (float)vs[0]; continue; }
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vs), pf, o[dt], 0, 0, 0);
+            }
+        }
+        // write-late: the next tile's rows (loaded during this tile) go to the other buffer, whose
+        // readers all passed the previous barrier; then the tile after that is requested
+        if (k0 + kBK < kend && kAbl2 != 4) {
+            stage(buf ^ 1);
+            if (k0 + 2 * kBK < kend) gather(k0 + 2 * kBK);
+        }
+        __syncthreads();
+    }
+
+    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
+    if (p.ksplit == 1) {
+        const float inv = 1.0f / l_run;
+        __bf16* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                store4(dst + 32 * dt + 8 * u, make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv,
+                                                          o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
+    } else {
+        const size_t row = pidx(p, b, wi, ks, tq);
+        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, wid)) + lane;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
+        if (h == 0) {
+            part.m[row] = m_run * kLn2;  // the combine kernel takes natural-log maxima
+            part.l[row] = l_run;
+        }
+    }
+}
+
 }  // namespace winattn
 }  // namespace tsplat
 
@@ -1567,9 +1812,14 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     }
     hipStream_t stream = (hipStream_t)stream_;
     TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
-    hipLaunchKernelGGL(win_attn_bf16_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
-                       dim3(kThreads), 0, stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
-                       (__bf16*)out, part);
+    if (env_is("TSPLAT_WINATTN_BF16", "v1"))
+        hipLaunchKernelGGL(win_attn_bf16_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
+                           dim3(kThreads), 0, stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
+                           (__bf16*)out, part);
+    else
+        hipLaunchKernelGGL(win_attn_bf16_v2_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
+                           dim3(kThreads), 0, stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
+                           (__bf16*)out, part);
     if (p.ksplit > 1)
         hipLaunchKernelGGL(win_attn_combine_x32_kernel<__bf16>, dim3(p.L / kBQ3 * 16, splits * splits, batch),
                            dim3(kThreads), 0, stream, p, part, (__bf16*)out);
