@@ -336,6 +336,19 @@ int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x2, int32_t 
                           const float* bias, float* y, int32_t batch, int32_t height, int32_t width, int32_t c_out,
                           int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit, void* stream);
 
+/* 3x3 / stride 1 / padding 1 convolution as Winograd F(2x2, 3x3) on exact-fp32 MFMA (replaces the
+ * nn.Conv2d(c_in, c_out, 3, 1, 1) calls of the depth predictor's full-resolution heads and U-Net
+ * levels, reference src/model/encoder/matching/depth_predictor_trans.py:110-125 and
+ * ldm_unet/unet.py ResBlock, which PyTorch hands to MIOpen). x [batch, c_in, height, width] and
+ * y [batch, c_out, height, width] NCHW fp32; w_packed = tsplat_wino_weight_f32(weight) (the
+ * transformed filters G g G^T, tsplat_wino_weight_floats(c_out, c_in) floats); bias may be null;
+ * y = act(conv(x) + bias), act 0 none, 1 ReLU, 2 GELU (erf). */
+size_t tsplat_wino_weight_floats(int32_t c_out, int32_t c_in);
+int tsplat_wino_weight_f32(const float* weight, float* w_packed, int32_t c_out, int32_t c_in, void* stream);
+int tsplat_conv3x3_wino_f32_fwd(const float* x, const float* w_packed, const float* bias, float* y, int32_t batch,
+                                int32_t c_in, int32_t height, int32_t width, int32_t c_out, int32_t act,
+                                void* stream);
+
 /* Channels-last form of tsplat_conv2d_f32_fwd for the Depth-Anything DPT head (reference
  * src/depth_anything_v2/util/blocks.py ResidualConvUnit / FeatureFusionBlock.out_conv), whose conv
  * chain runs on channels-last maps: x [batch, height, width, c_in], y and residual

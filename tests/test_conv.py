@@ -180,3 +180,47 @@ def test_unet_full_res_1x1_gemm_path(device, monkeypatch):
             ref = conv(x)
             out = U.conv(conv.to(device), x.to(device)).cpu()
         assert (out - ref).abs().max().item() < 2e-5 * ref.abs().max().item()
+
+
+WINO_CASES = [
+    # n, ci, co, h, w, bias, act
+    (2, 163, 168, 32, 32, True, "gelu"),   # to_gaussians' shape class: ci % 8 != 0, co % 32 != 0
+    (2, 168, 84, 16, 40, True, "none"),    # to_disparity-like, tile rows of 20 (tbx 16)
+    (2, 32, 32, 64, 64, False, "relu"),
+    (1, 38, 32, 17, 21, True, "none"),     # odd sizes: half tiles on the last row / column (tbx 8)
+    (1, 128, 128, 18, 18, True, "gelu"),   # tw 9 -> tbx 8
+    (3, 16, 16, 9, 70, False, "none"),     # tw 35 -> tbx 32, a partial second tile block per row
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES)
+def test_conv3x3_wino_kernel(device, n, ci, co, h, w, bias, act):
+    """Winograd F(2x2, 3x3) fp32 MFMA convolution (tsplat_conv3x3_wino_f32_fwd) against torch's
+    conv2d in float64 on the CPU. The transforms reassociate the products (as MIOpen's Winograd
+    solvers do), so the bound is 2e-5 of the output's max magnitude, like the direct kernel's."""
+    from transplat_amd import kernels as K
+
+    x = seeded((n, ci, h, w), 41)
+    wt = seeded((co, ci, 3, 3), 42) * (1.0 / (9 * ci) ** 0.5)
+    b = seeded((co,), 43) if bias else None
+    ref = torch.nn.functional.conv2d(x.double(), wt.double(), b.double() if bias else None, padding=1)
+    ref = {"none": ref, "relu": torch.relu(ref), "gelu": torch.nn.functional.gelu(ref)}[act].float()
+    out = K.conv3x3_wino(x.to(device), wt.to(device), b.to(device) if bias else None, act).cpu()
+    err = (out - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-5, err
+
+
+@pytest.mark.gpu
+def test_conv3x3_wino_weight_cache_tracks_updates(device):
+    """The transformed-filter cache is keyed on the live weight tensor and its version: an in-place
+    update of the weight is picked up."""
+    from transplat_amd import kernels as K
+
+    x = seeded((1, 16, 8, 8), 44).to(device)
+    wt = (seeded((16, 16, 3, 3), 45) * 0.1).to(device)
+    y1 = K.conv3x3_wino(x, wt)
+    with torch.no_grad():
+        wt.mul_(2.0)
+    y2 = K.conv3x3_wino(x, wt)
+    torch.testing.assert_close(y2, 2.0 * y1, rtol=1e-5, atol=1e-6)

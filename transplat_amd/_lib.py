@@ -74,6 +74,9 @@ SIGNATURES = {
                                                                                        _I32, _P]),
     "tsplat_linear_f32_fwd": (ctypes.c_int, [_P, _I32, _P, _I32] + [_P] * 4 + [ctypes.c_float, _P, _P, ctypes.c_int64]
                               + [_I32] * 3 + [_P]),
+    "tsplat_wino_weight_floats": (ctypes.c_size_t, [_I32, _I32]),
+    "tsplat_wino_weight_f32": (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
+    "tsplat_conv3x3_wino_f32_fwd": (ctypes.c_int, [_P, _P, _P, _P] + [_I32] * 6 + [_P]),
 }
 
 ERRORS = {-1: "invalid argument", -2: "HIP launch error"}
@@ -125,7 +128,7 @@ def stream_ptr(device: torch.device | None = None) -> int:
 
 PROF_IDS = {"raster_preprocess": 1, "raster_scan": 2, "raster_scatter": 3, "raster_render": 4,
             "uv_coarse": 5, "uv_cross": 6, "msda": 7, "win_attn": 8, "raster": 9,
-            "group_norm": 10, "uv_cross_table": 11, "linear": 12, "mha": 13, "conv": 14}
+            "group_norm": 10, "uv_cross_table": 11, "linear": 12, "mha": 13, "conv": 14, "wino_conv": 15}
 
 
 def prof_enable(name: str | None) -> None:

@@ -23,7 +23,8 @@ enum KernelId : int {
     kLinear = 12,     // tsplat_linear_f32_fwd
     kMha = 13,        // tsplat_mha_f32_fwd
     kConv = 14,       // tsplat_conv2d_f32_fwd
-    kNumKernels = 15,
+    kWinoConv = 15,   // tsplat_conv3x3_wino_f32_fwd
+    kNumKernels = 16,
 };
 
 int active();                 // kernel id being timed (0 = off)

@@ -173,6 +173,10 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
     if not x.is_cuda:
         raise RuntimeError("transplat HIP ops need device tensors (no CPU path)")
     fused = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32 and _NO_CONV_EPI not in ("all", site)
+    if (fused and residual is None and act in _WINO_ACT and x.is_contiguous()
+            and conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups)):
+        # the Winograd kernel's epilogue applies the bias and the activation itself
+        return conv3x3_wino(x, conv.weight, conv.bias, act)
     if fused:
         y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
         # the kernel indexes the residual with y's NCHW layout: a broadcastable residual ([C, 1, 1],
@@ -451,6 +455,91 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
                                    _lib.ptr(pb), _lib.ptr(y), n, h, w, co, k, stride, int(upsample), ksplit,
                                    _lib.stream_ptr(x1.device))
     _lib.check(rc, "tsplat_conv2d_f32_fwd")
+    return y
+
+
+# Winograd-transformed weights per weight tensor (same caching rule as _CONV_PACKED)
+_WINO_PACKED: dict = {}
+# Which 3x3 convolutions go to tsplat_conv3x3_wino_f32_fwd: "auto" (the shapes where it beats
+# MIOpen, see conv3x3_wino_ok), "off", "all" (every 3x3 / stride 1 / pad 1 fp32 conv; tests / A/B)
+_WINO_MODE = os.environ.get("TSPLAT_WINO", "auto")
+_WINO_ACT = {"none": 0, "relu": 1, "gelu": 2}
+
+
+def wino_pack_weight(weight):
+    """[cout, cin, 3, 3] -> the transformed filters G g G^T in the A-operand order of
+    tsplat_conv3x3_wino_f32_fwd, cached per weight tensor version."""
+    hit = _WINO_PACKED.get(id(weight))
+    if hit is not None and hit[0]() is weight and hit[1] == weight._version:
+        return hit[2]
+    lib = _lib.load()
+    co, ci = weight.shape[:2]
+    packed = torch.empty(int(lib.tsplat_wino_weight_floats(co, ci)), dtype=torch.float32, device=weight.device)
+    w = weight.detach().float().contiguous()
+    _lib.check(lib.tsplat_wino_weight_f32(_lib.ptr(w), _lib.ptr(packed), co, ci, _lib.stream_ptr(weight.device)),
+               "tsplat_wino_weight_f32")
+    if len(_WINO_PACKED) > 512:
+        for k in [k for k, v in _WINO_PACKED.items() if v[0]() is None]:
+            del _WINO_PACKED[k]
+    _WINO_PACKED[id(weight)] = (weakref.ref(weight), weight._version, packed)
+    return packed
+
+
+def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1) -> bool:
+    """True when tsplat_conv3x3_wino_f32_fwd takes conv2d(x, weight) on the NCHW map x and (mode
+    "auto") it is one of the 3x3s where it beats MIOpen's kernels (tools/bench_wino.py): above the
+    direct kernel's FLOP range, and not the few-tile / long-reduction shapes (256 input channels
+    at 32^2: 64 workgroups of 32 serial chunks) where MIOpen stays faster."""
+    if _WINO_MODE == "off" or not x.is_cuda or torch.is_autocast_enabled("cuda") or not x.is_contiguous():
+        return False
+    if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4 or weight.dim() != 4:
+        return False
+    as_int = lambda v: v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else -1)
+    if tuple(weight.shape[2:]) != (3, 3) or as_int(stride) != 1 or as_int(padding) != 1:
+        return False
+    if as_int(dilation) != 1 or groups != 1 or weight.shape[1] != x.shape[1]:
+        return False
+    if _WINO_MODE == "all":
+        return True
+    n, ci, h, w = x.shape
+    co = weight.shape[0]
+    groups_ = n * ((h + 1) // 2 * ((w + 1) // 2) + 31) // 32 * ((co + 31) // 32)  # ~ workgroups
+    return (ci >= 16 and co >= 16 and 2.0 * n * h * w * co * ci * 9 > _CONV_MAX_FLOP
+            and (ci <= 192 or groups_ >= 256))
+
+
+def conv2d_forward(mod, x):
+    """nn.Conv2d.forward with the 3x3s that conv3x3_wino_ok admits on the Winograd kernel (installed
+    on the encoder's Conv2d modules by install_conv2d_dispatch)."""
+    if conv3x3_wino_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation, mod.groups) and mod.padding_mode == "zeros":
+        return conv3x3_wino(x, mod.weight, mod.bias)
+    return mod._conv_forward(x, mod.weight, mod.bias)
+
+
+def install_conv2d_dispatch(module) -> int:
+    """Route every nn.Conv2d under `module` through conv2d_forward (same parameters, same state
+    dict); returns the number of modules routed."""
+    import functools
+
+    n = 0
+    for m in module.modules():
+        if type(m) is torch.nn.Conv2d:
+            m.forward = functools.partial(conv2d_forward, m)
+            n += 1
+    return n
+
+
+def conv3x3_wino(x, weight, bias=None, act: str = "none"):
+    """act(conv2d(x, weight, bias, stride 1, padding 1)) via Winograd F(2x2, 3x3) on fp32 MFMA."""
+    lib = _lib.load()
+    a = _f32(x)
+    n, ci, h, w = a.shape
+    co = weight.shape[0]
+    y = torch.empty((n, co, h, w), dtype=torch.float32, device=x.device)
+    pb = _f32(bias) if bias is not None else None
+    rc = lib.tsplat_conv3x3_wino_f32_fwd(_lib.ptr(a), _lib.ptr(wino_pack_weight(weight)), _lib.ptr(pb),
+                                         _lib.ptr(y), n, ci, h, w, co, _WINO_ACT[act], _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_conv3x3_wino_f32_fwd")
     return y
 
 

@@ -93,6 +93,9 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         # constants as non-persistent buffers: no host->device copy inside forward (graph capture)
         self.register_buffer("img_mean", torch.tensor([0.485, 0.456, 0.406]), persistent=False)
         self.register_buffer("img_std", torch.tensor([0.229, 0.224, 0.225]), persistent=False)
+        # every plain Conv2d: the large 3x3s on the Winograd fp32 MFMA kernel, the rest unchanged
+        # (kernels.conv2d_forward; CPU tensors and bf16 autocast keep the module's own conv)
+        kernels.install_conv2d_dispatch(self)
 
     def map_pdf_to_opacity(self, pdf, global_step: int):
         """(reference :139-152)"""

@@ -59,6 +59,9 @@ def conv(conv: nn.Module, x, x2=None, upsample: bool = False, bias: bool = True)
         x = torch.cat([x, x2], dim=1)
     if upsample:
         x = F.interpolate(x, scale_factor=2, mode="nearest")
+    if isinstance(conv, nn.Conv2d) and kernels.conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding,
+                                                               conv.dilation, conv.groups):
+        return kernels.conv3x3_wino(x, conv.weight, b)
     if (_GEMM_1X1 and isinstance(conv, nn.Conv2d) and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
             and conv.groups == 1
             and conv.padding == (0, 0) and x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32
