@@ -295,13 +295,15 @@ extern "C" int tsplat_conv3x3_wino_f32_fwd(const float* x, const float* packed, 
     a.act = act;
     hipStream_t stream = (hipStream_t)stream_;
     TSPLAT_PROF_BEGIN(prof::kWinoConv, stream);
-    // 16-channel chunks (half the barriers, 32 MFMAs per wave between them) unless TSPLAT_WINO_CIB=8
+    // 8-channel chunks: 3 workgroups per CU (16-channel chunks, 2 per CU, measured 2-5 % slower;
+    // TSPLAT_WINO_CIB=16 selects them). Two 32-channel output blocks per workgroup (128
+    // accumulators per lane) spilled at 2 waves per SIMD and ran 1.3-2x slower.
     const char* e = getenv("TSPLAT_WINO_CIB");
-    if (e && atoi(e) == 8)
-        hipLaunchKernelGGL(wino::conv_kernel<8>, dim3(n * a.bx * a.by, a.co_blocks), dim3(wino::kThreads), 0, stream,
-                           a);
-    else
+    if (e && atoi(e) == 16)
         hipLaunchKernelGGL(wino::conv_kernel<16>, dim3(n * a.bx * a.by, a.co_blocks), dim3(wino::kThreads), 0,
+                           stream, a);
+    else
+        hipLaunchKernelGGL(wino::conv_kernel<8>, dim3(n * a.bx * a.by, a.co_blocks), dim3(wino::kThreads), 0,
                            stream, a);
     TSPLAT_PROF_END(prof::kWinoConv, stream);
     TSPLAT_CHECK_LAUNCH();
