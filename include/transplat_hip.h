@@ -348,6 +348,13 @@ int tsplat_wino_weight_f32(const float* weight, float* w_packed, int32_t c_out, 
 int tsplat_conv3x3_wino_f32_fwd(const float* x, const float* w_packed, const float* bias, float* y, int32_t batch,
                                 int32_t c_in, int32_t height, int32_t width, int32_t c_out, int32_t act,
                                 void* stream);
+/* The same on the channel concatenation of n_src (1..6) NCHW inputs, read in place (replaces the
+ * torch.cat feeding the reference's to_gaussians head, depth_predictor_trans.py:486-489, and the
+ * U-Net output blocks' skip concatenation, ldm_unet/unet.py:1130): srcs / chans are HOST arrays of
+ * n_src device pointers [batch, chans[s], height, width] and their channel counts (sum = c_in). */
+int tsplat_conv3x3_wino_cat_f32_fwd(const float* const* srcs, const int32_t* chans, int32_t n_src,
+                                    const float* w_packed, const float* bias, float* y, int32_t batch,
+                                    int32_t height, int32_t width, int32_t c_out, int32_t act, void* stream);
 
 /* Channels-last form of tsplat_conv2d_f32_fwd for the Depth-Anything DPT head (reference
  * src/depth_anything_v2/util/blocks.py ResidualConvUnit / FeatureFusionBlock.out_conv), whose conv

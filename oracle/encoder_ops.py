@@ -257,9 +257,10 @@ def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", 
     return y
 
 
-def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
-    """conv -> (GELU | ReLU) [-> + residual (-> ReLU)] as the reference module chains compute it."""
-    y = conv(x)
+def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = "", extra=()):
+    """conv(cat([x, *extra], 1)) -> (GELU | ReLU) [-> + residual (-> ReLU)] as the reference module
+    chains compute it (the reference materialises the concatenation with torch.cat)."""
+    y = conv(torch.cat([x, *extra], dim=1) if extra else x)
     if act == "gelu":
         y = torch.nn.functional.gelu(y)
     elif act == "relu":

@@ -224,3 +224,18 @@ def test_conv3x3_wino_weight_cache_tracks_updates(device):
         wt.mul_(2.0)
     y2 = K.conv3x3_wino(x, wt)
     torch.testing.assert_close(y2, 2.0 * y1, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_conv3x3_wino_reads_concat_in_place(device):
+    """tsplat_conv3x3_wino_cat_f32_fwd on three sources (the to_gaussians head's cat of refine_out,
+    images and the upsampled features: 32 + 3 + 128 channels) equals the kernel on the materialised
+    concatenation bit for bit (same channel order, same arithmetic)."""
+    from transplat_amd import kernels as K
+
+    parts = [seeded((2, c, 20, 36), 50 + c).to(device) for c in (32, 3, 128)]
+    wt = (seeded((84, 163, 3, 3), 53) * 0.03).to(device)
+    b = seeded((84,), 54).to(device)
+    y_cat = K.conv3x3_wino(parts[0], wt, b, "gelu", extra=tuple(parts[1:]))
+    y_ref = K.conv3x3_wino(torch.cat(parts, 1), wt, b, "gelu")
+    assert torch.equal(y_cat, y_ref)

@@ -32,8 +32,12 @@ constexpr int kCiB = 8;      // channel padding granule; a chunk is CIB = 8 or 1
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+constexpr int kMaxSrc = 6;  // input sources concatenated along channels (read in place)
+
 struct Args {
-    const float* x;      // [n][ci][h][w]
+    const float* src[kMaxSrc];  // source s: [n][cs[s]][h][w]; channel c of the conv input is
+    int cs[kMaxSrc];            // channel c - (cs[0] + .. + cs[s-1]) of the source it falls in
+    int nsrc;
     const float* u;      // packed U: [16][co_blocks][ci_pad / 2][2][32]
     const float* bias;   // [co] or null
     float* y;            // [n][co][h][w]
@@ -98,7 +102,6 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(Args a) {
     const bool tile_ok = ty < a.th && tx < a.tw;
     const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
     const size_t hw = (size_t)a.h * a.w;
-    const float* xin = a.x + (size_t)img * a.ci * hw;
     // per-row / per-column validity of the 4x4 patch (zero padding)
     bool rok[4], cok[4];
 #pragma unroll
@@ -111,7 +114,20 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(Args a) {
 #pragma unroll
         for (int k = 0; k < kP; ++k) {
             const int c = chunk * CIB + cc + 8 * k;
-            const float* src = xin + (size_t)min(c, a.ci - 1) * hw;
+            // the source holding input channel c (channels past ci read the last one, zeroed)
+            const float* src = nullptr;
+            {
+                int rem = min(c, a.ci - 1);
+#pragma unroll
+                for (int q = 0; q < kMaxSrc; ++q) {
+                    if (q < a.nsrc && !src) {
+                        if (rem < a.cs[q])
+                            src = a.src[q] + ((size_t)img * a.cs[q] + rem) * hw;
+                        else
+                            rem -= a.cs[q];
+                    }
+                }
+            }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -257,13 +273,21 @@ extern "C" int tsplat_wino_weight_f32(const float* weight, float* packed, int32_
     return TSPLAT_OK;
 }
 
-extern "C" int tsplat_conv3x3_wino_f32_fwd(const float* x, const float* packed, const float* bias, float* y,
-                                           int32_t n, int32_t ci, int32_t h, int32_t w, int32_t co, int32_t act,
-                                           void* stream_) {
-    if (!x || !packed || !y || n <= 0 || ci <= 0 || h <= 0 || w <= 0 || co <= 0 || act < 0 || act > 2)
+static int wino_launch(const float* const* srcs, const int32_t* chans, int32_t nsrc, const float* packed,
+                       const float* bias, float* y, int32_t n, int32_t h, int32_t w, int32_t co, int32_t act,
+                       void* stream_) {
+    if (!srcs || !chans || nsrc <= 0 || nsrc > wino::kMaxSrc || !packed || !y || n <= 0 || h <= 0 || w <= 0 ||
+        co <= 0 || act < 0 || act > 2)
         return TSPLAT_EINVAL;
     wino::Args a;
-    a.x = x;
+    int ci = 0;
+    for (int q = 0; q < wino::kMaxSrc; ++q) {
+        a.src[q] = q < nsrc ? srcs[q] : nullptr;
+        a.cs[q] = q < nsrc ? chans[q] : 0;
+        if (q < nsrc && (!srcs[q] || chans[q] <= 0)) return TSPLAT_EINVAL;
+        ci += a.cs[q];
+    }
+    a.nsrc = nsrc;
     a.u = packed;
     a.bias = bias;
     a.y = y;
@@ -308,4 +332,16 @@ extern "C" int tsplat_conv3x3_wino_f32_fwd(const float* x, const float* packed, 
     TSPLAT_PROF_END(prof::kWinoConv, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
+}
+
+extern "C" int tsplat_conv3x3_wino_f32_fwd(const float* x, const float* packed, const float* bias, float* y,
+                                           int32_t n, int32_t ci, int32_t h, int32_t w, int32_t co, int32_t act,
+                                           void* stream_) {
+    return wino_launch(&x, &ci, 1, packed, bias, y, n, h, w, co, act, stream_);
+}
+
+extern "C" int tsplat_conv3x3_wino_cat_f32_fwd(const float* const* srcs, const int32_t* chans, int32_t nsrc,
+                                               const float* packed, const float* bias, float* y, int32_t n,
+                                               int32_t h, int32_t w, int32_t co, int32_t act, void* stream_) {
+    return wino_launch(srcs, chans, nsrc, packed, bias, y, n, h, w, co, act, stream_);
 }

@@ -160,7 +160,7 @@ _AFFINE_ID: dict = {}
 _NO_CONV_EPI = os.environ.get("TSPLAT_NO_CONV_EPI", "")  # A/B timing knob only: "all" or a site name
 
 
-def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
+def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = "", extra=()):
     """conv(x) + bias -> act [-> + residual (-> relu for "relu")] with the bias, activation and
     residual in ONE pass after the bias-free MIOpen convolution (tsplat_bias_act_fwd). Under bf16
     autocast (config C3's dense layers) or for outputs the kernel's float4 layout cannot take, the
@@ -173,10 +173,13 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = ""):
     if not x.is_cuda:
         raise RuntimeError("transplat HIP ops need device tensors (no CPU path)")
     fused = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32 and _NO_CONV_EPI not in ("all", site)
-    if (fused and residual is None and act in _WINO_ACT and x.is_contiguous()
-            and conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups)):
-        # the Winograd kernel's epilogue applies the bias and the activation itself
-        return conv3x3_wino(x, conv.weight, conv.bias, act)
+    if (fused and residual is None and act in _WINO_ACT
+            and conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra)):
+        # the Winograd kernel reads the concatenation in place and applies the bias and the
+        # activation in its epilogue
+        return conv3x3_wino(x, conv.weight, conv.bias, act, extra)
+    if extra:
+        x = torch.cat([x, *extra], dim=1)
     if fused:
         y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
         # the kernel indexes the residual with y's NCHW layout: a broadcastable residual ([C, 1, 1],
@@ -485,23 +488,28 @@ def wino_pack_weight(weight):
     return packed
 
 
-def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1) -> bool:
+def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=()) -> bool:
     """True when tsplat_conv3x3_wino_f32_fwd takes conv2d(x, weight) on the NCHW map x and (mode
     "auto") it is one of the 3x3s where it beats MIOpen's kernels (tools/bench_wino.py): above the
     direct kernel's FLOP range, and not the few-tile / long-reduction shapes (256 input channels
     at 32^2: 64 workgroups of 32 serial chunks) where MIOpen stays faster."""
-    if _WINO_MODE == "off" or not x.is_cuda or torch.is_autocast_enabled("cuda") or not x.is_contiguous():
+    if _WINO_MODE == "off" or not x.is_cuda or torch.is_autocast_enabled("cuda") or len(extra) > 5:
         return False
-    if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4 or weight.dim() != 4:
+    for t in (x, *extra):
+        if (t.dtype != torch.float32 or t.dim() != 4 or not t.is_contiguous() or t.device != x.device
+                or t.shape[0] != x.shape[0] or t.shape[2:] != x.shape[2:]):
+            return False
+    if weight.dtype != torch.float32 or weight.dim() != 4:
         return False
     as_int = lambda v: v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else -1)
     if tuple(weight.shape[2:]) != (3, 3) or as_int(stride) != 1 or as_int(padding) != 1:
         return False
-    if as_int(dilation) != 1 or groups != 1 or weight.shape[1] != x.shape[1]:
+    ci = sum(t.shape[1] for t in (x, *extra))
+    if as_int(dilation) != 1 or groups != 1 or weight.shape[1] != ci:
         return False
     if _WINO_MODE == "all":
         return True
-    n, ci, h, w = x.shape
+    n, _, h, w = x.shape
     co = weight.shape[0]
     groups_ = n * ((h + 1) // 2 * ((w + 1) // 2) + 31) // 32 * ((co + 31) // 32)  # ~ workgroups
     return (ci >= 16 and co >= 16 and 2.0 * n * h * w * co * ci * 9 > _CONV_MAX_FLOP
@@ -529,17 +537,23 @@ def install_conv2d_dispatch(module) -> int:
     return n
 
 
-def conv3x3_wino(x, weight, bias=None, act: str = "none"):
-    """act(conv2d(x, weight, bias, stride 1, padding 1)) via Winograd F(2x2, 3x3) on fp32 MFMA."""
+def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=()):
+    """act(conv2d(cat([x, *extra], 1), weight, bias, stride 1, padding 1)) via Winograd F(2x2, 3x3)
+    on fp32 MFMA; the concatenation is read in place (tsplat_conv3x3_wino_cat_f32_fwd)."""
+    import ctypes
+
     lib = _lib.load()
-    a = _f32(x)
-    n, ci, h, w = a.shape
+    srcs = [_f32(t) for t in (x, *extra)]
+    n, _, h, w = srcs[0].shape
     co = weight.shape[0]
     y = torch.empty((n, co, h, w), dtype=torch.float32, device=x.device)
     pb = _f32(bias) if bias is not None else None
-    rc = lib.tsplat_conv3x3_wino_f32_fwd(_lib.ptr(a), _lib.ptr(wino_pack_weight(weight)), _lib.ptr(pb),
-                                         _lib.ptr(y), n, ci, h, w, co, _WINO_ACT[act], _lib.stream_ptr(x.device))
-    _lib.check(rc, "tsplat_conv3x3_wino_f32_fwd")
+    ptrs = (ctypes.c_void_p * len(srcs))(*[_lib.ptr(t) for t in srcs])
+    chans = (ctypes.c_int32 * len(srcs))(*[t.shape[1] for t in srcs])
+    rc = lib.tsplat_conv3x3_wino_cat_f32_fwd(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p),
+                                             len(srcs), _lib.ptr(wino_pack_weight(weight)), _lib.ptr(pb),
+                                             _lib.ptr(y), n, h, w, co, _WINO_ACT[act], _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_conv3x3_wino_cat_f32_fwd")
     return y
 
 

@@ -31,12 +31,14 @@ def _conv_upsample_gelu(seq: nn.Sequential, x):
     return kernels.upsample_bilinear_act(y, int(up.scale_factor), conv.bias, "gelu")
 
 
-def _conv_gelu_conv(seq: nn.Sequential, x):
-    """Sequential(Conv2d, GELU, Conv2d) head with each conv's bias (and the GELU) applied in one
-    pass after the bias-free convolution (kernels.conv_bias_act)."""
+def _conv_gelu_conv(seq: nn.Sequential, x, extra=()):
+    """Sequential(Conv2d, GELU, Conv2d) head on cat([x, *extra], 1) with each conv's bias (and the
+    GELU) applied in one pass after the bias-free convolution (kernels.conv_bias_act; on the
+    Winograd path the concatenation is read in place and bias / GELU are its epilogue)."""
     if not (len(seq) == 3 and isinstance(seq[1], nn.GELU) and seq[1].approximate == "none"):
-        return seq(x)
-    return kernels.conv_bias_act(seq[2], kernels.conv_bias_act(seq[0], x, "gelu", site="head"), site="head")
+        return seq(torch.cat([x, *extra], dim=1) if extra else x)
+    return kernels.conv_bias_act(seq[2], kernels.conv_bias_act(seq[0], x, "gelu", site="head", extra=extra),
+                                 site="head")
 
 
 @torch.autocast("cuda", enabled=False)
@@ -210,8 +212,8 @@ class DepthPredictorTrans(nn.Module):
         refine_out = run_sequential(self.refine_unet, torch.cat((extra_info["images"], da_depth, proj_feature, fullres_disps,
                                                  pdf_max), dim=1))
 
-        raw_gaussians = _conv_gelu_conv(self.to_gaussians,
-                                        torch.cat([refine_out, extra_info["images"], proj_feat_in_fullres], dim=1))
+        raw_gaussians = _conv_gelu_conv(self.to_gaussians, refine_out,
+                                        extra=(extra_info["images"], proj_feat_in_fullres))
         raw_gaussians = rearrange(raw_gaussians, "(v b) c h w -> b v (h w) c", v=v, b=b)
         delta_disps, raw_densities = _conv_gelu_conv(self.to_disparity, refine_out).split(gaussians_per_pixel, dim=1)
         densities = repeat(F.sigmoid(raw_densities), "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)

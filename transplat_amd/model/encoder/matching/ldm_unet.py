@@ -55,6 +55,10 @@ def conv(conv: nn.Module, x, x2=None, upsample: bool = False, bias: bool = True)
             and kernels.conv2d_direct_ok(x.unsqueeze(-1), conv.weight)):
         # the attention blocks' qkv / proj_out: a 1x1 over [n, c, t] viewed as [n, c, t, 1]
         return kernels.conv2d_direct(x.unsqueeze(-1), conv.weight, b).squeeze(-1)
+    extra = (x2,) if x2 is not None else ()
+    if (isinstance(conv, nn.Conv2d) and not upsample
+            and kernels.conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra)):
+        return kernels.conv3x3_wino(x, conv.weight, b, extra=extra)  # the skip concat read in place
     if x2 is not None:
         x = torch.cat([x, x2], dim=1)
     if upsample:
