@@ -52,4 +52,13 @@ with torch.no_grad():
         tot[1] += min(t1, t2) * calls
         print(f"{t1:8.1f} {t2:8.1f} {gf:6.2f} {gf / t2 * 1e3:6.1f} {calls:5d}  {(n, ci, co, h, w)} rel.err={err:.1e}",
               flush=True)
+    # the to_gaussians head reads its input concatenation (refine_out, images, projected features) in
+    # place: the same 163 -> 168 conv through the multi-source entry point
+    parts = [torch.randn(2, c, 256, 256, device=dev) for c in (32, 3, 128)]
+    wt = torch.randn(168, 163, 3, 3, device=dev) * (1.0 / (9 * 163) ** 0.5)
+    b = torch.randn(168, device=dev)
+    t2 = timeit(lambda: K.conv3x3_wino(parts[0], wt, b, extra=tuple(parts[1:])))
+    ref = F.conv2d(torch.cat(parts, 1), wt, b, 1, 1)
+    err = ((K.conv3x3_wino(parts[0], wt, b, extra=tuple(parts[1:])) - ref).abs().max() / ref.abs().max()).item()
+    print(f"{'':8s} {t2:8.1f}  (2, 32+3+128, 168, 256, 256) read in place, rel.err={err:.1e}")
 print(f"total per step: miopen {tot[0]:.1f} us, best-of {tot[1]:.1f} us")

@@ -9,14 +9,18 @@
 //   U = G g G^T for the 3x3 filter g (precomputed once per weight version, tsplat_wino_weight_f32),
 //   16 independent GEMMs (xi = 4 r + s) in v_mfma_f32_32x32x2_f32 -- 2.25x fewer products than
 //   the direct convolution, at the same exact-fp32 MFMA rate.
-// Workgroup = 4 waves = 32 output channels x 32 output tiles (2x2 pixels each, a TBY x TBX patch
-// of tiles), wave w owns transform row r = w (xi = 4w .. 4w + 3: 64 accumulator registers).
-// Per 8-channel chunk: every thread transforms one (tile, channel) patch into a double-buffered
-// LDS image sV[xi][ci][tile] (loads of the next chunk issued before this chunk's MFMAs), one
-// barrier, then 16 MFMAs per wave (A = the packed U fragment, 256 contiguous bytes per wave,
-// prefetched a chunk ahead; B = one LDS float per lane). Epilogue: each wave folds its row of M
-// into Z[r][j] = (M A)[r][j], the 4 rows meet in LDS, and Y = A^T Z + bias (+ ReLU / GELU) is
-// stored as float2 pixel pairs.
+// Two workgroup shapes over the same packed filters (one transform row r of 4 GEMMs per wave, 64
+// accumulator registers):
+//  * conv_kernel (4 waves): 32 output channels x 32 output tiles (2x2 pixels each, a TBY x TBX
+//    patch of tiles). Per 8-channel chunk every thread transforms one (tile, channel) patch into a
+//    double-buffered LDS image sV[xi][ci][tile] (the next chunk's loads fly during this chunk's
+//    MFMAs), one barrier, 16 MFMAs per wave.
+//  * conv64_kernel (8 waves): 64 output channels x 32 tiles, so each input transform feeds twice
+//    the MFMAs; 16-channel chunks, 32 MFMAs per wave per chunk, and the transform of chunk c + 1
+//    is done between the two halves of chunk c's MFMAs (its loads were issued a chunk earlier).
+// A = the packed U fragment (float4 loads, prefetched a chunk ahead), B = one LDS float per lane.
+// Epilogue: each wave folds its row of M into Z[r][j] = (M A)[r][j], the rows meet in LDS, and
+// Y = A^T Z + bias (+ ReLU / GELU) is stored as float2 pixel pairs.
 #include <stdlib.h>
 
 #include "common.h"
@@ -28,20 +32,22 @@ namespace wino {
 constexpr int kThreads = 256;
 constexpr int kCoB = 32;     // output channels per workgroup
 constexpr int kTiles = 32;   // output tiles per workgroup
-constexpr int kCiB = 8;      // channel padding granule; a chunk is CIB = 8 or 16 channels
+constexpr int kCiB = 8;      // channels per chunk of conv_kernel (16 for conv64_kernel)
+constexpr int kGroup = 16;   // packed-filter channel group: [xi][co block][group][lane][8 slots]
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-constexpr int kMaxSrc = 6;  // input sources concatenated along channels (read in place)
+constexpr int kMaxSrc = 6;     // input sources concatenated along channels (read in place)
+constexpr int kMaxCiPad = 1024;  // input channels (padded to 16) of one launch
 
 struct Args {
     const float* src[kMaxSrc];  // source s: [n][cs[s]][h][w]; channel c of the conv input is
     int cs[kMaxSrc];            // channel c - (cs[0] + .. + cs[s-1]) of the source it falls in
     int nsrc;
-    const float* u;      // packed U: [16][co_blocks][ci_pad / 2][2][32]
+    const float* u;      // packed U: [16][cobs][ci_pad / 16][64 lanes][8 slots]
     const float* bias;   // [co] or null
     float* y;            // [n][co][h][w]
-    int n, ci, h, w, co, ci_pad, co_blocks;
+    int n, ci, h, w, co, ci_pad, cobs;  // cobs = 32-channel blocks in the packing (even)
     int th, tw, tbx, tby, bx, by;  // tiles per image, tile-block shape, tile blocks per image row / column
     int act;             // 0 none, 1 ReLU, 2 GELU (erf)
 };
@@ -53,12 +59,16 @@ __device__ __forceinline__ float act_fn(float v, int act) {
 }
 
 // U = G g G^T, G = [[1, 0, 0], [1/2, 1/2, 1/2], [1/2, -1/2, 1/2], [0, 0, 1]], packed as the A
-// operand of v_mfma_f32_32x32x2_f32: lane l of k-step (ci pair) p reads U[co = 32 b + (l & 31)]
-// [ci = 2 p + (l >> 5)], i.e. 64 consecutive floats. Padded co / ci entries are 0.
+// operand of v_mfma_f32_32x32x2_f32: lane l (co = 32 b + (l & 31), k half h = l >> 5) of channel
+// group gr holds 8 consecutive floats, slot 4 q + k <- ci = 16 gr + 8 q + 4 h + k, so an 8-channel
+// chunk q is one float4 per lane and a 16-channel chunk two. MFMA k-step k of a chunk therefore
+// pairs channels 4 h + k (the B operand reads the same rows). Padded co / ci entries are 0.
+__device__ __forceinline__ int chunk_row(int h, int k) { return 8 * (k >> 2) + 4 * h + (k & 3); }
+
 __global__ void __launch_bounds__(256) weight_kernel(const float* __restrict__ g, float* __restrict__ u, int co,
-                                                     int ci, int ci_pad, int co_blocks) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;  // over co_blocks * 32 * ci_pad
-    if (idx >= co_blocks * 32 * ci_pad) return;
+                                                     int ci, int ci_pad, int cobs) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;  // over cobs * 32 * ci_pad
+    if (idx >= cobs * 32 * ci_pad) return;
     const int c = idx % ci_pad, o = idx / ci_pad;
     float k[3][3];
     const bool ok = o < co && c < ci;
@@ -75,101 +85,161 @@ __global__ void __launch_bounds__(256) weight_kernel(const float* __restrict__ g
         t[3][j] = k[2][j];
     }
     const int b = o / 32, ol = o % 32;
-    const size_t plane = (size_t)co_blocks * ci_pad * 32;  // floats per xi
+    const int gr = c / kGroup, rem = c % kGroup;
+    const int q = rem >> 3, h = (rem >> 2) & 1, kk = rem & 3;
+    const size_t plane = (size_t)cobs * ci_pad * 32;  // floats per xi
+    const size_t off = (((size_t)b * (ci_pad / kGroup) + gr) * 64 + 32 * h + ol) * 8 + 4 * q + kk;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         const float uu[4] = {t[r][0], 0.5f * (t[r][0] + t[r][1] + t[r][2]), 0.5f * (t[r][0] - t[r][1] + t[r][2]),
                              t[r][2]};
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-            u[(4 * r + s) * plane + (((size_t)b * (ci_pad / 2) + c / 2) * 2 + (c & 1)) * 32 + ol] = uu[s];
+        for (int s = 0; s < 4; ++s) u[(4 * r + s) * plane + off] = uu[s];
     }
 }
 
-template <int CIB>
-__global__ void __launch_bounds__(kThreads) conv_kernel(Args a) {
-    constexpr int kP = CIB * kTiles / kThreads;  // (tile, channel) patches per thread per chunk
-    __shared__ __attribute__((aligned(16))) float smem[2 * 16 * CIB * kTiles];  // sV x2, then Z
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int cob = blockIdx.y;
-    const int blocks_per_img = a.bx * a.by;
-    const int img = blockIdx.x / blocks_per_img, blk = blockIdx.x % blocks_per_img;
-    const int ty0 = (blk / a.bx) * a.tby, tx0 = (blk % a.bx) * a.tbx;
-
-    // this thread's transform slots: tile tt, channels cc + 8 k of each chunk
-    const int tt = tid % kTiles, cc = tid / kTiles;
-    const int ty = ty0 + tt / a.tbx, tx = tx0 + tt % a.tbx;
-    const bool tile_ok = ty < a.th && tx < a.tw;
-    const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
-    const size_t hw = (size_t)a.h * a.w;
-    // per-row / per-column validity of the 4x4 patch (zero padding)
+// One thread's (tile, channel) transform slot: the 4x4 input patch of output tile tt of the
+// workgroup's tile block, for channel cc of every chunk.
+struct Patch {
+    int img, tt, y0, x0;
     bool rok[4], cok[4];
+    size_t hw;
+
+    __device__ __forceinline__ Patch(const Args& a, int blk_linear, int tid) {
+        const int blocks_per_img = a.bx * a.by;
+        img = blk_linear / blocks_per_img;
+        const int blk = blk_linear % blocks_per_img;
+        const int ty0 = (blk / a.bx) * a.tby, tx0 = (blk % a.bx) * a.tbx;
+        tt = tid % kTiles;
+        const int ty = ty0 + tt / a.tbx, tx = tx0 + tt % a.tbx;
+        const bool tile_ok = ty < a.th && tx < a.tw;
+        y0 = 2 * ty - 1;
+        x0 = 2 * tx - 1;
+        hw = (size_t)a.h * a.w;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        rok[i] = tile_ok && y0 + i >= 0 && y0 + i < a.h;
-        cok[i] = x0 + i >= 0 && x0 + i < a.w;
-    }
-    float d[kP][16];
-    auto load_patch = [&](int chunk) {
-#pragma unroll
-        for (int k = 0; k < kP; ++k) {
-            const int c = chunk * CIB + cc + 8 * k;
-            // the source holding input channel c (channels past ci read the last one, zeroed)
-            const float* src = nullptr;
-            {
-                int rem = min(c, a.ci - 1);
-#pragma unroll
-                for (int q = 0; q < kMaxSrc; ++q) {
-                    if (q < a.nsrc && !src) {
-                        if (rem < a.cs[q])
-                            src = a.src[q] + ((size_t)img * a.cs[q] + rem) * hw;
-                        else
-                            rem -= a.cs[q];
-                    }
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const bool ok = c < a.ci && rok[i] && cok[j];
-                    d[k][4 * i + j] = ok ? src[(size_t)(y0 + i) * a.w + (x0 + j)] : 0.0f;
-                }
+        for (int i = 0; i < 4; ++i) {  // per-row / per-column validity (zero padding)
+            rok[i] = tile_ok && y0 + i >= 0 && y0 + i < a.h;
+            cok[i] = x0 + i >= 0 && x0 + i < a.w;
         }
-    };
-    auto transform_store = [&](float* sV) {
+    }
+
+    // this image's plane of every (padded) input channel, in the source holding it (past ci: the
+    // last channel's, never dereferenced); filled once per workgroup, so the per-chunk lookup is one
+    // LDS read for concatenated inputs too
+    __device__ __forceinline__ void fill_planes(const Args& a, const float** planes, int tid, int nthreads) const {
+        for (int c = tid; c < a.ci_pad; c += nthreads) {
+            const float* src = nullptr;
+            int rem = min(c, a.ci - 1);
+            for (int q = 0; q < a.nsrc && !src; ++q) {
+                if (rem < a.cs[q])
+                    src = a.src[q] + ((size_t)img * a.cs[q] + rem) * hw;
+                else
+                    rem -= a.cs[q];
+            }
+            planes[c] = src;
+        }
+    }
+
+    // input channel c (channels past ci are zero). Loads stay predicated: unconditional loads from
+    // clamped addresses with the zero padding applied in the transform measured slower (more
+    // registers; 3 -> 2 waves per SIMD for conv_kernel).
+    __device__ __forceinline__ void load(const Args& a, const float* const* planes, int c, float (&d)[16]) const {
+        // global address space: a pointer read from LDS would otherwise make these flat loads
+        const __attribute__((address_space(1))) float* src =
+            (const __attribute__((address_space(1))) float*)planes[c];
 #pragma unroll
-        for (int k = 0; k < kP; ++k) {
-            const float* dd = d[k];
-            const int cl = cc + 8 * k;
-            float t[16];  // B^T d
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                t[0 + j] = dd[0 + j] - dd[8 + j];
-                t[4 + j] = dd[4 + j] + dd[8 + j];
-                t[8 + j] = dd[8 + j] - dd[4 + j];
-                t[12 + j] = dd[4 + j] - dd[12 + j];
+                const bool ok = c < a.ci && rok[i] && cok[j];
+                d[4 * i + j] = ok ? src[(size_t)(y0 + i) * a.w + (x0 + j)] : 0.0f;
             }
+    }
+
+    // V = B^T d B into sV[xi][row][tile] (row stride kTiles, xi stride rows * kTiles)
+    __device__ __forceinline__ void transform_store(const float (&dd)[16], float* sV, int row, int rows) const {
+        float t[16];  // B^T d
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {  // (B^T d) B
-                const float v0 = t[4 * r] - t[4 * r + 2], v1 = t[4 * r + 1] + t[4 * r + 2];
-                const float v2 = t[4 * r + 2] - t[4 * r + 1], v3 = t[4 * r + 1] - t[4 * r + 3];
-                sV[((4 * r + 0) * CIB + cl) * kTiles + tt] = v0;
-                sV[((4 * r + 1) * CIB + cl) * kTiles + tt] = v1;
-                sV[((4 * r + 2) * CIB + cl) * kTiles + tt] = v2;
-                sV[((4 * r + 3) * CIB + cl) * kTiles + tt] = v3;
-            }
+        for (int j = 0; j < 4; ++j) {
+            t[0 + j] = dd[0 + j] - dd[8 + j];
+            t[4 + j] = dd[4 + j] + dd[8 + j];
+            t[8 + j] = dd[8 + j] - dd[4 + j];
+            t[12 + j] = dd[4 + j] - dd[12 + j];
         }
-    };
-    // A fragments of one chunk for this wave's 4 xi: [s][k-step]
-    const size_t plane = (size_t)a.co_blocks * a.ci_pad * 32;
-    const float* ub = a.u + (size_t)(4 * wid) * plane + (size_t)cob * (a.ci_pad / 2) * 64 + lane;
-    float af[4][CIB / 2];
-    auto load_a = [&](int chunk) {
+        float* p = sV + row * kTiles + tt;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {  // (B^T d) B
+            p[(4 * r + 0) * rows * kTiles] = t[4 * r] - t[4 * r + 2];
+            p[(4 * r + 1) * rows * kTiles] = t[4 * r + 1] + t[4 * r + 2];
+            p[(4 * r + 2) * rows * kTiles] = t[4 * r + 2] - t[4 * r + 1];
+            p[(4 * r + 3) * rows * kTiles] = t[4 * r + 1] - t[4 * r + 3];
+        }
+    }
+};
+
+// Z[r][j] = (M A)[r][j] of one wave's transform row r (acc[s] = M[4 r + s]) into
+// zs[(r * 2 + j) * 1024 + co * 32 + tile]; C layout of 32x32x2: lane l holds tile l & 31, rows (co)
+// (e & 3) + 8 (e >> 2) + 4 (l >> 5).
+__device__ __forceinline__ void fold_row(const floatx16 (&acc)[4], float* zs, int r, int lane) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const int col = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        zs[((r * 2 + 0) * kCoB + col) * kTiles + (lane & 31)] = acc[0][e] + acc[1][e] + acc[2][e];
+        zs[((r * 2 + 1) * kCoB + col) * kTiles + (lane & 31)] = acc[1][e] - acc[2][e] - acc[3][e];
+    }
+}
+
+// Y = A^T Z + bias (+ act) for output channel o (Z slab zs) and workgroup tile t2
+__device__ __forceinline__ void store_tile(const Args& a, const float* zs, int col, int t2, int o, int img,
+                                           int blk_linear) {
+    const int blk = blk_linear % (a.bx * a.by);
+    const int oty = (blk / a.bx) * a.tby + t2 / a.tbx, otx = (blk % a.bx) * a.tbx + t2 % a.tbx;
+    if (o >= a.co || oty >= a.th || otx >= a.tw) return;
+    const size_t hw = (size_t)a.h * a.w;
+    const float bv = a.bias ? a.bias[o] : 0.0f;
+    float z[4][2];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) z[r][j] = zs[((r * 2 + j) * kCoB + col) * kTiles + t2];
+    float* dst = a.y + ((size_t)img * a.co + o) * hw;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int py = 2 * oty + i;
+        if (py >= a.h) continue;
+        const float y0v = i == 0 ? z[0][0] + z[1][0] + z[2][0] : z[1][0] - z[2][0] - z[3][0];
+        const float y1v = i == 0 ? z[0][1] + z[1][1] + z[2][1] : z[1][1] - z[2][1] - z[3][1];
+        const float r0 = act_fn(y0v + bv, a.act), r1 = act_fn(y1v + bv, a.act);
+        const int px = 2 * otx;
+        float* p = dst + (size_t)py * a.w + px;
+        if (px + 1 < a.w && ((reinterpret_cast<uintptr_t>(p) & 7) == 0)) {
+            *reinterpret_cast<float2*>(p) = make_float2(r0, r1);
+        } else {
+            p[0] = r0;
+            if (px + 1 < a.w) p[1] = r1;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kThreads) conv_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) float smem[2 * 16 * kCiB * kTiles];  // sV x2, then Z
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int cob = blockIdx.y;
+    __shared__ const float* planes[kMaxCiPad];
+    const Patch pt(a, blockIdx.x, tid);
+    const int cc = tid / kTiles;  // channel of each chunk this thread transforms
+    float d[16];
+    pt.fill_planes(a, planes, tid, kThreads);
+    __syncthreads();
+
+    // A fragments of one chunk for this wave's 4 xi: 8-channel chunk ch = half ch & 1 of group ch >> 1
+    const size_t plane = (size_t)a.cobs * a.ci_pad * 32;
+    const float* ub = a.u + (size_t)(4 * wid) * plane + (size_t)cob * (a.ci_pad / kGroup) * 512 + lane * 8;
+    float4 af[4];
+    auto load_a = [&](int chunk, float4 (&f)[4]) {
 #pragma unroll
         for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int kp = 0; kp < CIB / 2; ++kp) af[s][kp] = ub[s * plane + (size_t)(chunk * (CIB / 2) + kp) * 64];
+            f[s] = *reinterpret_cast<const float4*>(ub + s * plane + (size_t)(chunk >> 1) * 512 + 4 * (chunk & 1));
     };
 
     floatx16 acc[4];
@@ -178,72 +248,122 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[s][r] = 0.0f;
 
-    const int nchunks = a.ci_pad / CIB;
-    load_patch(0);
-    load_a(0);
+    const int nchunks = a.ci_pad / kCiB;
+    pt.load(a, planes, cc, d);
+    load_a(0, af);
     for (int ch = 0; ch < nchunks; ++ch) {
-        float* sV = smem + (ch & 1) * (16 * CIB * kTiles);
-        transform_store(sV);
+        float* sV = smem + (ch & 1) * (16 * kCiB * kTiles);
+        pt.transform_store(d, sV, cc, kCiB);
         __syncthreads();  // sV(ch) complete; every wave is done with sV(ch - 2) = this buffer's last use
-        float an[4][CIB / 2];
+        float4 an[4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int kp = 0; kp < CIB / 2; ++kp) an[s][kp] = af[s][kp];
+        for (int s = 0; s < 4; ++s) an[s] = af[s];
         if (ch + 1 < nchunks) {  // the next chunk's loads fly during this chunk's MFMAs
-            load_patch(ch + 1);
-            load_a(ch + 1);
+            pt.load(a, planes, (ch + 1) * kCiB + cc, d);
+            load_a(ch + 1, af);
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-            const float* bsrc = sV + ((4 * wid + s) * CIB) * kTiles + lane;  // [2kp + (l >> 5)][l & 31]
+            // k-step k: lane half h reads channel row 4 h + k
+            const float* bsrc = sV + ((4 * wid + s) * kCiB) * kTiles + (lane & 31) + 4 * kTiles * (lane >> 5);
+            const float av[4] = {an[s].x, an[s].y, an[s].z, an[s].w};
 #pragma unroll
-            for (int kp = 0; kp < CIB / 2; ++kp)
-                acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(an[s][kp], bsrc[2 * kp * kTiles], acc[s], 0, 0, 0);
+            for (int k = 0; k < 4; ++k)
+                acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[k], bsrc[k * kTiles], acc[s], 0, 0, 0);
         }
     }
     __syncthreads();  // all MFMAs' LDS reads done: smem becomes Z[r][j][co 32][tile 32]
-    // C layout of 32x32x2: lane l holds tile l & 31, rows (co) (e & 3) + 8 (e >> 2) + 4 (l >> 5)
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        const int col = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        const float z0 = acc[0][e] + acc[1][e] + acc[2][e];
-        const float z1 = acc[1][e] - acc[2][e] - acc[3][e];
-        smem[((wid * 2 + 0) * kCoB + col) * kTiles + (lane & 31)] = z0;
-        smem[((wid * 2 + 1) * kCoB + col) * kTiles + (lane & 31)] = z1;
-    }
+    fold_row(acc, smem, wid, lane);
     __syncthreads();
-    const size_t out_img = (size_t)img * a.co * hw;
 #pragma unroll
     for (int k = 0; k < (kCoB * kTiles) / kThreads; ++k) {
         const int pidx = tid + kThreads * k;
-        const int col = pidx / kTiles, t2 = pidx % kTiles;
-        const int o = cob * kCoB + col;
-        const int oty = ty0 + t2 / a.tbx, otx = tx0 + t2 % a.tbx;
-        if (o >= a.co || oty >= a.th || otx >= a.tw) continue;
-        const float bv = a.bias ? a.bias[o] : 0.0f;
-        float z[4][2];
+        const int col = pidx / kTiles;
+        store_tile(a, smem, col, pidx % kTiles, cob * kCoB + col, pt.img, blockIdx.x);
+    }
+}
+
+// 8 waves: wave w = (co half hh = w >> 2, transform row r = w & 3); 16-channel chunks, thread tid
+// transforms channel tid / 32 of each chunk (one patch). Per chunk c: A(c + 1) prefetch, MFMA
+// k-steps 0..3, transform of patch c + 1 into the other sV buffer and the loads of patch c + 2,
+// MFMA k-steps 4..7, one barrier.
+constexpr int kThreads64 = 512;
+constexpr int kCiB64 = 16;
+
+__global__ void __launch_bounds__(kThreads64) conv64_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) float smem[2 * 16 * kCiB64 * kTiles];  // sV x2 (64 KB), then Z
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int hh = wid >> 2, rr = wid & 3;
+    const int cob = blockIdx.y;  // 64-channel block = 32-channel blocks 2 cob, 2 cob + 1
+    __shared__ const float* planes[kMaxCiPad];
+    const Patch pt(a, blockIdx.x, tid);
+    const int cc = tid / kTiles;
+    float d[16];
+    pt.fill_planes(a, planes, tid, kThreads64);
+    __syncthreads();
+
+    const size_t plane = (size_t)a.cobs * a.ci_pad * 32;
+    const float* ub =
+        a.u + (size_t)(4 * rr) * plane + (size_t)(2 * cob + hh) * (a.ci_pad / kGroup) * 512 + lane * 8;
+    auto load_a = [&](int chunk, float4 (&f)[4][2]) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-            for (int j = 0; j < 2; ++j) z[r][j] = smem[((r * 2 + j) * kCoB + col) * kTiles + t2];
-        float* dst = a.y + out_img + (size_t)o * hw;
+            for (int q = 0; q < 2; ++q)
+                f[s][q] = *reinterpret_cast<const float4*>(ub + s * plane + (size_t)chunk * 512 + 4 * q);
+    };
+
+    floatx16 acc[4];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int py = 2 * oty + i;
-            if (py >= a.h) continue;
-            const float y0v = i == 0 ? z[0][0] + z[1][0] + z[2][0] : z[1][0] - z[2][0] - z[3][0];
-            const float y1v = i == 0 ? z[0][1] + z[1][1] + z[2][1] : z[1][1] - z[2][1] - z[3][1];
-            const float r0 = act_fn(y0v + bv, a.act), r1 = act_fn(y1v + bv, a.act);
-            const int px = 2 * otx;
-            float* p = dst + (size_t)py * a.w + px;
-            if (px + 1 < a.w && ((reinterpret_cast<uintptr_t>(p) & 7) == 0)) {
-                *reinterpret_cast<float2*>(p) = make_float2(r0, r1);
-            } else {
-                p[0] = r0;
-                if (px + 1 < a.w) p[1] = r1;
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[s][r] = 0.0f;
+
+    // k-steps [q * 4, q * 4 + 4) of chunk ch (lane half h reads channel row chunk_row(h, k))
+    auto mfma_half = [&](const float* sV, const float4 (&f)[4][2], int q) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const float* bsrc = sV + ((4 * rr + s) * kCiB64 + chunk_row(lane >> 5, 4 * q + k)) * kTiles + (lane & 31);
+                const float av = k == 0 ? f[s][q].x : k == 1 ? f[s][q].y : k == 2 ? f[s][q].z : f[s][q].w;
+                acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, *bsrc, acc[s], 0, 0, 0);
             }
+    };
+
+    const int nchunks = a.ci_pad / kCiB64;
+    auto step = [&](int ch, const float4 (&cur)[4][2], float4 (&nxt)[4][2]) {
+        const float* sV = smem + (ch & 1) * (16 * kCiB64 * kTiles);
+        float* sN = smem + ((ch + 1) & 1) * (16 * kCiB64 * kTiles);
+        const bool more = ch + 1 < nchunks;
+        if (more) load_a(ch + 1, nxt);
+        mfma_half(sV, cur, 0);
+        if (more) {
+            pt.transform_store(d, sN, cc, kCiB64);
+            if (ch + 2 < nchunks) pt.load(a, planes, (ch + 2) * kCiB64 + cc, d);
         }
+        mfma_half(sV, cur, 1);
+        if (more) __syncthreads();  // sV(ch + 1) complete; every wave is done reading sV(ch)
+    };
+    float4 af[4][2], af2[4][2];
+    pt.load(a, planes, cc, d);
+    load_a(0, af);
+    pt.transform_store(d, smem, cc, kCiB64);
+    if (nchunks > 1) pt.load(a, planes, kCiB64 + cc, d);
+    __syncthreads();
+    for (int ch = 0; ch < nchunks; ch += 2) {
+        step(ch, af, af2);
+        if (ch + 1 < nchunks) step(ch + 1, af2, af);
+    }
+    __syncthreads();  // all MFMAs' LDS reads done: smem becomes Z[hh][r][j][co 32][tile 32]
+    fold_row(acc, smem + hh * (8 * kCoB * kTiles), rr, lane);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < (2 * kCoB * kTiles) / kThreads64; ++k) {
+        const int pidx = tid + kThreads64 * k;
+        const int colg = pidx / kTiles;  // 0..63
+        store_tile(a, smem + (colg >> 5) * (8 * kCoB * kTiles), colg & 31, pidx % kTiles, cob * 64 + colg, pt.img,
+                   blockIdx.x);
     }
 }
 
@@ -252,20 +372,20 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(Args a) {
 
 using namespace tsplat;
 
-// input channels are padded to 16 (the larger chunk) in the packed filters
-static int wino_ci_pad(int ci) { return (ci + 15) / 16 * 16; }
+// input channels are padded to the 16-channel group, output channels to 64 (an even number of
+// 32-channel blocks, so both workgroup shapes read the same packing)
+static int wino_ci_pad(int ci) { return (ci + wino::kGroup - 1) / wino::kGroup * wino::kGroup; }
+static int wino_cobs(int co) { return (co + 63) / 64 * 2; }
 
 extern "C" size_t tsplat_wino_weight_floats(int32_t co, int32_t ci) {
     if (co <= 0 || ci <= 0) return 0;
-    const int ci_pad = wino_ci_pad(ci);
-    const int cob = (co + wino::kCoB - 1) / wino::kCoB;
-    return (size_t)16 * cob * ci_pad * 32;
+    return (size_t)16 * wino_cobs(co) * wino_ci_pad(ci) * 32;
 }
 
 extern "C" int tsplat_wino_weight_f32(const float* weight, float* packed, int32_t co, int32_t ci, void* stream_) {
     if (!weight || !packed || co <= 0 || ci <= 0) return TSPLAT_EINVAL;
     const int ci_pad = wino_ci_pad(ci);
-    const int cob = (co + wino::kCoB - 1) / wino::kCoB;
+    const int cob = wino_cobs(co);
     const int total = cob * 32 * ci_pad;
     hipLaunchKernelGGL(wino::weight_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream_, weight,
                        packed, co, ci, ci_pad, cob);
@@ -297,7 +417,8 @@ static int wino_launch(const float* const* srcs, const int32_t* chans, int32_t n
     a.w = w;
     a.co = co;
     a.ci_pad = wino_ci_pad(ci);
-    a.co_blocks = (co + wino::kCoB - 1) / wino::kCoB;
+    if (a.ci_pad > wino::kMaxCiPad) return TSPLAT_EINVAL;
+    a.cobs = wino_cobs(co);
     a.th = (h + 1) / 2;
     a.tw = (w + 1) / 2;
     // tile block of 32 tiles: the widest of 32 x 1, 16 x 2, 8 x 4 with the fewest padded tiles
@@ -319,16 +440,18 @@ static int wino_launch(const float* const* srcs, const int32_t* chans, int32_t n
     a.act = act;
     hipStream_t stream = (hipStream_t)stream_;
     TSPLAT_PROF_BEGIN(prof::kWinoConv, stream);
-    // 8-channel chunks: 3 workgroups per CU (16-channel chunks, 2 per CU, measured 2-5 % slower;
-    // TSPLAT_WINO_CIB=16 selects them). Two 32-channel output blocks per workgroup (128
-    // accumulators per lane) spilled at 2 waves per SIMD and ran 1.3-2x slower.
-    const char* e = getenv("TSPLAT_WINO_CIB");
-    if (e && atoi(e) == 16)
-        hipLaunchKernelGGL(wino::conv_kernel<16>, dim3(n * a.bx * a.by, a.co_blocks), dim3(wino::kThreads), 0,
-                           stream, a);
+    // 64-channel workgroups where they pad no more output channels than 32-channel ones and the
+    // grid still covers most of the 256 CUs (measured per shape with tools/bench_wino.py: at 128
+    // workgroups the 32-channel grid's 256 is faster, from 160 up the 64-channel one);
+    // TSPLAT_WINO_WG=32 / 64 forces one shape.
+    const int blocks = n * a.bx * a.by;
+    const int cob32 = (co + wino::kCoB - 1) / wino::kCoB, cob64 = (co + 63) / 64;
+    bool wide = cob32 % 2 == 0 && blocks * cob64 >= 160;
+    if (const char* e = getenv("TSPLAT_WINO_WG")) wide = atoi(e) == 64;
+    if (wide)
+        hipLaunchKernelGGL(wino::conv64_kernel, dim3(blocks, cob64), dim3(wino::kThreads64), 0, stream, a);
     else
-        hipLaunchKernelGGL(wino::conv_kernel<8>, dim3(n * a.bx * a.by, a.co_blocks), dim3(wino::kThreads), 0,
-                           stream, a);
+        hipLaunchKernelGGL(wino::conv_kernel, dim3(blocks, cob32), dim3(wino::kThreads), 0, stream, a);
     TSPLAT_PROF_END(prof::kWinoConv, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
