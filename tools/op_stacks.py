@@ -1,11 +1,40 @@
-"""Which Python call sites launch the small copy / add kernels of one e2e step (torch.profiler stacks)."""
+"""Which Python call sites launch the small PyTorch kernels (copies, elementwise, cat, GELU, clamp ...)
+of one e2e step: a TorchDispatchMode records every launching aten op with the innermost repo frame
+that called it (torch.profiler's with_stack comes back empty on this build)."""
 import collections
+import traceback
 
 import torch
-from torch.profiler import ProfilerActivity, profile
+from torch.utils._python_dispatch import TorchDispatchMode
 
 from transplat_amd import synthetic as S
 from transplat_amd.e2e import build_model
+
+# ops that only reshape metadata (no kernel)
+VIEWS = {"view", "_unsafe_view", "reshape", "permute", "transpose", "t", "expand", "unsqueeze", "squeeze", "slice",
+         "select", "as_strided", "alias", "detach", "split", "split_with_sizes", "chunk", "unbind", "narrow",
+         "unflatten", "flatten", "contiguous", "empty", "empty_like", "empty_strided", "new_empty", "lift_fresh",
+         "is_same_size", "size", "stride", "movedim", "unfold", "view_as", "diagonal", "_reshape_alias",
+         "set_", "resize_", "_local_scalar_dense", "item"}
+
+
+class Sites(TorchDispatchMode):
+    def __init__(self):
+        super().__init__()
+        self.agg = collections.Counter()
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        name = func.__name__.split(".")[0]
+        if name not in VIEWS:
+            frames = [f for f in traceback.extract_stack() if "transplat_amd/" in f.filename]
+            where = f"{frames[-1].filename.split('transplat_amd/')[-1]}:{frames[-1].lineno}" if frames else "?"
+            if name == "convolution":  # which convolutions stay on MIOpen
+                x, w = args[0], args[1]
+                where += (f" x{tuple(x.shape)} w{tuple(w.shape)} s{args[3]} bias={args[2] is not None}"
+                          f" cl={x.is_contiguous(memory_format=torch.channels_last)}")
+            self.agg[(name, where)] += 1
+        return func(*args, **(kwargs or {}))
+
 
 dev = torch.device("cuda:0")
 model = build_model(dev)
@@ -13,18 +42,9 @@ data = S.make_batch(1, image_shape=(256, 256), device=dev)
 for _ in range(2):
     model.test_step(data)
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU], with_stack=True, record_shapes=True) as prof:
+mode = Sites()
+with mode:
     model.test_step(data)
-    torch.cuda.synchronize()
-agg = collections.Counter()
-shown = False
-for ev in prof.events():
-    if not shown and ev.name == "aten::copy_":
-        print("sample stack:", ev.stack[:8] if ev.stack else ev.stack)
-        shown = True
-    if ev.name in ("aten::copy_", "aten::add_", "aten::add", "aten::mul", "aten::cat", "aten::fill_", "aten::div"):
-        frames = [f for f in (ev.stack or []) if "transplat_amd" in f or "repo/" in f]
-        where = frames[0] if frames else "?"
-        agg[(ev.name, where)] += 1
-for (name, where), n in agg.most_common(40):
-    print(f"{n:4d} {name:12s} {where}")
+torch.cuda.synchronize()
+for (name, where), n in mode.agg.most_common(90):
+    print(f"{n:4d} {name:24s} {where}")

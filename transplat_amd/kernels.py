@@ -174,7 +174,8 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = "", ext
         raise RuntimeError("transplat HIP ops need device tensors (no CPU path)")
     fused = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32 and _NO_CONV_EPI not in ("all", site)
     if (fused and residual is None and act in _WINO_ACT
-            and conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra)):
+            and conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra,
+                                vs_miopen=True)):
         # the Winograd kernel reads the concatenation in place and applies the bias and the
         # activation in its epilogue
         return conv3x3_wino(x, conv.weight, conv.bias, act, extra)
@@ -464,7 +465,9 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
 # Winograd-transformed weights per weight tensor (same caching rule as _CONV_PACKED)
 _WINO_PACKED: dict = {}
 # Which 3x3 convolutions go to tsplat_conv3x3_wino_f32_fwd: "auto" (the shapes where it beats
-# MIOpen, see conv3x3_wino_ok), "off", "all" (every 3x3 / stride 1 / pad 1 fp32 conv; tests / A/B)
+# MIOpen, see conv3x3_wino_ok), "off", "all" (every 3x3 / stride 1 / pad 1 fp32 conv; tests / A/B),
+# "big" (auto with the direct kernel's FLOP floor also where MIOpen is the alternative; A/B only:
+# same box 322.1 / 322.9 vs auto 323.4 / 323.7 views/s)
 _WINO_MODE = os.environ.get("TSPLAT_WINO", "auto")
 _WINO_ACT = {"none": 0, "relu": 1, "gelu": 2}
 
@@ -488,11 +491,13 @@ def wino_pack_weight(weight):
     return packed
 
 
-def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=()) -> bool:
+def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=(), vs_miopen=False) -> bool:
     """True when tsplat_conv3x3_wino_f32_fwd takes conv2d(x, weight) on the NCHW map x and (mode
     "auto") it is one of the 3x3s where it beats MIOpen's kernels (tools/bench_wino.py): above the
-    direct kernel's FLOP range, and not the few-tile / long-reduction shapes (256 input channels
-    at 32^2: 64 workgroups of 32 serial chunks) where MIOpen stays faster."""
+    direct kernel's FLOP range (unless `vs_miopen`: the caller's alternative is MIOpen, which the
+    Winograd kernel also beats below that range, e.g. 96 -> 96 at 64^2: 20.8 vs 27.1 us), and not
+    the few-tile / long-reduction shapes (256 input channels at 32^2: 64 workgroups of 32 serial
+    chunks) where MIOpen stays faster."""
     if _WINO_MODE == "off" or not x.is_cuda or torch.is_autocast_enabled("cuda") or len(extra) > 5:
         return False
     for t in (x, *extra):
@@ -512,14 +517,16 @@ def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=
     n, _, h, w = x.shape
     co = weight.shape[0]
     groups_ = n * ((h + 1) // 2 * ((w + 1) // 2) + 31) // 32 * ((co + 31) // 32)  # ~ workgroups
-    return (ci >= 16 and co >= 16 and 2.0 * n * h * w * co * ci * 9 > _CONV_MAX_FLOP
+    vs_miopen = vs_miopen and _WINO_MODE != "big"  # "big": the FLOP floor everywhere (A/B knob)
+    return (ci >= 16 and co >= 16 and (vs_miopen or 2.0 * n * h * w * co * ci * 9 > _CONV_MAX_FLOP)
             and (ci <= 192 or groups_ >= 256))
 
 
 def conv2d_forward(mod, x):
     """nn.Conv2d.forward with the 3x3s that conv3x3_wino_ok admits on the Winograd kernel (installed
     on the encoder's Conv2d modules by install_conv2d_dispatch)."""
-    if conv3x3_wino_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation, mod.groups) and mod.padding_mode == "zeros":
+    if (conv3x3_wino_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation, mod.groups, vs_miopen=True)
+            and mod.padding_mode == "zeros"):
         return conv3x3_wino(x, mod.weight, mod.bias)
     return mod._conv_forward(x, mod.weight, mod.bias)
 
