@@ -410,7 +410,8 @@ def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsa
             return False
         weight = weight.unsqueeze(-1)
     co, ci, k, k2 = weight.shape
-    if k != k2 or k not in (1, 3) or stride not in (1, 2) or (upsample and stride != 1):
+    # (the kernel has no strided 1x1 variant: tsplat_conv2d_f32_fwd rejects it)
+    if k != k2 or k not in (1, 3) or stride not in (1, 2) or (upsample and stride != 1) or (k == 1 and stride != 1):
         return False
     pad = padding if padding is not None else k // 2
     if isinstance(pad, (tuple, list)):
@@ -522,12 +523,21 @@ def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=
             and (ci <= 192 or groups_ >= 256))
 
 
+_ENC_DIRECT = os.environ.get("TSPLAT_ENC_DIRECT", "1") != "0"  # A/B knob for conv2d_forward's direct route
+
+
 def conv2d_forward(mod, x):
-    """nn.Conv2d.forward with the 3x3s that conv3x3_wino_ok admits on the Winograd kernel (installed
-    on the encoder's Conv2d modules by install_conv2d_dispatch)."""
-    if (conv3x3_wino_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation, mod.groups, vs_miopen=True)
-            and mod.padding_mode == "zeros"):
-        return conv3x3_wino(x, mod.weight, mod.bias)
+    """nn.Conv2d.forward (installed on the encoder's Conv2d modules by install_conv2d_dispatch):
+    the 3x3s that conv3x3_wino_ok admits on the Winograd kernel, the latency-bound 1x1 / 3x3
+    (stride 1 or 2) ones that conv2d_direct_ok admits on the direct kernel (bias in the epilogue
+    instead of MIOpen's separate bias launch), the rest through MIOpen."""
+    if mod.padding_mode == "zeros" and mod.groups == 1 and tuple(mod.dilation) == (1, 1):
+        if conv3x3_wino_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation, mod.groups, vs_miopen=True):
+            return conv3x3_wino(x, mod.weight, mod.bias)
+        st = mod.stride[0] if mod.stride[0] == mod.stride[1] else 0
+        if (_ENC_DIRECT and st and x.is_contiguous() and x.dtype == torch.float32
+                and conv2d_direct_ok(x, mod.weight, st, mod.padding)):
+            return conv2d_direct(x, mod.weight, mod.bias, st)
     return mod._conv_forward(x, mod.weight, mod.bias)
 
 
