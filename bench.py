@@ -314,6 +314,30 @@ def main():
 
     traffic, traffic_src = committed_traffic(info["dominant"], args.dense_dtype, args.batch)
 
+    # the step's largest hand-written kernel by time (SURVEY §8d's kernel #1 above stays the
+    # headline roofline): the Winograd convolution launches of one step, timed the same way
+    conv_roofline = None
+    if args.workload == "e2e" and args.dense_dtype == "fp32":
+        from transplat_amd import kernels as K
+
+        K.WINO_FLOP_LOG = []
+        _lib.prof_enable("wino_conv")
+        for _ in range(n_prof):
+            prof_step()
+        cms, claunches = _lib.prof_read()
+        _lib.prof_enable(None)
+        log, K.WINO_FLOP_LOG = K.WINO_FLOP_LOG, None
+        if claunches and cms > 0 and len(log) == claunches:
+            gemm = sum(f for f, _ in log) / (cms * 1e-3) / 1e12
+            direct = sum(f for _, f in log) / (cms * 1e-3) / 1e12
+            conv_roofline = {
+                "kernel": "wino_conv", "bound": "mfma", "achieved": gemm, "peak": FP32_MFMA_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": gemm / FP32_MFMA_PEAK_TFS,
+                "flops": "Winograd GEMM products 2*16*ci*co*tiles (the 16 F(2x2,3x3) GEMMs, unpadded)",
+                "direct_equivalent_achieved": direct, "launches_per_step": claunches / n_prof,
+                "ms_per_step": cms / n_prof, "share_of_step": cms / n_prof / (elapsed / args.steps * 1e3),
+            }
+
     views = world * info["views_per_step"] * args.steps
     result = {
         "metric": "novel views/sec at 256x256, 2 ctx views; PSNR parity vs reference",
@@ -349,6 +373,8 @@ def main():
             "launches": launches,
         },
     }
+    if conv_roofline is not None:
+        result["roofline_step_dominant"] = conv_roofline
     if rank == 0 and not args.no_cpu_baseline and cpu_inputs is not None:
         if isinstance(cpu_inputs, tuple) and cpu_inputs[0] == "e2e":
             result["cpu_baseline"] = cpu_baseline_e2e(cpu_inputs[1], args.cpu_baseline_seconds)

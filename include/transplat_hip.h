@@ -163,6 +163,22 @@ int tsplat_msda_fwd(const float* value, const float* loc, const float* weights, 
                     int32_t n, int32_t height, int32_t width, int32_t channels, int32_t queries,
                     int32_t points, void* stream);
 
+/* Multi-scale deformable attention with mmcv's ms_deform_attn_forward contract (replaces
+ * ext_module.ms_deform_attn_forward called from the reference's
+ * MultiScaleDeformableAttnFunction_fp32.forward, src/model/utils/multi_scale_deformable_attn_function.py:111-117,
+ * itself reached from src/model/utils/attention.py:265-267): value [batch, num_keys, num_heads, head_dim],
+ * spatial_shapes [num_levels, 2] int64 (h, w) and level_start_index [num_levels] int64 (first key
+ * of each level) in device memory, sampling_loc [batch, num_queries, num_heads, num_levels,
+ * num_points, 2] (x, y in [0, 1]), attn_weight [batch, num_queries, num_heads, num_levels,
+ * num_points] -> out [batch, num_queries, num_heads * head_dim], fp32. Bilinear sampling at
+ * (x W - 1/2, y H - 1/2) with zero padding, as mmcv. im2col_step: as mmcv, min(batch,
+ * im2col_step) must divide batch (TSPLAT_EINVAL otherwise); it does not change the result.
+ * num_keys must equal sum_l h_l w_l (not checked: the shapes live on the device). */
+int tsplat_ms_deform_attn_fwd(const float* value, const int64_t* spatial_shapes, const int64_t* level_start_index,
+                              const float* sampling_loc, const float* attn_weight, float* out, int32_t batch,
+                              int32_t num_keys, int32_t num_heads, int32_t head_dim, int32_t num_levels,
+                              int32_t num_queries, int32_t num_points, int32_t im2col_step, void* stream);
+
 /* Real-SH rotation matrices, block-diagonal over degrees 0..isqrt(d_sh)-1 (<= 4), one per
  * camera: replaces the reference's e3nn call chain in rotate_sh (src/misc/sh_rotation.py:10-30:
  * matrix_to_angles + wigner_D per degree). rotations [n, 3, 3] row-major float32 (the c2w

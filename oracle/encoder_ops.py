@@ -188,6 +188,28 @@ def msda(value, loc, weights, h: int, w: int):
     return torch.stack(out)
 
 
+def ms_deform_attn(value, spatial_shapes, level_start_index, sampling_locations, attention_weights):
+    """mmcv ms_deform_attn_forward, multi-level multi-head (the contract of the reference's
+    MultiScaleDeformableAttnFunction_fp32, src/model/utils/multi_scale_deformable_attn_function.py:87-121;
+    mmcv itself is absent here, its published im2col bilinear is restated): value
+    [bs, keys, heads, hd] with level l's h x w map at keys [start_l, start_l + h w),
+    sampling_locations [bs, nq, heads, L, P, 2] (x, y in [0, 1]), attention_weights
+    [bs, nq, heads, L, P] -> [bs, nq, heads * hd]; bilinear at (x w - 1/2, y h - 1/2), zero padding."""
+    bs, _, nh, hd = value.shape
+    _, nq, _, nl, _, _ = sampling_locations.shape
+    out = torch.zeros((bs, nq, nh, hd), dtype=torch.float32)
+    for lvl in range(nl):
+        h, w = int(spatial_shapes[lvl, 0]), int(spatial_shapes[lvl, 1])
+        s = int(level_start_index[lvl])
+        for b in range(bs):
+            for m in range(nh):
+                img = value[b, s:s + h * w, m].reshape(h, w, hd).float()
+                loc = sampling_locations[b, :, m, lvl].float()  # [nq, P, 2]
+                smp = bilinear_zero(img, loc[..., 0] * w - 0.5, loc[..., 1] * h - 0.5)  # [nq, P, hd]
+                out[b, :, m] += (smp * attention_weights[b, :, m, lvl].float()[..., None]).sum(1)
+    return out.reshape(bs, nq, nh * hd)
+
+
 # --------------------------------------------------------------------- Gaussian adapter (A1-A4)
 def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape, scale_min: float,
                      scale_max: float, opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1):
@@ -423,7 +445,7 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     return fused_linear(msg, merge_weight, ln=ln, residual=residual)
 
 
-KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "gaussian_adapter", "group_norm",
+KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "ms_deform_attn", "gaussian_adapter", "group_norm",
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
                        "conv_bias_act", "mha", "residual_ln", "depth_softmax", "conv2d_direct_ok",
                        "conv2d_direct", "conv2d_nhwc_ok", "conv2d_nhwc",

@@ -194,12 +194,18 @@ WINO_CASES = [
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("wg", ["auto", "32", "64"])
 @pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES)
-def test_conv3x3_wino_kernel(device, n, ci, co, h, w, bias, act):
+def test_conv3x3_wino_kernel(device, monkeypatch, wg, n, ci, co, h, w, bias, act):
     """Winograd F(2x2, 3x3) fp32 MFMA convolution (tsplat_conv3x3_wino_f32_fwd) against torch's
-    conv2d in float64 on the CPU. The transforms reassociate the products (as MIOpen's Winograd
-    solvers do), so the bound is 2e-5 of the output's max magnitude, like the direct kernel's."""
+    conv2d in float64 on the CPU, with the launch's own workgroup shape choice and with each shape
+    forced (TSPLAT_WINO_WG: 32 output channels / 4 waves, 64 / 8 waves; the 64-wide one pads
+    co to 64). The transforms reassociate the products (as MIOpen's Winograd solvers do), so the
+    bound is 2e-5 of the output's max magnitude, like the direct kernel's."""
     from transplat_amd import kernels as K
+
+    if wg != "auto":
+        monkeypatch.setenv("TSPLAT_WINO_WG", wg)
 
     x = seeded((n, ci, h, w), 41)
     wt = seeded((co, ci, 3, 3), 42) * (1.0 / (9 * ci) ** 0.5)
@@ -239,3 +245,18 @@ def test_conv3x3_wino_reads_concat_in_place(device):
     y_cat = K.conv3x3_wino(parts[0], wt, b, "gelu", extra=tuple(parts[1:]))
     y_ref = K.conv3x3_wino(torch.cat(parts, 1), wt, b, "gelu")
     assert torch.equal(y_cat, y_ref)
+
+
+@pytest.mark.gpu
+def test_conv3x3_wino_wide_shape_at_production_size(device):
+    """The launch picks the 64-output-channel workgroups for the to_gaussians head at 256^2
+    (2 x 163 -> 168, three sources read in place); checked against MIOpen's fp32 conv2d on the
+    materialised concatenation (the full-size float64 CPU reference would take minutes)."""
+    from transplat_amd import kernels as K
+
+    parts = [seeded((2, c, 256, 256), 60 + c).to(device) for c in (32, 3, 128)]
+    wt = (seeded((168, 163, 3, 3), 63) * (1.0 / (9 * 163) ** 0.5)).to(device)
+    b = seeded((168,), 64).to(device)
+    y = K.conv3x3_wino(parts[0], wt, b, extra=tuple(parts[1:]))
+    ref = torch.nn.functional.conv2d(torch.cat(parts, 1), wt, b, padding=1)
+    assert ((y - ref).abs().max() / ref.abs().max()).item() < 2e-5

@@ -148,6 +148,88 @@ def test_msda_kernel(device):
     assert (out - ref).abs().max().item() < 1e-5
 
 
+# ---- mmcv-shaped multi-level / multi-head MSDA (tsplat_ms_deform_attn_fwd)
+def _msda_pytorch(value, shapes, loc, wts):
+    """mmcv's multi_scale_deformable_attn_pytorch (grid_sample form, the published fallback the
+    reference imports at src/model/utils/attention.py:8), restated as the independent check."""
+    import torch.nn.functional as F
+
+    bs, _, nh, hd = value.shape
+    _, nq, _, nl, npt, _ = loc.shape
+    vals = value.split([int(h) * int(w) for h, w in shapes], dim=1)
+    grids = 2 * loc - 1
+    outs = []
+    for lvl, (h, w) in enumerate(shapes):
+        v = vals[lvl].flatten(2).transpose(1, 2).reshape(bs * nh, hd, int(h), int(w))
+        g = grids[:, :, :, lvl].transpose(1, 2).flatten(0, 1)
+        outs.append(F.grid_sample(v, g, mode="bilinear", padding_mode="zeros", align_corners=False))
+    a = wts.transpose(1, 2).reshape(bs * nh, 1, nq, nl * npt)
+    out = (torch.stack(outs, dim=-2).flatten(-2) * a).sum(-1).view(bs, nh * hd, nq)
+    return out.transpose(1, 2).contiguous()
+
+
+def _msda_case(bs, nh, hd, shapes, nq, npt, seed):
+    shapes_t = torch.tensor(shapes, dtype=torch.int64)
+    starts = torch.cat([torch.zeros(1, dtype=torch.int64), (shapes_t[:, 0] * shapes_t[:, 1]).cumsum(0)[:-1]])
+    nk = int((shapes_t[:, 0] * shapes_t[:, 1]).sum())
+    value = seeded((bs, nk, nh, hd), seed)
+    loc = seeded((bs, nq, nh, len(shapes), npt, 2), seed + 1, kind="rand") * 1.3 - 0.15  # some off-map
+    wts = torch.softmax(seeded((bs, nq, nh, len(shapes) * npt), seed + 2), -1).reshape(bs, nq, nh, len(shapes), npt)
+    return value, shapes_t, starts, loc, wts
+
+
+MSDA_CASES = [  # bs, heads, head dim, level shapes, queries, points
+    (2, 8, 32, [(16, 16), (8, 8), (4, 4), (2, 2)], 50, 4),  # deformable-DETR style
+    (1, 1, 128, [(16, 16)], 256, 4),                        # TranSplat's UV self-attention shape
+    (3, 2, 6, [(7, 5), (3, 9)], 33, 3),                     # head dim not a multiple of 4, ragged maps
+]
+
+
+@pytest.mark.parametrize("case", MSDA_CASES)
+def test_oracle_ms_deform_attn_matches_mmcv_pytorch(case):
+    value, shapes, starts, loc, wts = _msda_case(*case, seed=71)
+    ref = _msda_pytorch(value, shapes, loc, wts)
+    out = E.ms_deform_attn(value, shapes, starts, loc, wts)
+    assert (out - ref).abs().max().item() < 1e-5
+
+
+def test_oracle_ms_deform_attn_single_level_is_msda():
+    value, shapes, starts, loc, wts = _msda_case(2, 1, 128, [(12, 12)], 40, 4, seed=75)
+    a = E.ms_deform_attn(value, shapes, starts, loc, wts)
+    b = E.msda(value[:, :, 0], loc[:, :, 0, 0], wts[:, :, 0, 0], 12, 12)
+    assert (a - b).abs().max().item() < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", MSDA_CASES)
+def test_ms_deform_attn_kernel(device, case):
+    from transplat_amd.model.utils.multi_scale_deformable_attn_function import MultiScaleDeformableAttnFunction_fp32
+
+    value, shapes, starts, loc, wts = _msda_case(*case, seed=81)
+    ref = E.ms_deform_attn(value, shapes, starts, loc, wts)
+    out = MultiScaleDeformableAttnFunction_fp32.apply(*(t.to(device) for t in (value, shapes, starts, loc, wts)), 64)
+    assert out.shape == ref.shape and out.dtype == torch.float32
+    assert (out.cpu() - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.gpu
+def test_ms_deform_attn_level_start_index_and_im2col_step(device):
+    """Levels are read from level_start_index (not re-derived from the shapes), and the batch must
+    be divisible by min(batch, im2col_step) as mmcv asserts."""
+    from transplat_amd import kernels as K
+
+    value, shapes, starts, loc, wts = _msda_case(4, 2, 8, [(6, 6), (3, 3)], 20, 2, seed=85)
+    # the same levels stored in the opposite order in value
+    a, b = value[:, :36], value[:, 36:]
+    swapped = torch.cat([b, a], 1)
+    starts2 = torch.tensor([9, 0], dtype=torch.int64)
+    ref = E.ms_deform_attn(value, shapes, starts, loc, wts)
+    out = K.ms_deform_attn(*(t.to(device) for t in (swapped, shapes, starts2, loc, wts)), im2col_step=2)
+    assert (out.cpu() - ref).abs().max().item() < 1e-5
+    with pytest.raises(RuntimeError, match="invalid argument"):
+        K.ms_deform_attn(*(t.to(device) for t in (value, shapes, starts, loc, wts)), im2col_step=3)
+
+
 def _adapter_inputs(b=2, v=2, h=24, w=32, d_sh=25):
     raw = seeded((b, v, h * w, 9 + 3 * d_sh), 61)
     depths = 1.0 + 20 * seeded((b, v, h * w), 62, kind="rand")

@@ -478,10 +478,115 @@ msda_kernel(Geo g, int Q, int P, const float* __restrict__ value, const float* _
     o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
 }
 
+// ---- mmcv ms_deform_attn_forward, general form: value [bs][num_keys][heads][hd] (level l's
+// H_l x W_l map starts at key level_start[l]), sampling_loc [bs][nq][heads][L][P][2] (x, y in
+// [0, 1]), attn_weight [bs][nq][heads][L][P] -> out [bs][nq][heads * hd]. One thread per (query,
+// head, VEC channels): consecutive threads read consecutive channels of a value row. Sampling as
+// mmcv's im2col bilinear: h = y H - 1/2, w = x W - 1/2, taken only for -1 < h < H, -1 < w < W,
+// corners outside the map read as 0, val = w1 v1 + w2 v2 + w3 v3 + w4 v4, col += val * weight.
+template <int VEC>
+__global__ void __launch_bounds__(kThreads)
+ms_deform_attn_kernel(const float* __restrict__ value, const int64_t* __restrict__ shapes,
+                      const int64_t* __restrict__ starts, const float* __restrict__ loc,
+                      const float* __restrict__ attw, float* __restrict__ out, int nk, int nh, int hd, int L,
+                      int nq, int P, size_t total) {
+    const size_t idx = (size_t)blockIdx.x * kThreads + threadIdx.x;
+    if (idx >= total) return;
+    const int groups = hd / VEC;
+    const int cg = (int)(idx % groups);
+    size_t t = idx / groups;
+    const int head = (int)(t % nh);
+    t /= nh;  // = b * nq + q
+    const size_t b = t / nq;
+    const size_t row = (size_t)nh * hd;  // floats per key
+    const float* lw = attw + (t * nh + head) * (size_t)L * P;
+    const float* ll = loc + (t * nh + head) * (size_t)L * P * 2;
+    float acc[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+    for (int l = 0; l < L; ++l) {
+        const int H = (int)shapes[2 * l], W = (int)shapes[2 * l + 1];
+        const float* base = value + (b * nk + (size_t)starts[l]) * row + (size_t)head * hd + cg * VEC;
+        for (int p = 0; p < P; ++p) {
+            const float hi = ll[2 * (l * P + p) + 1] * (float)H - 0.5f;
+            const float wi = ll[2 * (l * P + p)] * (float)W - 0.5f;
+            const float wt = lw[l * P + p];
+            if (!(hi > -1.0f && wi > -1.0f && hi < (float)H && wi < (float)W)) continue;
+            const int h0 = (int)floorf(hi), w0 = (int)floorf(wi), h1 = h0 + 1, w1 = w0 + 1;
+            const float lh = hi - (float)h0, lwt = wi - (float)w0, hh = 1.0f - lh, hwt = 1.0f - lwt;
+            const float f1 = hh * hwt, f2 = hh * lwt, f3 = lh * hwt, f4 = lh * lwt;
+            const bool ok1 = h0 >= 0 && w0 >= 0, ok2 = h0 >= 0 && w1 <= W - 1;
+            const bool ok3 = h1 <= H - 1 && w0 >= 0, ok4 = h1 <= H - 1 && w1 <= W - 1;
+            float v1[VEC], v2[VEC], v3[VEC], v4[VEC];
+            auto fetch = [&](bool ok, int y, int x, float (&v)[VEC]) {
+                if (ok) {
+                    const float* src = base + ((size_t)y * W + x) * row;
+                    if constexpr (VEC == 4) {
+                        const float4 f = *reinterpret_cast<const float4*>(src);
+                        v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < VEC; ++i) v[i] = src[i];
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < VEC; ++i) v[i] = 0.f;
+                }
+            };
+            fetch(ok1, h0, w0, v1);
+            fetch(ok2, h0, w1, v2);
+            fetch(ok3, h1, w0, v3);
+            fetch(ok4, h1, w1, v4);
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) acc[i] += (f1 * v1[i] + f2 * v2[i] + f3 * v3[i] + f4 * v4[i]) * wt;
+        }
+    }
+    float* o = out + (t * nh + head) * (size_t)hd + cg * VEC;
+    if constexpr (VEC == 4) {
+        *reinterpret_cast<float4*>(o) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) o[i] = acc[i];
+    }
+}
+
 }  // namespace corr
 }  // namespace tsplat
 
 using namespace tsplat;
+
+extern "C" int tsplat_ms_deform_attn_fwd(const float* value, const int64_t* spatial_shapes,
+                                         const int64_t* level_start_index, const float* sampling_loc,
+                                         const float* attn_weight, float* out, int32_t batch, int32_t num_keys,
+                                         int32_t num_heads, int32_t head_dim, int32_t num_levels,
+                                         int32_t num_queries, int32_t num_points, int32_t im2col_step,
+                                         void* stream_) {
+    using namespace tsplat::corr;
+    if (!value || !spatial_shapes || !level_start_index || !sampling_loc || !attn_weight || !out || batch <= 0 ||
+        num_keys <= 0 || num_heads <= 0 || head_dim <= 0 || num_levels <= 0 || num_queries <= 0 ||
+        num_points <= 0 || im2col_step <= 0)
+        return TSPLAT_EINVAL;
+    // mmcv: im2col_step_ = min(batch, im2col_step) must divide the batch (it only chunks the
+    // batch for its column buffer; the result does not depend on it)
+    const int step = im2col_step < batch ? im2col_step : batch;
+    if (batch % step) return TSPLAT_EINVAL;
+    const bool v4 = head_dim % 4 == 0 && ((uintptr_t)value & 15) == 0 && ((uintptr_t)out & 15) == 0;
+    const size_t total = (size_t)batch * num_queries * num_heads * (head_dim / (v4 ? 4 : 1));
+    hipStream_t stream = (hipStream_t)stream_;
+    const dim3 grid((unsigned)ceil_div(total, (size_t)kThreads));
+    TSPLAT_PROF_BEGIN(prof::kMsda, stream);
+    if (v4)
+        hipLaunchKernelGGL(ms_deform_attn_kernel<4>, grid, dim3(kThreads), 0, stream, value, spatial_shapes,
+                           level_start_index, sampling_loc, attn_weight, out, num_keys, num_heads, head_dim,
+                           num_levels, num_queries, num_points, total);
+    else
+        hipLaunchKernelGGL(ms_deform_attn_kernel<1>, grid, dim3(kThreads), 0, stream, value, spatial_shapes,
+                           level_start_index, sampling_loc, attn_weight, out, num_keys, num_heads, head_dim,
+                           num_levels, num_queries, num_points, total);
+    TSPLAT_PROF_END(prof::kMsda, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
 
 extern "C" int tsplat_uv_coarse_fwd(const float* feat, const float* cams, const float* disp,
                                     float* out, int32_t batch, int32_t height, int32_t width,

@@ -125,6 +125,30 @@ def uv_cross_direct(value, key, intr, pose, disp, offsets, logits, h: int, w: in
     return out
 
 
+def ms_deform_attn(value, value_spatial_shapes, value_level_start_index, sampling_locations, attention_weights,
+                   im2col_step: int = 64):
+    """mmcv ext_module.ms_deform_attn_forward (tsplat_ms_deform_attn_fwd): value [bs, keys, heads, hd],
+    spatial shapes [L, 2] / level starts [L] (int64), sampling_locations [bs, nq, heads, L, P, 2],
+    attention_weights [bs, nq, heads, L, P] -> [bs, nq, heads * hd] fp32. Raises, as mmcv's
+    assertion does, when min(bs, im2col_step) does not divide bs."""
+    lib = _lib.load()
+    bs, nk, nh, hd = value.shape
+    _, nq, nh2, nl, npt, two = sampling_locations.shape
+    if nh2 != nh or two != 2 or tuple(attention_weights.shape) != (bs, nq, nh, nl, npt):
+        raise ValueError("sampling_locations / attention_weights do not match value's heads")
+    shapes = value_spatial_shapes.to(device=value.device, dtype=torch.int64).contiguous()
+    starts = value_level_start_index.to(device=value.device, dtype=torch.int64).contiguous()
+    if tuple(shapes.shape) != (nl, 2) or tuple(starts.shape) != (nl,):
+        raise ValueError(f"spatial shapes {tuple(shapes.shape)} / level starts {tuple(starts.shape)} != {nl} levels")
+    out = torch.empty((bs, nq, nh * hd), dtype=torch.float32, device=value.device)
+    rc = lib.tsplat_ms_deform_attn_fwd(_lib.ptr(_f32(value)), _lib.ptr(shapes), _lib.ptr(starts),
+                                       _lib.ptr(_f32(sampling_locations)), _lib.ptr(_f32(attention_weights)),
+                                       _lib.ptr(out), bs, nk, nh, hd, nl, nq, npt, int(im2col_step),
+                                       _lib.stream_ptr(value.device))
+    _lib.check(rc, "tsplat_ms_deform_attn_fwd")
+    return out
+
+
 def msda(value, loc, weights, h: int, w: int):
     """Single-level single-head deformable sampling. value [N, HW, C], loc [N, Q, P, 2],
     weights [N, Q, P] -> [N, Q, C] (see oracle.msda)."""
@@ -554,6 +578,11 @@ def install_conv2d_dispatch(module) -> int:
     return n
 
 
+# bench.py's roofline pass sets a list here: one (Winograd GEMM FLOPs, direct-equivalent FLOPs) pair
+# per launch (GEMM FLOPs = 2 * 16 * ci * co * output tiles, the products the 16 MFMA GEMMs compute)
+WINO_FLOP_LOG = None
+
+
 def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=()):
     """act(conv2d(cat([x, *extra], 1), weight, bias, stride 1, padding 1)) via Winograd F(2x2, 3x3)
     on fp32 MFMA; the concatenation is read in place (tsplat_conv3x3_wino_cat_f32_fwd)."""
@@ -563,6 +592,9 @@ def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=()):
     srcs = [_f32(t) for t in (x, *extra)]
     n, _, h, w = srcs[0].shape
     co = weight.shape[0]
+    if WINO_FLOP_LOG is not None:
+        ci = sum(t.shape[1] for t in srcs)
+        WINO_FLOP_LOG.append((2.0 * 16 * ci * co * n * ((h + 1) // 2) * ((w + 1) // 2), 2.0 * n * h * w * co * ci * 9))
     y = torch.empty((n, co, h, w), dtype=torch.float32, device=x.device)
     pb = _f32(bias) if bias is not None else None
     ptrs = (ctypes.c_void_p * len(srcs))(*[_lib.ptr(t) for t in srcs])
