@@ -194,18 +194,20 @@ WINO_CASES = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("wg", ["auto", "32", "64"])
+@pytest.mark.parametrize("wg", ["auto", "32", "32x2", "64"])
 @pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES)
 def test_conv3x3_wino_kernel(device, monkeypatch, wg, n, ci, co, h, w, bias, act):
     """Winograd F(2x2, 3x3) fp32 MFMA convolution (tsplat_conv3x3_wino_f32_fwd) against torch's
     conv2d in float64 on the CPU, with the launch's own workgroup shape choice and with each shape
-    forced (TSPLAT_WINO_WG: 32 output channels / 4 waves, 64 / 8 waves; the 64-wide one pads
-    co to 64). The transforms reassociate the products (as MIOpen's Winograd solvers do), so the
+    forced (TSPLAT_WINO_WG: 32 output channels / 4 waves, 64 / 8 waves, the 64-wide one padding
+    co to 64; TSPLAT_WINO_KS: the 32-wide one with its chunks split over two 4-wave groups). The
+    transforms reassociate the products (as MIOpen's Winograd solvers do), so the
     bound is 2e-5 of the output's max magnitude, like the direct kernel's."""
     from transplat_amd import kernels as K
 
     if wg != "auto":
-        monkeypatch.setenv("TSPLAT_WINO_WG", wg)
+        monkeypatch.setenv("TSPLAT_WINO_WG", wg[:2])
+        monkeypatch.setenv("TSPLAT_WINO_KS", "2" if wg == "32x2" else "1")
 
     x = seeded((n, ci, h, w), 41)
     wt = seeded((co, ci, 3, 3), 42) * (1.0 / (9 * ci) ** 0.5)

@@ -221,15 +221,21 @@ __device__ __forceinline__ void store_tile(const Args& a, const float* zs, int c
     }
 }
 
-__global__ void __launch_bounds__(kThreads) conv_kernel(Args a) {
-    __shared__ __attribute__((aligned(16))) float smem[2 * 16 * kCiB * kTiles];  // sV x2, then Z
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int cob = blockIdx.y;
+// KS k-groups of 4 waves (KS = 2: 8 waves) split the 8-channel chunks of one 32 x 32 output block
+// (group g takes chunks g, g + KS, ...; ci_pad / 8 is even, so both groups run the same number of
+// iterations and meet at every barrier), each with its own double-buffered sV; their Z slabs are
+// summed in the epilogue. For the few-workgroup grids of the 32^2-64^2 maps (one 4-wave workgroup
+// per CU otherwise: one wave per SIMD through 16-32 serial chunks).
+template <int KS>
+__global__ void __launch_bounds__(kThreads * KS) conv_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) float smem[KS * 2 * 16 * kCiB * kTiles];  // sV x2 per group, then Z
     __shared__ const float* planes[kMaxCiPad];
+    const int kg = threadIdx.x / kThreads, tid = threadIdx.x % kThreads, lane = tid & 63, wid = tid >> 6;
+    const int cob = blockIdx.y;
     const Patch pt(a, blockIdx.x, tid);
     const int cc = tid / kTiles;  // channel of each chunk this thread transforms
     float d[16];
-    pt.fill_planes(a, planes, tid, kThreads);
+    pt.fill_planes(a, planes, threadIdx.x, kThreads * KS);
     __syncthreads();
 
     // A fragments of one chunk for this wave's 4 xi: 8-channel chunk ch = half ch & 1 of group ch >> 1
@@ -248,19 +254,20 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[s][r] = 0.0f;
 
-    const int nchunks = a.ci_pad / kCiB;
-    pt.load(a, planes, cc, d);
-    load_a(0, af);
-    for (int ch = 0; ch < nchunks; ++ch) {
-        float* sV = smem + (ch & 1) * (16 * kCiB * kTiles);
+    const int nchunks = a.ci_pad / kCiB;  // even
+    float* sG = smem + kg * (2 * 16 * kCiB * kTiles);
+    pt.load(a, planes, kg * kCiB + cc, d);
+    load_a(kg, af);
+    for (int it = 0, ch = kg; ch < nchunks; ++it, ch += KS) {
+        float* sV = sG + (it & 1) * (16 * kCiB * kTiles);
         pt.transform_store(d, sV, cc, kCiB);
-        __syncthreads();  // sV(ch) complete; every wave is done with sV(ch - 2) = this buffer's last use
+        __syncthreads();  // sV(ch) complete; every wave is done with this buffer's previous chunk
         float4 an[4];
 #pragma unroll
         for (int s = 0; s < 4; ++s) an[s] = af[s];
-        if (ch + 1 < nchunks) {  // the next chunk's loads fly during this chunk's MFMAs
-            pt.load(a, planes, (ch + 1) * kCiB + cc, d);
-            load_a(ch + 1, af);
+        if (ch + KS < nchunks) {  // the next chunk's loads fly during this chunk's MFMAs
+            pt.load(a, planes, (ch + KS) * kCiB + cc, d);
+            load_a(ch + KS, af);
         }
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -272,12 +279,19 @@ __global__ void __launch_bounds__(kThreads) conv_kernel(Args a) {
                 acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[k], bsrc[k * kTiles], acc[s], 0, 0, 0);
         }
     }
-    __syncthreads();  // all MFMAs' LDS reads done: smem becomes Z[r][j][co 32][tile 32]
-    fold_row(acc, smem, wid, lane);
+    __syncthreads();  // all MFMAs' LDS reads done: smem becomes Z[group][r][j][co 32][tile 32]
+    fold_row(acc, smem + kg * (8 * kCoB * kTiles), wid, lane);
     __syncthreads();
+    if (KS > 1) {  // sum the groups' slabs into slab 0
+        for (int i = threadIdx.x; i < 8 * kCoB * kTiles; i += kThreads * KS) {
+            float z = smem[i];
 #pragma unroll
-    for (int k = 0; k < (kCoB * kTiles) / kThreads; ++k) {
-        const int pidx = tid + kThreads * k;
+            for (int g = 1; g < KS; ++g) z += smem[g * (8 * kCoB * kTiles) + i];
+            smem[i] = z;
+        }
+        __syncthreads();
+    }
+    for (int pidx = threadIdx.x; pidx < kCoB * kTiles; pidx += kThreads * KS) {
         const int col = pidx / kTiles;
         store_tile(a, smem, col, pidx % kTiles, cob * kCoB + col, pt.img, blockIdx.x);
     }
@@ -448,10 +462,16 @@ static int wino_launch(const float* const* srcs, const int32_t* chans, int32_t n
     const int cob32 = (co + wino::kCoB - 1) / wino::kCoB, cob64 = (co + 63) / 64;
     bool wide = cob32 % 2 == 0 && blocks * cob64 >= 160;
     if (const char* e = getenv("TSPLAT_WINO_WG")) wide = atoi(e) == 64;
+    // 32-channel workgroups: split each block's chunks over two 4-wave groups while the grid alone
+    // gives at most one workgroup per CU (TSPLAT_WINO_KS=1 / 2 forces)
+    int ks = blocks * cob32 <= 256 ? 2 : 1;
+    if (const char* e = getenv("TSPLAT_WINO_KS")) ks = atoi(e) == 2 ? 2 : 1;
     if (wide)
         hipLaunchKernelGGL(wino::conv64_kernel, dim3(blocks, cob64), dim3(wino::kThreads64), 0, stream, a);
+    else if (ks == 2)
+        hipLaunchKernelGGL(wino::conv_kernel<2>, dim3(blocks, cob32), dim3(2 * wino::kThreads), 0, stream, a);
     else
-        hipLaunchKernelGGL(wino::conv_kernel, dim3(blocks, cob32), dim3(wino::kThreads), 0, stream, a);
+        hipLaunchKernelGGL(wino::conv_kernel<1>, dim3(blocks, cob32), dim3(wino::kThreads), 0, stream, a);
     TSPLAT_PROF_END(prof::kWinoConv, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
