@@ -47,3 +47,27 @@ for name, k1, k2, n, kw in cases:
     fl = 2.0 * M * (k1 + k2) * n
     print(f"{name:16s} M={M} K={k1 + k2} N={n}: fused {us:6.1f} us ({fl / us / 1e6:5.1f} TF, "
           f"{fl / us / 1e6 / 157.3 * 100:4.1f} %)   torch F.linear {tus:6.1f} us", flush=True)
+
+# DINOv2 ViT-B (2 images x 325 tokens): qkv / proj / fc1 (+ exact GELU) / fc2, all with bias, vs
+# hipBLASLt F.linear (+ F.gelu for fc1)
+M = 650
+for name, k, n, gelu in [("dino qkv", 768, 2304, False), ("dino proj", 768, 768, False),
+                         ("dino fc1+gelu", 768, 3072, True), ("dino fc2", 3072, 768, False)]:
+    x, w, bias = r(M, k), r(n, k), r(n)
+    ours = lambda: K.fused_linear(x, w, bias=bias, gelu=gelu)
+    ref = (lambda: F.gelu(F.linear(x, w, bias))) if gelu else (lambda: F.linear(x, w, bias))
+    err = ((ours() - ref()).abs().max() / ref().abs().max()).item()
+    ts = []
+    for fn in (ours, ref):
+        for _ in range(3):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(50):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1) / 50 * 1e3)
+    fl = 2.0 * M * k * n
+    print(f"{name:16s} M={M} K={k} N={n}: fused {ts[0]:6.1f} us ({fl / ts[0] / 1e6:5.1f} TF)   "
+          f"torch {ts[1]:6.1f} us ({fl / ts[1] / 1e6:5.1f} TF)  rel.err={err:.1e}", flush=True)
