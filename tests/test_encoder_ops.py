@@ -322,12 +322,17 @@ def test_window_attention_dtu_stress(device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kern", ["auto", "v2", "v3"])
 @pytest.mark.parametrize("hw,m,shift,b", [(64, 1, False, 2), (64, 1, True, 2), (64, 2, True, 3), (32, 1, True, 16)])
-def test_window_attention_bf16_kernel(device, hw, m, shift, b):
+def test_window_attention_bf16_kernel(device, monkeypatch, kern, hw, m, shift, b):
     """bf16 MFMA variant (config C3) vs the fp32 oracle on the same bf16-rounded inputs: P is
     rounded to bf16 for the PV product, so the bound is bf16-level (1.5e-2 absolute on O(1)
-    outputs)."""
+    outputs). The launch's own kernel choice and each kernel forced (TSPLAT_WINATTN_BF16: v2 =
+    4 waves / 128 queries with key splits, v3 = 8 staggered waves / 256 queries)."""
     from transplat_amd import kernels as K
+
+    if kern != "auto":
+        monkeypatch.setenv("TSPLAT_WINATTN_BF16", kern)
 
     q = seeded((b, hw * hw, 128), 91).bfloat16()
     k = (seeded((b, m, hw * hw, 128), 92) if m > 1 else seeded((b, hw * hw, 128), 92)).bfloat16()
@@ -340,14 +345,17 @@ def test_window_attention_bf16_kernel(device, hw, m, shift, b):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kern", ["auto", "v3"])
 @pytest.mark.parametrize("shift,b", [(False, 2), (True, 2), (True, 16)])
-def test_window_attention_bf16_growing_scores(device, shift, b):
+def test_window_attention_bf16_growing_scores(device, monkeypatch, kern, shift, b):
     """Scores that grow along the key order (keys scaled up to 4x, queries 3x) so the running max
     keeps moving past the bf16 kernel's deferred-rescale threshold on later key tiles (random O(1)
     scores would only take the branch on the first tile); b = 2 runs the split-key partials path,
-    b = 16 the single-pass one."""
+    b = 16 the single-pass one (v3 by default); kern = v3 forces the 8-wave kernel at every b."""
     from transplat_amd import kernels as K
 
+    if kern != "auto":
+        monkeypatch.setenv("TSPLAT_WINATTN_BF16", kern)
     hw = 64
     q = (seeded((b, hw * hw, 128), 94) * 3.0).bfloat16()
     # in-window key position t of pixel (y, x) is (y % 32) * 32 + x % 32: scale by it

@@ -1573,6 +1573,215 @@ win_attn_bf16_v2_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
     }
 }
 
+// ============================================================================================
+// bf16 v3: 8 waves = two 4-wave groups (A: queries 0-127, B: 128-255 of a 256-query block) on the
+// same K / V tiles, staggered by one phase so each SIMD pairs one group's MFMA phase with the other
+// group's VALU phase (cdna_hip_programming.md / MI355X_MICROARCH.md "two waves per SIMD"):
+//   group-local step s (A: s = i, B: s = i - 1 for global interval i, one s_barrier per interval)
+//     s = 2t     (MFMA): O += V(t-1)^T P(t-1)^T (t >= 1), then S(t) = K(t) Q^T (+ mask step)
+//     s = 2t + 1 (VALU): online softmax of S(t) -> P(t) (bf16), and staging: A writes its half of
+//                        tile t + 1, B its half of tile t + 2, then each loads its next half.
+// Tile u lives in LDS buffer u % 3 from its first write (interval 2u - 1 / 2u - 2) to its last
+// read (B's PV at interval 2u + 3); three buffers keep every write after the previous occupant's
+// last read (checked in the comments at the staging code). Operand maps, log2-domain softmax with
+// deferred rescale and the mask step are those of win_attn_bf16_v2_kernel. ksplit == 1 only.
+// ============================================================================================
+constexpr int kThreads8 = 512;
+constexpr int kBQ8 = 256;  // queries per workgroup
+constexpr int kNBuf = 3;
+
+__device__ __forceinline__ void lds_barrier() {
+    // LDS writes complete, then the workgroup barrier; outstanding global loads (the prefetched
+    // tile halves) stay in flight across it (a __syncthreads fence would drain them)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+__global__ void __launch_bounds__(kThreads8, 1)
+win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __restrict__ k,
+                        const __bf16* __restrict__ v, __bf16* __restrict__ out) {
+    __shared__ __attribute__((aligned(16))) __bf16 sKb[kNBuf][kBK * kC];
+    __shared__ __attribute__((aligned(16))) unsigned char sVb[kNBuf][kBK * kC * 2];
+    __shared__ __attribute__((aligned(16))) bf16x8 sMaskAb[kNBuf][kBK][2];
+
+    int qblk, wi, b;
+    xcd_block_coords(qblk, wi, b);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wid >> 2, wq = wid & 3;
+    const int c = lane & 31, h = lane >> 5;
+    const size_t HW = (size_t)p.H * p.W;
+    const int kvb = (b + p.kv_shift) % p.nbatch;
+    const __bf16* qb = q + (size_t)b * HW * kC;
+    const __bf16* kb = k + (size_t)kvb * p.m * HW * kC;
+    const __bf16* vb = v + (size_t)kvb * p.m * HW * kC;
+    const float cl2 = p.scale * kLog2e;
+
+    const int tq = qblk * kBQ8 + grp * kBQ3 + wq * kQW + c;
+    const int qpix = win_pixel(p, wi, tq);
+    bf16x8 qf[8];
+    {
+        const bf16x8* src = reinterpret_cast<const bf16x8*>(qb + (size_t)qpix * kC + 8 * h);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qf[i] = src[2 * i];
+    }
+    bf16x8 qmask;
+    {
+        const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qmask[j] = (__bf16)(qreg == 8 * h + j ? 1.0f : 0.0f);
+    }
+    floatx16 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    // staging: a group moves its half of a tile: thread (key row grow, part gp) holds 16-B chunks
+    // 8 grp + 2 gp + {0, 1} of the row's K and V (and, for gp == 0, the row's mask fragment grp)
+    const int t8 = tid & 255, grow = t8 & 63, gp = t8 >> 6;
+    const int ntiles = p.L * p.m / kBK;
+    bf16x8 kv[2], vv[2];
+    int kreg = 0;
+    auto gather = [&](int tile) {
+        const int j = tile * kBK + grow;
+        const int tk = j / p.m, vi = j - tk * p.m;
+        const int kpix = win_pixel(p, wi, tk);
+        const int ch0 = 8 * grp + 2 * gp;
+        const bf16x8* ksrc = reinterpret_cast<const bf16x8*>(kb + ((size_t)vi * HW + kpix) * kC) + ch0;
+        const bf16x8* vsrc = reinterpret_cast<const bf16x8*>(vb + ((size_t)vi * HW + kpix) * kC) + ch0;
+        kv[0] = ksrc[0];
+        kv[1] = ksrc[1];
+        vv[0] = vsrc[0];
+        vv[1] = vsrc[1];
+        kreg = p.shift ? win_region(p, wi, j % p.L) : 0;
+    };
+    auto stage = [&](int tile) {
+        const int buf = tile % kNBuf;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int chunk = 8 * grp + 2 * gp + i;
+            *reinterpret_cast<bf16x8*>(&sKb[buf][grow * kC + ((chunk ^ (grow & 15)) * 8)]) = kv[i];
+            *reinterpret_cast<bf16x8*>(&sVb[buf][vimg_off(grow, chunk)]) = vv[i];
+        }
+        if (p.shift && gp == 0) {
+            bf16x8 a;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = (__bf16)(kreg == 8 * grp + j ? kMaskBonus : 0.0f);
+            sMaskAb[buf][grow][grp] = a;
+        }
+    };
+    // prologue: tile 0 (both halves) and tile 1's B half in LDS; registers: A holds tile 1's half
+    // (written in A's step 1), B tile 2's (written in B's step 1)
+    gather(0);
+    stage(0);
+    if (grp == 1 && ntiles > 1) {
+        gather(1);
+        stage(1);
+    }
+    if (grp == 0 ? ntiles > 1 : ntiles > 2) gather(grp == 0 ? 1 : 2);
+    lds_barrier();
+
+    // group B runs one interval behind A: one barrier before its loop (A: one after), so every
+    // wave passes 2 (ntiles + 1) + 1 barriers
+    if (grp == 1) lds_barrier();
+    bf16x8 pf[4];
+    for (int t = 0; t <= ntiles; ++t) {
+        // ======== MFMA interval: O += V(t-1)^T P(t-1)^T, then S(t) = K(t) Q^T (+ mask step)
+        if (t >= 1) {
+            const unsigned char* sV = sVb[(t - 1) % kNBuf];
+#pragma unroll
+            for (int ksx = 0; ksx < 4; ++ksx) {
+                const int gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+                const int r0 = 16 * ksx + 4 * h + qq;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt) {
+                    const int c0 = 4 * dt + 2 * ((lane >> 4) & 1) + (pp >> 1);
+                    const shortx4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (__attribute__((address_space(3))) shortx4*)(sV + vimg_off(r0, c0) + 8 * (pp & 1)));
+                    const shortx4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                        (__attribute__((address_space(3))) shortx4*)(sV + vimg_off(r0 + 8, c0) + 8 * (pp & 1)));
+                    typedef short shortx8 __attribute__((ext_vector_type(8)));
+                    const shortx8 vs = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vs), pf[ksx], o[dt], 0,
+                                                                    0, 0);
+                }
+            }
+        }
+        floatx16 sacc[2];
+        if (t < ntiles) {
+            const __bf16* sK = sKb[t % kNBuf];
+#pragma unroll
+            for (int sub = 0; sub < 2; ++sub) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sacc[sub][r] = 0.f;
+                bf16x8 kk[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int row = 32 * sub + c, chunk = 2 * i + h;
+                    kk[i] = *reinterpret_cast<const bf16x8*>(&sK[row * kC + ((chunk ^ (row & 15)) * 8)]);
+                }
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+                    sacc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk[i], qf[i], sacc[sub], 0, 0, 0);
+                if (p.shift)
+                    sacc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sMaskAb[t % kNBuf][32 * sub + c][h], qmask,
+                                                                        sacc[sub], 0, 0, 0);
+            }
+        }
+        lds_barrier();
+        if (t == ntiles) break;
+        // ======== VALU interval: staging, then the online softmax of S(t) -> P(t)
+        // A writes tile t + 1 into buffer (t + 1) % 3, whose previous tile t - 2 was last read by
+        // B's PV one interval earlier; B writes tile t + 2 into (t + 2) % 3, last read (tile t - 1)
+        // by B's own PV in its previous interval. Both halves of tile u are in place before A's
+        // QK(u).
+        {
+            const int wtile = t + 1 + grp;
+            if (wtile < ntiles) {
+                stage(wtile);
+                if (wtile + 1 < ntiles) gather(wtile + 1);
+            }
+        }
+        float bmax = max3_raw(sacc[0][0], sacc[1][0], sacc[0][1]);
+        bmax = max3_raw(bmax, sacc[1][1], sacc[0][2]);
+#pragma unroll
+        for (int r = 2; r < 15; ++r) bmax = max3_raw(bmax, sacc[1][r], sacc[0][r + 1]);
+        bmax = fmaxf(bmax, sacc[1][15]);
+        const float bm2 = halves_max(bmax) * cl2;
+        if (__any(bm2 > m_run + kThr)) {
+            const float m_new = fmaxf(m_run, bm2);
+            const float corr = fast_exp2(m_run - m_new);
+            l_run *= corr;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+            m_run = m_new;
+        }
+        float bsum = 0.f;
+#pragma unroll
+        for (int ksx = 0; ksx < 4; ++ksx)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float ex = fast_exp2(fmaf(sacc[ksx >> 1][8 * (ksx & 1) + e], cl2, -m_run));
+                bsum += ex;
+                pf[ksx][e] = (__bf16)ex;
+            }
+        l_run += halves_sum(bsum);
+        lds_barrier();
+    }
+    if (grp == 0) lds_barrier();
+
+    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
+    const float inv = 1.0f / l_run;
+    __bf16* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            store4(dst + 32 * dt + 8 * u, make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv,
+                                                      o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
+}
+
 }  // namespace winattn
 }  // namespace tsplat
 
@@ -1799,8 +2008,13 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
     if (p.L % kBQ3 || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
+    // v3 (8 staggered waves, 256 queries per workgroup, no key split) where the launch gives
+    // >= 1 workgroup per CU without splitting keys; TSPLAT_WINATTN_BF16=v1 / v2 / v3 selects
+    const bool v3 = p.L % kBQ8 == 0 &&
+                    (env_is("TSPLAT_WINATTN_BF16", "v3") ||
+                     (!getenv("TSPLAT_WINATTN_BF16") && (p.L / kBQ8) * splits * splits * batch >= 256));
     const int base = (p.L / kBQ3) * splits * splits * batch;
-    p.ksplit = choose_ksplit(base, p.L * p.m / kBK, 512);
+    p.ksplit = v3 ? 1 : choose_ksplit(base, p.L * p.m / kBK, 512);
     p.keys_per_split = p.L * p.m / p.ksplit;
     Partials part{nullptr, nullptr, nullptr};
     if (p.ksplit > 1) {
@@ -1816,6 +2030,9 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
         hipLaunchKernelGGL(win_attn_bf16_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
                            dim3(kThreads), 0, stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
                            (__bf16*)out, part);
+    else if (v3)
+        hipLaunchKernelGGL(win_attn_bf16_v3_kernel, dim3(p.L / kBQ8, splits * splits, batch), dim3(kThreads8), 0,
+                           stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (__bf16*)out);
     else
         hipLaunchKernelGGL(win_attn_bf16_v2_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
                            dim3(kThreads), 0, stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
