@@ -1596,12 +1596,28 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// LDS of v3: [K0 K1 K2][V0 V1 V2][M0 M1 M2]. K rows padded to 272 B and not swizzled: the QK^T
+// operand reads (lane (c, h): row c, 16-B chunk 2i + h) then all sit at ONE per-lane address plus
+// compile-time offsets, and a ds_read_b128 lane group's 16 rows land on 16 distinct 4-bank sets.
+// V keeps image (b) (transposed tr16 reads), whose per-lane part takes 8 precomputed addresses.
+// With the tile loop unrolled by three the ring-buffer offsets are immediates too.
+constexpr int kKRowB = kC * 2 + 16;           // 272
+constexpr int kKBufB = kBK * kKRowB;          // 17,408
+constexpr int kVBufB = kBK * kC * 2;          // 16,384
+constexpr int kMBufB = kBK * 2 * 16;          // 2,048 (one-hot mask fragments)
+constexpr int kVOff = kNBuf * kKBufB;         // 52,224
+constexpr int kMOff = kVOff + kNBuf * kVBufB; // 101,376
+constexpr int kLds3 = kMOff + kNBuf * kMBufB; // 107,520
+
+template <int N>
+struct IC {
+    static constexpr int value = N;
+};
+
 __global__ void __launch_bounds__(kThreads8, 1)
 win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                         const __bf16* __restrict__ v, __bf16* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) __bf16 sKb[kNBuf][kBK * kC];
-    __shared__ __attribute__((aligned(16))) unsigned char sVb[kNBuf][kBK * kC * 2];
-    __shared__ __attribute__((aligned(16))) bf16x8 sMaskAb[kNBuf][kBK][2];
+    __shared__ __attribute__((aligned(16))) unsigned char smem[kLds3];
 
     int qblk, wi, b;
     xcd_block_coords(qblk, wi, b);
@@ -1637,6 +1653,20 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
         for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
     float m_run = -INFINITY, l_run = 0.f;
 
+    // per-lane LDS read addresses (byte offsets into smem), loop invariant
+    const unsigned aK = c * kKRowB + h * 16;
+    const unsigned aM = kMOff + c * 32 + h * 16;
+    unsigned aV[2][4];  // [lo / hi key half][dt]: image (b) of keys 16 ksx + 4h + qq (+ 8)
+    {
+        const int gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+        const int x = 2 * ((lane >> 4) & 1) + (pp >> 1);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            aV[0][dt] = kVOff + 256 * (4 * h + qq) + 64 * (dt ^ qq) + 16 * (x ^ h) + 8 * (pp & 1);
+            aV[1][dt] = kVOff + 256 * (4 * h + qq + 8) + 64 * (dt ^ qq) + 16 * (x ^ (h + 2)) + 8 * (pp & 1);
+        }
+    }
+
     // staging: a group moves its half of a tile: thread (key row grow, part gp) holds 16-B chunks
     // 8 grp + 2 gp + {0, 1} of the row's K and V (and, for gp == 0, the row's mask fragment grp)
     const int t8 = tid & 255, grow = t8 & 63, gp = t8 >> 6;
@@ -1645,7 +1675,11 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
     int kreg = 0;
     auto gather = [&](int tile) {
         const int j = tile * kBK + grow;
-        const int tk = j / p.m, vi = j - tk * p.m;
+        int tk = j, vi = 0;
+        if (p.m != 1) {  // (single key view: no division)
+            tk = j / p.m;
+            vi = j - tk * p.m;
+        }
         const int kpix = win_pixel(p, wi, tk);
         const int ch0 = 8 * grp + 2 * gp;
         const bf16x8* ksrc = reinterpret_cast<const bf16x8*>(kb + ((size_t)vi * HW + kpix) * kC) + ch0;
@@ -1654,25 +1688,24 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
         kv[1] = ksrc[1];
         vv[0] = vsrc[0];
         vv[1] = vsrc[1];
-        kreg = p.shift ? win_region(p, wi, j % p.L) : 0;
+        if (p.shift) kreg = win_region(p, wi, p.m == 1 ? j : j % p.L);
     };
-    auto stage = [&](int tile) {
-        const int buf = tile % kNBuf;
+    auto stage = [&](int buf) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int chunk = 8 * grp + 2 * gp + i;
-            *reinterpret_cast<bf16x8*>(&sKb[buf][grow * kC + ((chunk ^ (grow & 15)) * 8)]) = kv[i];
-            *reinterpret_cast<bf16x8*>(&sVb[buf][vimg_off(grow, chunk)]) = vv[i];
+            *reinterpret_cast<bf16x8*>(smem + buf * kKBufB + grow * kKRowB + chunk * 16) = kv[i];
+            *reinterpret_cast<bf16x8*>(smem + kVOff + buf * kVBufB + vimg_off(grow, chunk)) = vv[i];
         }
         if (p.shift && gp == 0) {
             bf16x8 a;
 #pragma unroll
             for (int j = 0; j < 8; ++j) a[j] = (__bf16)(kreg == 8 * grp + j ? kMaskBonus : 0.0f);
-            sMaskAb[buf][grow][grp] = a;
+            *reinterpret_cast<bf16x8*>(smem + kMOff + buf * kMBufB + grow * 32 + grp * 16) = a;
         }
     };
     // prologue: tile 0 (both halves) and tile 1's B half in LDS; registers: A holds tile 1's half
-    // (written in A's step 1), B tile 2's (written in B's step 1)
+    // (written in A's first VALU interval), B tile 2's (written in B's)
     gather(0);
     stage(0);
     if (grp == 1 && ntiles > 1) {
@@ -1681,56 +1714,53 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
     }
     if (grp == 0 ? ntiles > 1 : ntiles > 2) gather(grp == 0 ? 1 : 2);
     lds_barrier();
-
     // group B runs one interval behind A: one barrier before its loop (A: one after), so every
     // wave passes 2 (ntiles + 1) + 1 barriers
     if (grp == 1) lds_barrier();
+
     bf16x8 pf[4];
-    for (int t = 0; t <= ntiles; ++t) {
+    // tile t (t % 3 == BUF); returns true after the final (PV-only) MFMA interval
+    auto iter = [&](int t, auto bufc) -> bool {
+        constexpr int BUF = decltype(bufc)::value;
+        constexpr int PBUF = (BUF + 2) % 3;  // tile t - 1
         // ======== MFMA interval: O += V(t-1)^T P(t-1)^T, then S(t) = K(t) Q^T (+ mask step)
         if (t >= 1) {
-            const unsigned char* sV = sVb[(t - 1) % kNBuf];
 #pragma unroll
-            for (int ksx = 0; ksx < 4; ++ksx) {
-                const int gi = lane & 15, qq = gi >> 2, pp = gi & 3;
-                const int r0 = 16 * ksx + 4 * h + qq;
+            for (int ksx = 0; ksx < 4; ++ksx)
 #pragma unroll
                 for (int dt = 0; dt < 4; ++dt) {
-                    const int c0 = 4 * dt + 2 * ((lane >> 4) & 1) + (pp >> 1);
+                    const int off = PBUF * kVBufB + 4096 * ksx;
                     const shortx4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) shortx4*)(sV + vimg_off(r0, c0) + 8 * (pp & 1)));
+                        (__attribute__((address_space(3))) shortx4*)(smem + aV[0][dt] + off));
                     const shortx4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                        (__attribute__((address_space(3))) shortx4*)(sV + vimg_off(r0 + 8, c0) + 8 * (pp & 1)));
+                        (__attribute__((address_space(3))) shortx4*)(smem + aV[1][dt] + off));
                     typedef short shortx8 __attribute__((ext_vector_type(8)));
                     const shortx8 vs = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
                     o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vs), pf[ksx], o[dt], 0,
                                                                     0, 0);
                 }
-            }
         }
         floatx16 sacc[2];
         if (t < ntiles) {
-            const __bf16* sK = sKb[t % kNBuf];
 #pragma unroll
             for (int sub = 0; sub < 2; ++sub) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sacc[sub][r] = 0.f;
                 bf16x8 kk[8];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int row = 32 * sub + c, chunk = 2 * i + h;
-                    kk[i] = *reinterpret_cast<const bf16x8*>(&sK[row * kC + ((chunk ^ (row & 15)) * 8)]);
-                }
-#pragma unroll
                 for (int i = 0; i < 8; ++i)
+                    kk[i] = *reinterpret_cast<const bf16x8*>(smem + aK + BUF * kKBufB + sub * 32 * kKRowB + 32 * i);
+                const floatx16 zero = {};
+                sacc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk[0], qf[0], zero, 0, 0, 0);
+#pragma unroll
+                for (int i = 1; i < 8; ++i)
                     sacc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk[i], qf[i], sacc[sub], 0, 0, 0);
                 if (p.shift)
-                    sacc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sMaskAb[t % kNBuf][32 * sub + c][h], qmask,
-                                                                        sacc[sub], 0, 0, 0);
+                    sacc[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        *reinterpret_cast<const bf16x8*>(smem + aM + BUF * kMBufB + sub * 1024), qmask, sacc[sub], 0,
+                        0, 0);
             }
         }
         lds_barrier();
-        if (t == ntiles) break;
+        if (t == ntiles) return true;
         // ======== VALU interval: staging, then the online softmax of S(t) -> P(t)
         // A writes tile t + 1 into buffer (t + 1) % 3, whose previous tile t - 2 was last read by
         // B's PV one interval earlier; B writes tile t + 2 into (t + 2) % 3, last read (tile t - 1)
@@ -1739,7 +1769,7 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
         {
             const int wtile = t + 1 + grp;
             if (wtile < ntiles) {
-                stage(wtile);
+                stage(grp == 0 ? (BUF + 1) % 3 : (BUF + 2) % 3);
                 if (wtile + 1 < ntiles) gather(wtile + 1);
             }
         }
@@ -1768,6 +1798,12 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
             }
         l_run += halves_sum(bsum);
         lds_barrier();
+        return false;
+    };
+    for (int t = 0;; t += 3) {
+        if (iter(t, IC<0>{})) break;
+        if (iter(t + 1, IC<1>{})) break;
+        if (iter(t + 2, IC<2>{})) break;
     }
     if (grp == 0) lds_barrier();
 
