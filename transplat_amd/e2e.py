@@ -142,6 +142,9 @@ def _copy_batch(dst, src):
 
 
 def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: str = "fp32", graph: bool = True):
+    from .gemm_tuning import use_tuned_gemms
+
+    use_tuned_gemms(device, dense_dtype)  # recorded library GEMM solutions (replay only), before any capture
     model = build_model(device, dense_dtype)
     data = S.make_batch(batch, image_shape=(256, 256), scene_offset=scene_offset, device=device)
     if graph:
