@@ -1,10 +1,17 @@
 """Direct conv kernel (tsplat_conv2d_f32_fwd) vs MIOpen (algorithm search on, cat / upsample glue
-included as the module path runs it) on the U-Nets' convolution shapes, graph-timed."""
+included as the module path runs it) on the U-Nets' convolution shapes, graph-timed; `route` is
+what the dispatch rules pick for the shape (wino = conv3x3_wino_ok, direct = conv2d_direct_ok,
+else MIOpen). --scale 4 multiplies the batch (2 views x b = 1 -> b = 4 x 2 = 8 maps; C2 b = 8)."""
+import argparse
+
 import torch
 import torch.nn.functional as F
 
 from transplat_amd import kernels as K
 
+ap = argparse.ArgumentParser()
+ap.add_argument("--scale", type=int, default=1, help="batch multiplier for every shape")
+args = ap.parse_args()
 torch.backends.cudnn.benchmark = True
 dev = torch.device("cuda:0")
 # n, c1, c2, h, w, cout, k, stride, upsample, calls per step
@@ -46,9 +53,10 @@ def timeit(fn, n=20):
 
 
 tot = [0.0, 0.0]
-print(f"{'miopen':>8s} {'direct':>8s} {'GFLOP':>6s} {'TF/s':>6s} calls  shape")
+print(f"{'miopen':>8s} {'direct':>8s} {'GFLOP':>6s} {'TF/s':>6s} calls  route  shape")
 with torch.no_grad():
     for (n, c1, c2, h, w, co, k, st, up, calls) in SHAPES:
+        n *= args.scale
         x1 = torch.randn(n, c1, h, w, device=dev)
         x2 = torch.randn(n, c2, h, w, device=dev) if c2 else None
         wt = torch.randn(co, c1 + c2, k, k, device=dev) * 0.05
@@ -65,8 +73,10 @@ with torch.no_grad():
         err = (K.conv2d_direct(x1, wt, b, st, x2=x2, upsample=up) - ref()).abs().max().item()
         hh, ww = (2 * h, 2 * w) if up else (h, w)
         gf = 2.0 * n * (hh // st) * (ww // st) * co * (c1 + c2) * k * k / 1e9
+        route = ("wino" if not up and K.conv3x3_wino_ok(x1, wt, st, k // 2, extra=(x2,) if x2 is not None else ())
+                 else "direct" if K.conv2d_direct_ok(x1, wt, st, c2=c2, upsample=up) else "miopen")
         tot[0] += t1 * calls
         tot[1] += t2 * calls
-        print(f"{t1:8.1f} {t2:8.1f} {gf:6.3f} {gf / t2 * 1e3:6.1f} {calls:5d}  {(n, c1, c2, h, w, co, k, st, up)} "
-              f"err={err:.1e}", flush=True)
+        print(f"{t1:8.1f} {t2:8.1f} {gf:6.3f} {gf / t2 * 1e3:6.1f} {calls:5d}  {route:6s} "
+              f"{(n, c1, c2, h, w, co, k, st, up)} err={err:.1e}", flush=True)
 print(f"total per step: miopen {tot[0]:.1f} us, direct {tot[1]:.1f} us")
