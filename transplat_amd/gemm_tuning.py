@@ -29,5 +29,6 @@ def use_tuned_gemms(device, dense_dtype: str = "fp32") -> bool:
     tun.tuning_enable(False)
     tun.record_untuned_enable(False)
     # anything TunableOp writes back goes to a scratch file, never over the committed results
-    tun.set_filename(str(Path(tempfile.gettempdir()) / "tsplat_tunableop_out.csv"))
+    # (one file per process: the ranks of a multi-GPU bench all exit at once)
+    tun.set_filename(str(Path(tempfile.gettempdir()) / f"tsplat_tunableop_out_{os.getpid()}.csv"))
     return bool(tun.read_file(str(TUNED_FILE)))
