@@ -23,6 +23,10 @@ from torch import nn
 from ... import kernels
 
 
+_REF2D: dict = {}  # (h, w, dtype, device) -> [1, h*w, 2] reference points
+_WH: dict = {}     # (w, h, dtype, device) -> tensor([w, h])
+
+
 class UVSelfAttention(nn.Module):
     """4-point deformable self-attention on the query grid (reference attention.py:145-277)."""
 
@@ -51,8 +55,13 @@ class UVSelfAttention(nn.Module):
         value = self.value_proj(value)
         offsets = self.sampling_offsets(query).view(bsv, nq, self.num_points, 2)
         weights = self.attention_weights(query).view(bsv, nq, self.num_points).softmax(-1)
-        # offset / (W, H) per coordinate (the reference divides by the spatial-shape tensor)
-        loc = ref_2d[:, :, None, :] + torch.stack((offsets[..., 0] / bev_w, offsets[..., 1] / bev_h), -1)
+        # offset / (W, H) per coordinate (the reference divides by the spatial-shape tensor): one
+        # broadcast division by a cached (W, H) tensor
+        key = (bev_w, bev_h, offsets.dtype, str(offsets.device))
+        wh = _WH.get(key)
+        if wh is None:
+            wh = _WH[key] = torch.tensor([bev_w, bev_h], dtype=offsets.dtype, device=offsets.device)
+        loc = ref_2d[:, :, None, :] + offsets / wh
         return kernels.msda(value, loc, weights, bev_h, bev_w)
 
     def forward(self, query, value, query_pos, ref_2d, bev_h: int, bev_w: int):
@@ -197,12 +206,17 @@ class UVTransformerEncoder(nn.Module):
 
     @staticmethod
     def reference_points_2d(bev_h, bev_w, n, dtype, device):
-        """ref_2d pixel centres (i + 0.5) / size, (x, y) (reference encoder.py:61-71)."""
-        ref_y, ref_x = torch.meshgrid(
-            torch.linspace(0.5, bev_h - 0.5, bev_h, dtype=dtype, device=device),
-            torch.linspace(0.5, bev_w - 0.5, bev_w, dtype=dtype, device=device), indexing="ij")
-        ref = torch.stack((ref_x.reshape(-1) / bev_w, ref_y.reshape(-1) / bev_h), -1)
-        return ref[None].expand(n, -1, -1)
+        """ref_2d pixel centres (i + 0.5) / size, (x, y) (reference encoder.py:61-71); a constant of
+        the shape, built once per (shape, dtype, device) instead of ~7 launches per call."""
+        key = (bev_h, bev_w, dtype, str(device))
+        ref = _REF2D.get(key)
+        if ref is None:
+            ref_y, ref_x = torch.meshgrid(
+                torch.linspace(0.5, bev_h - 0.5, bev_h, dtype=dtype, device=device),
+                torch.linspace(0.5, bev_w - 0.5, bev_w, dtype=dtype, device=device), indexing="ij")
+            ref = torch.stack((ref_x.reshape(-1) / bev_w, ref_y.reshape(-1) / bev_h), -1)[None]
+            _REF2D[key] = ref
+        return ref.expand(n, -1, -1)
 
     def forward(self, query, key_cl, bev_h, bev_w, bev_pos=None, cameras=None):
         # query, bev_pos: [(b v), HW, C]; key_cl: [B, 2, HW, C]
