@@ -2,7 +2,11 @@
 16 img2world entries -> MLP -> SE gate on conv3x3-BN-ReLU(feature) -> 1x1 conv."""
 from __future__ import annotations
 
+import torch
+import torch.nn.functional as F
 from torch import nn
+
+from transplat_amd import kernels
 
 
 class Mlp(nn.Module):
@@ -51,8 +55,41 @@ class cam_param_encoder(nn.Module):  # noqa: N801  (reference class name kept fo
         self.context_mlp = Mlp(self.cam_param_len, mid_channels, mid_channels)
         self.context_se = SELayer(mid_channels)
 
+    def _folded(self):
+        """Eval-mode BatchNorms folded into their neighbours, cached per parameter version:
+        reduce_conv's BatchNorm2d into the 3x3 conv's weight / bias, and the BatchNorm1d on the
+        camera vector into context_mlp.fc1 (fc1(s x + c) = (W diag s) x + (W c + b))."""
+        conv, bn2, fc1 = self.reduce_conv[0], self.reduce_conv[1], self.context_mlp.fc1
+        params = (conv.weight, conv.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var, fc1.weight,
+                  fc1.bias, self.bn.weight, self.bn.bias, self.bn.running_mean, self.bn.running_var)
+        key = tuple((t.data_ptr(), t._version) for t in params)
+        hit = self.__dict__.get("_fold")
+        if hit is None or hit[0] != key:
+            with torch.no_grad():
+                s2 = bn2.weight / torch.sqrt(bn2.running_var + bn2.eps)
+                w = (conv.weight * s2[:, None, None, None]).contiguous()
+                b = ((conv.bias - bn2.running_mean) * s2 + bn2.bias).contiguous()
+                s1 = self.bn.weight / torch.sqrt(self.bn.running_var + self.bn.eps)
+                c1 = self.bn.bias - self.bn.running_mean * s1
+                w1 = (fc1.weight * s1[None, :]).contiguous()
+                b1 = (fc1.bias + fc1.weight @ c1).contiguous()
+            hit = (key, w, b, w1, b1)
+            self.__dict__["_fold"] = hit
+        return hit[1:]
+
     def forward(self, feat, cam_params):
         vb = feat.shape[0]
+        conv = self.reduce_conv[0]
+        if (not self.training and feat.is_cuda and feat.dtype == torch.float32 and conv.bias is not None
+                and not torch.is_autocast_enabled("cuda")
+                and kernels.conv3x3_wino_ok(feat, conv.weight, conv.stride, conv.padding, conv.dilation,
+                                            conv.groups, vs_miopen=True)):
+            # inference: both BatchNorms folded, conv + bias + ReLU as one Winograd launch
+            w, b, w1, b1 = self._folded()
+            feat = kernels.conv3x3_wino(feat, w, b, act="relu")
+            mlp = self.context_mlp
+            context_se = mlp.fc2(mlp.act(F.linear(cam_params.reshape(vb, -1), w1, b1)))[..., None, None]
+            return self.context_conv(self.context_se(feat, context_se))
         mlp_input = self.bn(cam_params.reshape(vb, -1))
         feat = self.reduce_conv(feat)
         context_se = self.context_mlp(mlp_input)[..., None, None]
