@@ -38,6 +38,19 @@ void end(int, hipStream_t s) {
     g_open = false;
 }
 
+ExtEvents ext_events(int kid) {
+    ExtEvents r;
+    if (g_active != kid || g_open) return r;
+    const size_t used = g_used;
+    r.start = next_event();
+    r.stop = next_event();
+    if (!r.start || !r.stop) {  // keep begin / end pairs aligned
+        g_used = used;
+        r = ExtEvents{};
+    }
+    return r;
+}
+
 }  // namespace prof
 }  // namespace tsplat
 

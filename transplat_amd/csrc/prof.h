@@ -2,6 +2,8 @@
 // duration on the stream it is launched on). Disabled by default: one branch per launch.
 #pragma once
 
+#include <hip/hip_ext.h>
+
 #include "common.h"
 
 namespace tsplat {
@@ -30,6 +32,14 @@ enum KernelId : int {
 int active();                 // kernel id being timed (0 = off)
 void begin(int kid, hipStream_t s);
 void end(int kid, hipStream_t s);
+
+// Start / stop events for hipExtLaunchKernelGGL when `kid` is being timed (both null otherwise):
+// the dispatch packet itself records them, so the pair brackets the kernel's execution as
+// rocprof's dispatch timestamps do, without the separate event packets' dispatch gap.
+struct ExtEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+ExtEvents ext_events(int kid);
 
 }  // namespace prof
 }  // namespace tsplat

@@ -1999,10 +1999,9 @@ extern "C" int tsplat_win_attn_partials_fwd(const float* q, const float* k, cons
     part.m = part.o + n * kC;
     part.l = part.m + n;
     hipStream_t stream = (hipStream_t)stream_;
-    TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
-    hipLaunchKernelGGL(win_attn_f32x32_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit), dim3(kThreads),
-                       0, stream, p, q, k, v, nullptr, part);
-    TSPLAT_PROF_END(prof::kWinAttn, stream);
+    const prof::ExtEvents ev = prof::ext_events(prof::kWinAttn);  // kernel timestamps when timed
+    hipExtLaunchKernelGGL(win_attn_f32x32_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
+                          dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p, q, k, v, (float*)nullptr, part);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
@@ -2061,22 +2060,21 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
         part.l = part.m + n;
     }
     hipStream_t stream = (hipStream_t)stream_;
-    TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
+    // the main kernel's own dispatch timestamps when timed (the split path's combine is not in it)
+    const prof::ExtEvents ev = prof::ext_events(prof::kWinAttn);
+    const __bf16 *qh = (const __bf16*)q, *kh = (const __bf16*)k, *vh = (const __bf16*)v;
     if (env_is("TSPLAT_WINATTN_BF16", "v1"))
-        hipLaunchKernelGGL(win_attn_bf16_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
-                           dim3(kThreads), 0, stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
-                           (__bf16*)out, part);
+        hipExtLaunchKernelGGL(win_attn_bf16_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
+                              dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p, qh, kh, vh, (__bf16*)out, part);
     else if (v3)
-        hipLaunchKernelGGL(win_attn_bf16_v3_kernel, dim3(p.L / kBQ8, splits * splits, batch), dim3(kThreads8), 0,
-                           stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v, (__bf16*)out);
+        hipExtLaunchKernelGGL(win_attn_bf16_v3_kernel, dim3(p.L / kBQ8, splits * splits, batch), dim3(kThreads8), 0,
+                              stream, ev.start, ev.stop, 0, p, qh, kh, vh, (__bf16*)out);
     else
-        hipLaunchKernelGGL(win_attn_bf16_v2_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
-                           dim3(kThreads), 0, stream, p, (const __bf16*)q, (const __bf16*)k, (const __bf16*)v,
-                           (__bf16*)out, part);
+        hipExtLaunchKernelGGL(win_attn_bf16_v2_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
+                              dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p, qh, kh, vh, (__bf16*)out, part);
     if (p.ksplit > 1)
         hipLaunchKernelGGL(win_attn_combine_x32_kernel<__bf16>, dim3(p.L / kBQ3 * 16, splits * splits, batch),
                            dim3(kThreads), 0, stream, p, part, (__bf16*)out);
-    TSPLAT_PROF_END(prof::kWinAttn, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }

@@ -453,7 +453,7 @@ static int wino_launch(const float* const* srcs, const int32_t* chans, int32_t n
     a.by = (a.th + a.tby - 1) / a.tby;
     a.act = act;
     hipStream_t stream = (hipStream_t)stream_;
-    TSPLAT_PROF_BEGIN(prof::kWinoConv, stream);
+    const prof::ExtEvents ev = prof::ext_events(prof::kWinoConv);  // kernel timestamps when timed
     // 64-channel workgroups where they pad no more output channels than 32-channel ones and the
     // grid still covers most of the 256 CUs (measured per shape with tools/bench_wino.py: at 128
     // workgroups the 32-channel grid's 256 is faster, from 160 up the 64-channel one);
@@ -467,12 +467,14 @@ static int wino_launch(const float* const* srcs, const int32_t* chans, int32_t n
     int ks = blocks * cob32 <= 256 ? 2 : 1;
     if (const char* e = getenv("TSPLAT_WINO_KS")) ks = atoi(e) == 2 ? 2 : 1;
     if (wide)
-        hipLaunchKernelGGL(wino::conv64_kernel, dim3(blocks, cob64), dim3(wino::kThreads64), 0, stream, a);
+        hipExtLaunchKernelGGL(wino::conv64_kernel, dim3(blocks, cob64), dim3(wino::kThreads64), 0, stream, ev.start,
+                              ev.stop, 0, a);
     else if (ks == 2)
-        hipLaunchKernelGGL(wino::conv_kernel<2>, dim3(blocks, cob32), dim3(2 * wino::kThreads), 0, stream, a);
+        hipExtLaunchKernelGGL(wino::conv_kernel<2>, dim3(blocks, cob32), dim3(2 * wino::kThreads), 0, stream,
+                              ev.start, ev.stop, 0, a);
     else
-        hipLaunchKernelGGL(wino::conv_kernel<1>, dim3(blocks, cob32), dim3(wino::kThreads), 0, stream, a);
-    TSPLAT_PROF_END(prof::kWinoConv, stream);
+        hipExtLaunchKernelGGL(wino::conv_kernel<1>, dim3(blocks, cob32), dim3(wino::kThreads), 0, stream, ev.start,
+                              ev.stop, 0, a);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
