@@ -250,6 +250,22 @@ def test_conv3x3_wino_reads_concat_in_place(device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("co", [84, 96])
+def test_conv3x3_wino_split_launch_at_production_size(device, co):
+    """An odd number of 32-channel output blocks on a big grid (to_disparity's 168 -> 84 at 256^2)
+    runs as a 64-channel launch for the even part plus a 32-channel launch for the last block
+    (Args.cob_base); checked against MIOpen's fp32 conv2d."""
+    from transplat_amd import kernels as K
+
+    x = seeded((2, 168, 256, 256), 70).to(device)
+    wt = (seeded((co, 168, 3, 3), 71) * (1.0 / (9 * 168) ** 0.5)).to(device)
+    b = seeded((co,), 72).to(device)
+    y = K.conv3x3_wino(x, wt, b, "gelu")
+    ref = torch.nn.functional.gelu(torch.nn.functional.conv2d(x, wt, b, padding=1))
+    assert ((y - ref).abs().max() / ref.abs().max()).item() < 2e-5
+
+
+@pytest.mark.gpu
 def test_conv3x3_wino_wide_shape_at_production_size(device):
     """The launch picks the 64-output-channel workgroups for the to_gaussians head at 256^2
     (2 x 163 -> 168, three sources read in place); checked against MIOpen's fp32 conv2d on the

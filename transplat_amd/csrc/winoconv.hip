@@ -50,6 +50,7 @@ struct Args {
     int n, ci, h, w, co, ci_pad, cobs;  // cobs = 32-channel blocks in the packing (even)
     int th, tw, tbx, tby, bx, by;  // tiles per image, tile-block shape, tile blocks per image row / column
     int act;             // 0 none, 1 ReLU, 2 GELU (erf)
+    int cob_base;        // first 32-channel output block of this launch (a split launch's offset)
 };
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -231,7 +232,7 @@ __global__ void __launch_bounds__(kThreads * KS) conv_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) float smem[KS * 2 * 16 * kCiB * kTiles];  // sV x2 per group, then Z
     __shared__ const float* planes[kMaxCiPad];
     const int kg = threadIdx.x / kThreads, tid = threadIdx.x % kThreads, lane = tid & 63, wid = tid >> 6;
-    const int cob = blockIdx.y;
+    const int cob = a.cob_base + blockIdx.y;  // 32-channel output block
     const Patch pt(a, blockIdx.x, tid);
     const int cc = tid / kTiles;  // channel of each chunk this thread transforms
     float d[16];
@@ -308,7 +309,7 @@ __global__ void __launch_bounds__(kThreads64) conv64_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) float smem[2 * 16 * kCiB64 * kTiles];  // sV x2 (64 KB), then Z
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int hh = wid >> 2, rr = wid & 3;
-    const int cob = blockIdx.y;  // 64-channel block = 32-channel blocks 2 cob, 2 cob + 1
+    const int cob = blockIdx.y;  // 64-channel block = 32-channel blocks cob_base + 2 cob (+ 1)
     __shared__ const float* planes[kMaxCiPad];
     const Patch pt(a, blockIdx.x, tid);
     const int cc = tid / kTiles;
@@ -318,7 +319,7 @@ __global__ void __launch_bounds__(kThreads64) conv64_kernel(Args a) {
 
     const size_t plane = (size_t)a.cobs * a.ci_pad * 32;
     const float* ub =
-        a.u + (size_t)(4 * rr) * plane + (size_t)(2 * cob + hh) * (a.ci_pad / kGroup) * 512 + lane * 8;
+        a.u + (size_t)(4 * rr) * plane + (size_t)(a.cob_base + 2 * cob + hh) * (a.ci_pad / kGroup) * 512 + lane * 8;
     auto load_a = [&](int chunk, float4 (&f)[4][2]) {
 #pragma unroll
         for (int s = 0; s < 4; ++s)
@@ -376,7 +377,8 @@ __global__ void __launch_bounds__(kThreads64) conv64_kernel(Args a) {
     for (int k = 0; k < (2 * kCoB * kTiles) / kThreads64; ++k) {
         const int pidx = tid + kThreads64 * k;
         const int colg = pidx / kTiles;  // 0..63
-        store_tile(a, smem + (colg >> 5) * (8 * kCoB * kTiles), colg & 31, pidx % kTiles, cob * 64 + colg, pt.img,
+        store_tile(a, smem + (colg >> 5) * (8 * kCoB * kTiles), colg & 31, pidx % kTiles,
+                   a.cob_base * kCoB + cob * 64 + colg, pt.img,
                    blockIdx.x);
     }
 }
@@ -461,15 +463,28 @@ static int wino_launch(const float* const* srcs, const int32_t* chans, int32_t n
     const int blocks = n * a.bx * a.by;
     const int cob32 = (co + wino::kCoB - 1) / wino::kCoB, cob64 = (co + 63) / 64;
     bool wide = cob32 % 2 == 0 && blocks * cob64 >= 160;
-    if (const char* e = getenv("TSPLAT_WINO_WG")) wide = atoi(e) == 64;
+    // an odd number of 32-channel blocks on a big grid (168 -> 84 at 256^2): the even part as
+    // 64-channel workgroups, the last block as a second, 32-channel launch
+    bool split = cob32 % 2 == 1 && cob32 > 1 && blocks * (cob32 / 2) >= 160;
+    if (const char* e = getenv("TSPLAT_WINO_WG")) {
+        wide = atoi(e) == 64;
+        split = false;
+    }
+    a.cob_base = 0;
     // 32-channel workgroups: split each block's chunks over two 4-wave groups while the grid alone
     // gives at most one workgroup per CU (TSPLAT_WINO_KS=1 / 2 forces)
     int ks = blocks * cob32 <= 256 ? 2 : 1;
     if (const char* e = getenv("TSPLAT_WINO_KS")) ks = atoi(e) == 2 ? 2 : 1;
-    if (wide)
+    if (wide) {
         hipExtLaunchKernelGGL(wino::conv64_kernel, dim3(blocks, cob64), dim3(wino::kThreads64), 0, stream, ev.start,
                               ev.stop, 0, a);
-    else if (ks == 2)
+    } else if (split) {
+        hipExtLaunchKernelGGL(wino::conv64_kernel, dim3(blocks, cob32 / 2), dim3(wino::kThreads64), 0, stream,
+                              ev.start, nullptr, 0, a);
+        a.cob_base = cob32 - 1;
+        hipExtLaunchKernelGGL(wino::conv_kernel<1>, dim3(blocks, 1), dim3(wino::kThreads), 0, stream, nullptr,
+                              ev.stop, 0, a);
+    } else if (ks == 2)
         hipExtLaunchKernelGGL(wino::conv_kernel<2>, dim3(blocks, cob32), dim3(2 * wino::kThreads), 0, stream,
                               ev.start, ev.stop, 0, a);
     else
