@@ -394,6 +394,13 @@ int tsplat_upsample_bilinear_act_fwd(const float* x, const float* bias, float* y
 int tsplat_resize_bilinear_nhwc_fwd(const float* x, float* y, int32_t n, int32_t height, int32_t width, int32_t c,
                                     int32_t out_height, int32_t out_width, void* stream);
 
+/* F.interpolate(x, (out_height, out_width), mode="bilinear", align_corners=True) on an NCHW fp32
+ * tensor of `planes` = N * C maps (replaces the PyTorch resizes at the reference's
+ * encoder_trans.py DA-V2 input / depth resize and depth_predictor_trans.py DINO-feature resize);
+ * torch's arithmetic (source = dst * (in - 1) / (out - 1) in float). */
+int tsplat_resize_bilinear_nchw_fwd(const float* x, float* y, int32_t planes, int32_t height, int32_t width,
+                                    int32_t out_height, int32_t out_width, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -188,6 +188,14 @@ def msda(value, loc, weights, h: int, w: int):
     return torch.stack(out)
 
 
+def resize_bilinear_nchw(x, size):
+    """F.interpolate(x, size, mode="bilinear", align_corners=True) on NCHW maps (the PyTorch calls
+    at the reference's encoder_trans.py / depth_predictor_trans.py resizes), on the CPU."""
+    import torch.nn.functional as F
+
+    return F.interpolate(x.float(), size=tuple(size), mode="bilinear", align_corners=True)
+
+
 def ms_deform_attn(value, spatial_shapes, level_start_index, sampling_locations, attention_weights):
     """mmcv ms_deform_attn_forward, multi-level multi-head (the contract of the reference's
     MultiScaleDeformableAttnFunction_fp32, src/model/utils/multi_scale_deformable_attn_function.py:87-121;

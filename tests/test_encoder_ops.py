@@ -148,6 +148,29 @@ def test_msda_kernel(device):
     assert (out - ref).abs().max().item() < 1e-5
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,size", [((6, 3, 256, 256), (252, 252)), ((2, 64, 18, 18), (64, 64)),
+                                        ((16, 1, 252, 252), (256, 256)), ((3, 5, 7, 9), (13, 4)),
+                                        ((2, 2, 1, 1), (3, 5)), ((2, 4, 64, 64), (256, 256))])
+def test_resize_bilinear_nchw_kernel(device, shape, size):
+    """tsplat_resize_bilinear_nchw_fwd (align_corners=True, any size, NCHW) vs the oracle
+    (F.interpolate on the CPU, whose interpolation weights are computed differently: 2e-5 of the
+    output's magnitude) and vs PyTorch's own GPU kernel, whose float arithmetic it restates (1e-6)."""
+    import torch.nn.functional as F
+
+    from transplat_amd import kernels as K
+
+    x = seeded(shape, 33)
+    ref = E.resize_bilinear_nchw(x, size)
+    xd = x.to(device)
+    out = K.interpolate_bilinear_ac(xd, size)
+    scale = max(1.0, ref.abs().max().item())
+    assert out.shape == ref.shape
+    assert (out.cpu() - ref).abs().max().item() < 2e-5 * scale
+    ref_gpu = F.interpolate(xd, size, mode="bilinear", align_corners=True)
+    assert (out - ref_gpu).abs().max().item() < 1e-6 * scale
+
+
 # ---- mmcv-shaped multi-level / multi-head MSDA (tsplat_ms_deform_attn_fwd)
 def _msda_pytorch(value, shapes, loc, wts):
     """mmcv's multi_scale_deformable_attn_pytorch (grid_sample form, the published fallback the

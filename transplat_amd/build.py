@@ -32,7 +32,8 @@ HIPCC_FLAGS = [
 # raster.hip: the blend loop is scalar fp32 by design (v_pk_fma_f32 runs at v_fma_f32's FLOP rate,
 # and the SLP vectoriser's packed form needs operand-pairing register moves: 84 -> 74 cycles per
 # (entry, pixel) without it)
-FILE_FLAGS = {"raster.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"raster.hip": ["-fno-slp-vectorize"],
+              "upsample.hip": ["-ffp-contract=off"]}  # torch's rounding of the interpolation weights
 
 
 def _hipcc() -> str:

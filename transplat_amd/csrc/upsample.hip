@@ -1,4 +1,7 @@
 // Bilinear upsampling (align_corners = True, integer factor) with the producing convolution's bias
+// Built with -ffp-contract=off (transplat_amd/build.py): `hr - h0` contracted into
+// fma(rh, oy, -h0) takes the interpolation weight from the unrounded source coordinate (up to one
+// ulp of it, 1.5e-5 at 255) instead of torch's rounded one: 5.7e-5 off F.interpolate.
 // and the following activation in one pass, on gfx950.
 //
 // Semantics: reference src/model/encoder/matching/depth_predictor_trans.py (upsampler =
@@ -83,6 +86,31 @@ __global__ void __launch_bounds__(256) bilinear_ac_nhwc_kernel(const float* __re
     reinterpret_cast<float4*>(y)[i] = o;
 }
 
+// F.interpolate(x, size, mode="bilinear", align_corners=True) on NCHW fp32 maps of any size (the
+// DA-V2 input / depth resizes, reference encoder_trans.py, and the DINO feature resize,
+// depth_predictor_trans.py): one thread per output element, consecutive threads along the output
+// row (coalesced stores, neighbouring reads), so the work spreads over all N*C planes -- PyTorch's
+// generic NCHW kernel loops over the N*C planes inside each output pixel's thread. Same
+// arithmetic as torch's upsample_bilinear2d: source = dst * (in - 1) / (out - 1) in float.
+__global__ void __launch_bounds__(256) bilinear_ac_nchw_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                               int h, int w, int ho, int wo, float rh, float rw,
+                                                               size_t total) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total) return;
+    const int ox = (int)(i % wo);
+    const size_t t = i / wo;
+    const int oy = (int)(t % ho);
+    const size_t plane = t / ho;
+    const float hr = rh * (float)oy, wr = rw * (float)ox;
+    const int h0 = (int)hr, w0 = (int)wr;
+    const int h1 = h0 + (h0 < h - 1 ? 1 : 0), w1 = w0 + (w0 < w - 1 ? 1 : 0);
+    const float l1 = hr - (float)h0, l0 = 1.f - l1, m1 = wr - (float)w0, m0 = 1.f - m1;
+    const float* src = x + plane * h * w;
+    const float a = src[(size_t)h0 * w + w0], b = src[(size_t)h0 * w + w1];
+    const float cq = src[(size_t)h1 * w + w0], d = src[(size_t)h1 * w + w1];
+    y[i] = l0 * (m0 * a + m1 * b) + l1 * (m0 * cq + m1 * d);
+}
+
 }  // namespace upsample
 }  // namespace tsplat
 
@@ -125,6 +153,21 @@ extern "C" int tsplat_resize_bilinear_nhwc_fwd(const float* x, float* y, int32_t
     hipStream_t stream = (hipStream_t)stream_;
     hipLaunchKernelGGL(bilinear_ac_nhwc_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, y,
                        height, width, c / 4, out_height, out_width, rh, rw, total);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_resize_bilinear_nchw_fwd(const float* x, float* y, int32_t planes, int32_t height,
+                                               int32_t width, int32_t out_height, int32_t out_width, void* stream_) {
+    using namespace tsplat::upsample;
+    if (!x || !y || planes <= 0 || height <= 0 || width <= 0 || out_height <= 0 || out_width <= 0)
+        return TSPLAT_EINVAL;
+    const size_t total = (size_t)planes * out_height * out_width;
+    const float rh = out_height > 1 ? (float)(height - 1) / (float)(out_height - 1) : 0.f;
+    const float rw = out_width > 1 ? (float)(width - 1) / (float)(out_width - 1) : 0.f;
+    hipStream_t stream = (hipStream_t)stream_;
+    hipLaunchKernelGGL(bilinear_ac_nchw_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, x, y,
+                       height, width, out_height, out_width, rh, rw, total);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }

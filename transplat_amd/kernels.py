@@ -706,6 +706,25 @@ def resize_bilinear_nhwc(x, size):
     return y
 
 
+def interpolate_bilinear_ac(x, size):
+    """F.interpolate(x, size, mode="bilinear", align_corners=True). NCHW-contiguous fp32 device maps
+    go through tsplat_resize_bilinear_nchw_fwd (one thread per output element; PyTorch's generic
+    kernel serialises the N*C planes per output pixel: 240 us per call at C3's batch 8); anything
+    else takes F.interpolate."""
+    import torch.nn.functional as F
+
+    size = (int(size[0]), int(size[1]))
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous()):
+        return F.interpolate(x, size, mode="bilinear", align_corners=True)
+    n, c, h, w = x.shape
+    y = torch.empty((n, c, size[0], size[1]), dtype=torch.float32, device=x.device)
+    lib = _lib.load()
+    rc = lib.tsplat_resize_bilinear_nchw_fwd(_lib.ptr(x), _lib.ptr(y), n * c, h, w, size[0], size[1],
+                                             _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_resize_bilinear_nchw_fwd")
+    return y
+
+
 def sh_rotation(rotations, d_sh: int):
     """[n, 3, 3] rotations -> [n, d_sh, d_sh] block-diagonal real-SH rotations (e3nn's
     wigner_D per degree, see misc/sh_rotation.py), one kernel launch."""

@@ -33,8 +33,9 @@ def _resize(x, modifier: dict, align_corners: bool):
     """F.interpolate(x, **modifier, mode="bilinear", align_corners=...); the channels-last fp32 maps
     of the head go through one kernel (kernels.resize_bilinear_nhwc) instead of torch's NHWC
     interpolation kernel."""
+    # (F.interpolate keeps the input dtype under autocast, so an fp32 map takes the kernel there too)
     if (_DPT_EPI and align_corners and x.is_cuda and x.dtype == torch.float32 and x.shape[1] % 4 == 0
-            and x.is_contiguous(memory_format=torch.channels_last) and not torch.is_autocast_enabled("cuda")):
+            and x.is_contiguous(memory_format=torch.channels_last)):
         if "size" in modifier:
             size = modifier["size"]
         else:

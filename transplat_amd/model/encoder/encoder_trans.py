@@ -142,9 +142,9 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
             da_images = self.normalize_images(context["image"])
             da_images = torch.cat((da_images[:, :, 2:3], da_images[:, :, 0:2]), dim=2)
             da_images = da_images.reshape(b * v, 3, h, w)
-            da_images = F.interpolate(da_images, (252, 252), mode="bilinear", align_corners=True)
+            da_images = kernels.interpolate_bilinear_ac(da_images, (252, 252))
             da_depth, out_feature = self.da_model(da_images)
-            da_depth = F.interpolate(da_depth[None].float(), (h, w), mode="bilinear", align_corners=True)
+            da_depth = kernels.interpolate_bilinear_ac(da_depth[None].float().contiguous(), (h, w))
             da_depth = da_depth.view(b, v, 1, h, w).flatten(2)
             # per-view min / max in two aminmax stages (rows of w, then the h row results): the
             # single-row reductions ran on 2 workgroups each (~20 us apiece); exact either way

@@ -180,7 +180,7 @@ class DepthPredictorTrans(nn.Module):
             cnn_features = rearrange(cnn_features, "b v ... -> (v b) ...")
         if dino_feature is not None:
             dino_feature = rearrange(dino_feature, "b v ... -> (v b) ...")
-            dino_feature = F.interpolate(dino_feature, size=(h, w), mode="bilinear", align_corners=True)
+            dino_feature = kernels.interpolate_bilinear_ac(dino_feature, (h, w))
         feat_comb_lists, intr_curr, pose_curr_lists, disp_candi_curr = prepare_feat_proj_data_lists(
             features, intrinsics, extrinsics, near, far, num_samples=self.num_depth_candidates)
         feat01 = feat_comb_lists[0]
@@ -204,8 +204,9 @@ class DepthPredictorTrans(nn.Module):
             coarse_disps = (disp_candi_curr * pdf).sum(dim=1, keepdim=True)
             pdf_max = torch.max(pdf, dim=1, keepdim=True)[0]
         pdf_max = F.interpolate(pdf_max, scale_factor=self.upscale_factor)
-        fullres_disps = F.interpolate(coarse_disps, scale_factor=self.upscale_factor, mode="bilinear",
-                                      align_corners=True)
+        up = int(self.upscale_factor)  # align_corners: the ratio comes from the sizes, as torch's
+        fullres_disps = kernels.interpolate_bilinear_ac(coarse_disps, (coarse_disps.shape[-2] * up,
+                                                                       coarse_disps.shape[-1] * up))
 
         proj_feat_in_fullres = _conv_upsample_gelu(self.upsampler, torch.cat((feat01, cnn_features), dim=1))
         proj_feature = self.proj_feature(proj_feat_in_fullres)
