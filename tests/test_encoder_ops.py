@@ -510,11 +510,15 @@ def test_conv_bias_act(device, cin, cout, hw, act, res):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("form", ["16", "16x8", "32"])
 @pytest.mark.parametrize("b,n,heads", [(2, 325, 12), (1, 37, 12), (3, 5, 2), (1, 1025, 4)])
-def test_mha_kernel(device, b, n, heads):
+def test_mha_kernel(device, b, n, heads, form, monkeypatch):
     """DINOv2 multi-head attention (tsplat_mha_f32_fwd, straight from the qkv layout) vs torch SDPA
-    math on the CPU; N = 325 is the 256x256 token count, N = 5 leaves a wave without keys."""
+    math on the CPU, for each kernel form (TSPLAT_MHA: 16-query blocks with 4 or 8 waves, 32-query
+    blocks); N = 325 is the 256x256 token count, N = 5 leaves waves without keys."""
     from transplat_amd import kernels as K
+
+    monkeypatch.setenv("TSPLAT_MHA", form)
 
     qkv = seeded((b, n, 3 * heads * 64), 71) * 2.0
     ref = E.mha(qkv, heads, 64 ** -0.5)

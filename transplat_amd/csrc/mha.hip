@@ -36,13 +36,22 @@ __device__ __forceinline__ float halves_sum(float x) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
+// lanes l and l ^ 16 (v_permlane16_swap exchanges 16-lane rows 0 <-> 1 and 2 <-> 3, VALU only)
+__device__ __forceinline__ float rows_max(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float rows_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 struct Tile {
     floatx4 k[8];  // this lane's key row, dims 32 h .. 32 h + 31
     float v[32];   // V[key 8u + 4h + j][32 dt + c] for (u, j, dt): index (u * 4 + j) * 2 + dt
 };
 
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(2, 2)))
 mha_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, int H, float scale) {
     __shared__ float sO[4][2][16][64];
     __shared__ float sML[4][2][kQW];
@@ -334,6 +343,170 @@ mha_cf32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int B, i
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same attention on 16-query blocks with v_mfma_f32_16x16x4_f32 (the same fp32 FLOP rate as
+// the 32x32x2 form). Why: at the DINOv2 shape the 32-query kernel makes 24 x 11 = 264 workgroups of
+// 4 waves at 1 wave per SIMD (276 registers), so 8 CUs run a second workgroup after the first and a
+// lone wave per SIMD exposes every load and softmax latency (SQ counters: 63 % of wave time in
+// issue stalls). Here: 24 x 21 = 504 workgroups of W waves on 16 queries, each wave a tile-aligned
+// share of the 16-key tiles (no per-wave key-range masking), ~100 registers, so every workgroup is
+// resident at once and a SIMD's waves overlap one's softmax with another's MFMAs.
+// Operand maps (lane = 16 g + c):
+//   S^T = K Q^T, k-step t contracts dim 16 g + t at lane group g (any dim permutation is a valid
+//     contraction order as long as A and B agree): A = K[key c][16 g + t], B = Q[query c][16 g + t]
+//     -> each lane's K and Q operands are one 64-B contiguous run; s[i] = S^T[key 4 g + i][query c];
+//   O^T += V^T P^T, k-step t contracts keys {4 g + t}: B = P^T[key 4 g + t][query c] = s[t] itself,
+//     A = V[key 4 g + t][16 dt + c]; o[dt][i] = O^T[d = 16 dt + 4 g + i][query c].
+// Per-query softmax statistics reduce over the 4 registers and the 4 lane groups.
+template <int W>
+__global__ void __launch_bounds__(W * 64)
+mha16_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, int H, float scale) {
+    __shared__ float sO[W][16][64];
+    __shared__ float sML[W][2][16];
+
+    // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so consecutive linear ids
+    // would spread one (image, head)'s query blocks over every XCD's L2; remapped, XCD x runs the
+    // logical ids [x * total / 8, (x + 1) * total / 8), i.e. whole (image, head) K / V sets
+    const int nq = gridDim.x, total = nq * gridDim.y;
+    int lin = blockIdx.x + blockIdx.y * nq;
+    if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
+    const int bh = lin / nq, qblk = lin - bh * nq;
+    const int b = bh / H, head = bh - b * H;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    const size_t tok = (size_t)3 * H * kD;
+    const float* base = qkv + (size_t)b * N * tok + (size_t)head * kD;
+    const float* kb = base + (size_t)H * kD;
+    const float* vb = base + (size_t)2 * H * kD;
+
+    const int nt = (N + 15) / 16;
+    const int t_lo = wid * nt / W, t_hi = (wid + 1) * nt / W;
+    const int q = qblk * 16 + c;
+
+    float qr[16];
+    {
+        const float qs = scale * kLog2e;
+        const floatx4* src = reinterpret_cast<const floatx4*>(base + (size_t)min(q, N - 1) * tok + 16 * g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const floatx4 t = src[i];
+            qr[4 * i] = t.x * qs;
+            qr[4 * i + 1] = t.y * qs;
+            qr[4 * i + 2] = t.z * qs;
+            qr[4 * i + 3] = t.w * qs;
+        }
+    }
+    struct Tile16 {
+        floatx4 k[4];  // K[key c][16 g .. 16 g + 15]
+        float v[16];   // V[key 4 g + t][16 dt + c] at t * 4 + dt
+    };
+    auto load_tile = [&](int tile, Tile16& T) {
+        const int k0 = tile * 16;
+        const floatx4* ks = reinterpret_cast<const floatx4*>(kb + (size_t)min(k0 + c, N - 1) * tok + 16 * g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) T.k[i] = ks[i];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float* vs = vb + (size_t)min(k0 + 4 * g + t, N - 1) * tok + c;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) T.v[t * 4 + dt] = vs[16 * dt];
+        }
+    };
+
+    floatx4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = (floatx4){0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.f;
+    Tile16 cur, nxt;
+    if (t_lo < t_hi) load_tile(t_lo, cur);
+    for (int tile = t_lo; tile < t_hi; ++tile) {
+        const bool has_next = tile + 1 < t_hi;
+        if (has_next) load_tile(tile + 1, nxt);
+        // two independent accumulation chains (dims 16 g + 0..7 / 8..15), summed once
+        floatx4 s = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            s = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.k[i].x, qr[4 * i + 0], s, 0, 0, 0);
+            s2 = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.k[i + 2].x, qr[4 * i + 8], s2, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.k[i].y, qr[4 * i + 1], s, 0, 0, 0);
+            s2 = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.k[i + 2].y, qr[4 * i + 9], s2, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.k[i].z, qr[4 * i + 2], s, 0, 0, 0);
+            s2 = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.k[i + 2].z, qr[4 * i + 10], s2, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.k[i].w, qr[4 * i + 3], s, 0, 0, 0);
+            s2 = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.k[i + 2].w, qr[4 * i + 11], s2, 0, 0, 0);
+        }
+        s += s2;
+        // keys past N (the last tile only) score -inf: their exp is exactly 0
+        const int kg = tile * 16 + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (kg + i >= N) s[i] = -INFINITY;
+        float bmax = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
+        bmax = halves_max(rows_max(bmax));
+        const float m_new = fmaxf(m_run, bmax);  // finite: every tile holds a key < N
+        if (__any(m_new > m_run)) {
+            const float corr = __builtin_amdgcn_exp2f(m_run - m_new);
+            l_run *= corr;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+            m_run = m_new;
+        }
+        float bsum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            s[i] = __builtin_amdgcn_exp2f(s[i] - m_run);
+            bsum += s[i];
+        }
+        l_run += halves_sum(rows_sum(bsum));
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.v[t * 4 + dt], s[t], o[dt], 0, 0, 0);
+        if (has_next) cur = nxt;
+    }
+
+    // merge the W key shares
+    if (g == 0) {
+        sML[wid][0][c] = m_run;
+        sML[wid][1][c] = l_run;
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sO[wid][dt * 4 + i][lane] = o[dt][i];
+    __syncthreads();
+    // 16 queries x 16 runs of 4 dims: run j holds d = 4 j .. 4 j + 3 = 16 dt + 4 g' + i (dt = j >> 2,
+    // g' = j & 3) of query qq, i.e. sO[w][4 dt + i][16 g' + qq]
+    if (tid >= 256) return;
+    const int qq = tid >> 4, j = tid & 15;
+    const int qo = qblk * 16 + qq;
+    if (qo >= N) return;
+    float mw[W], M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        mw[w] = sML[w][0][qq];
+        M = fmaxf(M, mw[w]);
+    }
+    float a[W], L = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        a[w] = mw[w] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw[w] - M);
+        L += a[w] * sML[w][1][qq];
+    }
+    const float inv = 1.0f / L;
+    float acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < W; ++w) t += a[w] * sO[w][(j >> 2) * 4 + i][(j & 3) * 16 + qq];
+        acc[i] = t * inv;
+    }
+    float* dst = out + (((size_t)b * N + qo) * H + head) * kD + 4 * j;
+    *reinterpret_cast<floatx4*>(dst) = (floatx4){acc[0], acc[1], acc[2], acc[3]};
+}
+
 }  // namespace mha
 }  // namespace tsplat
 
@@ -343,9 +516,20 @@ extern "C" int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, i
     if (!qkv || !out || batch <= 0 || tokens <= 0 || heads <= 0 || head_dim != kD) return TSPLAT_EINVAL;
     if ((int64_t)batch * heads > 65535) return TSPLAT_EINVAL;
     hipStream_t stream = (hipStream_t)stream_;
+    // TSPLAT_MHA: "16" (default, 4 waves per 16-query block), "16x8" (8 waves), "32" (the
+    // 32-query kernel); A/B knob
+    const char* env = getenv("TSPLAT_MHA");
+    const int form = !env ? 0 : (env[0] == '3' ? 2 : (env[2] == 'x' ? 1 : 0));
     TSPLAT_PROF_BEGIN(tsplat::prof::kMha, stream);
-    hipLaunchKernelGGL(mha_f32_kernel, dim3((tokens + kQW - 1) / kQW, batch * heads), dim3(kThreads), 0, stream, qkv,
-                       out, tokens, heads, scale);
+    if (form == 2)
+        hipLaunchKernelGGL(mha_f32_kernel, dim3((tokens + kQW - 1) / kQW, batch * heads), dim3(kThreads), 0, stream,
+                           qkv, out, tokens, heads, scale);
+    else if (form == 1)
+        hipLaunchKernelGGL(mha16_f32_kernel<8>, dim3((tokens + 15) / 16, batch * heads), dim3(512), 0, stream, qkv,
+                           out, tokens, heads, scale);
+    else
+        hipLaunchKernelGGL(mha16_f32_kernel<4>, dim3((tokens + 15) / 16, batch * heads), dim3(256), 0, stream, qkv,
+                           out, tokens, heads, scale);
     TSPLAT_PROF_END(tsplat::prof::kMha, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
