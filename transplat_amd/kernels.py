@@ -402,6 +402,11 @@ _CONV_PACKED: dict = {}
 _CONV_MODE = os.environ.get("TSPLAT_CONV", "auto")
 _CONV_KSPLIT = int(os.environ.get("TSPLAT_CONV_KSPLIT", "0"))  # tuning override (tools/bench_conv.py)
 _CONV_MAX_FLOP = 1.5e9  # above this MIOpen's kernels are as fast or faster (tools/bench_conv.py)
+# 1x1 launch shape: grid cap in waves and minimum ci pairs per wave. Same-box A/B (tools/ab_conv1.sh):
+# 16384 / 8 reads 338.98 / 338.99 views/s vs 337.91 / 337.58 for the 3x3 rule (4096 / 16); 8192 / 16
+# and 16384 / 4 sit in between
+_CONV1_WAVES = int(os.environ.get("TSPLAT_CONV1_WAVES", "16384"))
+_CONV1_PAIRS = int(os.environ.get("TSPLAT_CONV1_PAIRS", "8"))
 
 
 def conv_pack_weight(weight):
@@ -471,12 +476,14 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
     hv, wv = (2 * h, 2 * w) if upsample else (h, w)
     hout, wout = (hv + 2 * (k // 2) - k) // stride + 1, (wv + 2 * (k // 2) - k) // stride + 1
     y = torch.empty((n, co, hout, wout), dtype=torch.float32, device=x1.device)
-    # waves per 32 x 32 tile: the ci pairs split over up to 16 waves (>= 2 pairs of a 3x3, >= 16 of a
-    # 1x1 each) while the grid stays <= 4096 waves
+    # waves per 32 x 32 tile: the ci pairs split over up to 16 waves (>= 2 pairs of a 3x3 each while
+    # the grid stays <= 4096 waves; >= 8 pairs of a 1x1 each up to 16384 waves: its waves are short,
+    # one or two batches of loads, so more of them in flight hide more of the latency)
     tiles = ((n * hout * wout + 31) // 32) * ((co + 31) // 32)
     pairs = ci // 2
     ksplit = 16
-    while ksplit > 1 and (tiles * ksplit > 4096 or pairs < (2 if k == 3 else 16) * ksplit):
+    cap, min_pairs = (4096, 2) if k == 3 else (_CONV1_WAVES, _CONV1_PAIRS)
+    while ksplit > 1 and (tiles * ksplit > cap or pairs < min_pairs * ksplit):
         ksplit //= 2
     ksplit = _CONV_KSPLIT or ksplit
     pb = _f32(bias) if bias is not None else None
