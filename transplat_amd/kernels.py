@@ -407,6 +407,10 @@ _CONV_MAX_FLOP = 1.5e9  # above this MIOpen's kernels are as fast or faster (too
 # and 16384 / 4 sit in between
 _CONV1_WAVES = int(os.environ.get("TSPLAT_CONV1_WAVES", "16384"))
 _CONV1_PAIRS = int(os.environ.get("TSPLAT_CONV1_PAIRS", "8"))
+# the same for 3x3 (tools/ab_conv3.sh, same box: 8192 / 2 reads 340.3 / 339.7 views/s vs 339.3 /
+# 339.2 at 4096 / 2; 16384 / 1 and 8192 / 1 in between)
+_CONV3_WAVES = int(os.environ.get("TSPLAT_CONV3_WAVES", "8192"))
+_CONV3_PAIRS = int(os.environ.get("TSPLAT_CONV3_PAIRS", "2"))
 
 
 def conv_pack_weight(weight):
@@ -477,12 +481,12 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
     hout, wout = (hv + 2 * (k // 2) - k) // stride + 1, (wv + 2 * (k // 2) - k) // stride + 1
     y = torch.empty((n, co, hout, wout), dtype=torch.float32, device=x1.device)
     # waves per 32 x 32 tile: the ci pairs split over up to 16 waves (>= 2 pairs of a 3x3 each while
-    # the grid stays <= 4096 waves; >= 8 pairs of a 1x1 each up to 16384 waves: its waves are short,
+    # the grid stays <= 8192 waves; >= 8 pairs of a 1x1 each up to 16384 waves: its waves are short,
     # one or two batches of loads, so more of them in flight hide more of the latency)
     tiles = ((n * hout * wout + 31) // 32) * ((co + 31) // 32)
     pairs = ci // 2
     ksplit = 16
-    cap, min_pairs = (4096, 2) if k == 3 else (_CONV1_WAVES, _CONV1_PAIRS)
+    cap, min_pairs = (_CONV3_WAVES, _CONV3_PAIRS) if k == 3 else (_CONV1_WAVES, _CONV1_PAIRS)
     while ksplit > 1 and (tiles * ksplit > cap or pairs < min_pairs * ksplit):
         ksplit //= 2
     ksplit = _CONV_KSPLIT or ksplit
