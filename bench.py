@@ -13,6 +13,12 @@ Workloads (a "step" = one pass of the hot path over one batch of synthetic scene
   raster : the decoder alone on precomputed synthetic Gaussians (G = 131,072 per scene)
 Scenes shard embarrassingly across ranks (rank r renders its own B scenes; no data-path
 collective); one all-reduce of the timing and a gather of per-rank counts close the run.
+
+Self-launch: `python bench.py --gpus N` with N > 1 and no torch.distributed environment starts
+`torch.distributed.run --nproc-per-node N` itself (as a child process, before anything touches the
+GPU) and exits with its status; under a launcher, --gpus must equal WORLD_SIZE or the run fails.
+`--workload selftest` is a CPU-only stand-in step (no GPU, no kernels) that exercises exactly
+this launch / barrier / max-over-ranks / JSON path (tests/test_distributed.py).
 """
 from __future__ import annotations
 
@@ -20,6 +26,8 @@ import argparse
 import json
 import os
 import platform
+import subprocess
+import sys
 import time
 from pathlib import Path
 
@@ -37,7 +45,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workload", choices=["e2e", "raster"], default="e2e")
+    ap.add_argument("--workload", choices=["e2e", "raster", "selftest"], default="e2e")
     ap.add_argument("--dense-dtype", choices=["fp32", "bf16"], default="fp32")
     ap.add_argument("--dominant", default=None, help="kernel timed for the roofline object")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
@@ -48,6 +56,27 @@ def parse():
                     help="MIOpen's default convolution algorithm choice instead of its measured search "
                          "(torch.backends.cudnn.benchmark, on by default: +2.4%% e2e at b = 1)")
     return ap.parse_args()
+
+
+def self_launch(args) -> int | None:
+    """--gpus N > 1 without a launcher: run this script under torch.distributed.run with N local
+    ranks (a child process; this one has not touched the GPU) and return its exit status. Under a
+    launcher, a --gpus that disagrees with WORLD_SIZE is an error (the JSON would misreport)."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if args.gpus != int(world):
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+
+    with socket.socket() as sk:  # a free rendezvous port on the loopback interface
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    return subprocess.call(cmd)
 
 
 def init_dist():
@@ -62,7 +91,8 @@ def init_dist():
         local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
+        if backend == "nccl" or torch.cuda.device_count() > 0:
+            torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
         else:
@@ -260,9 +290,36 @@ def cpu_baseline_raster(cpu_inputs, seconds: float):
     }
 
 
+def selftest_main(args, world, rank):
+    """CPU stand-in step (a small matmul, plus rank-dependent sleep so the max-over-ranks is
+    observable): the launch, barrier, timing all-reduce and JSON line of the real bench, no GPU."""
+    x = torch.randn(128, 128)
+
+    def step():
+        time.sleep(0.01 * (rank + 1))
+        return x @ x
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed_steps(step, args.steps, world, lambda: None, torch.device("cpu"))
+    if rank == 0:
+        print(json.dumps({"metric": "selftest steps/s", "value": world * args.steps / elapsed, "unit": "steps/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "config": {"workload": "selftest (CPU)", "parallelism": f"scene-shard x{world}"}}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     world, rank, local = init_dist()
+    if args.workload == "selftest":
+        return selftest_main(args, world, rank)
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
     if not args.no_conv_search:

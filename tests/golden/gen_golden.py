@@ -330,9 +330,7 @@ def gen_depth_predictor():
          raw_rows=raw_s)
 
 
-def gen_depth_predictor_v3():
-    """Three context views (DTU-style nctx = 3 at 256x256): the reference's pairwise match_two
-    averaging path (depth_predictor_trans.py:351-373)."""
+def _gen_depth_predictor_multiview(nv, seed, sd, subset_seeds, name):
     dp = imp("src.model.encoder.matching.depth_predictor_trans")
     from transplat_amd import synthetic as S
 
@@ -340,23 +338,34 @@ def gen_depth_predictor_v3():
         feature_channels=128, upscale_factor=4, num_depth_candidates=128,
         costvolume_unet_feat_dim=128, costvolume_unet_channel_mult=(1, 1, 1),
         costvolume_unet_attn_res=(4,), gaussian_raw_channels=84, gaussians_per_pixel=1,
-        num_views=3, depth_unet_feat_dim=32, depth_unet_attn_res=[16],
+        num_views=nv, depth_unet_feat_dim=32, depth_unet_attn_res=[16],
         depth_unet_channel_mult=[1, 1, 1, 1, 1], DA_size=64)
-    m = canonical_init(m, seed=33).eval()
-    ctx = S.make_batch(1, num_context=3, image_shape=(256, 256))["context"]
-    feats = seeded((1, 3, 128, 64, 64), 511, 0.5)
-    cnn = seeded((1, 3, 128, 64, 64), 512, 0.5)
-    da_depth = seeded((1, 3, 1, 256, 256), 513, 1.0, kind="rand")
-    dino = seeded((1, 3, 64, 144, 144), 514, 0.5)
-    extra = {"images": ctx["image"].permute(1, 0, 2, 3, 4).reshape(3, 3, 256, 256), "scene_names": None}
+    m = canonical_init(m, seed=seed).eval()
+    ctx = S.make_batch(1, num_context=nv, image_shape=(256, 256))["context"]
+    feats = seeded((1, nv, 128, 64, 64), sd[0], 0.5)
+    cnn = seeded((1, nv, 128, 64, 64), sd[1], 0.5)
+    da_depth = seeded((1, nv, 1, 256, 256), sd[2], 1.0, kind="rand")
+    dino = seeded((1, nv, 64, 144, 144), sd[3], 0.5)
+    extra = {"images": ctx["image"].permute(1, 0, 2, 3, 4).reshape(nv, 3, 256, 256), "scene_names": None}
     with torch.no_grad():
         depths, dens, raw = m(feats, ctx["intrinsics"], ctx["extrinsics"], ctx["near"], ctx["far"],
                               gaussians_per_pixel=1, deterministic=True, extra_info=extra,
                               cnn_features=cnn, da_depth=da_depth, dino_feature=dino)
-    idx, raw_s = subset_rows(raw.reshape(-1, raw.shape[-1]), 4096, 9)
-    didx, d_s = subset_rows(depths.flatten(), 16384, 10)
-    save("depth_predictor_v3", depth_idx=didx, depths=d_s, densities=dens.flatten()[didx], raw_idx=idx,
-         raw_rows=raw_s)
+    idx, raw_s = subset_rows(raw.reshape(-1, raw.shape[-1]), 4096, subset_seeds[0])
+    didx, d_s = subset_rows(depths.flatten(), 16384, subset_seeds[1])
+    save(name, depth_idx=didx, depths=d_s, densities=dens.flatten()[didx], raw_idx=idx, raw_rows=raw_s)
+
+
+def gen_depth_predictor_v3():
+    """Three context views (DTU-style nctx = 3 at 256x256): the reference's pairwise match_two
+    averaging path (depth_predictor_trans.py:351-373)."""
+    _gen_depth_predictor_multiview(3, 33, (511, 512, 513, 514), (9, 10), "depth_predictor_v3")
+
+
+def gen_depth_predictor_v4():
+    """Four context views: the reference's six-pair match_two averaging path
+    (depth_predictor_trans.py:374-414)."""
+    _gen_depth_predictor_multiview(4, 35, (521, 522, 523, 524), (11, 12), "depth_predictor_v4")
 
 
 def gen_unet():
@@ -636,6 +645,7 @@ ALL = {
     "unet": gen_unet,
     "depth_predictor": gen_depth_predictor,
     "depth_predictor_v3": gen_depth_predictor_v3,
+    "depth_predictor_v4": gen_depth_predictor_v4,
     "depth_anything": gen_depth_anything,
     "covariance": gen_covariance,
     "crop_shim": gen_crop_shim,

@@ -278,3 +278,19 @@ def test_conv3x3_wino_wide_shape_at_production_size(device):
     y = K.conv3x3_wino(parts[0], wt, b, extra=tuple(parts[1:]))
     ref = torch.nn.functional.conv2d(torch.cat(parts, 1), wt, b, padding=1)
     assert ((y - ref).abs().max() / ref.abs().max()).item() < 2e-5
+
+
+@pytest.mark.gpu
+def test_conv3x3_wino_ok_rejects_wide_input(device):
+    """More input channels than the Winograd launch's plane table (kMaxCiPad = 1024 after padding to
+    16) must route to MIOpen instead of reaching the kernel's EINVAL (advisor finding, round 2)."""
+    from transplat_amd import kernels
+
+    x = torch.randn(1, 1040, 20, 20, device=device)
+    conv = torch.nn.Conv2d(1040, 32, 3, padding=1).to(device)
+    assert not kernels.conv3x3_wino_ok(x, conv.weight, vs_miopen=True)
+    with torch.no_grad():
+        y = kernels.conv2d_forward(conv, x)
+        ref = torch.nn.functional.conv2d(x, conv.weight, conv.bias, padding=1)
+    torch.cuda.synchronize()
+    assert (y - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()

@@ -131,3 +131,37 @@ def test_bench_timed_steps_world2_gloo():
     assert [r[1] for r in res] == [5, 5]  # exactly `steps` calls per rank
     assert res[0][2] == res[1][2]  # every rank reports the max
     assert 0.2 <= res[1][2] < 0.6  # rank 1: 5 x 40 ms
+
+
+def _run_bench(*argv, env_extra=None, timeout=240):
+    import subprocess
+    import sys
+
+    repo = Path(__file__).resolve().parents[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(TSPLAT_DIST_BACKEND="gloo", **(env_extra or {}))
+    return subprocess.run([sys.executable, str(repo / "bench.py"), *argv], cwd=repo, env=env,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_main_self_launches_world2_gloo():
+    """`python bench.py --gpus 2` with no launcher environment starts torch.distributed.run with two
+    ranks itself; bench.main() then runs end to end on each rank (CPU selftest step, gloo) and rank 0
+    prints one JSON line with n_gpus = 2 and the max-over-ranks time (rank 1 sleeps 20 ms per step,
+    rank 0 10 ms)."""
+    import json
+
+    out = _run_bench("--gpus", "2", "--workload", "selftest", "--steps", "10", "--warmup", "1")
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["steps"] == 10
+    assert 20.0 <= res["ms_per_step"] < 60.0  # the slower rank's 20 ms steps
+    assert abs(res["value"] - 2 * 10 / (res["ms_per_step"] * 10 / 1e3)) < 1e-6 * res["value"]
+
+
+def test_bench_gpus_must_match_world_size():
+    out = _run_bench("--gpus", "2", "--workload", "selftest", "--steps", "1", "--warmup", "0",
+                     env_extra={"WORLD_SIZE": "1"})
+    assert out.returncode != 0 and "WORLD_SIZE=1" in (out.stderr + out.stdout)

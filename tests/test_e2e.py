@@ -147,3 +147,42 @@ def test_c3_batch8_bf16_step(device):
     assert mad < 2e-2 and psnr > 30.0
     assert mad_ge < 2e-2 and psnr_ge > 30.0
     assert mad_one < 1e-4
+
+
+@pytest.mark.gpu
+def test_tuned_gemms_keep_outputs(device):
+    """The bench step replays the committed TunableOp GEMM choices (transplat_amd/tuned/
+    gemms_gfx950.csv, gemm_tuning.use_tuned_gemms). The same eager step with and without them must
+    agree within the envelope two eager steps already show (library reduction orders differ per
+    call: test_e2e_graph_matches_eager), on the Gaussians and on the rendered views."""
+    import torch.cuda.tunable as tun
+
+    from transplat_amd.e2e import build_model
+    from transplat_amd.gemm_tuning import use_tuned_gemms
+
+    model = build_model(device)
+    data = S.make_batch(1, image_shape=(256, 256), device=device)
+
+    def run():
+        with torch.no_grad():
+            b = model.data_shim(data)
+            g = model.encoder(b["context"], 0, deterministic=True)
+            out = model.test_step(data).color
+        torch.cuda.synchronize()
+        return g.means.clone(), g.harmonics.clone(), out.clone()
+
+    was = tun.is_enabled()
+    tun.enable(False)
+    try:
+        ref = run()
+        assert use_tuned_gemms(device), "committed GEMM solutions not loaded (validator mismatch?)"
+        assert tun.is_enabled() and not tun.tuning_is_enabled()
+        tuned = run()
+    finally:
+        tun.enable(was)
+    rel = lambda a, b: ((a - b).abs().max() / b.abs().max()).item()
+    print(f"tuned vs default GEMMs: means {rel(tuned[0], ref[0]):.2e}, harmonics {rel(tuned[1], ref[1]):.2e}, "
+          f"pixels max {(tuned[2] - ref[2]).abs().max().item():.2e} mean {(tuned[2] - ref[2]).abs().mean().item():.2e}")
+    assert rel(tuned[0], ref[0]) < 1e-3 and rel(tuned[1], ref[1]) < 1e-2
+    assert (tuned[2] - ref[2]).abs().max().item() < 2e-2
+    assert (tuned[2] - ref[2]).abs().mean().item() < 1e-4

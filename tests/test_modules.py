@@ -166,7 +166,8 @@ def test_unet_gpu(device, tag, ch, mult, attn, hw):
 
 
 # ------------------------------------------------------------------ full depth predictor
-_DP_CASES = {2: ("depth_predictor", 31, (501, 502, 503, 504)), 3: ("depth_predictor_v3", 33, (511, 512, 513, 514))}
+_DP_CASES = {2: ("depth_predictor", 31, (501, 502, 503, 504)), 3: ("depth_predictor_v3", 33, (511, 512, 513, 514)),
+             4: ("depth_predictor_v4", 35, (521, 522, 523, 524))}  # V = 4: six match_two pairs (:374-414)
 
 
 def _depth_predictor(dev, nv=2):
@@ -206,7 +207,7 @@ def test_depth_predictor_cpu(cpu_ops, nv):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nv", [2, 3])
+@pytest.mark.parametrize("nv", [2, 3, 4])
 def test_depth_predictor_gpu(device, nv):
     _check_depth_predictor(_run(device, lambda d: _depth_predictor(d, nv)), 2e-3, nv)
 

@@ -1,8 +1,18 @@
 """Rasterizer parity: gfx950 kernel (tsplat_raster_fwd) vs the scalar C restatement (oracle/).
 
-CPU tests check the oracle itself (single-Gaussian closed form in float64, culling rules);
-GPU tests compare the HIP path through the C-ABI with the oracle on identical inputs.
-Tolerance (BASELINE.json north_star): L-inf <= 1e-4 on fp32 images, radii identical.
+The oracle's LITERAL mode restates the upstream graphdeco forward expression by expression
+(oracle/raster_ref.c header), independent of the kernel's arithmetic (the kernel evaluates the
+power in the log2 domain with the hardware exp2, and its EWA covariance in another order).
+CPU tests check the oracle itself (single-Gaussian closed form in float64, culling rules, the
+literal vs kernel-order modes, the threshold flags); GPU tests compare the HIP path through the
+C-ABI with the literal oracle on identical inputs.
+
+Tolerance (BASELINE.json north_star): L-inf <= 1e-4 on fp32 images. The blend's decisions are
+discontinuous (alpha >= 1/255, T < 1e-4, power > 0, the tile rect / radius / near-plane cull), so
+pixels where the oracle finds one of them within a rounding margin of its threshold (flags from
+oracle.raster.render_flagged) are excluded from the L-inf check -- counted, printed and bounded
+(<= MAX_FLAGGED of the image) -- and radii must be identical for every Gaussian whose radius /
+rect / cull is not itself ambiguous.
 """
 import math
 
@@ -15,6 +25,7 @@ from transplat_amd import synthetic as S
 from transplat_amd.model.decoder.hip_splatting import RasterCameras, prepare_cameras, rasterize
 
 ATOL = 1e-4
+MAX_FLAGGED = 0.01  # fraction of pixels the threshold flags may exclude
 
 
 def _cams(ext, K, near, far, bg):
@@ -114,19 +125,37 @@ def test_oracle_depth_order_front_to_back():
 
 
 def _run_both(g, cams_cpu, hw, vps, deg, device, capacity=None):
-    color_ref, radii_ref, counts = oracle_raster.render(
+    color_ref, radii_ref, counts, pflag, gflag = oracle_raster.render_flagged(
         g["means"], g["covariances"], g["harmonics"], g["opacities"], cams_cpu, hw, vps, deg)
     gd = {k: v.to(device) for k, v in g.items()}
     color, radii = rasterize(gd["means"], gd["covariances"], gd["harmonics"], gd["opacities"],
                              cams_cpu.to(device), hw, vps, sh_degree=deg, capacity=capacity)
     torch.cuda.synchronize()
-    return color.cpu().numpy(), radii.cpu().numpy(), color_ref, radii_ref, counts
+    return color.cpu().numpy(), radii.cpu().numpy(), (color_ref, radii_ref, pflag, gflag), counts
 
 
-def _assert_parity(color, radii, color_ref, radii_ref):
-    np.testing.assert_array_equal(radii, radii_ref)
-    err = np.abs(color - color_ref).max()
-    assert err <= ATOL, f"L-inf {err:.3e} > {ATOL}"
+def parity_report(color, radii, ref, atol=ATOL, max_flagged=MAX_FLAGGED, tag=""):
+    """Kernel vs literal oracle: L-inf over unflagged pixels, radii over unambiguous Gaussians.
+    Returns (linf_unflagged, n_flagged, n_pixels, linf_all) and prints them."""
+    color_ref, radii_ref, pflag, gflag = ref
+    err = np.abs(color - color_ref).max(axis=1)  # [V, H, W] over channels
+    clear = pflag == 0
+    linf = float(err[clear].max()) if clear.any() else 0.0
+    n_flag = int((~clear).sum())
+    print(f"raster parity{tag}: L-inf {linf:.3e} over {int(clear.sum())} unflagged pixels; "
+          f"{n_flag} flagged ({n_flag / clear.size:.3%}; rect {int(((pflag & oracle_raster.FLAG_RECT) > 0).sum())}, "
+          f"power {int(((pflag & oracle_raster.FLAG_POWER) > 0).sum())}, alpha {int(((pflag & oracle_raster.FLAG_ALPHA) > 0).sum())}, "
+          f"T {int(((pflag & oracle_raster.FLAG_T) > 0).sum())}), L-inf incl. flagged {float(err.max()):.3e}; "
+          f"ambiguous radii {int(gflag.sum())}")
+    bad = (radii != radii_ref) & ~gflag
+    assert not bad.any(), f"{int(bad.sum())} radii differ (first at {np.argwhere(bad)[0]})"
+    assert linf <= atol, f"L-inf {linf:.3e} > {atol} on unflagged pixels"
+    assert n_flag <= max_flagged * clear.size, f"{n_flag} flagged pixels > {max_flagged:.1%}"
+    return linf, n_flag, clear.size, float(err.max())
+
+
+def _assert_parity(color, radii, ref, *_):
+    parity_report(color, radii, ref)
 
 
 def _target_cams(batch, hw, bg=None):
@@ -154,13 +183,54 @@ def test_oracle_thread_count_invariant():
     assert np.array_equal(c1, c4) and np.array_equal(r1, r4) and n1 == n4
 
 
+def test_oracle_literal_vs_kernel_order_modes():
+    """The two arithmetic orders of the oracle (literal upstream expressions vs the round-2
+    kernel's Horner power + Cephes exp) agree within the north-star tolerance wherever the
+    literal mode's flags call every decision clear -- the same check the GPU tests apply."""
+    hw = (64, 64)
+    g = S.make_gaussians(1, image_shape=hw)
+    cams = _target_cams(S.make_batch(1, image_shape=hw), hw, bg=(0.1, 0.2, 0.3))
+    args = (g["means"], g["covariances"], g["harmonics"], g["opacities"], cams, hw, 3, 4)
+    ck, rk, nk = oracle_raster.render(*args, mode="kernel")
+    ref = oracle_raster.render_flagged(*args)
+    lit, rl, nl = oracle_raster.render(*args)
+    assert np.array_equal(lit, ref[0]) and np.array_equal(rl, ref[1]) and nl == ref[2] == nk
+    parity_report(ck, rk, (ref[0], ref[1], ref[3], ref[4]), tag=" (oracle kernel-order vs literal)")
+
+
+def test_oracle_flags_alpha_threshold():
+    """A Gaussian centred on a pixel (W = H = 33: ndc 0 -> pixel 16) whose opacity is one ulp above
+    1/255: alpha = o exactly there, so that pixel -- and only that one -- is flagged (bit 4)."""
+    hw = (33, 33)
+    o = float(np.nextafter(np.float32(1 / 255), np.float32(1)))
+    means, cov, sh, op, cams = single_gaussian_scene((0.0, 0.0, 4.0), 0.01, o, (0.4, 0.4, 0.4), (0, 0, 0), hw)
+    img, radii, _, pflag, gflag = oracle_raster.render_flagged(means, cov, sh, op, cams, hw, 1, 0)
+    assert radii[0, 0] > 0 and not gflag.any()
+    assert pflag[0, 16, 16] & oracle_raster.FLAG_ALPHA
+    assert (pflag > 0).sum() == 1
+    assert img[0, :, 16, 16].max() > 0  # alpha = o >= 1/255: blended
+
+
+def test_oracle_flags_transmittance_threshold():
+    """Two opaque Gaussians stacked on a pixel: alpha clamps to 0.99f twice and T (1 - 0.99f)^2
+    lands within a few ulps of the 1e-4 stop threshold -> flagged (bit 8)."""
+    hw = (33, 33)
+    means = torch.tensor([[[0.0, 0.0, 4.0], [0.0, 0.0, 5.0]]])
+    cov = (torch.eye(3) * 0.05).expand(1, 2, 3, 3).clone()
+    sh = torch.zeros((1, 2, 3, 1))
+    op = torch.ones((1, 2))
+    cams = _cams(torch.eye(4)[None], S.intrinsics(1), torch.ones(1), torch.full((1,), 100.0), torch.zeros(1, 3))
+    _, _, _, pflag, _ = oracle_raster.render_flagged(means, cov, sh, op, cams, hw, 1, 0)
+    assert pflag[0, 16, 16] & oracle_raster.FLAG_T
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("deg", [3, 4, 0])
 def test_raster_small_scene_parity(device, deg):
     hw = (64, 64)
     g = S.make_gaussians(1, image_shape=hw)
     cams = _target_cams(S.make_batch(1, image_shape=hw), hw)
-    _assert_parity(*_run_both(g, cams, hw, 3, deg, device)[:4])
+    _assert_parity(*_run_both(g, cams, hw, 3, deg, device))
 
 
 @pytest.mark.gpu
@@ -168,7 +238,7 @@ def test_raster_multi_scene_batch_nonzero_bg(device):
     hw = (48, 80)  # not a multiple of 16 in one axis, non-square
     g = S.make_gaussians(3, image_shape=hw)
     cams = _target_cams(S.make_batch(3, image_shape=hw), hw, bg=(0.3, 0.6, 0.9))
-    _assert_parity(*_run_both(g, cams, hw, 3, 3, device)[:4])
+    _assert_parity(*_run_both(g, cams, hw, 3, 3, device))
 
 
 @pytest.mark.gpu
@@ -176,8 +246,8 @@ def test_raster_full_size_scene_parity(device):
     hw = (256, 256)
     g = S.make_gaussians(1, image_shape=hw)
     cams = _target_cams(S.make_batch(1, image_shape=hw), hw)
-    color, radii, cref, rref, counts = _run_both(g, cams, hw, 3, 3, device)
-    _assert_parity(color, radii, cref, rref)
+    color, radii, ref, counts = _run_both(g, cams, hw, 3, 3, device)
+    parity_report(color, radii, ref, tag=" (256x256, G=131072, 3 views)")
     assert min(counts) > 100_000
 
 
@@ -186,9 +256,9 @@ def test_raster_near_plane_and_behind_camera(device):
     hw = (64, 64)
     g = S.make_gaussians(1, image_shape=hw, depth_range=(0.05, 3.0))  # many below z = 0.2
     cams = _target_cams(S.make_batch(1, image_shape=hw), hw)
-    color, radii, cref, rref, _ = _run_both(g, cams, hw, 3, 3, device)
-    _assert_parity(color, radii, cref, rref)
-    assert (rref == 0).sum() > 0
+    color, radii, ref, _ = _run_both(g, cams, hw, 3, 3, device)
+    _assert_parity(color, radii, ref)
+    assert (ref[1] == 0).sum() > 0
 
 
 @pytest.mark.gpu
@@ -205,17 +275,18 @@ def test_raster_long_tile_lists_global_sort_path(device):
     op = torch.rand((1, n), generator=gen) * 0.3
     g = {"means": means, "covariances": cov, "harmonics": sh, "opacities": op}
     cams = _cams(torch.eye(4)[None], S.intrinsics(1), torch.ones(1), torch.full((1,), 100.0), torch.zeros(1, 3))
-    color, radii, cref, rref, counts = _run_both(g, cams, (64, 64), 1, 3, device)
+    color, radii, ref, counts = _run_both(g, cams, (64, 64), 1, 3, device)
     assert max(counts) > 4096
-    _assert_parity(color, radii, cref, rref)
+    _assert_parity(color, radii, ref)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("depths", ["ties", "one_depth", "two_clusters"])
 @pytest.mark.parametrize("sort", ["count", "bitonic"])
 def test_raster_tile_sort_ties_and_clustered_depths(device, depths, sort, monkeypatch):
-    """Tile lists of 257..4096 keys: the counting sort on depth bits (buckets finished by an
-    insertion sort on (depth, id)) and its bitonic fallback for clustered depths must both give the
+    """Tile lists of 257..4096 keys: the counting sort on depth bits (each key's slot = its bucket
+    start + the number of bucket members with a smaller (depth, id) key; a bucket of more than
+    kFixMax = 32 keys sends the tile to the bitonic network) and that bitonic path must both give the
     reference's stable (depth, id) order. 'ties': 2,500 Gaussians on 64 distinct depths (every
     bucket a run of exact ties, resolved by id); 'one_depth': all at one depth (one bucket: the
     fallback); 'two_clusters': two depth values 1 ulp apart, plus a spread-out minority."""
@@ -239,8 +310,8 @@ def test_raster_tile_sort_ties_and_clustered_depths(device, depths, sort, monkey
     op = 0.05 + torch.rand((1, n), generator=gen) * 0.2
     g = {"means": means, "covariances": cov, "harmonics": sh, "opacities": op}
     cams = _cams(torch.eye(4)[None], S.intrinsics(1), torch.ones(1), torch.full((1,), 100.0), torch.zeros(1, 3))
-    color, radii, cref, rref, counts = _run_both(g, cams, (64, 64), 1, 3, device)
-    _assert_parity(color, radii, cref, rref)
+    color, radii, ref, counts = _run_both(g, cams, (64, 64), 1, 3, device)
+    _assert_parity(color, radii, ref)
 
 
 @pytest.mark.gpu
@@ -254,7 +325,7 @@ def test_raster_saturation_and_early_stop(device):
     op = torch.ones((1, n))
     g = {"means": means, "covariances": cov, "harmonics": sh, "opacities": op}
     cams = _cams(torch.eye(4)[None], S.intrinsics(1), torch.ones(1), torch.full((1,), 100.0), torch.full((1, 3), 0.5))
-    _assert_parity(*_run_both(g, cams, (32, 32), 1, 0, device)[:4])
+    _assert_parity(*_run_both(g, cams, (32, 32), 1, 0, device))
 
 
 @pytest.mark.gpu
@@ -311,8 +382,8 @@ def test_raster_dtu_stress_parity(device):
     g = S.make_gaussians(1, num_context=3, image_shape=hw)
     assert g["means"].shape[1] == 589_824
     cams = _target_cams(S.make_batch(1, num_context=3, num_target=1, image_shape=hw), hw)
-    color, radii, color_ref, radii_ref, counts = _run_both(g, cams, hw, 1, 3, device)
-    _assert_parity(color, radii, color_ref, radii_ref)
+    color, radii, ref, counts = _run_both(g, cams, hw, 1, 3, device)
+    parity_report(color, radii, ref, tag=" (DTU 512x384, G=589824)")
 
 
 @pytest.mark.gpu

@@ -47,6 +47,20 @@ def _rel(out, ref):
     return np.abs(out - ref).max() / max(np.abs(ref).max(), 1e-6)
 
 
+def _rel_sh(out, ref):
+    """Harmonics error per degree block: max over l of max|out_l - ref_l| / max|ref_l| on the
+    coefficient axis (last). The adapter pre-scales degree l by 0.1 * 0.25^l, so a check relative to
+    the global max would let the degree-3/4 coefficients be several percent wrong."""
+    out = np.asarray(out, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    d_sh = ref.shape[-1]
+    worst = 0.0
+    for l in range(int(round(d_sh ** 0.5))):
+        sl = slice(l * l, (l + 1) * (l + 1))
+        worst = max(worst, np.abs(out[..., sl] - ref[..., sl]).max() / max(np.abs(ref[..., sl]).max(), 1e-12))
+    return worst
+
+
 def _dec():
     g = np.load(GOLD / "decoder_calls.npz")
     return {k: torch.from_numpy(g[k]) for k in g.files}
@@ -83,13 +97,18 @@ def _sym(cov6):
                         torch.stack([xz, yz, zz], -1)], -2)
 
 
-def _render_recorded(d, sh_deg, prefix="color_", shs=None, bg=None):
-    """The oracle on the reference's own rasterizer inputs: one call per recorded view."""
+def _render_recorded(d, sh_deg, prefix="color_", shs=None, bg=None, flagged=False):
+    """The literal oracle on the reference's own rasterizer inputs: one call per recorded view
+    (flagged=True also returns the threshold flags, see oracle.raster.render_flagged)."""
     n = d[f"{prefix}viewmatrix"].shape[0]
     shs = d[f"{prefix}shs"] if shs is None else shs
     h, w = (int(x) for x in d["in_image_shape"])
-    return oracle_raster.render(d["color_means3D"], _sym(d["color_cov3D_precomp"]), shs.transpose(-1, -2),
-                                d["color_opacities"][..., 0], _recorded_cameras(d, prefix, bg), (h, w), 1, sh_deg)[:2]
+    args = (d["color_means3D"], _sym(d["color_cov3D_precomp"]), shs.transpose(-1, -2), d["color_opacities"][..., 0],
+            _recorded_cameras(d, prefix, bg), (h, w), 1, sh_deg)
+    if flagged:
+        c, r, _, pf, gf = oracle_raster.render_flagged(*args)
+        return c, r, pf, gf
+    return oracle_raster.render(*args)[:2]
 
 
 # --------------------------------------------------------------------------- decoder call sites
@@ -138,7 +157,8 @@ def test_decoder_cameras_host_vs_reference():
 def test_oracle_decode_matches_reference_inputs():
     """The oracle fed the raw Gaussians + the camera constants (it applies the scale and reads the
     upper triangle and the [3, M] SH layout itself) renders what the oracle renders on the
-    reference's own rasterizer inputs: pins the decode the HIP kernel shares with the oracle."""
+    reference's own rasterizer inputs: pins the decode the HIP kernel shares with the oracle.
+    (Host camera math = recorded matrices to ~1e-7, so no pixel crosses a threshold here.)"""
     from transplat_amd.model.decoder.hip_splatting import prepare_cameras
 
     d = _dec()
@@ -181,7 +201,9 @@ def test_raster_cameras_kernel_vs_reference(device):
 @pytest.mark.parametrize("deg", [3, 4])
 def test_hip_decoder_vs_reference_rasterizer_inputs(device, deg):
     """tsplat_raster_fwd on the raw Gaussians + tsplat_raster_cameras (the HIP decoder path)
-    against the oracle on the reference's recorded rasterizer inputs: L-inf <= 1e-4."""
+    against the literal oracle: L-inf <= 1e-4 on every pixel whose blend decisions are clear."""
+    from test_raster import parity_report
+
     from transplat_amd.model.decoder.hip_splatting import prepare_cameras, rasterize
 
     d = _dec()
@@ -190,27 +212,22 @@ def test_hip_decoder_vs_reference_rasterizer_inputs(device, deg):
     cams = prepare_cameras(*(t.to(device) for t in (ext, intr, near, far, bg)))
     g = [d[k].to(device) for k in ("in_means", "in_covariances", "in_harmonics", "in_opacities")]
     out, radii = rasterize(*g, cams, (h, w), v, sh_degree=deg)
-    out = out.cpu().numpy()
+    out, radii = out.cpu().numpy(), radii.cpu().numpy()
     # (1) the kernel on the camera constants it computed: the oracle fed the same constants
-    mine, mine_radii = oracle_raster.render(d["in_means"], d["in_covariances"], d["in_harmonics"], d["in_opacities"],
-                                            cams.to("cpu"), (h, w), v, deg)[:2]
-    assert np.abs(out - mine).max() <= 1e-4
-    assert np.array_equal(radii.cpu().numpy(), mine_radii)
-    # (2) end to end against the reference's recorded rasterizer inputs: the GPU camera kernel's
-    # matrices differ from the recorded ones by ~1e-7 relative (test_raster_cameras_kernel_vs_
-    # reference), and the blend's threshold tests (alpha >= 1/255, T < 1e-4) are discontinuous, so
-    # a handful of pixels may take the other side of a threshold; every other pixel is within 1e-4
-    ref, ref_radii = _render_recorded(d, deg)
-    err = np.abs(out - ref)
-    assert (err > 1e-4).mean() <= 1e-3 and err.max() <= 2e-2
-    assert np.array_equal(radii.cpu().numpy(), ref_radii)
+    c, r, _, pf, gf = oracle_raster.render_flagged(d["in_means"], d["in_covariances"], d["in_harmonics"],
+                                                   d["in_opacities"], cams.to("cpu"), (h, w), v, deg)
+    parity_report(out, radii, (c, r, pf, gf), tag=f" (decoder, own cameras, deg {deg})")
+    # (2) end to end against the reference's recorded rasterizer inputs (the GPU camera kernel's
+    # matrices differ from the recorded ones by ~1e-7 relative): same flagged tolerance
+    parity_report(out, radii, _render_recorded(d, deg, flagged=True), tag=f" (decoder, recorded inputs, deg {deg})")
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["depth", "disparity", "relative_disparity", "log"])
 def test_hip_render_depth_vs_reference_inputs(device, mode):
-    """DecoderSplattingHIP.render_depth (reference render_depth_cuda path) against the oracle on
-    the reference's recorded depth-mode rasterizer inputs (fake colours, degree 0, bg 0)."""
+    """DecoderSplattingHIP.render_depth (reference render_depth_cuda path) against the literal
+    oracle on the reference's recorded depth-mode rasterizer inputs (fake colours, degree 0, bg 0):
+    L-inf <= 1e-4 (relative to the depth scale) on every pixel whose blend decisions are clear."""
     from types import SimpleNamespace
 
     from transplat_amd.model.decoder.decoder_splatting_hip import DecoderSplattingHIP, DecoderSplattingHIPCfg
@@ -223,14 +240,15 @@ def test_hip_render_depth_vs_reference_inputs(device, mode):
     cam = [d[k].to(device) for k in ("in_extrinsics", "in_intrinsics", "in_near", "in_far")]
     depth = dec.render_depth(gs, *cam, (h, w), mode).cpu()
     n = d[f"{mode}_shs"].shape[0]
-    ref, _ = _render_recorded(d, 0, prefix="color_", shs=d[f"{mode}_shs"], bg=d[f"{mode}_bg"])
+    ref, _, pf, _ = _render_recorded(d, 0, prefix="color_", shs=d[f"{mode}_shs"], bg=d[f"{mode}_bg"], flagged=True)
     ref = torch.from_numpy(ref).mean(dim=1).reshape(depth.shape)
+    clear = torch.from_numpy(pf == 0).reshape(depth.shape)
     scale = max(float(ref.abs().max()), 1.0)
-    # GPU camera constants vs the recorded ones differ by ~1e-7 relative, so a handful of pixels
-    # may take the other side of a discontinuous blend threshold (see the colour test above, which
-    # also checks the kernel bit-exactly against the oracle on its own camera constants)
     err = (depth - ref).abs()
-    assert float((err > 1e-4 * scale).float().mean()) <= 1e-3 and float(err.max()) <= 2e-2 * scale
+    print(f"render_depth {mode}: L-inf {float(err[clear].max()):.3e} (scale {scale:.3g}), "
+          f"{int((~clear).sum())} of {clear.numel()} pixels flagged")
+    assert float(err[clear].max()) <= 1e-4 * scale
+    assert int((~clear).sum()) <= 0.01 * clear.numel()
     assert n == depth.shape[0] * depth.shape[1]
 
 
@@ -253,7 +271,7 @@ def _check_adapter(out, g, tol_harm):
     assert _rel(means, g["means"]) < 2e-6
     assert _rel(cov, g["covariances"]) < 2e-5
     assert _rel(opac, g["opacities"]) < 1e-6
-    assert _rel(harm, g["harmonics"]) < tol_harm
+    assert _rel_sh(harm, g["harmonics"]) < tol_harm
 
 
 def test_adapter_oracle_vs_reference():
@@ -286,7 +304,8 @@ def _check_encoder(gs, tol):
     g = np.load(GOLD / "encoder_256.npz")
     idx = torch.from_numpy(g["idx"])
     for k in ("means", "covariances", "harmonics", "opacities"):
-        err = _rel(getattr(gs, k)[0].cpu()[idx], g[k])
+        rel = _rel_sh if k == "harmonics" else _rel
+        err = rel(getattr(gs, k)[0].cpu()[idx], g[k])
         assert err < tol, f"{k}: {err:.3e}"
 
 

@@ -1,11 +1,13 @@
 """Build the gfx950 HIP C-ABI library in-tree (no JIT cache: the .so travels with the repo).
 
 `python -m transplat_amd.build` compiles every `csrc/*.hip` with hipcc for gfx950 into
-`transplat_amd/libtransplat_hip.so`. Objects are cached next to the sources under `build/` and
-rebuilt only when a source or header is newer.
+`transplat_amd/libtransplat_hip.so`. Objects are cached under `build/hip/` and rebuilt when a
+source or header is newer OR when the compile command (hipcc path, flags, per-file flags) differs
+from the one recorded next to the object (`<stem>.cmd`).
 """
 from __future__ import annotations
 
+import hashlib
 import os
 import shutil
 import subprocess
@@ -57,13 +59,17 @@ def build(verbose: bool = False, jobs: int = 8) -> Path:
     objs = []
     for src in srcs:
         obj = BUILD / (src.stem + ".o")
+        stamp = BUILD / (src.stem + ".cmd")
         objs.append(obj)
-        if obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, dep_t):
-            continue
         cmd = [hipcc, *HIPCC_FLAGS, *FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)]
+        key = hashlib.sha256("\0".join(cmd).encode()).hexdigest()
+        if (obj.exists() and obj.stat().st_mtime >= max(src.stat().st_mtime, dep_t)
+                and stamp.exists() and stamp.read_text() == key):
+            continue
+        stamp.unlink(missing_ok=True)
         if verbose:
             print(" ".join(cmd), flush=True)
-        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT), stamp, key))
         if len(procs) >= jobs:
             _wait(procs.pop(0))
     for pr in procs:
@@ -77,11 +83,12 @@ def build(verbose: bool = False, jobs: int = 8) -> Path:
 
 
 def _wait(item) -> None:
-    src, proc = item
+    src, proc, stamp, key = item
     out, _ = proc.communicate()
     if proc.returncode != 0:
         sys.stderr.write(out.decode(errors="replace"))
         raise RuntimeError(f"hipcc failed on {src.name}")
+    stamp.write_text(key)
 
 
 if __name__ == "__main__":

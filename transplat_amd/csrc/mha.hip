@@ -13,6 +13,8 @@
 // (each lane loads its own key row for S^T = K Q^T and one 128-B V segment per k-step for
 // O^T += V^T P^T, the next tile prefetched into registers), and the four (max, sum, O) partials are
 // merged once through LDS. 24 x 11 query blocks = 264 workgroups, ~1 wave per SIMD.
+#include <string.h>
+
 #include "common.h"
 #include "prof.h"
 
@@ -519,7 +521,7 @@ extern "C" int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, i
     // TSPLAT_MHA: "16" (default, 4 waves per 16-query block), "16x8" (8 waves), "32" (the
     // 32-query kernel); A/B knob
     const char* env = getenv("TSPLAT_MHA");
-    const int form = !env ? 0 : (env[0] == '3' ? 2 : (env[2] == 'x' ? 1 : 0));
+    const int form = !env ? 0 : (!strcmp(env, "32") ? 2 : (!strcmp(env, "16x8") ? 1 : 0));
     TSPLAT_PROF_BEGIN(tsplat::prof::kMha, stream);
     if (form == 2)
         hipLaunchKernelGGL(mha_f32_kernel, dim3((tokens + kQW - 1) / kQW, batch * heads), dim3(kThreads), 0, stream,

@@ -19,10 +19,13 @@
 //   * the blend is scalar fp32 (v_pk_fma_f32 has v_fma_f32's FLOP rate and packing costs moves;
 //     built with -fno-slp-vectorize), 4 entries per LDS read group.
 //
-// Floating point: contraction is OFF in this file so that the preprocess / alpha arithmetic is
-// reproducible bit for bit by the CPU restatement in oracle/raster_ref.c (same op order, same
-// exp polynomial). Threshold tests (alpha < 1/255, radius ceil, depth order) are discontinuous,
-// so bitwise agreement is what makes an L-inf 1e-4 image check meaningful.
+// Floating point: contraction is OFF in this file, so the view-space depth (the sort key) is the
+// reference's transformPoint4x3 expression bit for bit -- the front-to-back order, ties included,
+// is exactly the reference's. Everything else is this kernel's own arithmetic: the EWA covariance
+// as (J R) Sigma (J R)^T, the power in the log2 domain (log2 e folded into the stored conic) and
+// the hardware exp2 (v_exp_f32). Parity is held against oracle/raster_ref.c's LITERAL restatement
+// of the upstream expressions to L-inf 1e-4, excluding only the pixels whose blend decisions the
+// oracle flags as within a rounding margin of their thresholds (tests/test_raster.py).
 #pragma clang fp contract(off)
 
 #include <stdlib.h>
@@ -55,33 +58,12 @@ __constant__ float kSH_C4[9] = {2.5033429417967046f, -1.7701307697799304f, 0.946
                                 -0.6690465435572892f, 0.10578554691520431f, -0.6690465435572892f,
                                 0.47308734787878004f, -1.7701307697799304f, 0.6258357354491761f};
 
-// exp(x) for x <= 0: Cephes range reduction + degree-5 polynomial written with explicit fmaf, the
-// same op sequence as exp_neg() in oracle/raster_ref.c, so both sides produce the same float for
-// x >= -87. Below -87 the oracle returns 0 and this clamps (one v_max instead of a compare and two
-// selects): a tiny positive number, and alpha = o * e < 1/255 either way, so every blend decision
-// -- and therefore the image -- is unchanged. The 2^k scaling is v_ldexp_f32 (exact: = p * 2^k for
-// the k >= -126 the clamp allows).
-__device__ __forceinline__ float exp_neg_clamped(float x_in) {
-    const float x = fmaxf(x_in, -87.0f);
-    const float kf = rintf(x * 1.44269504088896341f);
-    float r = fmaf(kf, -0.693359375f, x);
-    r = fmaf(kf, 2.12194440e-4f, r);
-    const float z = r * r;
-    float p = 1.9875691500e-4f;
-    p = fmaf(p, r, 1.3981999507e-3f);
-    p = fmaf(p, r, 8.3334519073e-3f);
-    p = fmaf(p, r, 4.1665795894e-2f);
-    p = fmaf(p, r, 1.6666665459e-1f);
-    p = fmaf(p, r, 5.0000001201e-1f);
-    p = fmaf(p, z, r) + 1.0f;
-    return __builtin_amdgcn_ldexpf(p, (int)kf);
-}
-
 struct Workspace {
     // [V*G] 64-byte records, one per (view, Gaussian), so the render kernel's gather of an entry
     // touches one cache line (three SoA arrays cost three lines per entry):
     //   rec[4i + 0] pixel-space mean + half-extents of the alpha >= 1/255 ellipse
-    //   rec[4i + 1] conic (a, b, c) as (-a/2, -b, -c/2) (the blend's power form) + opacity
+    //   rec[4i + 1] conic (a, b, c) as log2(e) (-a/2, -b, -c/2) (the blend's log2-domain power
+    //               form) + opacity
     //   rec[4i + 2] rgb + view-space depth
     //   rec[4i + 3] block-cull constants: threshold q, -b/a, -b/c (ellipse_meets_block)
     float4* rec;
@@ -282,9 +264,12 @@ preprocess_kernel(Params p, const float* __restrict__ means, const float* __rest
             }
             float4* rec = ws.rec + 4 * vg;
             rec[0] = make_float4(px, py, ex, ey);
-            rec[1] = make_float4(-0.5f * conic_a, -conic_b, -0.5f * conic_c, o);  // exact scalings
+            // power * log2(e): alpha = o * 2^(power2) is one v_exp_f32 in the blend
+            constexpr float kLog2e = 1.44269504088896341f;
+            rec[1] = make_float4(-0.5f * kLog2e * conic_a, -kLog2e * conic_b, -0.5f * kLog2e * conic_c, o);
             rec[2] = make_float4(rgb[0], rgb[1], rgb[2], vz);
-            rec[3] = make_float4(2.0f * __logf(255.0f * o) * 1.001f + 1e-3f,
+            // cull threshold in the same log2 units as the stored conic: 2 log2(255 o), + margins
+            rec[3] = make_float4(2.0f * __log2f(255.0f * o) * 1.001f + 1.5e-3f,
                                  -conic_b * __builtin_amdgcn_rcpf(conic_a), -conic_b * __builtin_amdgcn_rcpf(conic_c),
                                  0.0f);
             for (int ty = y0; ty < y1; ++ty)
@@ -642,7 +627,8 @@ __device__ __forceinline__ bool counting_sort(const uint64_t* __restrict__ keys,
 // axis-aligned box test keeps for rotated / elongated splats.
 __device__ __forceinline__ bool ellipse_meets_block(float mx, float my, float4 co, float4 cull, float x0, float x1,
                                                     float y0, float y1) {
-    // co = (-a/2, -b, -c/2, o) as stored; cull = (2 ln(255 o) * 1.001 + 1e-3, -b/a, -b/c),
+    // co = log2(e) (-a/2, -b, -c/2) and o as stored; cull = (2 log2(255 o) * 1.001 + 1.5e-3, -b/a,
+    // -b/c): Q and q both carry the log2(e) factor,
     // precomputed per (view, Gaussian) by the preprocess kernel (approximate reciprocals: a clamped
     // minimiser off by an ulp raises Q by O(ulp^2), far inside the margins above)
     const float a = -2.0f * co.x, b = -co.y, c = -2.0f * co.z;
@@ -724,17 +710,18 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     float (*w_rec)[kWave] = s_rec[wid];
 
     // power = -0.5 (a dx^2 + c dy^2) - b dx dy, alpha = min(0.99, o e^power), T' = T (1 - alpha),
-    // C += rgb alpha T, written with explicit fmaf (same sequence in oracle/raster_ref.c). Scalar
-    // fp32 on purpose: v_pk_fma_f32 has the same FLOP rate as v_fma_f32 (twice the cycles), and
-    // packing the operands costs register moves.
+    // C += rgb alpha T (reference renderCUDA), here with the power scaled by log2(e) so that
+    // e^power = 2^power2 is one v_exp_f32, and the quadratic in Horner form (2 FMAs + 3 multiplies).
+    // Scalar fp32 on purpose: v_pk_fma_f32 has the same FLOP rate as v_fma_f32 (twice the cycles),
+    // and packing the operands costs register moves.
     auto blend = [&](float x, float y, float ca, float cb, float cc, float o, float r, float g, float bl) {
-        // (ca, cb, cc) = (-a/2, -b, -c/2): power = dy (-c/2 dy - b dx) + (-a/2 dx) dx
+        // (ca, cb, cc) = log2(e) (-a/2, -b, -c/2): power2 = dy (cc dy + cb dx) + (ca dx) dx
         const float dx = x - pfx, dy = y - pfy;
-        const float power = fmaf(dy, fmaf(cc, dy, cb * dx), (ca * dx) * dx);
-        const float alpha = fminf(0.99f, o * exp_neg_clamped(power));
+        const float power2 = fmaf(dy, fmaf(cc, dy, cb * dx), (ca * dx) * dx);
+        const float alpha = fminf(0.99f, o * __builtin_amdgcn_exp2f(power2));
         const float test_T = fmaf(-alpha, T, T);
         // reference order: skip power > 0, skip alpha < 1/255, stop if test_T < 1e-4
-        const bool contrib = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const bool contrib = !done && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
         const bool stop = contrib && (test_T < 0.0001f);
         const bool acc = contrib && !stop;
         const float w = acc ? alpha * T : 0.0f;  // a skipped entry adds c * 0 = +0: C unchanged

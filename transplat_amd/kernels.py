@@ -527,6 +527,9 @@ def wino_pack_weight(weight):
     return packed
 
 
+WINO_MAX_CI_PAD = 1024  # winoconv.hip kMaxCiPad: input channels (padded to 16) of one launch
+
+
 def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=(), vs_miopen=False) -> bool:
     """True when tsplat_conv3x3_wino_f32_fwd takes conv2d(x, weight) on the NCHW map x and (mode
     "auto") it is one of the 3x3s where it beats MIOpen's kernels (tools/bench_wino.py): above the
@@ -547,6 +550,8 @@ def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=
         return False
     ci = sum(t.shape[1] for t in (x, *extra))
     if as_int(dilation) != 1 or groups != 1 or weight.shape[1] != ci:
+        return False
+    if (ci + 15) // 16 * 16 > WINO_MAX_CI_PAD:  # the launch's LDS plane table (winoconv.hip kMaxCiPad)
         return False
     if _WINO_MODE == "all":
         return True
