@@ -349,8 +349,13 @@ def main():
 
     # dominant-kernel timing (HIP events on the launch stream), separate from the timed region;
     # event records cannot live inside a replayed hipGraph, so this pass launches eagerly (the
-    # kernel and its inputs are the same)
+    # kernel and its inputs are the same). The encoder's concurrent Depth-Anything branch is
+    # serialised for it, so a kernel's duration is its own, not shared with the other branch.
     prof_step = info.get("eager_step", step)
+    from transplat_amd import streams
+
+    serial = streams.serial()
+    serial.__enter__()
     prof_step()
     torch.cuda.synchronize()
     _lib.prof_enable(info["dominant"])
@@ -395,6 +400,7 @@ def main():
                 "ms_per_step": cms / n_prof, "share_of_step": cms / n_prof / (elapsed / args.steps * 1e3),
             }
 
+    serial.__exit__(None, None, None)
     views = world * info["views_per_step"] * args.steps
     result = {
         "metric": "novel views/sec at 256x256, 2 ctx views; PSNR parity vs reference",

@@ -18,7 +18,7 @@ import torch.nn.functional as F
 from einops import rearrange
 from torch import nn
 
-from ... import kernels
+from ... import kernels, streams
 from ..depth_anything.dpt import DepthAnythingV2
 from ..types import Gaussians
 from .backbone.backbone_multiview import BackboneMultiview
@@ -130,29 +130,39 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
             camk[:, :, :3, :3] = intr_curr
             img2world = torch.matmul(context["extrinsics"].clone().detach(), kernels.small_inverse(camk))
 
-        with bench("encoder_2_backbone"), self._dense():
-            trans_features, cnn_features = self.backbone(context["image"], attn_splits=self.cfg.multiview_trans_attn_split,
-                                                         return_cnn_features=True, img2world=img2world)
-        trans_features = trans_features.float()
-        cnn_features = cnn_features.float()
+        def depth_anything():
+            with bench("encoder_3_depth_anything"), torch.no_grad(), self._dense():
+                # channel order (2, 0, 1) as the reference, by slicing: a list index would be a
+                # pageable host-to-device copy, which is not allowed inside hipGraph capture
+                da_images = self.normalize_images(context["image"])
+                da_images = torch.cat((da_images[:, :, 2:3], da_images[:, :, 0:2]), dim=2)
+                da_images = da_images.reshape(b * v, 3, h, w)
+                da_images = kernels.interpolate_bilinear_ac(da_images, (252, 252))
+                da_depth, out_feature = self.da_model(da_images)
+                da_depth = kernels.interpolate_bilinear_ac(da_depth[None].float().contiguous(), (h, w))
+                da_depth = da_depth.view(b, v, 1, h, w).flatten(2)
+                # per-view min / max in two aminmax stages (rows of w, then the h row results): the
+                # single-row reductions ran on 2 workgroups each (~20 us apiece); exact either way
+                lo, hi = torch.aminmax(da_depth.view(b, v, h, w), dim=-1)
+                da_min = lo.amin(dim=-1, keepdim=True)
+                da_max = hi.amax(dim=-1, keepdim=True)
+                da_depth = ((da_depth - da_min) / (da_max - da_min)).reshape(b, v, 1, h, w)
+                return da_depth, out_feature.float()
 
-        with bench("encoder_3_depth_anything"), torch.no_grad(), self._dense():
-            # channel order (2, 0, 1) as the reference, by slicing: a list index would be a pageable
-            # host-to-device copy, which is not allowed inside hipGraph capture
-            da_images = self.normalize_images(context["image"])
-            da_images = torch.cat((da_images[:, :, 2:3], da_images[:, :, 0:2]), dim=2)
-            da_images = da_images.reshape(b * v, 3, h, w)
-            da_images = kernels.interpolate_bilinear_ac(da_images, (252, 252))
-            da_depth, out_feature = self.da_model(da_images)
-            da_depth = kernels.interpolate_bilinear_ac(da_depth[None].float().contiguous(), (h, w))
-            da_depth = da_depth.view(b, v, 1, h, w).flatten(2)
-            # per-view min / max in two aminmax stages (rows of w, then the h row results): the
-            # single-row reductions ran on 2 workgroups each (~20 us apiece); exact either way
-            lo, hi = torch.aminmax(da_depth.view(b, v, h, w), dim=-1)
-            da_min = lo.amin(dim=-1, keepdim=True)
-            da_max = hi.amax(dim=-1, keepdim=True)
-            da_depth = ((da_depth - da_min) / (da_max - da_min)).reshape(b, v, 1, h, w)
-        dino_feature = out_feature.float().view(b, v, *out_feature.shape[1:])
+        def backbone():
+            with bench("encoder_2_backbone"), self._dense():
+                tf, cf = self.backbone(context["image"], attn_splits=self.cfg.multiview_trans_attn_split,
+                                       return_cnn_features=True, img2world=img2world)
+            return tf.float(), cf.float()
+
+        # Stages 2 and 3 read only the context images: on a GPU, Depth-Anything runs on a side
+        # stream concurrently with the backbone (transplat_amd/streams.py; captured into the step's
+        # hipGraph as two branches). Both are chains of small launches (DINOv2's M = 650 GEMMs, the
+        # MVT's 256-workgroup kernels) that leave CUs idle on their own.
+        da = streams.fork(device, depth_anything)
+        trans_features, cnn_features = backbone()
+        da_depth, out_feature = streams.join(da)
+        dino_feature = out_feature.view(b, v, *out_feature.shape[1:])
 
         extra_info = {"images": rearrange(context["image"], "b v c h w -> (v b) c h w"), "scene_names": scene_names}
         gpp = self.cfg.gaussians_per_pixel

@@ -12,7 +12,7 @@ import torch.nn.functional as F
 from einops import rearrange, repeat
 from torch import nn
 
-from .... import kernels
+from .... import kernels, streams
 from ...utils.cam_param_encoder import cam_param_encoder
 from ...utils.uv_transformer import UVTransformer
 from .ldm_unet import UNetModel, run_sequential
@@ -184,6 +184,14 @@ class DepthPredictorTrans(nn.Module):
         feat_comb_lists, intr_curr, pose_curr_lists, disp_candi_curr = prepare_feat_proj_data_lists(
             features, intrinsics, extrinsics, near, far, num_samples=self.num_depth_candidates)
         feat01 = feat_comb_lists[0]
+
+        def projection(feat01, cnn_features):  # (reference :448-452) reads backbone features only
+            proj_feat_in_fullres = _conv_upsample_gelu(self.upsampler, torch.cat((feat01, cnn_features), dim=1))
+            return proj_feat_in_fullres, self.proj_feature(proj_feat_in_fullres)
+
+        # the full-resolution feature projection runs on a side stream beside the cost volume
+        # (matching, refine U-Net, depth head: a chain of 64^2 launches), transplat_amd/streams.py
+        proj = streams.fork(features.device, projection, feat01, cnn_features)
         if v == 2:
             raw_correlation_in = self.match_two(intr_curr, pose_curr_lists[0], extrinsics, disp_candi_curr,
                                                 dino_feature, features)
@@ -208,8 +216,7 @@ class DepthPredictorTrans(nn.Module):
         fullres_disps = kernels.interpolate_bilinear_ac(coarse_disps, (coarse_disps.shape[-2] * up,
                                                                        coarse_disps.shape[-1] * up))
 
-        proj_feat_in_fullres = _conv_upsample_gelu(self.upsampler, torch.cat((feat01, cnn_features), dim=1))
-        proj_feature = self.proj_feature(proj_feat_in_fullres)
+        proj_feat_in_fullres, proj_feature = streams.join(proj)
         refine_out = run_sequential(self.refine_unet, torch.cat((extra_info["images"], da_depth, proj_feature, fullres_disps,
                                                  pdf_max), dim=1))
 
