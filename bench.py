@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--batch", type=int, default=1, help="scenes per step per GPU")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-1thread", action="store_true",
+                    help="also time the e2e CPU port on ONE thread (one full scene: several minutes)")
     ap.add_argument("--no-conv-search", action="store_true",
                     help="MIOpen's default convolution algorithm choice instead of its measured search "
                          "(torch.backends.cudnn.benchmark, on by default: +2.4%% e2e at b = 1)")
@@ -204,7 +206,7 @@ def cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline_e2e(model, seconds: float):
+def cpu_baseline_e2e(model, seconds: float, one_thread: bool = False):
     """The same test_step on the host: the build's modules with the oracle's CPU restatements in
     place of the HIP kernels and the C oracle rasterizer (kind 'port'), on >= 1 scene. Torch and the
     rasterizer's OpenMP both use torch.get_num_threads() threads (the process's CPU share: 16 on
@@ -221,12 +223,11 @@ def cpu_baseline_e2e(model, seconds: float):
     for n in saved:
         setattr(kernels, n, getattr(E, n))
     threads = torch.get_num_threads()
-    oracle_raster.set_threads(threads)
-    t_raster = 0.0
-    try:
-        enc = copy.deepcopy(model.encoder).float().cpu()
-        enc.cfg.dense_dtype = "fp32"
-        n_views, t0 = 0, time.perf_counter()
+
+    def run(budget, nthreads):
+        torch.set_num_threads(nthreads)
+        oracle_raster.set_threads(nthreads)
+        t_raster, n_views, t0 = 0.0, 0, time.perf_counter()
         while True:
             batch = S.make_batch(1, image_shape=(256, 256))
             with torch.no_grad():
@@ -238,18 +239,31 @@ def cpu_baseline_e2e(model, seconds: float):
             t_raster += time.perf_counter() - tr
             n_views += 3
             el = time.perf_counter() - t0
-            if el >= seconds:
-                break
+            if el >= budget:
+                return n_views, el, t_raster
+
+    try:
+        enc = copy.deepcopy(model.encoder).float().cpu()
+        enc.cfg.dense_dtype = "fp32"
+        n_views, el, t_raster = run(seconds, threads)
+        one = run(0.0, 1) if one_thread else None  # one full scene on one thread
     finally:
+        torch.set_num_threads(threads)
+        oracle_raster.set_threads(threads)
         for n, f in saved.items():
             setattr(kernels, n, f)
-    return {
+    res = {
         "value": n_views / el, "unit": "views/s", "cores": threads, "kind": "port",
         "sample": f"{n_views // 3} scene(s) x 3 views, 256x256: the build's encoder modules on CPU (torch, "
                   f"{threads} threads) with oracle/encoder_ops.py restatements for the HIP kernels + "
-                  f"oracle/raster_ref.c (OpenMP, {threads} threads; raster {t_raster / n_views * 1e3:.0f} ms/view), "
-                  f"{el:.1f} s, host {cpu_model()}, nproc={os.cpu_count()}",
+                  f"oracle/raster_ref.c (literal mode; OpenMP, {threads} threads; raster "
+                  f"{t_raster / n_views * 1e3:.0f} ms/view), {el:.1f} s, host {cpu_model()}, nproc={os.cpu_count()}",
     }
+    if one is not None:
+        res["value_1thread"] = one[0] / one[1]
+        res["sample"] += (f"; 1 thread: one scene in {one[1]:.1f} s = {one[0] / one[1]:.4f} views/s "
+                          f"(raster {one[2] / one[0] * 1e3:.0f} ms/view)")
+    return res
 
 
 def cpu_baseline_raster(cpu_inputs, seconds: float):
@@ -440,7 +454,8 @@ def main():
         result["roofline_step_dominant"] = conv_roofline
     if rank == 0 and not args.no_cpu_baseline and cpu_inputs is not None:
         if isinstance(cpu_inputs, tuple) and cpu_inputs[0] == "e2e":
-            result["cpu_baseline"] = cpu_baseline_e2e(cpu_inputs[1], args.cpu_baseline_seconds)
+            result["cpu_baseline"] = cpu_baseline_e2e(cpu_inputs[1], args.cpu_baseline_seconds,
+                                                      args.cpu_baseline_1thread)
         else:
             result["cpu_baseline"] = cpu_baseline_raster(cpu_inputs, args.cpu_baseline_seconds)
     if rank == 0:

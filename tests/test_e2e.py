@@ -17,13 +17,22 @@ def test_encoder_cpu_with_oracle_ops(monkeypatch):
 
     for n in E.KERNEL_RESTATEMENTS:
         monkeypatch.setattr(kernels, n, getattr(E, n))
+    from transplat_amd.misc.benchmarker import Benchmarker
+
     enc = S.init_synthetic_weights(EncoderTrans(EncoderTransCfg()).eval())
     batch = S.make_batch(1, image_shape=(128, 128))
+    bm = Benchmarker()
     with torch.no_grad():
-        g = enc(batch["context"], 0, deterministic=True)
+        g = enc(batch["context"], 0, deterministic=True, benchmarker=bm)
     assert g.means.shape == (1, 2 * 128 * 128, 3) and g.harmonics.shape == (1, 2 * 128 * 128, 3, 25)
     for t in (g.means, g.covariances, g.harmonics, g.opacities):
         assert torch.isfinite(t).all()
+    # the reference's stage tags (encoder_trans.py:188-294, depth_predictor_trans.py:320-456)
+    tags = set(bm.summary())
+    assert {"encoder_1_prep_intrinsics", "encoder_2_backbone", "encoder_3_depth_anything",
+            "encoder_4_depth_predictor", "encoder_5_gaussian_adapter", "encoder_4a_prep_features",
+            "encoder_4b_cost_volume_matching", "encoder_4c_cost_volume_unet", "encoder_4d_coarse_depth",
+            "encoder_4e_depth_refine_unet", "encoder_4f_gaussian_head"} <= tags
 
 
 @pytest.mark.gpu

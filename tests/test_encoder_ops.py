@@ -64,16 +64,20 @@ def test_camera_prep_matches_reference_golden():
 
 # ------------------------------------------------------------------ HIP kernels vs oracle
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["auto", "quad"])
+@pytest.mark.parametrize("variant", ["auto", "x32", "quad"])
 @pytest.mark.parametrize("hw,m,shift,b", [(16, 1, False, 2), (16, 1, True, 2), (16, 2, True, 2), (64, 1, False, 2),
-                                          (64, 1, True, 2), (64, 2, True, 2), (32, 2, False, 2), (64, 1, True, 8)])
+                                          (64, 1, True, 2), (64, 2, True, 2), (32, 2, False, 2), (64, 1, True, 8),
+                                          (64, 1, True, 1), (64, 1, False, 1)])
 def test_window_attention_kernel(device, monkeypatch, hw, m, shift, b, variant):
-    """auto: the 128-query 32x32x2 kernel with its global key split + combine (b = 2 at 64x64), without
-    split at b = 8, the 64-query 16x16x4 kernel for 8x8 windows; "quad": the opt-in split-free kernel
-    (4 waves x key quarters on 32 queries) where its shapes allow, else the same defaults."""
+    """auto: 128-query blocks as 8 waves x 16 queries (16x16x4, round 3) with the global key split +
+    combine (b = 1 / 2 at 64x64), without split at b = 8, the 64-query 16x16x4 kernel for 8x8
+    windows; "x32": the same blocks as 4 waves x 32 queries (32x32x2, TSPLAT_WA16=0); "quad": the
+    opt-in split-free kernel (4 waves x key quarters on 32 queries) where its shapes allow."""
     from transplat_amd import kernels as K
 
-    if variant != "auto":
+    if variant == "x32":
+        monkeypatch.setenv("TSPLAT_WA16", "0")
+    elif variant != "auto":
         monkeypatch.setenv("TSPLAT_WINATTN", variant)
     q = seeded((b, hw * hw, 128), 11)
     k = seeded((b, m, hw * hw, 128), 12) if m > 1 else seeded((b, hw * hw, 128), 12)

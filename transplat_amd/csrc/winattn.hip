@@ -655,6 +655,222 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
 
 
 // ============================================================================================
+// 16-query waves (v_mfma_f32_16x16x4_f32) over the same 128-query block: 8 waves per workgroup,
+// so the launch that gives the 32-query kernel ONE wave per SIMD (b = 1: 64 query blocks x 4 key
+// splits = 256 workgroups on 256 CUs) runs TWO per SIMD here, with the same key split and the
+// same partial slabs: one wave's softmax, LDS waits and barrier run under the other's MFMAs.
+// 16x16x4 f32 does 2,048 FLOP in 32 cycles, the 32x32x2 rate.
+//   S^T = K Q^T per 16-key subtile: A = K[key 16 sub + (l & 15)][d], B = Q[q = l & 15][d], the k
+//     index of lane group g = l >> 4 at step s mapped to d = 32 g + s (a lane's 32 dims are
+//     contiguous: Q in 32 registers, K as one ds_read_b128 per 4 steps); lane l then holds
+//     S^T[key 16 sub + 4 g + i][q = l & 15] in s[sub][i].
+//   O^T += V^T P^T: step (sub, i) contracts keys 16 sub + 4 g + i, so B = s[sub][i] itself and
+//     A = V^T[d = 16 dt + (l & 15)][that key]: one ds_read_b128 of the transposed V tile gives
+//     the 4 steps i of a (sub, dt).
+//   K and V^T double-buffered in LDS (2 x (33.8 + 34.8) KB): tile t + 1 is loaded into registers
+//     at the start of tile t and stored into the other buffer after QK(t); one barrier per tile.
+//     Staging thread: key row = lane, 16-dim segment = wave.
+//   Row sums stay lane-partial (the running max is uniform over a query's 4 lanes) and are
+//   reduced once at the end. Partials go out in the 32-query kernel's lane-contiguous layout
+//   (lane_tile_base), so the merge projection and the combine read them unchanged.
+// ============================================================================================
+constexpr int kWaves16 = 8;
+constexpr int kThreads16 = 64 * kWaves16;
+constexpr int kKRow16 = kC + 4;    // padded K row (floats)
+constexpr int kVtRow16 = kBK + 4;  // padded transposed-V row (floats)
+
+// lanes l and l ^ 16 (v_permlane16_swap exchanges 16-lane rows 0 <-> 1 and 2 <-> 3, VALU only)
+__device__ __forceinline__ float rows_max(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float rows_sum(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+__global__ void __launch_bounds__(kThreads16, 1)
+win_attn_f32x16_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
+                       const float* __restrict__ v, float* __restrict__ out, Partials part) {
+    __shared__ __attribute__((aligned(16))) float sK[2][kBK * kKRow16];
+    __shared__ __attribute__((aligned(16))) float sVt[2][kC * kVtRow16];
+    __shared__ __attribute__((aligned(16))) int sReg[2][kBK];
+
+    int qblk, wi, bz;
+    xcd_block_coords(qblk, wi, bz);
+    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int n16 = lane & 15, g = lane >> 4;
+    const size_t HW = (size_t)p.H * p.W;
+    const float* qb = q + (size_t)b * HW * kC;
+    const int bkv = p.kv_shift ? (b + p.kv_shift) % p.nbatch : b;
+    const float* kb = k + (size_t)bkv * p.m * HW * kC;
+    const float* vb = v + (size_t)bkv * p.m * HW * kC;
+    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
+
+    floatx4 sk[4], sv[4];
+    int s_region = 0;
+    auto load_tile = [&](int k0) {
+        size_t off;
+        key_row(p, wi, HW, k0 + lane, off, s_region);
+        const floatx4* ksrc = reinterpret_cast<const floatx4*>(kb + off * kC + 16 * wid);
+        const floatx4* vsrc = reinterpret_cast<const floatx4*>(vb + off * kC + 16 * wid);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            sk[i] = ksrc[i];
+            sv[i] = vsrc[i];
+        }
+    };
+    auto store_tile = [&](int buf) {
+        float* dk = &sK[buf][lane * kKRow16 + 16 * wid];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) *reinterpret_cast<floatx4*>(dk + 4 * i) = sk[i];
+        float* dv = &sVt[buf][(16 * wid) * kVtRow16 + lane];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dv[(4 * i + j) * kVtRow16] = sv[i][j];
+        if (wid == 0 && p.shift) sReg[buf][lane] = s_region;
+    };
+
+    const int tq = qblk * kBQ3 + wid * 16 + n16;
+    const int qpix = win_pixel(p, wi, tq);
+    const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+    const float qscale = p.scale * kLog2e;  // log2-domain scores, bare v_exp_f32
+    float qr[32];
+    load_tile(kbeg);
+    {
+        const float4* src = reinterpret_cast<const float4*>(qb + (size_t)qpix * kC + 32 * g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 t4 = src[i];
+            qr[4 * i] = t4.x * qscale;
+            qr[4 * i + 1] = t4.y * qscale;
+            qr[4 * i + 2] = t4.z * qscale;
+            qr[4 * i + 3] = t4.w * qscale;
+        }
+    }
+    floatx4 o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (floatx4)(0.f);
+    float m_run = -INFINITY, l_run = 0.f;
+
+    store_tile(0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += kBK, buf ^= 1) {
+        const bool has_next = k0 + kBK < kend;
+        // unconditional (the last tile reloads itself, unused): a conditional load of the staging
+        // registers made the compiler keep them in scratch
+        load_tile(has_next ? k0 + kBK : k0);
+
+        // ---- S^T = K Q^T: four 16-key subtiles, their chains interleaved
+        floatx4 s[4];
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub) s[sub] = (floatx4)(0.f);
+        const float* kt = &sK[buf][n16 * kKRow16 + 32 * g];
+#pragma unroll
+        for (int s4 = 0; s4 < 8; ++s4) {
+            float4 kk[4];
+#pragma unroll
+            for (int sub = 0; sub < 4; ++sub)
+                kk[sub] = *reinterpret_cast<const float4*>(kt + 16 * sub * kKRow16 + 4 * s4);
+#pragma unroll
+            for (int sub = 0; sub < 4; ++sub) s[sub] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[sub].x, qr[4 * s4 + 0], s[sub], 0, 0, 0);
+#pragma unroll
+            for (int sub = 0; sub < 4; ++sub) s[sub] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[sub].y, qr[4 * s4 + 1], s[sub], 0, 0, 0);
+#pragma unroll
+            for (int sub = 0; sub < 4; ++sub) s[sub] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[sub].z, qr[4 * s4 + 2], s[sub], 0, 0, 0);
+#pragma unroll
+            for (int sub = 0; sub < 4; ++sub) s[sub] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[sub].w, qr[4 * s4 + 3], s[sub], 0, 0, 0);
+        }
+        // ---- shifted-window mask (region ids of the lane's keys 16 sub + 4 g + i)
+        if (p.shift) {
+#pragma unroll
+            for (int sub = 0; sub < 4; ++sub) {
+                const int4 rg = *reinterpret_cast<const int4*>(&sReg[buf][16 * sub + 4 * g]);
+                s[sub][0] += rg.x == qreg ? 0.0f : kMaskLog2;
+                s[sub][1] += rg.y == qreg ? 0.0f : kMaskLog2;
+                s[sub][2] += rg.z == qreg ? 0.0f : kMaskLog2;
+                s[sub][3] += rg.w == qreg ? 0.0f : kMaskLog2;
+            }
+        }
+        // ---- online softmax (a query's 64 keys live in its 4 lanes l & 15 + 16 g)
+        float bmax = -INFINITY;
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bmax = fmaxf(bmax, s[sub][i]);
+        bmax = halves_max(rows_max(bmax));
+        const float m_new = fmaxf(m_run, bmax);
+        if (__any(m_new > m_run)) {  // exact: corr == 1 for every lane otherwise
+            const float corr = fast_exp2(m_run - m_new);
+            l_run *= corr;
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) o[dt] *= corr;
+            m_run = m_new;
+        }
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float e = fast_exp2(s[sub][i] - m_run);
+                s[sub][i] = e;
+                l_run += e;
+            }
+        // the other buffer's last readers (tile t - 1) passed the previous barrier
+        if (has_next) store_tile(buf ^ 1);
+
+        // ---- O^T += V^T P^T: 8 d tiles' chains interleaved over the 16 key steps
+        const float* vt = &sVt[buf][n16 * kVtRow16 + 4 * g];
+#pragma unroll
+        for (int sub = 0; sub < 4; ++sub) {
+            float4 vv[8];
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) vv[dt] = *reinterpret_cast<const float4*>(vt + 16 * dt * kVtRow16 + 16 * sub);
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt].x, s[sub][0], o[dt], 0, 0, 0);
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt].y, s[sub][1], o[dt], 0, 0, 0);
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt].z, s[sub][2], o[dt], 0, 0, 0);
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt].w, s[sub][3], o[dt], 0, 0, 0);
+        }
+        __syncthreads();  // tile t's buffers are free; tile t + 1's are visible
+    }
+    l_run = halves_sum(rows_sum(l_run));
+
+    // O^T[d = 16 dt + 4 g + i][q] in o[dt][i]
+    if (p.ksplit == 1) {
+        const float inv = 1.0f / l_run;
+        float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * g;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+            *reinterpret_cast<float4*>(dst + 16 * dt) =
+                make_float4(o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
+    } else {
+        // the 32-query kernel's lane-contiguous partial layout: query t of the block sits in wave
+        // slot t >> 5, lane c = t & 31 (+ 32 for dims with bit 2 set); d = D .. D + 3 at float4
+        // ((D >> 5) * 4 + ((D >> 3) & 3)) * 64 + c + 32 ((D >> 2) & 1)
+        const int t = wid * 16 + n16;
+        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, t >> 5)) + (t & 31);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            const int D = 16 * dt + 4 * g;
+            dst[((D >> 5) * 4 + ((D >> 3) & 3)) * 64 + 32 * ((D >> 2) & 1)] =
+                make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
+        }
+        if (g == 0) {
+            const size_t row = pidx(p, b, wi, ks, tq);
+            part.m[row] = m_run * kLn2;  // natural-log domain for the combine
+            part.l[row] = l_run;
+        }
+    }
+}
+
+// ============================================================================================
 // Key-pair variant of the 32x32x2 kernel (for launches that need a key split): a workgroup of
 // 4 waves owns 64 queries; waves (2g, 2g + 1) share query group g and take the low / high 32 keys
 // of every 64-key tile, so each workgroup covers twice the keys of the 128-query kernel at the
@@ -1842,6 +2058,10 @@ static bool env_is(const char* name, const char* val) {
     return e && !strcmp(e, val);
 }
 
+// 128-query blocks run as 8 x 16-query waves (win_attn_f32x16_kernel) unless TSPLAT_WA16=0 (A/B:
+// the 4 x 32-query kernel)
+static bool use_x16() { return !env_is("TSPLAT_WA16", "0"); }
+
 // query-block size of the kernel used for window size L (128: 32x32x2 kernel, 64: 16x16x4)
 static int query_block(int L) {
     if (env_is("TSPLAT_WINATTN", "16")) return tsplat::winattn::kBQ;
@@ -1935,6 +2155,8 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     if (pair)
         hipLaunchKernelGGL(win_attn_f32_pair_kernel, dim3(p.L / 64, splits * splits, batch * p.ksplit),
                            dim3(kThreads), 0, stream, p, q, k, v, out, part);
+    else if (qb == kBQ3 && use_x16())
+        hipLaunchKernelGGL(win_attn_f32x16_kernel, grid, dim3(kThreads16), 0, stream, p, q, k, v, out, part);
     else if (qb == kBQ3)
         hipLaunchKernelGGL(win_attn_f32x32_kernel, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
     else
@@ -2000,8 +2222,12 @@ extern "C" int tsplat_win_attn_partials_fwd(const float* q, const float* k, cons
     part.l = part.m + n;
     hipStream_t stream = (hipStream_t)stream_;
     const prof::ExtEvents ev = prof::ext_events(prof::kWinAttn);  // kernel timestamps when timed
-    hipExtLaunchKernelGGL(win_attn_f32x32_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
-                          dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p, q, k, v, (float*)nullptr, part);
+    if (use_x16())
+        hipExtLaunchKernelGGL(win_attn_f32x16_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
+                              dim3(kThreads16), 0, stream, ev.start, ev.stop, 0, p, q, k, v, (float*)nullptr, part);
+    else
+        hipExtLaunchKernelGGL(win_attn_f32x32_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
+                              dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p, q, k, v, (float*)nullptr, part);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }

@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 
 from . import synthetic as S
+from .misc.benchmarker import stage
 from .model.decoder import DatasetCfgLite, DecoderSplattingHIP, DecoderSplattingHIPCfg
 from .model.encoder import EncoderTrans, EncoderTransCfg
 
@@ -25,12 +26,13 @@ class TransplatModel(torch.nn.Module):
         self.data_shim = self.encoder.get_data_shim()
 
     @torch.no_grad()
-    def test_step(self, batch: dict, global_step: int = 0):
+    def test_step(self, batch: dict, global_step: int = 0, benchmarker=None):
         batch = self.data_shim(batch)
         _, _, _, h, w = batch["target"]["image"].shape
-        gaussians = self.encoder(batch["context"], global_step, deterministic=True)
+        gaussians = self.encoder(batch["context"], global_step, deterministic=True, benchmarker=benchmarker)
         t = batch["target"]
-        return self.decoder(gaussians, t["extrinsics"], t["intrinsics"], t["near"], t["far"], (h, w))
+        with stage(benchmarker, "decoder"):  # reference model_wrapper.py:209-218 tags it "decoder"
+            return self.decoder(gaussians, t["extrinsics"], t["intrinsics"], t["near"], t["far"], (h, w))
 
     def load_checkpoint(self, path: str, strict: bool = True):
         """Lightning checkpoint of the reference (`state_dict` with `encoder.` / `decoder.` keys);

@@ -19,6 +19,7 @@ from einops import rearrange
 from torch import nn
 
 from ... import kernels, streams
+from ...misc.benchmarker import stage
 from ..depth_anything.dpt import DepthAnythingV2
 from ..types import Gaussians
 from .backbone.backbone_multiview import BackboneMultiview
@@ -119,8 +120,8 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         device = context["image"].device
         b, v, _, h, w = context["image"].shape
 
-        def bench(tag):
-            return benchmarker.time(tag) if benchmarker is not None else nullcontext()
+        def bench(tag):  # the reference's stage tags (encoder_trans.py:188-294) as roctx ranges
+            return stage(benchmarker, tag)
 
         with bench("encoder_1_prep_intrinsics"):
             intr_curr = context["intrinsics"][:, :, :3, :3].clone().detach()

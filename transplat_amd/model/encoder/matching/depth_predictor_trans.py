@@ -13,6 +13,7 @@ from einops import rearrange, repeat
 from torch import nn
 
 from .... import kernels, streams
+from ....misc.benchmarker import stage
 from ...utils.cam_param_encoder import cam_param_encoder
 from ...utils.uv_transformer import UVTransformer
 from .ldm_unet import UNetModel, run_sequential
@@ -174,24 +175,50 @@ class DepthPredictorTrans(nn.Module):
     def forward(self, features, intrinsics, extrinsics, near, far, gaussians_per_pixel=1, deterministic=True,
                 extra_info=None, cnn_features=None, da_depth=None, dino_feature=None, benchmarker=None):
         b, v, c, h, w = features.shape
-        if da_depth is not None:
-            da_depth = rearrange(da_depth, "b v ... -> (v b) ...")
-        if cnn_features is not None:
-            cnn_features = rearrange(cnn_features, "b v ... -> (v b) ...")
-        if dino_feature is not None:
-            dino_feature = rearrange(dino_feature, "b v ... -> (v b) ...")
-            dino_feature = kernels.interpolate_bilinear_ac(dino_feature, (h, w))
-        feat_comb_lists, intr_curr, pose_curr_lists, disp_candi_curr = prepare_feat_proj_data_lists(
-            features, intrinsics, extrinsics, near, far, num_samples=self.num_depth_candidates)
-        feat01 = feat_comb_lists[0]
+        # the reference's stage tags (depth_predictor_trans.py:320-456) as roctx ranges
 
         def projection(feat01, cnn_features):  # (reference :448-452) reads backbone features only
             proj_feat_in_fullres = _conv_upsample_gelu(self.upsampler, torch.cat((feat01, cnn_features), dim=1))
             return proj_feat_in_fullres, self.proj_feature(proj_feat_in_fullres)
 
-        # the full-resolution feature projection runs on a side stream beside the cost volume
-        # (matching, refine U-Net, depth head: a chain of 64^2 launches), transplat_amd/streams.py
-        proj = streams.fork(features.device, projection, feat01, cnn_features)
+        with stage(benchmarker, "encoder_4a_prep_features"):
+            if da_depth is not None:
+                da_depth = rearrange(da_depth, "b v ... -> (v b) ...")
+            if cnn_features is not None:
+                cnn_features = rearrange(cnn_features, "b v ... -> (v b) ...")
+            if dino_feature is not None:
+                dino_feature = rearrange(dino_feature, "b v ... -> (v b) ...")
+                dino_feature = kernels.interpolate_bilinear_ac(dino_feature, (h, w))
+            feat_comb_lists, intr_curr, pose_curr_lists, disp_candi_curr = prepare_feat_proj_data_lists(
+                features, intrinsics, extrinsics, near, far, num_samples=self.num_depth_candidates)
+            feat01 = feat_comb_lists[0]
+            # the full-resolution feature projection runs on a side stream beside the cost volume
+            # (matching, refine U-Net, depth head: a chain of 64^2 launches), transplat_amd/streams.py
+            proj = streams.fork(features.device, projection, feat01, cnn_features)
+        with stage(benchmarker, "encoder_4b_cost_volume_matching"):
+            raw_correlation_in = self._match(v, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr,
+                                             dino_feature, features, feat01)
+        with stage(benchmarker, "encoder_4c_cost_volume_unet"):
+            raw_correlation = (run_sequential(self.corr_refine_net, raw_correlation_in)
+                               + self.regressor_residual(raw_correlation_in))
+        with stage(benchmarker, "encoder_4d_coarse_depth"):
+            coarse_disps, pdf_max, fullres_disps = self._coarse_depth(raw_correlation, disp_candi_curr)
+        with stage(benchmarker, "encoder_4e_depth_refine_unet"):
+            proj_feat_in_fullres, proj_feature = streams.join(proj)
+            refine_out = run_sequential(self.refine_unet, torch.cat(
+                (extra_info["images"], da_depth, proj_feature, fullres_disps, pdf_max), dim=1))
+        with stage(benchmarker, "encoder_4f_gaussian_head"):
+            raw_gaussians = _conv_gelu_conv(self.to_gaussians, refine_out,
+                                            extra=(extra_info["images"], proj_feat_in_fullres))
+            raw_gaussians = rearrange(raw_gaussians, "(v b) c h w -> b v (h w) c", v=v, b=b)
+            delta_disps, raw_densities = _conv_gelu_conv(self.to_disparity, refine_out).split(gaussians_per_pixel, dim=1)
+            densities = repeat(F.sigmoid(raw_densities), "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
+            fine_disps = (fullres_disps + delta_disps).clamp(1.0 / rearrange(far, "b v -> (v b) () () ()"),
+                                                             1.0 / rearrange(near, "b v -> (v b) () () ()"))
+            depths = repeat(1.0 / fine_disps, "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
+        return depths, densities, raw_gaussians
+
+    def _match(self, v, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr, dino_feature, features, feat01):
         if v == 2:
             raw_correlation_in = self.match_two(intr_curr, pose_curr_lists[0], extrinsics, disp_candi_curr,
                                                 dino_feature, features)
@@ -200,10 +227,9 @@ class DepthPredictorTrans(nn.Module):
                                                   dino_feature, features)
         else:
             raise NotImplementedError(f"{v} context views (the reference handles 2, 3 and 4)")
-        raw_correlation_in = torch.cat((raw_correlation_in, feat01), dim=1)
+        return torch.cat((raw_correlation_in, feat01), dim=1)
 
-        raw_correlation = (run_sequential(self.corr_refine_net, raw_correlation_in)
-                           + self.regressor_residual(raw_correlation_in))
+    def _coarse_depth(self, raw_correlation, disp_candi_curr):
         logits = _conv_gelu_conv(self.depth_head_lowres, raw_correlation)
         if logits.dtype == torch.float32:  # softmax, expected disparity and max in one pass
             coarse_disps, pdf_max = kernels.depth_softmax(logits, disp_candi_curr)
@@ -215,17 +241,4 @@ class DepthPredictorTrans(nn.Module):
         up = int(self.upscale_factor)  # align_corners: the ratio comes from the sizes, as torch's
         fullres_disps = kernels.interpolate_bilinear_ac(coarse_disps, (coarse_disps.shape[-2] * up,
                                                                        coarse_disps.shape[-1] * up))
-
-        proj_feat_in_fullres, proj_feature = streams.join(proj)
-        refine_out = run_sequential(self.refine_unet, torch.cat((extra_info["images"], da_depth, proj_feature, fullres_disps,
-                                                 pdf_max), dim=1))
-
-        raw_gaussians = _conv_gelu_conv(self.to_gaussians, refine_out,
-                                        extra=(extra_info["images"], proj_feat_in_fullres))
-        raw_gaussians = rearrange(raw_gaussians, "(v b) c h w -> b v (h w) c", v=v, b=b)
-        delta_disps, raw_densities = _conv_gelu_conv(self.to_disparity, refine_out).split(gaussians_per_pixel, dim=1)
-        densities = repeat(F.sigmoid(raw_densities), "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
-        fine_disps = (fullres_disps + delta_disps).clamp(1.0 / rearrange(far, "b v -> (v b) () () ()"),
-                                                         1.0 / rearrange(near, "b v -> (v b) () () ()"))
-        depths = repeat(1.0 / fine_disps, "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
-        return depths, densities, raw_gaussians
+        return coarse_disps, pdf_max, fullres_disps

@@ -17,11 +17,12 @@ caching allocator never hands their memory to the other stream while it is still
 """
 from __future__ import annotations
 
+import os
 from contextlib import contextmanager
 
 import torch
 
-_ENABLED = True
+_ENABLED = os.environ.get("TSPLAT_STREAMS", "1") != "0"  # A/B knob
 _SIDE: dict = {}
 
 
