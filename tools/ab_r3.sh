@@ -8,7 +8,7 @@ OUT=gpurun_out/${TAG:-ab_r3}
 mkdir -p $OUT
 export PYTHONPATH=$(pwd)
 timeout -k 10 400 python -u -m pytest tests/test_encoder_ops.py tests/test_raster.py -m gpu -x -q -s --timeout 200 \
-    -k "window_attention_kernel or attention_merge or raster" > $OUT/pytest.log 2>&1 || { echo tests failed; tail -30 $OUT/pytest.log; exit 1; }
+    -k "window_attention_kernel or attention_merge or raster or uv_coarse" > $OUT/pytest.log 2>&1 || { echo tests failed; tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log; grep "raster parity (256\|raster parity (DTU" $OUT/pytest.log | cut -c1-200
 run() {  # name, env...
   local name=$1; shift
@@ -29,7 +29,13 @@ d = [json.loads(l) for l in open(sys.argv[1]) if l.startswith("{")][-1]
 print(f"{sys.argv[2]:24s} {d['value']:8.1f} views/s {d['ms_per_step']*1e3:7.1f} us/call  frac {d['roofline']['frac']:.3f}")
 PY
 }
-for arg in ${AB_LIST:-e2e raster}; do
+for arg in ${AB_LIST:-corr e2e raster}; do
+  if [ $arg = corr ]; then
+    for G in 1 0 1; do
+      TSPLAT_UV_COARSE_GROUP=$G timeout -k 10 120 python tools/bench_corr.py > $OUT/corr_g$G.log 2>&1 || { echo corr failed; tail -3 $OUT/corr_g$G.log; exit 1; }
+      echo "uv_coarse group=$G: $(tail -1 $OUT/corr_g$G.log)"
+    done
+  fi
   if [ $arg = e2e ]; then
     run base
     run x32 TSPLAT_WA16=0

@@ -1,4 +1,5 @@
-"""Which Python call sites launch the small PyTorch kernels (copies, elementwise, cat, GELU, clamp ...)
+"""usage: op_stacks.py [batch] [fp32|bf16]
+Which Python call sites launch the small PyTorch kernels (copies, elementwise, cat, GELU, clamp ...)
 of one e2e step: a TorchDispatchMode records every launching aten op with the innermost repo frame
 that called it (torch.profiler's with_stack comes back empty on this build)."""
 import collections
@@ -36,9 +37,13 @@ class Sites(TorchDispatchMode):
         return func(*args, **(kwargs or {}))
 
 
+import sys
+
+batch = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+dense = sys.argv[2] if len(sys.argv) > 2 else "fp32"
 dev = torch.device("cuda:0")
-model = build_model(dev)
-data = S.make_batch(1, image_shape=(256, 256), device=dev)
+model = build_model(dev, dense)
+data = S.make_batch(batch, image_shape=(256, 256), device=dev)
 for _ in range(2):
     model.test_step(data)
 torch.cuda.synchronize()
@@ -46,5 +51,5 @@ mode = Sites()
 with mode:
     model.test_step(data)
 torch.cuda.synchronize()
-for (name, where), n in mode.agg.most_common(90):
+for (name, where), n in mode.agg.most_common(150):
     print(f"{n:4d} {name:24s} {where}")

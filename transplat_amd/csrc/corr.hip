@@ -28,6 +28,7 @@ constexpr int kThreads = 256;  // 16 groups of 16 lanes
 constexpr int kGroups = kThreads / 16;
 constexpr int kMaxPoints = 8;
 
+
 struct Cam {
     float kinv[9], k[9], r[9], t[3];
 };

@@ -98,7 +98,6 @@ struct Params {
     int G, V, vps, H, W, M, deg, tiles_x, tiles_y, T, capacity;
     int diag;  // timing diagnostics only (TSPLAT_RASTER_DIAG; output is wrong when != 0)
     int count_sort;  // 1: counting sort for long tile lists (default); 0: bitonic only (A/B)
-    int sub;         // 1: 4x4 sub-block lists per 16-lane group (default); 0: one 8x8 list (A/B)
 };
 
 __device__ __forceinline__ void get_rect(float px, float py, int r, int tx, int ty, int& x0,
@@ -697,11 +696,7 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     // no workgroup barrier below this point: each wave walks the sorted list on its own
 
     const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    // pixel of this lane: 8x8 block per wave; in sub-block mode the 16-lane group g = lane >> 4
-    // owns the 4x4 quarter (g & 1, g >> 1) of it
-    const int sg = lane >> 4;
-    const int lx = (wid & 1) * 8 + (p.sub ? 4 * (sg & 1) + (lane & 3) : (lane & 7));
-    const int ly = (wid >> 1) * 8 + (p.sub ? 4 * (sg >> 1) + ((lane >> 2) & 3) : (lane >> 3));
+    const int lx = (wid & 1) * 8 + (lane & 7), ly = (wid >> 1) * 8 + (lane >> 3);
     const int pxi = tx * kTile + lx, pyi = ty * kTile + ly;
     const float wx0 = (float)(tx * kTile + (wid & 1) * 8), wx1 = wx0 + 7.0f;
     const float wy0 = (float)(ty * kTile + (wid >> 1) * 8), wy1 = wy0 + 7.0f;
@@ -719,15 +714,14 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     // e^power = 2^power2 is one v_exp_f32, and the quadratic in Horner form (2 FMAs + 3 multiplies).
     // Scalar fp32 on purpose: v_pk_fma_f32 has the same FLOP rate as v_fma_f32 (twice the cycles),
     // and packing the operands costs register moves.
-    auto blend = [&](float x, float y, float ca, float cb, float cc, float o, float r, float g, float bl,
-                     bool act = true) {
+    auto blend = [&](float x, float y, float ca, float cb, float cc, float o, float r, float g, float bl) {
         // (ca, cb, cc) = log2(e) (-a/2, -b, -c/2): power2 = dy (cc dy + cb dx) + (ca dx) dx
         const float dx = x - pfx, dy = y - pfy;
         const float power2 = fmaf(dy, fmaf(cc, dy, cb * dx), (ca * dx) * dx);
         const float alpha = fminf(0.99f, o * __builtin_amdgcn_exp2f(power2));
         const float test_T = fmaf(-alpha, T, T);
         // reference order: skip power > 0, skip alpha < 1/255, stop if test_T < 1e-4
-        const bool contrib = act && !done && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+        const bool contrib = !done && !(power2 > 0.0f) && !(alpha < 1.0f / 255.0f);
         const bool stop = contrib && (test_T < 0.0001f);
         const bool acc = contrib && !stop;
         const float w = acc ? alpha * T : 0.0f;  // a skipped entry adds c * 0 = +0: C unchanged
@@ -819,87 +813,7 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
             __builtin_amdgcn_wave_barrier();  // reads of this chunk's records precede the next writes
         }
     };
-    // Sub-block walk: the same chunked, depth-ordered walk, but every chunk entry is tested
-    // against the four 4x4 quarters of the wave's block (its alpha >= 1/255 box) and each 16-lane
-    // group blends only the entries of ITS quarter, all four groups in lockstep (iteration j:
-    // group g takes the j-th entry of its list). A Gaussian a few pixels wide touches far fewer
-    // 4x4 quarters than it touches whole 8x8 blocks, so a wave iterates max_g(len_g) times
-    // instead of len_8x8 (same per-pixel arithmetic, same depth order per pixel).
-    // LDS per wave (the same 2,304 B as the compacted layout): the chunk's records entry-major,
-    // [64][8] floats (x, y, conic, opacity, r, g: 2 x ds_read_b128 per entry) + [64] blue, one
-    // slot per chunk lane; four uint8 lists of slot indices live in s_cnt (free after the sort).
-    auto walk_sub = [&](auto lds_tag) {
-        constexpr bool kInLds = decltype(lds_tag)::value;
-        float* wr = &s_rec[wid][0][0];
-        float* wblue = wr + kWave * 8;
-        uint8_t* wl = reinterpret_cast<uint8_t*>(s_cnt) + 256 * wid;
-        float4 r_xy = make_float4(0.f, 0.f, 0.f, 0.f), r_co = r_xy, r_rgb = r_xy, r_cull = r_xy;
-        bool r_valid = false;
-        auto fetch = [&](int k) {
-            r_valid = k < n;
-            if (r_valid) {
-                uint32_t gid;
-                if constexpr (kInLds)
-                    gid = sids[k];
-                else
-                    gid = (uint32_t)gkeys[k];
-                const float4* rec = ws.rec + 4 * (vbase + gid);
-                r_xy = rec[0];
-                r_co = rec[1];
-                r_rgb = rec[2];
-                r_cull = rec[3];
-            }
-        };
-        const float qx = wx0 + 3.5f, qy = wy0 + 3.5f;  // the quarters split at x = wx0 + 3.5, y = ...
-        fetch(lane);
-        for (int c0 = 0; c0 < n; c0 += kWave) {
-            if (__all(done)) break;
-            const float4 xy = r_xy, co = r_co, rgb = r_rgb, cull = r_cull;
-            const bool valid = r_valid;
-            fetch(c0 + kWave + lane);
-            bool hit = valid && !(xy.x + xy.z < wx0 || xy.x - xy.z > wx1 || xy.y + xy.w < wy0 ||
-                                  xy.y - xy.w > wy1);
-            if (hit) hit = ellipse_meets_block(xy.x, xy.y, co, cull, wx0, wx1, wy0, wy1);
-            // quarter tests with the entry's alpha >= 1/255 box (the 8x8 tests above hold)
-            const bool left = xy.x - xy.z < qx, right = xy.x + xy.z > qx;
-            const bool top = xy.y - xy.w < qy, bottom = xy.y + xy.w > qy;
-            const uint64_t m0 = __ballot(hit && left && top), m1 = __ballot(hit && right && top);
-            const uint64_t m2 = __ballot(hit && left && bottom), m3 = __ballot(hit && right && bottom);
-            const int n0 = __popcll(m0), n1 = __popcll(m1), n2 = __popcll(m2), n3 = __popcll(m3);
-            const int nmax = p.diag == 4 ? 0 : max(max(n0, n1), max(n2, n3));
-            d_entries += nmax;
-            ++d_chunks;
-            if (hit) {
-                float4* dst = reinterpret_cast<float4*>(wr + lane * 8);
-                dst[0] = make_float4(xy.x, xy.y, co.x, co.y);
-                dst[1] = make_float4(co.z, co.w, rgb.x, rgb.y);
-                wblue[lane] = rgb.z;
-                if (left && top) wl[__popcll(m0 & lt_mask)] = (uint8_t)lane;
-                if (right && top) wl[64 + __popcll(m1 & lt_mask)] = (uint8_t)lane;
-                if (left && bottom) wl[128 + __popcll(m2 & lt_mask)] = (uint8_t)lane;
-                if (right && bottom) wl[192 + __popcll(m3 & lt_mask)] = (uint8_t)lane;
-            }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const int my_n = sg == 0 ? n0 : (sg == 1 ? n1 : (sg == 2 ? n2 : n3));
-            const uint8_t* my_list = wl + 64 * sg;
-            for (int j = 0; j < nmax; ++j) {
-                const bool act = j < my_n;
-                const int idx = my_list[j] & (kWave - 1);  // stale slots past my_n: any valid slot
-                const float4* src = reinterpret_cast<const float4*>(wr + idx * 8);
-                const float4 a = src[0], b = src[1];
-                blend(a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, wblue[idx], act);
-            }
-            __builtin_amdgcn_wave_barrier();  // reads of this chunk's records precede the next writes
-        }
-    };
-    if (p.sub) {
-        if (in_lds)
-            walk_sub(std::true_type{});
-        else
-            walk_sub(std::false_type{});
-    } else if (in_lds)
+    if (in_lds)
         walk(std::true_type{});
     else
         walk(std::false_type{});
@@ -971,8 +885,6 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
         p.diag = e ? atoi(e) : 0;
         const char* s = getenv("TSPLAT_RASTER_SORT");
         p.count_sort = !(s && !strcmp(s, "bitonic"));
-        const char* sb = getenv("TSPLAT_RASTER_SUB");
-        p.sub = !(sb && !strcmp(sb, "0"));
     }
     if ((size_t)p.T * 2 * sizeof(uint32_t) > 64 * 1024) return TSPLAT_EINVAL;  // LDS histogram
     Workspace ws = carve(workspace, p.G, p.V, p.T, p.capacity, nullptr);

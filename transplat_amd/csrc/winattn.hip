@@ -2058,9 +2058,11 @@ static bool env_is(const char* name, const char* val) {
     return e && !strcmp(e, val);
 }
 
-// 128-query blocks run as 8 x 16-query waves (win_attn_f32x16_kernel) unless TSPLAT_WA16=0 (A/B:
-// the 4 x 32-query kernel)
-static bool use_x16() { return !env_is("TSPLAT_WA16", "0"); }
+// 128-query blocks as 8 x 16-query waves (win_attn_f32x16_kernel) with TSPLAT_WA16=1; default the
+// 4 x 32-query kernel. Same-box A/B (round 3, tools/ab_r3.sh): x16 47.5 vs x32 50.0 us per launch at
+// the C2 shape, but the C2 step 355.9 / 357.1 vs 360.8 views/s with the concurrent encoder branches
+// (its 138 KB of LDS leaves no room on a CU for the other branch's workgroups).
+static bool use_x16() { return env_is("TSPLAT_WA16", "1"); }
 
 // query-block size of the kernel used for window size L (128: 32x32x2 kernel, 64: 16x16x4)
 static int query_block(int L) {
