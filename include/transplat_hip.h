@@ -204,6 +204,13 @@ int tsplat_group_norm_fwd(const float* x, const float* pre_bias, const float* ga
                           const float* residual,
                           float* y, void* workspace, int32_t n, int32_t c, int64_t hw, int32_t groups,
                           float eps, int32_t act, void* stream);
+/* The same with bf16 x / residual / y (fp32 statistics, gamma, beta, pre_bias): the bf16
+ * dense-layer mode (config C3), where the surrounding convolutions read and write bf16 -- the
+ * reference's GroupNorm32 likewise normalises x.float() and casts back to x's dtype
+ * (ldm_unet/util.py GroupNorm32.forward). */
+int tsplat_group_norm_bf16_fwd(const void* x, const float* pre_bias, const float* gamma, const float* beta,
+                               const void* residual, void* y, void* workspace, int32_t n, int32_t c, int64_t hw,
+                               int32_t groups, float eps, int32_t act, void* stream);
 
 /* Convolution epilogue without a norm: y = act(x + bias[c]) [+ residual] over [n, c, hw] fp32
  * (act as above; 3 with a residual = relu(residual + relu(.))), hw % 4 == 0, 16-B aligned; y may
@@ -227,6 +234,11 @@ int tsplat_bias_act_nhwc_fwd(const float* x, const float* bias, const float* res
  * (plain LayerNorm of x, x_out unused), ls may be NULL (no LayerScale). */
 int tsplat_residual_ln_fwd(const float* x, const float* y, const float* ls, const float* ln_w, const float* ln_b,
                            float ln_eps, float* x_out, float* n_out, int32_t rows, int32_t dim, void* stream);
+/* The same with a bf16 sub-layer output y and a bf16 n_out (bf16 dense mode: the linears read and
+ * write bf16), the residual stream x / x_out and all statistics fp32 -- what autocast computes
+ * (LayerNorm in fp32, cast to bf16 by the next linear). */
+int tsplat_residual_ln_bf16_fwd(const float* x, const void* y, const float* ls, const float* ln_w, const float* ln_b,
+                                float ln_eps, float* x_out, void* n_out, int32_t rows, int32_t dim, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Gaussian adapter (encoder stage 5 + GaussianAdapter.forward, reference

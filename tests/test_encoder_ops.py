@@ -320,6 +320,15 @@ def test_group_norm_kernel(device, shape, groups, act, res, pb):
     out = K.group_norm(x.to(device), groups, w.to(device), b.to(device), 1e-5, act,
                        r.to(device) if res else None, bias.to(device) if pb else None).cpu()
     assert (out - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
+    # bf16 activations (config C3): bf16 x / residual in, fp32 statistics, bf16 out -- the
+    # reference's GroupNorm32 normalises x.float() and casts back; checked on the same bf16 inputs
+    xb, rb = x.bfloat16(), (r.bfloat16() if res else None)
+    ref_b = E.group_norm(xb.float(), groups, w, b, 1e-5, act, rb.float() if res else None, bias)
+    out_b = K.group_norm(xb.to(device), groups, w.to(device), b.to(device), 1e-5, act,
+                         rb.to(device) if res else None, bias.to(device) if pb else None)
+    assert out_b.dtype == torch.bfloat16
+    # one bf16 rounding of the output (2^-8 relative) on top of fp32 arithmetic
+    assert (out_b.float().cpu() - ref_b).abs().max().item() < 8e-3 * max(1.0, ref_b.abs().max().item())
 
 
 @pytest.mark.gpu
@@ -553,6 +562,14 @@ def test_residual_ln_kernel(device, rows, dim, with_y, with_ls):
     ox, on = K.residual_ln(d(x), d(y), d(ls), norm.to(device))
     assert (ox.cpu() - rx).abs().max().item() < 1e-5
     assert (on.cpu() - rn).abs().max().item() < 2e-5
+    # bf16 form (bf16 dense mode): bf16 sub-layer output in, fp32 residual stream, bf16 LayerNorm
+    # out = the fp32 result rounded once
+    yb = y.bfloat16() if with_y else None
+    rxb, rnb = E.residual_ln(x, yb.float() if with_y else None, ls, norm.cpu())
+    oxb, onb = K.residual_ln(d(x), d(yb), d(ls), norm.to(device), bf16_out=True)
+    assert onb.dtype == torch.bfloat16 and oxb.dtype == torch.float32
+    assert (oxb.cpu() - rxb).abs().max().item() < 1e-5
+    assert (onb.float().cpu() - rnb).abs().max().item() < 8e-3 * max(1.0, rnb.abs().max().item())
 
 
 @pytest.mark.gpu

@@ -55,6 +55,8 @@ SIGNATURES = {
     "tsplat_win_attn_bf16_fwd": (ctypes.c_int, [_P] * 5 + [_I32] * 7 + [_P]),
     "tsplat_group_norm_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, ctypes.c_int64, _I32]),
     "tsplat_group_norm_fwd": (ctypes.c_int, [_P] * 7 + [_I32, _I32, ctypes.c_int64, _I32, ctypes.c_float, _I32, _P]),
+    "tsplat_group_norm_bf16_fwd": (ctypes.c_int, [_P] * 7 + [_I32, _I32, ctypes.c_int64, _I32, ctypes.c_float, _I32,
+                                                            _P]),
     "tsplat_sh_rotation_fwd": (ctypes.c_int, [_P] * 3 + [_I32] * 2 + [_P]),
     "tsplat_gaussian_adapter_fwd": (ctypes.c_int, [_P] * 9 + [_I32] * 6 + [ctypes.c_float] * 3 + [_I32, _I32, _P]),
     "tsplat_win_attn_split": (_I32, [_I32] * 5),
@@ -69,6 +71,7 @@ SIGNATURES = {
     "tsplat_upsample_bilinear_act_fwd": (ctypes.c_int, [_P, _P, _P] + [_I32] * 6 + [_P]),
     "tsplat_conv2d_f32_nhwc_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P] + [_I32] * 7 + [_P]),
     "tsplat_residual_ln_fwd": (ctypes.c_int, [_P] * 5 + [ctypes.c_float, _P, _P, _I32, _I32, _P]),
+    "tsplat_residual_ln_bf16_fwd": (ctypes.c_int, [_P] * 5 + [ctypes.c_float, _P, _P, _I32, _I32, _P]),
     "tsplat_bias_act_fwd": (ctypes.c_int, [_P] * 4 + [_I32, _I32, ctypes.c_int64, _I32, _P]),
     "tsplat_bias_act_nhwc_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int64, _I32, _I32, _P]),
     "tsplat_win_attn_partials_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 8 + [_P]),

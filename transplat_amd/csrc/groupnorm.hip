@@ -48,17 +48,35 @@ __device__ __forceinline__ Welford wave_reduce(Welford w) {
     return w;
 }
 
+// activation I/O: fp32, or bf16 (config C3's bf16 dense layers: the convolutions around the norm
+// read and write bf16, so the norm takes bf16 in and gives bf16 out, computing in fp32 -- the
+// reference's GroupNorm32 normalises x.float() and casts back to x's dtype)
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const __bf16* p) { return (float)*p; }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(__bf16* p, float v) { *p = (__bf16)v; }
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld4(const __bf16* p) {
+    const bf16x4_t v = *reinterpret_cast<const bf16x4_t*>(p);
+    return make_float4((float)v[0], (float)v[1], (float)v[2], (float)v[3]);
+}
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void st4(__bf16* p, float4 v) {
+    *reinterpret_cast<bf16x4_t*>(p) = bf16x4_t{(__bf16)v.x, (__bf16)v.y, (__bf16)v.z, (__bf16)v.w};
+}
+
 // Welford over this workgroup's chunk -> partials[seg * S + chunk] = (mean, M2)
 // pb (may be null): per-channel bias of the producing convolution, added on the fly (the conv
 // runs without its bias, so PyTorch's separate broadcast add disappears)
-template <bool VEC>
+template <bool VEC, typename T>
 __global__ void __launch_bounds__(kThreads)
-stats_kernel(const float* __restrict__ x, const float* __restrict__ pb, float2* __restrict__ partials,
+stats_kernel(const T* __restrict__ x, const float* __restrict__ pb, float2* __restrict__ partials,
              int64_t L, int S, int HW, int cpg, int G) {
     const int chunk = blockIdx.x, seg = blockIdx.y, tid = threadIdx.x;
     const int64_t start = (int64_t)chunk * kChunk;
     const int n_local = (int)min((int64_t)kChunk, L - start);
-    const float* p = x + (int64_t)seg * L + start;
+    const T* p = x + (int64_t)seg * L + start;
     const int c0 = (seg % G) * cpg;
     Welford w{0.f, 0.f, 0.f};
     if (VEC) {
@@ -67,7 +85,7 @@ stats_kernel(const float* __restrict__ x, const float* __restrict__ pb, float2* 
             const int i = (k * kThreads + tid) * 4;
             if (i < n_local) {
                 const float b = pb ? pb[c0 + (int)((start + i) / HW)] : 0.f;
-                const float4 v = *reinterpret_cast<const float4*>(p + i);
+                const float4 v = ld4(p + i);
                 w = push(w, v.x + b);
                 w = push(w, v.y + b);
                 w = push(w, v.z + b);
@@ -76,7 +94,7 @@ stats_kernel(const float* __restrict__ x, const float* __restrict__ pb, float2* 
         }
     } else {
         for (int i = tid; i < n_local; i += kThreads)
-            w = push(w, p[i] + (pb ? pb[c0 + (int)((start + i) / HW)] : 0.f));
+            w = push(w, ld1(p + i) + (pb ? pb[c0 + (int)((start + i) / HW)] : 0.f));
     }
     w = wave_reduce(w);
     __shared__ Welford sw[kThreads / kWave];
@@ -102,11 +120,11 @@ __device__ __forceinline__ float activate(float v) {
 template <int ACT>
 __device__ __forceinline__ float post_residual(float v) { return ACT == 3 ? fmaxf(v, 0.0f) : v; }
 
-template <bool VEC, int ACT, bool RES>
+template <bool VEC, int ACT, bool RES, typename T>
 __global__ void __launch_bounds__(kThreads)
-apply_kernel(const float* __restrict__ x, const float* __restrict__ pb, const float2* __restrict__ partials,
+apply_kernel(const T* __restrict__ x, const float* __restrict__ pb, const float2* __restrict__ partials,
              const float* __restrict__ gamma, const float* __restrict__ beta,
-             const float* __restrict__ res, float* __restrict__ y, int64_t L, int S, int HW, int C,
+             const T* __restrict__ res, T* __restrict__ y, int64_t L, int S, int HW, int C,
              int cpg, int G, float eps) {
     const int chunk = blockIdx.x, seg = blockIdx.y, tid = threadIdx.x;
     __shared__ float s_scale_shift[2];
@@ -139,7 +157,7 @@ apply_kernel(const float* __restrict__ x, const float* __restrict__ pb, const fl
                 const float sc = rstd * gamma[c];
                 const float sh = beta[c] - sc * mean;
                 const float b = pb ? pb[c] : 0.f;
-                float4 v = *reinterpret_cast<const float4*>(x + base + i);
+                float4 v = ld4(x + base + i);
                 v.x += b;
                 v.y += b;
                 v.z += b;
@@ -149,22 +167,22 @@ apply_kernel(const float* __restrict__ x, const float* __restrict__ pb, const fl
                 v.z = activate<ACT>(v.z * sc + sh);
                 v.w = activate<ACT>(v.w * sc + sh);
                 if (RES) {
-                    const float4 r = *reinterpret_cast<const float4*>(res + base + i);
+                    const float4 r = ld4(res + base + i);
                     v.x = post_residual<ACT>(v.x + r.x);
                     v.y = post_residual<ACT>(v.y + r.y);
                     v.z = post_residual<ACT>(v.z + r.z);
                     v.w = post_residual<ACT>(v.w + r.w);
                 }
-                *reinterpret_cast<float4*>(y + base + i) = v;
+                st4(y + base + i, v);
             }
         }
     } else {
         for (int i = tid; i < n_local; i += kThreads) {
             const int c = g * cpg + (int)((start + i) / HW);
             const float sc = rstd * gamma[c];
-            float v = activate<ACT>((x[base + i] + (pb ? pb[c] : 0.f)) * sc + (beta[c] - sc * mean));
-            if (RES) v = post_residual<ACT>(v + res[base + i]);
-            y[base + i] = v;
+            float v = activate<ACT>((ld1(x + base + i) + (pb ? pb[c] : 0.f)) * sc + (beta[c] - sc * mean));
+            if (RES) v = post_residual<ACT>(v + ld1(res + base + i));
+            st1(y + base + i, v);
         }
     }
 }
@@ -188,10 +206,10 @@ __device__ __forceinline__ float block_sum512(float v, float* red) {
     return t;
 }
 
-template <int NPT, int ACT, bool RES>
+template <int NPT, int ACT, bool RES, typename T>
 __global__ void __launch_bounds__(kFusedThreads)
-fused_kernel(const float* __restrict__ x, const float* __restrict__ pb, const float* __restrict__ gamma,
-             const float* __restrict__ beta, const float* __restrict__ res, float* __restrict__ y, int L, int HW,
+fused_kernel(const T* __restrict__ x, const float* __restrict__ pb, const float* __restrict__ gamma,
+             const float* __restrict__ beta, const T* __restrict__ res, T* __restrict__ y, int L, int HW,
              int cpg, int G, float eps) {
     __shared__ float red[kFusedThreads / kWave];
     const int seg = blockIdx.x, tid = threadIdx.x;
@@ -203,7 +221,7 @@ fused_kernel(const float* __restrict__ x, const float* __restrict__ pb, const fl
     for (int k = 0; k < NPT / 4; ++k) {
         const int i = (k * kFusedThreads + tid) * 4;  // HW % 4 == 0: one channel per float4
         if (i < L) {
-            v[k] = *reinterpret_cast<const float4*>(x + base + i);
+            v[k] = ld4(x + base + i);
             if (pb) {
                 const float b = pb[g * cpg + i / HW];
                 v[k].x += b;
@@ -237,13 +255,13 @@ fused_kernel(const float* __restrict__ x, const float* __restrict__ pb, const fl
             o.z = activate<ACT>(v[k].z * sc + sh);
             o.w = activate<ACT>(v[k].w * sc + sh);
             if (RES) {
-                const float4 r = *reinterpret_cast<const float4*>(res + base + i);
+                const float4 r = ld4(res + base + i);
                 o.x = post_residual<ACT>(o.x + r.x);
                 o.y = post_residual<ACT>(o.y + r.y);
                 o.z = post_residual<ACT>(o.z + r.z);
                 o.w = post_residual<ACT>(o.w + r.w);
             }
-            *reinterpret_cast<float4*>(y + base + i) = o;
+            st4(y + base + i, o);
         }
     }
 }
@@ -260,10 +278,10 @@ extern "C" size_t tsplat_group_norm_workspace_bytes(int32_t n, int32_t c, int64_
     return (size_t)n * groups * S * sizeof(float2);
 }
 
-extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, const float* gamma, const float* beta,
-                                     const float* residual, float* y, void* workspace, int32_t n,
-                                     int32_t c, int64_t hw, int32_t groups, float eps, int32_t act,
-                                     void* stream_) {
+template <typename T>
+static int group_norm_launch(const T* x, const float* pre_bias, const float* gamma, const float* beta,
+                             const T* residual, T* y, void* workspace, int32_t n, int32_t c, int64_t hw,
+                             int32_t groups, float eps, int32_t act, void* stream_) {
     using namespace tsplat::gn;
     if (!x || !gamma || !beta || !y || !workspace) return TSPLAT_EINVAL;
     if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups || act < 0 || act > 3 ||
@@ -275,14 +293,15 @@ extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, cons
     if (S > INT32_MAX || (int64_t)n * groups > 65535) return TSPLAT_EINVAL;
     hipStream_t stream = (hipStream_t)stream_;
     const dim3 grid((unsigned)S, (unsigned)(n * groups));
-    const bool vec = (hw % 4 == 0) && ((uintptr_t)x % 16 == 0) && ((uintptr_t)y % 16 == 0) &&
-                     (!residual || (uintptr_t)residual % 16 == 0);
+    const uintptr_t al = 4 * sizeof(T);  // one vector of 4 elements
+    const bool vec = (hw % 4 == 0) && ((uintptr_t)x % al == 0) && ((uintptr_t)y % al == 0) &&
+                     (!residual || (uintptr_t)residual % al == 0);
     if (vec && L <= (int64_t)kFusedThreads * 32 && x != y) {
         // the whole group fits one workgroup's registers: single launch
         const int npt = L <= kFusedThreads * 4 ? 4 : L <= kFusedThreads * 8 ? 8 : L <= kFusedThreads * 16 ? 16 : 32;
         TSPLAT_PROF_BEGIN(prof::kGroupNorm, stream);
 #define TSPLAT_GN_F(N, A, R)                                                                                  \
-    hipLaunchKernelGGL((fused_kernel<N, A, R>), dim3((unsigned)(n * groups)), dim3(kFusedThreads), 0, stream, x, \
+    hipLaunchKernelGGL((fused_kernel<N, A, R, T>), dim3((unsigned)(n * groups)), dim3(kFusedThreads), 0, stream, x, \
                        pre_bias, gamma, beta, residual, y, (int)L, (int)hw, cpg, groups, eps)
 #define TSPLAT_GN_FA(N, R)                   \
     switch (act) {                           \
@@ -309,14 +328,14 @@ extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, cons
     float2* part = (float2*)workspace;
     TSPLAT_PROF_BEGIN(prof::kGroupNorm, stream);
     if (vec)
-        hipLaunchKernelGGL(stats_kernel<true>, grid, dim3(kThreads), 0, stream, x, pre_bias, part, L, (int)S,
+        hipLaunchKernelGGL((stats_kernel<true, T>), grid, dim3(kThreads), 0, stream, x, pre_bias, part, L, (int)S,
                            (int)hw, cpg, groups);
     else
-        hipLaunchKernelGGL(stats_kernel<false>, grid, dim3(kThreads), 0, stream, x, pre_bias, part, L, (int)S,
+        hipLaunchKernelGGL((stats_kernel<false, T>), grid, dim3(kThreads), 0, stream, x, pre_bias, part, L, (int)S,
                            (int)hw, cpg, groups);
     TSPLAT_CHECK_LAUNCH();
 #define TSPLAT_GN_APPLY(V, A, R)                                                                   \
-    hipLaunchKernelGGL((apply_kernel<V, A, R>), grid, dim3(kThreads), 0, stream, x, pre_bias, part, gamma,  \
+    hipLaunchKernelGGL((apply_kernel<V, A, R, T>), grid, dim3(kThreads), 0, stream, x, pre_bias, part, gamma,  \
                        beta, residual, y, L, (int)S, (int)hw, c, cpg, groups, eps)
 #define TSPLAT_GN_ACT(V, R)              \
     switch (act) {                       \
@@ -335,6 +354,22 @@ extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, cons
     TSPLAT_PROF_END(prof::kGroupNorm, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
+}
+
+extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, const float* gamma, const float* beta,
+                                     const float* residual, float* y, void* workspace, int32_t n,
+                                     int32_t c, int64_t hw, int32_t groups, float eps, int32_t act,
+                                     void* stream_) {
+    return group_norm_launch<float>(x, pre_bias, gamma, beta, residual, y, workspace, n, c, hw, groups, eps, act,
+                                    stream_);
+}
+
+extern "C" int tsplat_group_norm_bf16_fwd(const void* x, const float* pre_bias, const float* gamma,
+                                          const float* beta, const void* residual, void* y, void* workspace,
+                                          int32_t n, int32_t c, int64_t hw, int32_t groups, float eps, int32_t act,
+                                          void* stream_) {
+    return group_norm_launch<__bf16>((const __bf16*)x, pre_bias, gamma, beta, (const __bf16*)residual, (__bf16*)y,
+                                     workspace, n, c, hw, groups, eps, act, stream_);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -473,11 +508,13 @@ extern "C" int tsplat_bias_act_nhwc_fwd(const float* x, const float* bias, const
 namespace tsplat {
 namespace gn {
 
-template <int V4>  // float4s per lane (dim = 256 V4)
+// TY / TN: the sub-layer output y and the normalised n in fp32, or bf16 (bf16 dense mode: the
+// linears read n and write y in bf16; the residual stream x stays fp32 as under autocast)
+template <int V4, typename TY, typename TN>  // float4s per lane (dim = 256 V4)
 __global__ void __launch_bounds__(kThreads)
-residual_ln_kernel(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ ls,
+residual_ln_kernel(const float* __restrict__ x, const TY* __restrict__ y, const float* __restrict__ ls,
                    const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ x_out,
-                   float* __restrict__ n_out, int rows, float eps) {
+                   TN* __restrict__ n_out, int rows, float eps) {
     const int row = blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= rows) return;
@@ -490,7 +527,7 @@ residual_ln_kernel(const float* __restrict__ x, const float* __restrict__ y, con
         const int c = 4 * (lane + 64 * k);
         v[k] = *reinterpret_cast<const float4*>(x + off + c);
         if (y) {
-            const float4 t = *reinterpret_cast<const float4*>(y + off + c);
+            const float4 t = ld4(y + off + c);
             float4 g = make_float4(1.f, 1.f, 1.f, 1.f);
             if (ls) g = *reinterpret_cast<const float4*>(ls + c);
             v[k].x += g.x * t.x;
@@ -517,26 +554,25 @@ residual_ln_kernel(const float* __restrict__ x, const float* __restrict__ y, con
         const int c = 4 * (lane + 64 * k);
         if (x_out) *reinterpret_cast<float4*>(x_out + off + c) = v[k];
         const float4 g = *reinterpret_cast<const float4*>(w + c), bt = *reinterpret_cast<const float4*>(b + c);
-        *reinterpret_cast<float4*>(n_out + off + c) =
-            make_float4((v[k].x - mean) * rstd * g.x + bt.x, (v[k].y - mean) * rstd * g.y + bt.y,
-                        (v[k].z - mean) * rstd * g.z + bt.z, (v[k].w - mean) * rstd * g.w + bt.w);
+        st4(n_out + off + c, make_float4((v[k].x - mean) * rstd * g.x + bt.x, (v[k].y - mean) * rstd * g.y + bt.y,
+                                         (v[k].z - mean) * rstd * g.z + bt.z, (v[k].w - mean) * rstd * g.w + bt.w));
     }
 }
 
 }  // namespace gn
 }  // namespace tsplat
 
-extern "C" int tsplat_residual_ln_fwd(const float* x, const float* y, const float* ls, const float* ln_w,
-                                      const float* ln_b, float ln_eps, float* x_out, float* n_out, int32_t rows,
-                                      int32_t dim, void* stream_) {
+template <typename TY, typename TN>
+static int residual_ln_launch(const float* x, const TY* y, const float* ls, const float* ln_w, const float* ln_b,
+                              float ln_eps, float* x_out, TN* n_out, int32_t rows, int32_t dim, void* stream_) {
     using namespace tsplat::gn;
     if (!x || !ln_w || !ln_b || !n_out || rows <= 0 || (ls && !y)) return TSPLAT_EINVAL;
     if (y && !x_out) return TSPLAT_EINVAL;
     hipStream_t stream = (hipStream_t)stream_;
     const dim3 grid((rows + kThreads / kWave - 1) / (kThreads / kWave));
 #define TSPLAT_RLN(V)                                                                                   \
-    hipLaunchKernelGGL(residual_ln_kernel<V>, grid, dim3(kThreads), 0, stream, x, y, ls, ln_w, ln_b, x_out, \
-                       n_out, rows, ln_eps)
+    hipLaunchKernelGGL((residual_ln_kernel<V, TY, TN>), grid, dim3(kThreads), 0, stream, x, y, ls, ln_w, ln_b, \
+                       x_out, n_out, rows, ln_eps)
     switch (dim) {
         case 256: TSPLAT_RLN(1); break;
         case 512: TSPLAT_RLN(2); break;
@@ -547,4 +583,17 @@ extern "C" int tsplat_residual_ln_fwd(const float* x, const float* y, const floa
 #undef TSPLAT_RLN
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
+}
+
+extern "C" int tsplat_residual_ln_fwd(const float* x, const float* y, const float* ls, const float* ln_w,
+                                      const float* ln_b, float ln_eps, float* x_out, float* n_out, int32_t rows,
+                                      int32_t dim, void* stream_) {
+    return residual_ln_launch<float, float>(x, y, ls, ln_w, ln_b, ln_eps, x_out, n_out, rows, dim, stream_);
+}
+
+extern "C" int tsplat_residual_ln_bf16_fwd(const float* x, const void* y, const float* ls, const float* ln_w,
+                                           const float* ln_b, float ln_eps, float* x_out, void* n_out, int32_t rows,
+                                           int32_t dim, void* stream_) {
+    return residual_ln_launch<__bf16, __bf16>(x, (const __bf16*)y, ls, ln_w, ln_b, ln_eps, x_out, (__bf16*)n_out,
+                                              rows, dim, stream_);
 }

@@ -98,6 +98,7 @@ struct Params {
     int G, V, vps, H, W, M, deg, tiles_x, tiles_y, T, capacity;
     int diag;  // timing diagnostics only (TSPLAT_RASTER_DIAG; output is wrong when != 0)
     int count_sort;  // 1: counting sort for long tile lists (default); 0: bitonic only (A/B)
+    int view_rot;    // render: view v's workgroups take tiles rotated by v * view_rot (load balance)
 };
 
 __device__ __forceinline__ void get_rect(float px, float py, int r, int tx, int ty, int& x0,
@@ -665,7 +666,12 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     __shared__ __attribute__((aligned(16))) float s_rec[kTileThreads / kWave][kRecFields][kWave];
 
     const int v = blockIdx.y;
-    const int tile = xcd_remap(blockIdx.x, gridDim.x);
+    // Workgroup (tile, v) and (tile, v') share an XCD and a CU slot in dispatch order, and a
+    // tile's cost is similar across the target views of a scene (central tiles are the heavy
+    // ones), so without the per-view rotation every CU would get the same tile three times.
+    // Rotating by whole tile rows keeps each XCD's band of rows contiguous (L2 reuse of records).
+    int tile = xcd_remap(blockIdx.x, gridDim.x) + v * p.view_rot;
+    tile %= p.T;
     const uint64_t t_begin = p.diag == 5 ? __builtin_amdgcn_s_memtime() : 0;
     int d_entries = 0, d_chunks = 0;  // diag 5 only
     const int tx = tile % p.tiles_x, ty = tile / p.tiles_x;
@@ -885,6 +891,10 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
         p.diag = e ? atoi(e) : 0;
         const char* s = getenv("TSPLAT_RASTER_SORT");
         p.count_sort = !(s && !strcmp(s, "bitonic"));
+        // rotation per view: about T / 3 tiles, rounded to whole rows (TSPLAT_RASTER_ROT=0: off)
+        const char* r = getenv("TSPLAT_RASTER_ROT");
+        const int rows = (p.tiles_y + 1) / 3;
+        p.view_rot = (r && !strcmp(r, "0")) ? 0 : rows * p.tiles_x;
     }
     if ((size_t)p.T * 2 * sizeof(uint32_t) > 64 * 1024) return TSPLAT_EINVAL;  // LDS histogram
     Workspace ws = carve(workspace, p.G, p.V, p.T, p.capacity, nullptr);

@@ -242,12 +242,30 @@ def instance_norm(x, eps: float, act: str = "none", residual=None):
     return group_norm(x, c, w, b, eps, act, residual)
 
 
+_BF16_NORMS = os.environ.get("TSPLAT_BF16_NORMS", "1") != "0"  # A/B knob: bf16-I/O norm kernels (C3)
+
+
 def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None, pre_bias=None):
-    """act(GroupNorm(x + pre_bias)) [+ residual] over [N, C, *spatial] fp32 (see
-    tsplat_group_norm_fwd); pre_bias is the bias of a convolution that ran without it."""
+    """act(GroupNorm(x + pre_bias)) [+ residual] over [N, C, *spatial] (see tsplat_group_norm_fwd);
+    pre_bias is the bias of a convolution that ran without it. A bf16 x (bf16 dense mode) is read
+    and the result written in bf16 (tsplat_group_norm_bf16_fwd, fp32 statistics), else fp32."""
     lib = _lib.load()
     n, c = x.shape[:2]
     hw = x[0, 0].numel()
+    if x.dtype == torch.bfloat16 and x.is_cuda and _BF16_NORMS:
+        xb = x.contiguous()
+        res = residual.to(torch.bfloat16).contiguous() if residual is not None else None
+        if res is not None and res.shape != x.shape:
+            raise ValueError(f"residual {tuple(res.shape)} != input {tuple(x.shape)}")
+        y = torch.empty_like(xb)
+        ws = torch.empty(int(lib.tsplat_group_norm_workspace_bytes(n, c, hw, num_groups)), dtype=torch.uint8,
+                         device=x.device)
+        pb = _f32(pre_bias) if pre_bias is not None else None
+        rc = lib.tsplat_group_norm_bf16_fwd(_lib.ptr(xb), _lib.ptr(pb), _lib.ptr(_f32(weight)), _lib.ptr(_f32(bias)),
+                                            _lib.ptr(res) if res is not None else None, _lib.ptr(y), _lib.ptr(ws),
+                                            n, c, hw, num_groups, float(eps), _ACTS[act], _lib.stream_ptr(x.device))
+        _lib.check(rc, "tsplat_group_norm_bf16_fwd")
+        return y
     xf = _f32(x)
     res = _f32(residual) if residual is not None else None
     if res is not None and res.shape != x.shape:
@@ -349,13 +367,24 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     return out
 
 
-def residual_ln(x, y, ls, norm):
+def residual_ln(x, y, ls, norm, bf16_out: bool = False):
     """(x + ls * y, LayerNorm(x + ls * y)) in one pass (tsplat_residual_ln_fwd); y None: (x, LN(x)).
-    norm: an nn.LayerNorm (weight, bias, eps); ls: LayerScale gamma or None."""
+    norm: an nn.LayerNorm (weight, bias, eps); ls: LayerScale gamma or None. A bf16 y, or
+    bf16_out, selects the bf16 form (y read and LN written in bf16; x fp32 either way)."""
     lib = _lib.load()
     d = x.shape[-1]
     xf = _f32(x)
     rows = xf.numel() // d
+    if _BF16_NORMS and (bf16_out or (y is not None and y.dtype == torch.bfloat16)):
+        yb = y.to(torch.bfloat16).contiguous() if y is not None else None
+        x_out = torch.empty_like(xf) if y is not None else xf
+        n_out = torch.empty(xf.shape, dtype=torch.bfloat16, device=xf.device)
+        rc = lib.tsplat_residual_ln_bf16_fwd(_lib.ptr(xf), _lib.ptr(yb), _lib.ptr(_f32(ls)) if ls is not None else None,
+                                             _lib.ptr(_f32(norm.weight)), _lib.ptr(_f32(norm.bias)), float(norm.eps),
+                                             _lib.ptr(x_out) if y is not None else None, _lib.ptr(n_out), rows, d,
+                                             _lib.stream_ptr(x.device))
+        _lib.check(rc, "tsplat_residual_ln_bf16_fwd")
+        return x_out, n_out
     yf = _f32(y) if y is not None else None
     x_out = torch.empty_like(xf) if y is not None else xf
     n_out = torch.empty_like(xf)

@@ -166,8 +166,11 @@ class DinoVisionTransformer(nn.Module):
         return x + self.interpolate_pos_encoding(x, w, h).to(x.dtype)
 
     def _fused_ok(self, x) -> bool:
-        return (x.dtype == torch.float32 and not torch.is_autocast_enabled(x.device.type)
-                and x.shape[-1] in (256, 512, 768, 1024)
+        # fp32, or bf16 autocast (the linears then read the bf16 LayerNorm outputs directly)
+        autocast = torch.is_autocast_enabled(x.device.type)
+        ok_dtype = (x.dtype == torch.float32 and not autocast) or (
+            autocast and torch.get_autocast_dtype(x.device.type) == torch.bfloat16 and x.is_cuda)
+        return (ok_dtype and x.shape[-1] in (256, 512, 768, 1024)
                 and all(isinstance(m, (LayerScale, nn.Identity)) for b in self.blocks for m in (b.ls1, b.ls2)))
 
     def _blocks_fused(self, x, take, norm: bool):
@@ -175,17 +178,22 @@ class DinoVisionTransformer(nn.Module):
         kernel (kernels.residual_ln) instead of mul + add + LayerNorm launches; same math."""
         gamma = lambda m: m.gamma if isinstance(m, LayerScale) else None
         blocks = self.blocks
-        _, h = kernels.residual_ln(x, None, None, blocks[0].norm1)
+        # bf16 autocast: the residual stream stays fp32 (as x + ls * y promotes it under autocast)
+        # and the normalised rows are handed to the bf16 linears as bf16
+        bf = torch.is_autocast_enabled(x.device.type)
+        x = x.float()
+        _, h = kernels.residual_ln(x, None, None, blocks[0].norm1, bf16_out=bf)
         outputs = []
         for i, blk in enumerate(blocks):
-            x, h2 = kernels.residual_ln(x, blk.attn(h), gamma(blk.ls1), blk.norm2)
+            x, h2 = kernels.residual_ln(x, blk.attn(h), gamma(blk.ls1), blk.norm2, bf16_out=bf)
             last = i + 1 == len(blocks)
-            x, h = kernels.residual_ln(x, blk.mlp(h2), gamma(blk.ls2), self.norm if last else blocks[i + 1].norm1)
+            x, h = kernels.residual_ln(x, blk.mlp(h2), gamma(blk.ls2), self.norm if last else blocks[i + 1].norm1,
+                                       bf16_out=bf)
             if i in take:
                 if not norm:
                     outputs.append(x)
                 else:  # the last block's step already produced self.norm(x)
-                    outputs.append(h if last else kernels.residual_ln(x, None, None, self.norm)[1])
+                    outputs.append(h if last else kernels.residual_ln(x, None, None, self.norm, bf16_out=bf)[1])
         return outputs
 
     def get_intermediate_layers(self, x, n=4, reshape=False, return_class_token=False, norm=True):
