@@ -237,6 +237,13 @@ int tsplat_residual_ln_fwd(const float* x, const float* y, const float* ls, cons
 /* The same with a bf16 sub-layer output y and a bf16 n_out (bf16 dense mode: the linears read and
  * write bf16), the residual stream x / x_out and all statistics fp32 -- what autocast computes
  * (LayerNorm in fp32, cast to bf16 by the next linear). */
+/* LayerNorm over rows of 128 with an optional post-norm residual: out = [residual +] LN(y; ln_w,
+ * ln_b, ln_eps), y and out fp32 or bf16 (y_bf16 / out_bf16), residual fp32 or NULL. The multi-view
+ * transformer's norm1 / norm2 with `source + message` (reference multiview_transformer.py:327-407)
+ * and the UV encoder layer's norms (utils/encoder.py:131-209) in the bf16 dense mode. */
+int tsplat_layer_norm128_fwd(const void* y, int32_t y_bf16, const float* residual, const float* ln_w,
+                             const float* ln_b, float ln_eps, void* out, int32_t out_bf16, int32_t rows,
+                             void* stream);
 int tsplat_residual_ln_bf16_fwd(const float* x, const void* y, const float* ls, const float* ln_w, const float* ln_b,
                                 float ln_eps, float* x_out, void* n_out, int32_t rows, int32_t dim, void* stream);
 

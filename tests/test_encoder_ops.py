@@ -122,19 +122,23 @@ def test_uv_coarse_kernel(device, monkeypatch, hw, b, variant):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("hw,b,variant", [(16, 1, "table"), (24, 2, "table"), (64, 1, "table"), (16, 1, "direct"),
-                                          (24, 2, "direct")])
+                                          (24, 2, "direct"), (24, 2, "table_bf16"), (64, 1, "table_bf16")])
 def test_uv_cross_kernel(device, hw, b, variant):
     """Both forms of the fine cross correlation: the correlation-table gather (default) and the
-    direct feature-row sampling kernel."""
+    direct feature-row sampling kernel; table_bf16: a bf16 value (bf16 dense mode, the value_proj
+    output) takes the split-bf16 table GEMM (key = hi + lo bf16 halves, fp32 accumulate), checked
+    against the fp32 restatement on the same bf16-exact values."""
     from transplat_amd import kernels as K
 
-    op = K.uv_cross if variant == "table" else K.uv_cross_direct
+    op = K.uv_cross if variant != "direct" else K.uv_cross_direct
     intr, pose, disp = _cams(b, hw)
     value = seeded((b, 2, hw * hw, 128), 41)
+    if variant == "table_bf16":
+        value = value.bfloat16()
     key = seeded((b, 2, hw * hw, 128), 42)
     offsets = seeded((b * 2, hw * hw, 128 * 4 * 2), 43, 2.0)
     logits = seeded((b * 2, hw * hw, 128 * 4), 44)
-    ref = E.uv_cross(value, key, intr, pose, disp, offsets, logits, hw, hw)
+    ref = E.uv_cross(value.float(), key, intr, pose, disp, offsets, logits, hw, hw)
     out = op(*(t.to(device) for t in (value, key, intr, pose, disp, offsets, logits)), hw, hw).cpu()
     assert (out - ref).abs().max().item() < 1e-4
 
@@ -647,3 +651,28 @@ def test_resize_bilinear_nhwc_kernel(device, shape, size):
     assert out.is_contiguous(memory_format=torch.channels_last)
     # fp32 source-coordinate rounding (see the upsample test): 1e-5 of the map's scale
     assert (out.cpu() - ref).abs().max().item() < 1e-5 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("y_bf16,out_bf16,res", [(False, False, False), (False, False, True), (True, False, True),
+                                                 (True, True, False), (False, True, False)])
+def test_layer_norm128_kernel(device, y_bf16, out_bf16, res):
+    """[residual +] LayerNorm over 128-wide rows (the bf16-mode MVT / UV norms) vs torch on CPU, on the
+    same (bf16-rounded where bf16) inputs; rows not a multiple of the 8 rows per workgroup."""
+    from transplat_amd import kernels as K
+
+    norm = torch.nn.LayerNorm(128)
+    with torch.no_grad():
+        norm.weight.copy_(seeded((128,), 86) * 0.1 + 1.0)
+        norm.bias.copy_(seeded((128,), 87) * 0.1)
+    y = seeded((3, 1001, 128), 88) * 2.0 + 0.5
+    if y_bf16:
+        y = y.bfloat16()
+    r = seeded((3, 1001, 128), 89) if res else None
+    with torch.no_grad():
+        ref = norm(y.float()) + (r if res else 0.0)
+    out = K.layer_norm128(y.to(device), norm.to(device), residual=r.to(device) if res else None,
+                          out_dtype=torch.bfloat16 if out_bf16 else torch.float32)
+    assert out.dtype == (torch.bfloat16 if out_bf16 else torch.float32)
+    tol = 8e-3 * ref.abs().max().item() if out_bf16 else 2e-5 * max(1.0, ref.abs().max().item())
+    assert (out.float().cpu() - ref).abs().max().item() < tol

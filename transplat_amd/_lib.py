@@ -55,6 +55,7 @@ SIGNATURES = {
     "tsplat_win_attn_bf16_fwd": (ctypes.c_int, [_P] * 5 + [_I32] * 7 + [_P]),
     "tsplat_group_norm_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, ctypes.c_int64, _I32]),
     "tsplat_group_norm_fwd": (ctypes.c_int, [_P] * 7 + [_I32, _I32, ctypes.c_int64, _I32, ctypes.c_float, _I32, _P]),
+    "tsplat_layer_norm128_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, ctypes.c_float, _P, _I32, _I32, _P]),
     "tsplat_group_norm_bf16_fwd": (ctypes.c_int, [_P] * 7 + [_I32, _I32, ctypes.c_int64, _I32, ctypes.c_float, _I32,
                                                             _P]),
     "tsplat_sh_rotation_fwd": (ctypes.c_int, [_P] * 3 + [_I32] * 2 + [_P]),

@@ -597,3 +597,66 @@ extern "C" int tsplat_residual_ln_bf16_fwd(const float* x, const void* y, const 
     return residual_ln_launch<__bf16, __bf16>(x, (const __bf16*)y, ls, ln_w, ln_b, ln_eps, x_out, (__bf16*)n_out,
                                               rows, dim, stream_);
 }
+
+// ---------------------------------------------------------------------------------------------
+// LayerNorm over rows of 128 (the multi-view transformer's and the UV transformer's d_model) with
+// an optional post-norm residual: out = [res +] LN(y). 32 lanes x float4 per row (two rows per
+// wave), two-pass statistics in fp32; y and out in fp32 or bf16, res fp32. For the bf16 dense mode
+// (config C3), where these norms otherwise run PyTorch's LayerNorm (65 us per call at batch 8 on
+// 128-wide rows) between autocast casts (reference multiview_transformer.py:327-407 norm1 / norm2,
+// utils/encoder.py:131-209 norms).
+namespace tsplat {
+namespace gn {
+
+template <typename TY, typename TO>
+__global__ void __launch_bounds__(kThreads)
+ln128_kernel(const TY* __restrict__ y, const float* __restrict__ res, const float* __restrict__ w,
+             const float* __restrict__ b, TO* __restrict__ out, int rows, float eps) {
+    const int row = (blockIdx.x * kThreads + threadIdx.x) >> 5;
+    const int l = threadIdx.x & 31;
+    if (row >= rows) return;  // whole 32-lane halves leave together; the shuffles stay in a half
+    const size_t off = (size_t)row * 128 + 4 * l;
+    const float4 v = ld4(y + off);
+    float s = (v.x + v.y) + (v.z + v.w);
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 32);
+    const float mean = s * (1.0f / 128.0f);
+    const float a = v.x - mean, bb = v.y - mean, c = v.z - mean, d = v.w - mean;
+    float q = (a * a + bb * bb) + (c * c + d * d);
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 32);
+    const float rstd = rsqrtf(q * (1.0f / 128.0f) + eps);
+    const float4 g = *reinterpret_cast<const float4*>(w + 4 * l), bt = *reinterpret_cast<const float4*>(b + 4 * l);
+    float4 n = make_float4(a * rstd * g.x + bt.x, bb * rstd * g.y + bt.y, c * rstd * g.z + bt.z, d * rstd * g.w + bt.w);
+    if (res) {
+        const float4 r = *reinterpret_cast<const float4*>(res + off);
+        n = make_float4(r.x + n.x, r.y + n.y, r.z + n.z, r.w + n.w);
+    }
+    st4(out + off, n);
+}
+
+}  // namespace gn
+}  // namespace tsplat
+
+extern "C" int tsplat_layer_norm128_fwd(const void* y, int32_t y_bf16, const float* residual, const float* ln_w,
+                                        const float* ln_b, float ln_eps, void* out, int32_t out_bf16, int32_t rows,
+                                        void* stream_) {
+    using namespace tsplat::gn;
+    if (!y || !ln_w || !ln_b || !out || rows <= 0) return TSPLAT_EINVAL;
+    const uintptr_t al = y_bf16 ? 8 : 16;
+    if ((uintptr_t)y % al || (uintptr_t)out % (out_bf16 ? 8 : 16) || (residual && (uintptr_t)residual % 16) ||
+        (uintptr_t)ln_w % 16 || (uintptr_t)ln_b % 16)
+        return TSPLAT_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    const dim3 grid((unsigned)(((int64_t)rows * 32 + kThreads - 1) / kThreads));
+#define TSPLAT_LN128(TY, TO)                                                                                 \
+    hipLaunchKernelGGL((ln128_kernel<TY, TO>), grid, dim3(kThreads), 0, stream, (const TY*)y, residual, ln_w, ln_b, \
+                       (TO*)out, rows, ln_eps)
+    if (y_bf16 && out_bf16) TSPLAT_LN128(__bf16, __bf16);
+    else if (y_bf16) TSPLAT_LN128(__bf16, float);
+    else if (out_bf16) TSPLAT_LN128(float, __bf16);
+    else TSPLAT_LN128(float, float);
+#undef TSPLAT_LN128
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

@@ -97,13 +97,28 @@ def uv_cross(value, key, intr, pose, disp, offsets, logits, h: int, w: int):
     b, _, hw, c = value.shape
     d = disp.shape[1]
     p = logits.shape[-1] // d
-    value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
+    if value.dtype == torch.bfloat16 and value.is_cuda and _UV_TABLE_BF16:
+        # bf16 dense mode: value is a bf16 linear output, so value^T is exact in bf16 and the table
+        # G = key value^T can run on bf16 MFMA with fp32 accumulation and output: key split as
+        # key_hi + key_lo (two bf16 halves, residual error ~2^-17 relative) and both halves taken
+        # in ONE GEMM with K = 2C ([key_hi | key_lo] x [value | value]^T)
+        kf = _f32(key).reshape(b * 2, hw, c)
+        k_hi = kf.to(torch.bfloat16)
+        k2 = torch.cat((k_hi, (kf - k_hi.float()).to(torch.bfloat16)), dim=-1)
+        vb = torch.flip(value, dims=[1]).reshape(b * 2, hw, c)
+        with torch.autocast("cuda", enabled=False):
+            table = torch.bmm(k2, torch.cat((vb, vb), dim=-1).transpose(1, 2), out_dtype=torch.float32)
+        value = None
+        key, offsets, logits, disp = map(_f32, (key, offsets, logits, disp))
+    else:
+        value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
+        with torch.autocast("cuda", enabled=False):
+            table = torch.bmm(key.reshape(b * 2, hw, c),
+                              torch.flip(value, dims=[1]).reshape(b * 2, hw, c).transpose(1, 2))
     cams = pack_cameras(intr, pose)
-    with torch.autocast("cuda", enabled=False):
-        table = torch.bmm(key.reshape(b * 2, hw, c), torch.flip(value, dims=[1]).reshape(b * 2, hw, c).transpose(1, 2))
-    out = torch.empty((b * 2, hw, d), dtype=torch.float32, device=value.device)
+    out = torch.empty((b * 2, hw, d), dtype=torch.float32, device=table.device)
     rc = lib.tsplat_uv_cross_table_fwd(_lib.ptr(table), _lib.ptr(cams), _lib.ptr(disp), _lib.ptr(offsets),
-                                       _lib.ptr(logits), _lib.ptr(out), b, h, w, c, d, p, _lib.stream_ptr(value.device))
+                                       _lib.ptr(logits), _lib.ptr(out), b, h, w, c, d, p, _lib.stream_ptr(table.device))
     _lib.check(rc, "tsplat_uv_cross_table_fwd")
     return out
 
@@ -243,6 +258,8 @@ def instance_norm(x, eps: float, act: str = "none", residual=None):
 
 
 _BF16_NORMS = os.environ.get("TSPLAT_BF16_NORMS", "1") != "0"  # A/B knob: bf16-I/O norm kernels (C3)
+BF16_NORMS = _BF16_NORMS
+_UV_TABLE_BF16 = os.environ.get("TSPLAT_UV_TABLE_BF16", "1") != "0"  # A/B knob: split-bf16 table GEMM (C3)
 
 
 def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None, pre_bias=None):
@@ -394,6 +411,26 @@ def residual_ln(x, y, ls, norm, bf16_out: bool = False):
                                     _lib.stream_ptr(x.device))
     _lib.check(rc, "tsplat_residual_ln_fwd")
     return x_out, n_out
+
+
+def layer_norm128(y, norm, residual=None, out_dtype=None):
+    """[residual +] LayerNorm(y) over rows of 128 (tsplat_layer_norm128_fwd); y fp32 or bf16,
+    residual fp32 (or None), output in out_dtype (default y's dtype)."""
+    lib = _lib.load()
+    if y.shape[-1] != 128:
+        raise ValueError("layer_norm128: last dim must be 128")
+    yc = y.contiguous() if y.dtype == torch.bfloat16 else _f32(y)
+    out_dtype = out_dtype or yc.dtype
+    res = _f32(residual) if residual is not None else None
+    if res is not None and res.shape != y.shape:
+        raise ValueError(f"residual {tuple(res.shape)} != {tuple(y.shape)}")
+    out = torch.empty(y.shape, dtype=out_dtype, device=y.device)
+    rc = lib.tsplat_layer_norm128_fwd(_lib.ptr(yc), int(yc.dtype == torch.bfloat16), _lib.ptr(res),
+                                      _lib.ptr(_f32(norm.weight)), _lib.ptr(_f32(norm.bias)), float(norm.eps),
+                                      _lib.ptr(out), int(out_dtype == torch.bfloat16), yc.numel() // 128,
+                                      _lib.stream_ptr(y.device))
+    _lib.check(rc, "tsplat_layer_norm128_fwd")
+    return out
 
 
 def depth_softmax(logits, disp):

@@ -42,6 +42,15 @@ def _resize(x, modifier: dict, align_corners: bool):
             sf = modifier["scale_factor"]
             size = (int(x.shape[-2] * sf), int(x.shape[-1] * sf))
         return kernels.resize_bilinear_nhwc(x, size)
+    if align_corners and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous():
+        # NCHW fp32 (the head's final resize in bf16 mode): PyTorch's generic NCHW kernel took
+        # 0.87 ms per call at C3's batch 8
+        if "size" in modifier:
+            size = modifier["size"]
+        else:
+            sf = modifier["scale_factor"]
+            size = (int(x.shape[-2] * sf), int(x.shape[-1] * sf))
+        return kernels.interpolate_bilinear_ac(x, size)
     return F.interpolate(x, **modifier, mode="bilinear", align_corners=align_corners)
 
 

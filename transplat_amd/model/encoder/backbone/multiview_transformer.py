@@ -83,10 +83,23 @@ class TransformerLayer(nn.Module):
         key = self.k_proj(target)
         value = self.v_proj(target)
         message = kernels.window_attention(query, key, value, height, width, attn_num_splits, self.with_shift)
+        if self._ln128_ok(source):
+            # bf16 dense mode: each LayerNorm (+ the `source + message` residual) as one kernel on
+            # the bf16 linear output (autocast would run PyTorch's LayerNorm in fp32 between casts)
+            if self.no_ffn:
+                return kernels.layer_norm128(self.merge(message), self.norm1, residual=source,
+                                             out_dtype=torch.float32)
+            message = kernels.layer_norm128(self.merge(message), self.norm1, out_dtype=torch.bfloat16)
+            hidden = self.mlp(torch.cat([source.to(torch.bfloat16), message], dim=-1))
+            return kernels.layer_norm128(hidden, self.norm2, residual=source, out_dtype=torch.float32)
         message = self.norm1(self.merge(message))
         if not self.no_ffn:
             message = self.norm2(self.mlp(torch.cat([source, message], dim=-1)))
         return source + message
+
+    def _ln128_ok(self, source) -> bool:
+        return (self.dim == 128 and source.is_cuda and torch.is_autocast_enabled(source.device.type)
+                and torch.get_autocast_dtype(source.device.type) == torch.bfloat16 and kernels.BF16_NORMS)
 
 
 class TransformerBlock(nn.Module):

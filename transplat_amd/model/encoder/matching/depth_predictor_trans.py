@@ -24,9 +24,10 @@ def _conv_upsample_gelu(seq: nn.Sequential, x):
     then interpolation + bias + GELU in one pass over the full-resolution map
     (kernels.upsample_bilinear_act) instead of bias add, interpolation and GELU kernels."""
     conv, up, act = seq
-    if (x.dtype != torch.float32 or torch.is_autocast_enabled("cuda") or not isinstance(act, nn.GELU)
-            or act.approximate != "none" or up.mode != "bilinear" or not up.align_corners
-            or float(up.scale_factor) != int(up.scale_factor)):
+    # (under bf16 autocast the convolution runs in bf16 and the interpolation + GELU in fp32, which
+    # is what autocast does with this Sequential: upsample_bilinear2d is on its fp32 list)
+    if (not isinstance(act, nn.GELU) or act.approximate != "none" or up.mode != "bilinear"
+            or not up.align_corners or float(up.scale_factor) != int(up.scale_factor)):
         return seq(x)
     y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     return kernels.upsample_bilinear_act(y, int(up.scale_factor), conv.bias, "gelu")

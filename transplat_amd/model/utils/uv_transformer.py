@@ -169,9 +169,17 @@ class UVTransformerEncoderLayer(nn.Module):
             return self.attentions[0](query, key_cl, cameras, bev_h, bev_w)
         if self._fused_ok(query):
             return self._fine_fused(query, key_cl, bev_pos, ref_2d, cameras, bev_h, bev_w)
-        query = self.norms[0](self.attentions[0](query, query, bev_pos, ref_2d, bev_h, bev_w))
-        query = self.norms[1](self.attentions[1](query, key_cl, key_cl, cameras, bev_h, bev_w))
-        return self.norms[2](self.ffns[0](query, None))
+        if self._ln128_ok(query):  # bf16 dense mode: the post-norms as kernels (fp32 in and out)
+            ln = lambda i, t: kernels.layer_norm128(t, self.norms[i], out_dtype=torch.float32)
+        else:
+            ln = lambda i, t: self.norms[i](t)
+        query = ln(0, self.attentions[0](query, query, bev_pos, ref_2d, bev_h, bev_w))
+        query = ln(1, self.attentions[1](query, key_cl, key_cl, cameras, bev_h, bev_w))
+        return ln(2, self.ffns[0](query, None))
+
+    def _ln128_ok(self, query) -> bool:
+        return (self.embed_dims == 128 and query.is_cuda and torch.is_autocast_enabled(query.device.type)
+                and torch.get_autocast_dtype(query.device.type) == torch.bfloat16 and kernels.BF16_NORMS)
 
     def _fused_ok(self, query) -> bool:
         ffn = self.ffns[0]
