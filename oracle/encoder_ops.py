@@ -396,11 +396,13 @@ def depth_softmax(logits, disp):
     return coarse, torch.max(pdf, dim=1, keepdim=True)[0]
 
 
-def residual_ln(x, y, ls, norm):
-    """DINOv2 pre-norm residual step: x' = x + ls * y (LayerScale), LayerNorm(x') with the next norm."""
+def residual_ln(x, y, ls, norm, bf16_out: bool = False):
+    """DINOv2 pre-norm residual step: x' = x + ls * y (LayerScale), LayerNorm(x') with the next norm
+    (rounded to bf16 when `bf16_out`, as the kernel's bf16 output)."""
     if y is not None:
-        x = x + (ls * y if ls is not None else y)
-    return x, torch.nn.functional.layer_norm(x, (x.shape[-1],), norm.weight, norm.bias, norm.eps)
+        x = x + (ls * y.float() if ls is not None else y.float())
+    h = torch.nn.functional.layer_norm(x, (x.shape[-1],), norm.weight, norm.bias, norm.eps)
+    return x, h.to(torch.bfloat16) if bf16_out else h
 
 
 def instance_norm(x, eps: float, act: str = "none", residual=None):

@@ -173,7 +173,7 @@ class DinoVisionTransformer(nn.Module):
         return (ok_dtype and x.shape[-1] in (256, 512, 768, 1024)
                 and all(isinstance(m, (LayerScale, nn.Identity)) for b in self.blocks for m in (b.ls1, b.ls2)))
 
-    def _blocks_fused(self, x, take, norm: bool):
+    def _blocks_fused(self, x, take, norm: bool, on_output=None):
         """The block chain with every pre-norm residual step x = x + ls(y), h = norm_next(x) as ONE
         kernel (kernels.residual_ln) instead of mul + add + LayerNorm launches; same math."""
         gamma = lambda m: m.gamma if isinstance(m, LayerScale) else None
@@ -194,21 +194,27 @@ class DinoVisionTransformer(nn.Module):
                     outputs.append(x)
                 else:  # the last block's step already produced self.norm(x)
                     outputs.append(h if last else kernels.residual_ln(x, None, None, self.norm, bf16_out=bf)[1])
+                if on_output is not None:
+                    on_output(len(outputs) - 1, outputs[-1])
         return outputs
 
-    def get_intermediate_layers(self, x, n=4, reshape=False, return_class_token=False, norm=True):
+    def get_intermediate_layers(self, x, n=4, reshape=False, return_class_token=False, norm=True,
+                                on_output=None):
+        """`on_output(k, tokens)` (not in the reference) is called as soon as the k-th taken layer's
+        normed tokens [B, 1 + N, C] exist, so a consumer can start on them while the later blocks
+        run (DepthAnythingV2.forward forks the DPT reassemble branches this way)."""
         x = self.prepare_tokens(x)
         take = range(len(self.blocks) - n, len(self.blocks)) if isinstance(n, int) else n
         if self._fused_ok(x):
-            outputs = self._blocks_fused(x, take, norm)
+            outputs = self._blocks_fused(x, take, norm, on_output)
         else:
             outputs = []
             for i, blk in enumerate(self.blocks):
                 x = blk(x)
                 if i in take:
-                    outputs.append(x)
-            if norm:
-                outputs = [self.norm(o) for o in outputs]
+                    outputs.append(self.norm(x) if norm else x)
+                    if on_output is not None:
+                        on_output(len(outputs) - 1, outputs[-1])
         class_tokens = [o[:, 0] for o in outputs]
         outputs = [o[:, 1:] for o in outputs]
         if return_class_token:

@@ -11,7 +11,7 @@ import torch.nn.functional as F
 from torch import nn
 
 
-from ... import kernels
+from ... import kernels, streams
 from .dinov2 import DINOv2
 
 # The token maps enter the DPT as channels-last views (permute of [B, N, C]); the whole conv chain
@@ -27,6 +27,9 @@ _DPT_CL_WEIGHTS = os.environ.get("TSPLAT_DPT_CL_WEIGHTS", "1") != "0"
 _DPT_DIRECT = os.environ.get("TSPLAT_DPT_DIRECT", "0")
 # conv epilogues (bias + ReLU, bias + residuals) fused after the MIOpen convolutions; "0" = A/B off
 _DPT_EPI = os.environ.get("TSPLAT_DPT_EPI", "1") != "0"
+# reassemble branches of ViT layers 1-3 forked onto a side stream while the later blocks run
+# (needs streams.enabled); "0" = A/B off
+_DPT_HOIST = os.environ.get("TSPLAT_DPT_HOIST", "1") != "0"
 
 
 def _resize(x, modifier: dict, align_corners: bool):
@@ -160,18 +163,27 @@ class DPTHead(nn.Module):
                 m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
         self._cl_done = True
 
-    def forward(self, out_features, patch_h, patch_w):
-        if _DPT_CL_WEIGHTS and not getattr(self, "_cl_done", False) and out_features[0][0].is_cuda:
+    def prepare(self, is_cuda: bool):
+        if _DPT_CL_WEIGHTS and not getattr(self, "_cl_done", False) and is_cuda:
             self._channels_last_weights()
-        out = []
+
+    def reassemble(self, i, x, patch_h, patch_w):
+        """Branch i of the head up to layer{i+1}_rn (reference dpt.py:121-140): tokens [B, N, C] ->
+        project (1x1) -> resize (convT / identity / strided conv) -> 3x3 layer_rn."""
+        x = x.permute(0, 2, 1).reshape((x.shape[0], x.shape[-1], patch_h, patch_w))
+        x = self.resize_layers[i](self.projects[i](x))
+        return getattr(self.scratch, f"layer{i + 1}_rn")(x)
+
+    def forward(self, out_features, patch_h, patch_w, rn=None):
+        """`rn` (not in the reference): branch outputs already computed by `reassemble` (None
+        entries are computed here)."""
+        self.prepare(out_features[0][0].is_cuda)
+        rn = list(rn) if rn is not None else [None] * len(out_features)
         for i, x in enumerate(out_features):
-            x = x[0]
-            x = x.permute(0, 2, 1).reshape((x.shape[0], x.shape[-1], patch_h, patch_w))
-            out.append(self.resize_layers[i](self.projects[i](x)))
-        layer_1, layer_2, layer_3, layer_4 = out
+            if rn[i] is None:
+                rn[i] = self.reassemble(i, x[0], patch_h, patch_w)
+        layer_1_rn, layer_2_rn, layer_3_rn, layer_4_rn = rn
         s = self.scratch
-        layer_1_rn, layer_2_rn = s.layer1_rn(layer_1), s.layer2_rn(layer_2)
-        layer_3_rn, layer_4_rn = s.layer3_rn(layer_3), s.layer4_rn(layer_4)
         path_4 = s.refinenet4(layer_4_rn, size=layer_3_rn.shape[2:])
         path_3 = s.refinenet3(path_4, layer_3_rn, size=layer_2_rn.shape[2:])
         path_2 = s.refinenet2(path_3, layer_2_rn, size=layer_1_rn.shape[2:])
@@ -200,7 +212,20 @@ class DepthAnythingV2(nn.Module):
 
     def forward(self, x):
         patch_h, patch_w = x.shape[-2] // 14, x.shape[-1] // 14
+        head = self.depth_head
+        head.prepare(x.is_cuda)
+        n_take = len(self.intermediate_layer_idx[self.encoder])
+        pending = {}
+
+        def on_output(k, tokens):
+            # branches 1-3 start on a side stream as soon as their ViT layer exists and overlap the
+            # remaining blocks; the last one has nothing left to overlap and runs inline
+            if k + 1 < n_take and _DPT_HOIST and streams.enabled(tokens.device):
+                pending[k] = streams.fork(tokens.device, head.reassemble, k, tokens[:, 1:], patch_h, patch_w,
+                                          slot=1)
+
         features = self.pretrained.get_intermediate_layers(x, self.intermediate_layer_idx[self.encoder],
-                                                           return_class_token=True)
-        depth, out_features = self.depth_head(features, patch_h, patch_w)
+                                                           return_class_token=True, on_output=on_output)
+        rn = [streams.join(pending[k]) if k in pending else None for k in range(n_take)]
+        depth, out_features = head(features, patch_h, patch_w, rn=rn)
         return F.relu(depth).squeeze(1), out_features

@@ -156,13 +156,15 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
                                        return_cnn_features=True, img2world=img2world)
             return tf.float(), cf.float()
 
-        # Stages 2 and 3 read only the context images: on a GPU, Depth-Anything runs on a side
-        # stream concurrently with the backbone (transplat_amd/streams.py; captured into the step's
-        # hipGraph as two branches). Both are chains of small launches (DINOv2's M = 650 GEMMs, the
-        # MVT's 256-workgroup kernels) that leave CUs idle on their own.
-        da = streams.fork(device, depth_anything)
-        trans_features, cnn_features = backbone()
-        da_depth, out_feature = streams.join(da)
+        # Stages 2 and 3 read only the context images: on a GPU, the backbone runs on a side stream
+        # concurrently with Depth-Anything (transplat_amd/streams.py; captured into the step's
+        # hipGraph as parallel branches). Both are chains of small launches (DINOv2's M = 650 GEMMs,
+        # the MVT's 256-workgroup kernels) that leave CUs idle on their own. Depth-Anything stays on
+        # the current stream because it forks again (its DPT reassemble branches, dpt.py): a fork
+        # from a side stream inside hipGraph capture crashed HIP's capture_end.
+        bb = streams.fork(device, backbone)
+        da_depth, out_feature = depth_anything()
+        trans_features, cnn_features = streams.join(bb)
         dino_feature = out_feature.view(b, v, *out_feature.shape[1:])
 
         extra_info = {"images": rearrange(context["image"], "b v c h w -> (v b) c h w"), "scene_names": scene_names}

@@ -48,6 +48,10 @@ def conv(conv: nn.Module, x, x2=None, upsample: bool = False, bias: bool = True)
     convolutions of the low-resolution levels run as one direct fp32 MFMA kernel that reads the
     concat / upsample in place (kernels.conv2d_direct); the rest materialise them and run MIOpen."""
     b = conv.bias if bias else None
+    extra = (x2,) if x2 is not None else ()
+    if (isinstance(conv, nn.Conv2d) and not upsample
+            and kernels.conv3x3_bf16_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra)):
+        return kernels.conv3x3_bf16(x, conv.weight, b, extra=extra)  # bf16 autocast (C3), concat read in place
     if _direct(conv, x, x2, upsample):
         return kernels.conv2d_direct(x, conv.weight, b, conv.stride[0], x2=x2, upsample=upsample)
     if (isinstance(conv, nn.Conv1d) and x2 is None and not upsample and conv.kernel_size == (1,)
@@ -55,7 +59,6 @@ def conv(conv: nn.Module, x, x2=None, upsample: bool = False, bias: bool = True)
             and kernels.conv2d_direct_ok(x.unsqueeze(-1), conv.weight)):
         # the attention blocks' qkv / proj_out: a 1x1 over [n, c, t] viewed as [n, c, t, 1]
         return kernels.conv2d_direct(x.unsqueeze(-1), conv.weight, b).squeeze(-1)
-    extra = (x2,) if x2 is not None else ()
     if (isinstance(conv, nn.Conv2d) and not upsample
             and kernels.conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra)):
         return kernels.conv3x3_wino(x, conv.weight, b, extra=extra)  # the skip concat read in place
