@@ -296,67 +296,78 @@ def test_conv3x3_wino_ok_rejects_wide_input(device):
     assert (y - ref).abs().max().item() <= 1e-3 * ref.abs().max().item()
 
 
-# ---------------------------------------------------------------- bf16 implicit-GEMM 3x3 (config C3)
+# ---------------------------------------------------------------- bf16 implicit-GEMM 3x3 / 1x1 (config C3)
 # Reference: F.conv2d under bf16 autocast = conv of bf16-rounded sources / weights / bias with fp32
-# accumulation, rounded to bf16. The check below is against the UNROUNDED fp32 result of those
-# bf16-rounded operands: the kernel's only differences are the summation order (<= 1e-5 relative
-# over <= 2304 exact products) and the final bf16 rounding (<= 2^-9 relative), so
+# accumulation, rounded to bf16. The check below is against the UNROUNDED float64 result of those
+# bf16-rounded operands: the kernel's only differences are the fp32 summation order (<= 1e-5
+# relative over <= 2304 exact products) and the final bf16 rounding (<= 2^-9 relative), so
 # |y - ref| <= 2^-8 |ref| + 1e-4 max|ref| (tolerance written here, not a PSNR).
 BF16_CASES = [
-    # n, chans (sources), h, w, cout, bias, act, src dtype
-    (2, (32,), 64, 64, 32, False, "none", "bf16"),        # U-Net 32-ch level (CT = 1, TW = 64)
-    (2, (128,), 32, 32, 128, False, "none", "bf16"),      # 128-ch level (CT = 2, TW = 32)
-    (2, (128, 128), 16, 16, 128, False, "none", "bf16"),  # output block on cat([h, skip]) (TW = 16)
-    (2, (64, 32), 16, 16, 32, True, "silu", "f32"),       # fp32 sources rounded on load, 2 sources
-    (1, (96,), 24, 24, 96, True, "gelu", "f32"),          # co % 64 != 0, W = 24 (partial 16-col tiles)
-    (1, (64,), 128, 128, 64, True, "relu", "bf16"),       # depth-predictor head shape (scaled down)
-    (3, (8,), 9, 8, 40, True, "none", "bf16"),            # TW = 8, H not a multiple of TH, tiny cin
-    (1, (40, 16, 8), 20, 72, 33, True, "gelu", "f32"),    # 3 sources, ci = 64 + pad, W = 72 (2 x-tiles)
+    # n, chans (sources), h, w (of the convolved map), cout, k, upsample, bias, act, src dtype
+    (2, (32,), 64, 64, 32, 3, False, False, "none", "bf16"),        # U-Net 32-ch level (CT = 1, TW = 64)
+    (2, (128,), 32, 32, 128, 3, False, False, "none", "bf16"),      # 128-ch level (CT = 2, TW = 32)
+    (2, (128, 128), 16, 16, 128, 3, False, False, "none", "bf16"),  # output block on cat([h, skip]) (TW = 16)
+    (2, (64, 32), 16, 16, 32, 3, False, True, "silu", "f32"),       # fp32 sources rounded on load, 2 sources
+    (1, (96,), 24, 24, 96, 3, False, True, "gelu", "f32"),          # co % 64 != 0, W = 24 (partial 16-col tiles)
+    (1, (64,), 128, 128, 64, 3, False, True, "relu", "bf16"),       # depth-predictor head shape (scaled down)
+    (3, (8,), 9, 8, 40, 3, False, True, "none", "bf16"),            # TW = 8, H not a multiple of TH, tiny cin
+    (1, (40, 16, 8), 20, 72, 33, 3, False, True, "gelu", "f32"),    # 3 sources, ci = 64 + pad, W = 72 (2 x-tiles)
+    (2, (256,), 32, 32, 128, 1, False, True, "none", "bf16"),       # ResBlock 1x1 skip
+    (2, (128, 64), 16, 16, 96, 1, False, True, "none", "f32"),      # 1x1 on a concat, co % 64 != 0
+    (2, (128,), 32, 32, 128, 3, True, True, "none", "bf16"),        # Upsample: nearest 2x (16^2 -> 32^2) + 3x3
+    (1, (32,), 64, 16, 32, 3, True, True, "none", "f32"),           # upsample, fp32 source, TW = 16
 ]
 
 
-def _bf16_ref(srcs, w, b, act):
+def _bf16_ref(srcs, w, b, act, up):
     x = torch.cat([s.double().bfloat16().double() if s.dtype == torch.float32 else s.double() for s in srcs], 1)
+    if up:
+        x = torch.nn.functional.interpolate(x, scale_factor=2, mode="nearest")
     wr = w.bfloat16().double()
     br = b.bfloat16().double() if b is not None else None
-    y = torch.nn.functional.conv2d(x, wr, br, padding=1)
+    y = torch.nn.functional.conv2d(x, wr, br, padding=w.shape[-1] // 2)
     return {"none": y, "relu": torch.relu(y), "silu": torch.nn.functional.silu(y),
             "gelu": torch.nn.functional.gelu(y)}[act]
 
 
-def test_conv3x3_bf16_weight_packing_layout():
-    """Host-side packing (kernels.conv3x3_bf16_pack_weight) against the A-operand map the kernel
-    reads: lane c + 32 h of block b, chunk k, tap holds w[32 b + c][16 k + 8 h + j][tap], zero pad."""
+@pytest.mark.parametrize("k", [3, 1])
+def test_conv_bf16_weight_packing_layout(k):
+    """Host-side packing (kernels.conv_bf16_pack_weight) against the A-operand map the kernel
+    reads: lane c + 32 h of block b, chunk j, tap holds w[32 b + c][16 j + 8 h + e][tap], zero pad."""
     from transplat_amd import kernels as K
-
-    co, ci = 40, 24
-    w = seeded((co, ci, 3, 3), 5)
-    p = K.conv3x3_bf16_pack_weight(w).view(2, 2, 9, 64, 8)
-    wb = w.bfloat16().reshape(co, ci, 9)
-    for b, k, tap, lane, j in [(0, 0, 0, 0, 0), (0, 1, 4, 37, 3), (1, 0, 8, 7, 7), (1, 1, 2, 63, 5), (0, 0, 5, 40, 6)]:
-        c, h = lane % 32, lane // 32
-        o, i = 32 * b + c, 16 * k + 8 * h + j
-        want = wb[o, i, tap] if (o < co and i < ci) else torch.zeros((), dtype=torch.bfloat16)
-        assert p[b, k, tap, lane, j] == want, (b, k, tap, lane, j)
     import transplat_amd._lib as L
-    assert K.conv3x3_bf16_pack_weight(w).numel() * 2 == 2 * 2 * 9 * 64 * 16  # = the C-ABI's byte count formula
-    assert "tsplat_conv3x3_bf16_weight_bytes" in L.SIGNATURES
+
+    co, ci, taps = 40, 24, k * k
+    w = seeded((co, ci, k, k), 5)
+    p = K.conv_bf16_pack_weight(w).view(2, 2, taps, 64, 8)
+    wb = w.bfloat16().reshape(co, ci, taps)
+    for b, j, tap, lane, e in [(0, 0, 0, 0, 0), (0, 1, 4, 37, 3), (1, 0, 8, 7, 7), (1, 1, 2, 63, 5), (0, 0, 5, 40, 6)]:
+        tap = tap % taps
+        c, h = lane % 32, lane // 32
+        o, i = 32 * b + c, 16 * j + 8 * h + e
+        want = wb[o, i, tap] if (o < co and i < ci) else torch.zeros((), dtype=torch.bfloat16)
+        assert p[b, j, tap, lane, e] == want, (b, j, tap, lane, e)
+    # byte count = the C-ABI's tsplat_conv2d_bf16_weight_bytes formula
+    assert K.conv_bf16_pack_weight(w).numel() * 2 == 2 * 2 * taps * 64 * 16
+    assert "tsplat_conv2d_bf16_weight_bytes" in L.SIGNATURES
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,chans,h,w,cout,has_bias,act,sdt", BF16_CASES)
-def test_conv3x3_bf16_kernel(device, n, chans, h, w, cout, has_bias, act, sdt):
+@pytest.mark.parametrize("n,chans,h,w,cout,k,up,has_bias,act,sdt", BF16_CASES)
+def test_conv_bf16_kernel(device, n, chans, h, w, cout, k, up, has_bias, act, sdt):
     from transplat_amd import kernels as K
 
     dt = torch.float32 if sdt == "f32" else torch.bfloat16
-    srcs = [seeded((n, c, h, w), 300 + i).to(dt) for i, c in enumerate(chans)]
-    wt = seeded((cout, sum(chans), 3, 3), 310) * 0.1
+    hs, ws = (h // 2, w // 2) if up else (h, w)
+    srcs = [seeded((n, c, hs, ws), 300 + i).to(dt) for i, c in enumerate(chans)]
+    wt = seeded((cout, sum(chans), k, k), 310) * 0.1
     b = seeded((cout,), 311) if has_bias else None
-    ref = _bf16_ref(srcs, wt, b, act)
+    ref = _bf16_ref(srcs, wt, b, act, up)
+    dsrc = [s.to(device) for s in srcs]
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        assert K.conv3x3_bf16_ok(srcs[0].to(device), wt, extra=tuple(s.to(device) for s in srcs[1:]))
-        y = K.conv3x3_bf16(srcs[0].to(device), wt.to(device), b.to(device) if b is not None else None, act,
-                           extra=tuple(s.to(device) for s in srcs[1:]))
+        assert K.conv_bf16_ok(dsrc[0], wt, extra=tuple(dsrc[1:]), upsample=up)
+        y = K.conv_bf16(dsrc[0], wt.to(device), b.to(device) if b is not None else None, act, extra=tuple(dsrc[1:]),
+                        upsample=up)
     assert y.dtype == torch.bfloat16 and tuple(y.shape) == (n, cout, h, w)
     err = (y.double().cpu() - ref).abs()
     bound = 2.0 ** -8 * ref.abs() + 1e-4 * ref.abs().max()
@@ -364,34 +375,43 @@ def test_conv3x3_bf16_kernel(device, n, chans, h, w, cout, has_bias, act, sdt):
 
 
 @pytest.mark.gpu
-def test_conv3x3_bf16_module_routes(device):
-    """Under bf16 autocast the U-Net conv helper and the installed Conv2d dispatch take the bf16
-    kernel (bf16 output, no MIOpen call), matching F.conv2d under autocast to bf16 rounding."""
+def test_conv_bf16_module_routes(device):
+    """Under bf16 autocast the U-Net conv helper (plain, 1x1, upsample) and the installed Conv2d
+    dispatch take the bf16 kernel (bf16 output, no MIOpen call), matching F.conv2d under autocast to
+    bf16 rounding."""
     from transplat_amd import kernels as K
     from transplat_amd.model.encoder.matching import ldm_unet as U
 
     conv = torch.nn.Conv2d(64, 64, 3, 1, 1).to(device)
+    conv1 = torch.nn.Conv2d(64, 32, 1).to(device)
+    conv1d = torch.nn.Conv1d(64, 96, 1).to(device)
+    t = seeded((2, 64, 256), 321).to(device)
     x = seeded((2, 64, 32, 32), 320).to(device)
+    F = torch.nn.functional
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
-        ref = torch.nn.functional.conv2d(x, conv.weight, conv.bias, padding=1)
-        y1 = U.conv(conv, x)
-        y2 = K.conv2d_forward(conv, x)
-    for y in (y1, y2):
-        assert y.dtype == torch.bfloat16
+        cases = [(U.conv(conv, x), F.conv2d(x, conv.weight, conv.bias, padding=1)),
+                 (K.conv2d_forward(conv, x), F.conv2d(x, conv.weight, conv.bias, padding=1)),
+                 (U.conv(conv1, x), F.conv2d(x, conv1.weight, conv1.bias)),
+                 (U.conv(conv1d, t), F.conv1d(t, conv1d.weight, conv1d.bias)),
+                 (U.conv(conv, x, upsample=True),
+                  F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), conv.weight, conv.bias, padding=1))]
+    for y, ref in cases:
+        assert y.dtype == torch.bfloat16 and y.shape == ref.shape
         assert (y.float() - ref.float()).abs().max() <= 2 * 2.0 ** -8 * ref.float().abs().max()
 
 
 @pytest.mark.gpu
-def test_conv3x3_bf16_rejects_unsupported(device):
+def test_conv_bf16_rejects_unsupported(device):
     from transplat_amd import kernels as K
 
     w = torch.zeros(32, 32, 3, 3, device=device)
     x = torch.zeros(1, 32, 16, 16, device=device)
-    assert not K.conv3x3_bf16_ok(x, w)  # autocast off
+    assert not K.conv_bf16_ok(x, w)  # autocast off
     with torch.autocast("cuda", dtype=torch.bfloat16):
-        assert K.conv3x3_bf16_ok(x, w)
-        assert not K.conv3x3_bf16_ok(torch.zeros(1, 32, 16, 12, device=device), w)   # width % 8
-        assert not K.conv3x3_bf16_ok(x, w, stride=2)
-        assert not K.conv3x3_bf16_ok(torch.zeros(1, 36, 16, 16, device=device), torch.zeros(32, 36, 3, 3, device=device))
-        assert not K.conv3x3_bf16_ok(x.to(memory_format=torch.channels_last)[:, :, :, :].contiguous(
-            memory_format=torch.channels_last), w)
+        assert K.conv_bf16_ok(x, w)
+        assert not K.conv_bf16_ok(torch.zeros(1, 32, 16, 12, device=device), w)   # width % 8
+        assert not K.conv_bf16_ok(x, w, stride=2)
+        assert not K.conv_bf16_ok(x, torch.zeros(32, 32, 5, 5, device=device))
+        assert not K.conv_bf16_ok(torch.zeros(1, 36, 16, 16, device=device), torch.zeros(32, 36, 3, 3, device=device))
+        assert not K.conv_bf16_ok(x.contiguous(memory_format=torch.channels_last), w)
+        assert not K.conv_bf16_ok(torch.zeros(1, 32, 16, 6, device=device), w, upsample=True)  # 12 % 8

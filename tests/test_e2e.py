@@ -98,7 +98,9 @@ def test_bf16_weight_precast_keeps_outputs(device):
 
     plain, ref = fresh("bf16"), fresh("fp32")
     n_bf16 = sum(p.dtype == torch.bfloat16 for p in cast.parameters())
-    assert n_bf16 > 300
+    # (the convolutions on the HIP bf16 kernel keep fp32 parameters: kernels.conv_bf16_pack_weight
+    # rounds them to bf16 once, into its packed operand layout)
+    assert n_bf16 > 200
     for (name, p), q in zip(cast.named_parameters(), plain.parameters()):
         if p.dtype == torch.bfloat16:
             assert "norm" not in name.split(".")[-2]

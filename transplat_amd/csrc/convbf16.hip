@@ -1,6 +1,7 @@
-// 3x3 / stride 1 / pad 1 convolution on bf16 MFMA (config C3's dense layers) for gfx950.
+// 3x3 and 1x1 / stride 1 convolutions on bf16 MFMA (config C3's dense layers) for gfx950.
 //
-// Semantics: F.conv2d(cat(srcs, 1), w, bias, stride 1, padding 1) under bf16 autocast (the
+// Semantics: F.conv2d(up(cat(srcs, 1)), w, bias, stride 1, padding k // 2) under bf16 autocast, up =
+// optional nearest 2x upsample (the U-Net Upsample block unet.py:105-137) read in place (the
 // reference's nn.Conv2d layers of the depth predictor U-Nets ldm_unet/unet.py:212-250 and its
 // conv heads depth_predictor_trans.py:110-125, run by the C3 config in bf16): sources bf16 or fp32
 // (rounded to bf16 on load, as autocast's cast would), weights and bias bf16, fp32 accumulation,
@@ -10,7 +11,7 @@
 // kernels wrapped in NCHW<->NHWC `batched_transpose` launches; together ~6 ms of C3's 28 ms step.
 // This kernel reads each NCHW input once into LDS and writes the NCHW output once.
 //
-// Implicit GEMM: Y[co][px] = sum_(tap, ci) W[co][tap, ci] X[ci][px + tap offset], one
+// Implicit GEMM: Y[co][px] = sum_(tap, ci) W[co][tap, ci] X[ci][px + tap offset] (9 taps or 1), one
 // v_mfma_f32_32x32x16_bf16 per (tap, 16-channel chunk, 32 x 32 output tile):
 //   A = W[co = 32 cb + c][ci = 16 k + 8 h + j]   (lane l = c + 32 h, element j; packed once on the host
 //       as [co block][chunk][tap][64 lanes][8] bf16, one 16-B load per lane and tap);
@@ -18,7 +19,7 @@
 //   C: lane holds pixel c, output channels 8 (r >> 2) + 4 h + (r & 3) in register r.
 // Workgroup = 4 waves over a TH x TW pixel block (P = TH TW = 128 or 256 pixels) x 32 CT output
 // channels: wave w takes co tile w % CT and NT = 2 column tiles of 32 pixels. Per chunk of 16 input
-// channels the block plus a 1-row / 8-column halo is staged as [row][channel half][column][8
+// channels the block (3x3: plus a 1-row / 8-column halo) is staged as [row][channel half][column][8
 // channels] (each pixel's 8 channels of a half = one 16-B LDS word, so a wave's B reads are
 // contiguous 16-lane runs): a thread loads 8 channels x 8 pixels (eight 16-B row segments of the
 // NCHW map, coalesced across lanes), transposes them in registers, writes 8 LDS words. Double
@@ -26,6 +27,8 @@
 // current chunk's 9 NT MFMAs. Epilogue: bias + act in fp32 -> bf16 tile [co][pixel] in LDS -> 16-B
 // row stores.
 #include <math.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "common.h"
 
@@ -46,8 +49,11 @@ struct Args {
     const uint4* w;  // packed weights
     const float* bias;
     __bf16* y;
-    int n, h, w_, ci, nchunk, co, act;
+    int n, h, w_, ci, nchunk, co, act;  // h, w_: OUTPUT size (= the convolved map's)
+    int up;                              // 1: sources are [h / 2, w_ / 2], nearest-upsampled on load
     int tiles_x, tiles_y;
+    int wg_target;  // workgroups per launch (all co blocks): a few per CU
+    int occ4;       // bf16 sources: the occupancy-4 register allocation (TSPLAT_CONVBF16_OCC=4)
 };
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -62,22 +68,61 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
     return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
 }
 
-// 8 bf16 pixels of one channel row segment (zeros outside the map / past the last channel)
+__device__ __forceinline__ uint32_t dup_bf16(uint32_t v16) { return (v16 & 0xffffu) * 0x10001u; }
+
+// The 8 x 8 block of one staging task: channels c0 .. c0 + 7 (c0 a multiple of 8, so all in one
+// source) x pixels x .. x + 7 (x a multiple of 8) of row y of the convolved map, as 8 channel rows
+// of 8 bf16; zeros outside the map or past the last channel. The source is chosen with constant
+// kernel-argument indices (a runtime index into the argument arrays would be a memory load per
+// access) and the 8 loads are independent.
 template <bool F32>
-__device__ __forceinline__ uint4 load8(const Args& a, int n, int c, int y, int x) {
-    if (c >= a.ci || y < 0 || y >= a.h || x < 0 || x >= a.w_) return make_uint4(0u, 0u, 0u, 0u);
-    int s = 0;
+__device__ __forceinline__ void load_block(const Args& a, int n, int c0, int y, int x, uint4 (&st)[8]) {
+    if (c0 >= a.ci || y < 0 || y >= a.h || x < 0 || x >= a.w_) {
 #pragma unroll
-    for (int i = 1; i < kMaxSrc; ++i)
-        if (i < a.nsrc && c >= a.src_begin[i]) s = i;
-    const int cs = a.src_begin[s + 1] - a.src_begin[s];
-    const size_t off = (((size_t)n * cs + (c - a.src_begin[s])) * a.h + y) * a.w_ + x;
-    if constexpr (F32) {
-        const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.src[s]) + off);
-        const float4 u = p[0], v = p[1];
-        return make_uint4(pack_bf16x2(u.x, u.y), pack_bf16x2(u.z, u.w), pack_bf16x2(v.x, v.y), pack_bf16x2(v.z, v.w));
-    } else {
-        return *reinterpret_cast<const uint4*>(reinterpret_cast<const __bf16*>(a.src[s]) + off);
+        for (int j = 0; j < 8; ++j) st[j] = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
+    const char* base = reinterpret_cast<const char*>(a.src[0]);
+    int cb = 0, ce = a.src_begin[1];
+#pragma unroll
+    for (int i = 1; i < kMaxSrc; ++i) {
+        if (i < a.nsrc && c0 >= a.src_begin[i]) {
+            base = reinterpret_cast<const char*>(a.src[i]);
+            cb = a.src_begin[i];
+            ce = a.src_begin[i + 1];
+        }
+    }
+    const int cs = ce - cb;
+    constexpr int kEl = F32 ? 4 : 2;
+    if (a.up) {  // source pixels x / 2 .. x / 2 + 3 of row y / 2, each used twice
+        const int hs = a.h >> 1, ws = a.w_ >> 1;
+        const size_t plane = (size_t)hs * ws;
+        const char* p = base + ((((size_t)n * cs + (c0 - cb)) * hs + (y >> 1)) * ws + (x >> 1)) * kEl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            if constexpr (F32) {
+                const float4 u = *reinterpret_cast<const float4*>(p + j * plane * kEl);
+                st[j] = make_uint4(pack_bf16x2(u.x, u.x), pack_bf16x2(u.y, u.y), pack_bf16x2(u.z, u.z),
+                                   pack_bf16x2(u.w, u.w));
+            } else {
+                const uint2 u = *reinterpret_cast<const uint2*>(p + j * plane * kEl);
+                st[j] = make_uint4(dup_bf16(u.x), dup_bf16(u.x >> 16), dup_bf16(u.y), dup_bf16(u.y >> 16));
+            }
+        }
+        return;
+    }
+    const size_t plane = (size_t)a.h * a.w_;
+    const char* p = base + ((((size_t)n * cs + (c0 - cb)) * a.h + y) * a.w_ + x) * kEl;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if constexpr (F32) {
+            const float4* q = reinterpret_cast<const float4*>(p + j * plane * kEl);
+            const float4 u = q[0], v = q[1];
+            st[j] = make_uint4(pack_bf16x2(u.x, u.y), pack_bf16x2(u.z, u.w), pack_bf16x2(v.x, v.y),
+                               pack_bf16x2(v.z, v.w));
+        } else {
+            st[j] = *reinterpret_cast<const uint4*>(p + j * plane * kEl);
+        }
     }
 }
 
@@ -97,82 +142,103 @@ __device__ __forceinline__ void transpose8(const uint4 (&in)[8], uint4 (&out)[8]
     }
 }
 
-template <int TW, int CT, bool F32>
-__global__ void __launch_bounds__(kThreads) conv3x3_bf16_kernel(Args a) {
+// OCC: waves per SIMD the register allocation targets (2: no spills; 4: more workgroups per CU to
+// hide the staging loads' latency, at the price of a few spilled registers on the 3x3 bf16 variants)
+template <int TW, int CT, int KS, bool F32, int OCC>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(OCC))) conv_bf16_kernel(Args a) {
     constexpr int P = 32 * (4 / CT) * kNT;  // pixels per workgroup
     constexpr int TH = P / TW;
-    constexpr int LW = TW + 16;    // staged columns: x0 - 8 .. x0 + TW + 7
-    constexpr int G = LW / 8;      // 8-pixel groups per staged row
-    constexpr int kTasks = (TH + 2) * 2 * G;
-    constexpr int kBuf = (TH + 2) * 2 * LW;  // 16-B words per buffer
+    constexpr int HY = KS / 2, HX = KS == 3 ? 8 : 0;  // staged halo rows / columns per side
+    constexpr int NTAP = KS * KS;
+    constexpr int LW = TW + 2 * HX;  // staged columns: x0 - HX .. x0 + TW + HX - 1
+    constexpr int G = LW / 8;        // 8-pixel groups per staged row
+    constexpr int SR = TH + 2 * HY;  // staged rows
+    constexpr int kTasks = SR * 2 * G;
+    constexpr int kBuf = SR * 2 * LW;  // 16-B words per buffer
     static_assert(kTasks <= kThreads, "one staging task per thread");
-    static_assert(2 * kBuf * 16 >= 32 * CT * P * 2, "epilogue tile fits the staging buffers");
-    __shared__ uint4 s_in[2][kBuf];
+    constexpr int kEpi = 32 * CT * P * 2 / 16;  // bf16 epilogue tile [32 CT][P] in 16-B words
+    __shared__ uint4 s_lds[2 * kBuf + kEpi];
+    __bf16* const tile_out = reinterpret_cast<__bf16*>(s_lds + 2 * kBuf);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int c = lane & 31, h = lane >> 5;
     const int per_img = a.tiles_x * a.tiles_y;
-    const int bx = blockIdx.x;
-    const int n = bx / per_img, t = bx - n * per_img;
-    const int y0 = (t / a.tiles_x) * TH, x0 = (t % a.tiles_x) * TW;
+    const int ntiles = a.n * per_img;
     const int ct = wid % CT, grp = wid / CT;
     const int cob = blockIdx.y * CT + ct;  // this wave's 32-channel output block
+    // this workgroup's pixel tiles: blockIdx.x, blockIdx.x + gridDim.x, ... (at least one)
+    const int my_tiles = (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
+    const int total = my_tiles * a.nchunk;  // flattened (tile, chunk) iterations
+    auto tile_origin = [&](int ti, int& n, int& y0, int& x0) {
+        const int t = (int)blockIdx.x + ti * (int)gridDim.x;
+        n = t / per_img;
+        const int r = t - n * per_img;
+        y0 = (r / a.tiles_x) * TH;
+        x0 = (r % a.tiles_x) * TW;
+    };
 
     // staging task: (row, channel half, 8-pixel group)
     const bool task = tid < kTasks;
     const int tg = tid % G, thf = (tid / G) & 1, trow = tid / (2 * G);
     uint4 st[8];
-    auto load_chunk = [&](int k) {
+    auto load_iter = [&](int it) {
         if (!task) return;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) st[j] = load8<F32>(a, n, 16 * k + 8 * thf + j, y0 - 1 + trow, x0 - 8 + 8 * tg);
+        const int ti = it / a.nchunk, k = it - ti * a.nchunk;
+        int n, y0, x0;
+        tile_origin(ti, n, y0, x0);
+        load_block<F32>(a, n, 16 * k + 8 * thf, y0 - HY + trow, x0 - HX + 8 * tg, st);
     };
     auto store_chunk = [&](int buf) {
         if (!task) return;
         uint4 px[8];
         transpose8(st, px);
-        uint4* dst = &s_in[buf][(trow * 2 + thf) * LW + 8 * tg];
+        uint4* dst = s_lds + buf * kBuf + (trow * 2 + thf) * LW + 8 * tg;
 #pragma unroll
         for (int p = 0; p < 8; ++p) dst[p] = px[p];
     };
     // a wave whose 32-channel block lies past c_out (c_out not a multiple of 32 CT) reads no
     // weights and multiplies zeros; its outputs are never stored
     const bool cvalid = 32 * cob < a.co;
-    const uint4* wsrc = a.w + (size_t)(cvalid ? cob : 0) * a.nchunk * 9 * 64 + lane;
-    uint4 wf[9];
-    auto load_w = [&](int k, uint4 (&dst)[9]) {
+    const uint4* wsrc = a.w + (size_t)(cvalid ? cob : 0) * a.nchunk * NTAP * 64 + lane;
+    uint4 wf[NTAP];
+    auto load_w = [&](int k, uint4 (&dst)[NTAP]) {
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) dst[tap] = cvalid ? wsrc[((size_t)k * 9 + tap) * 64] : make_uint4(0u, 0u, 0u, 0u);
+        for (int tap = 0; tap < NTAP; ++tap)
+            dst[tap] = cvalid ? wsrc[((size_t)k * NTAP + tap) * 64] : make_uint4(0u, 0u, 0u, 0u);
     };
 
-    // LDS word of (pixel p of column tile j) at tap (0, 0): row p / TW, column p % TW + 7
+    // LDS word of (pixel p of column tile j) at tap (0, 0): staged row p / TW, column p % TW + HX - KS / 2
     int bbase[kNT];
 #pragma unroll
     for (int k = 0; k < kNT; ++k) {
         const int p = 32 * (grp * kNT + k) + c;
-        bbase[k] = ((p / TW) * 2 + h) * LW + (p % TW) + 7;
+        bbase[k] = ((p / TW) * 2 + h) * LW + (p % TW) + HX - KS / 2;
     }
     floatx16 acc[kNT];
-#pragma unroll
-    for (int k = 0; k < kNT; ++k)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[k][r] = 0.0f;
 
-    load_chunk(0);
-    load_w(0, wf);
-    for (int k = 0; k < a.nchunk; ++k) {
-        const int buf = k & 1;
+    // software pipeline over the flattened (tile, chunk) sequence: the loads of iteration it + 1
+    // (next chunk, or the next tile's first chunk) fly during iteration it's MFMAs, so the
+    // workgroup streams tiles instead of paying a memory round trip per tile
+    // weights are loaded per iteration just before the barrier (L2 hits; no register prefetch,
+    // which would cost 4 NTAP VGPRs and an occupancy step)
+    load_iter(0);
+    for (int it = 0; it < total; ++it) {
+        const int ti = it / a.nchunk, k = it - ti * a.nchunk;
+        const int buf = it & 1;
         store_chunk(buf);
+        load_w(k, wf);
         __syncthreads();
-        uint4 wn[9];
-        if (k + 1 < a.nchunk) {
-            load_chunk(k + 1);
-            load_w(k + 1, wn);
-        }
-        const uint4* sb = s_in[buf];
+        if (it + 1 < total) load_iter(it + 1);
+        if (k == 0) {
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-            const int off = (tap / 3) * 2 * LW + (tap % 3);
+            for (int j = 0; j < kNT; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+        }
+        const uint4* sb = s_lds + buf * kBuf;
+#pragma unroll
+        for (int tap = 0; tap < NTAP; ++tap) {
+            const int off = (tap / KS) * 2 * LW + (tap % KS);
             const bf16x8 av = __builtin_bit_cast(bf16x8, wf[tap]);
 #pragma unroll
             for (int j = 0; j < kNT; ++j) {
@@ -180,78 +246,84 @@ __global__ void __launch_bounds__(kThreads) conv3x3_bf16_kernel(Args a) {
                 acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[j], 0, 0, 0);
             }
         }
-        if (k + 1 < a.nchunk) {
+        if (k + 1 == a.nchunk) {
+            // epilogue of tile ti: bias + act in fp32 -> bf16 [co_local][pixel] in its own LDS
+            // buffer (its previous readers finished before this iteration's barrier) -> 16-B stores
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap) wf[tap] = wn[tap];
-        }
-    }
-    __syncthreads();  // every wave is done reading the staging buffers
-
-    // epilogue: bias + act in fp32, bf16 tile [co_local][pixel] in LDS, then 16-B row stores
-    __bf16* tile = reinterpret_cast<__bf16*>(&s_in[0][0]);
+            for (int r = 0; r < 16; ++r) {
+                const int col = 32 * ct + 8 * (r >> 2) + 4 * h + (r & 3);
+                const int co = 32 * cob + 8 * (r >> 2) + 4 * h + (r & 3);
+                const float bias = (a.bias && co < a.co) ? a.bias[co] : 0.0f;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int col = 32 * ct + 8 * (r >> 2) + 4 * h + (r & 3);
-        const int co = 32 * cob + 8 * (r >> 2) + 4 * h + (r & 3);
-        const float b = (a.bias && co < a.co) ? a.bias[co] : 0.0f;
+                for (int j = 0; j < kNT; ++j)
+                    tile_out[col * P + 32 * (grp * kNT + j) + c] = (__bf16)act_fn(acc[j][r] + bias, a.act);
+            }
+            __syncthreads();
+            int n, y0, x0;
+            tile_origin(ti, n, y0, x0);
+            constexpr int kItems = 32 * CT * P / 8;
 #pragma unroll
-        for (int j = 0; j < kNT; ++j) tile[col * P + 32 * (grp * kNT + j) + c] = (__bf16)act_fn(acc[j][r] + b, a.act);
-    }
-    __syncthreads();
-    constexpr int kItems = 32 * CT * P / 8;
-#pragma unroll
-    for (int i = tid; i < kItems; i += kThreads) {
-        const int col = i / (P / 8), pg = i % (P / 8);
-        const int co = 32 * CT * blockIdx.y + col;
-        const int py = y0 + (8 * pg) / TW, px = x0 + (8 * pg) % TW;
-        if (co < a.co && py < a.h && px < a.w_) {
-            const uint4 v = *reinterpret_cast<const uint4*>(tile + col * P + 8 * pg);
-            *reinterpret_cast<uint4*>(a.y + (((size_t)n * a.co + co) * a.h + py) * a.w_ + px) = v;
+            for (int i = tid; i < kItems; i += kThreads) {
+                const int col = i / (P / 8), pg = i % (P / 8);
+                const int co = 32 * CT * blockIdx.y + col;
+                const int py = y0 + (8 * pg) / TW, px = x0 + (8 * pg) % TW;
+                if (co < a.co && py < a.h && px < a.w_) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(tile_out + col * P + 8 * pg);
+                    *reinterpret_cast<uint4*>(a.y + (((size_t)n * a.co + co) * a.h + py) * a.w_ + px) = v;
+                }
+            }
         }
     }
 }
 
-template <int TW, int CT>
+template <int TW, int CT, int KS>
 static void launch_tw(const Args& a, bool f32, hipStream_t stream) {
     constexpr int P = 32 * (4 / CT) * kNT;
     constexpr int TH = P / TW;
     Args b = a;
     b.tiles_x = ceil_div(a.w_, TW);
     b.tiles_y = ceil_div(a.h, TH);
-    dim3 grid(a.n * b.tiles_x * b.tiles_y, ceil_div(a.co, 32 * CT));
+    // enough workgroups to fill every CU a few times over; each streams its share of the tiles
+    const int ntiles = a.n * b.tiles_x * b.tiles_y, cob = ceil_div(a.co, 32 * CT);
+    const int want = std::max(1, a.wg_target / cob);
+    dim3 grid(std::min(ntiles, want), cob);
     if (f32)
-        hipLaunchKernelGGL((conv3x3_bf16_kernel<TW, CT, true>), grid, dim3(kThreads), 0, stream, b);
+        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, true, 2>), grid, dim3(kThreads), 0, stream, b);
+    else if (a.occ4)
+        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, false, 4>), grid, dim3(kThreads), 0, stream, b);
     else
-        hipLaunchKernelGGL((conv3x3_bf16_kernel<TW, CT, false>), grid, dim3(kThreads), 0, stream, b);
+        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, false, 2>), grid, dim3(kThreads), 0, stream, b);
 }
 
-template <int CT>
+template <int CT, int KS>
 static void launch_ct(const Args& a, bool f32, hipStream_t stream) {
     if (a.w_ >= 64)
-        launch_tw<64, CT>(a, f32, stream);
+        launch_tw<64, CT, KS>(a, f32, stream);
     else if (a.w_ >= 32)
-        launch_tw<32, CT>(a, f32, stream);
+        launch_tw<32, CT, KS>(a, f32, stream);
     else if (a.w_ >= 16)
-        launch_tw<16, CT>(a, f32, stream);
+        launch_tw<16, CT, KS>(a, f32, stream);
     else
-        launch_tw<8, CT>(a, f32, stream);
+        launch_tw<8, CT, KS>(a, f32, stream);
 }
 
 }  // namespace convbf16
 }  // namespace tsplat
 
-extern "C" size_t tsplat_conv3x3_bf16_weight_bytes(int32_t c_out, int32_t c_in) {
-    if (c_out <= 0 || c_in <= 0) return 0;
-    return (size_t)tsplat::ceil_div(c_out, 32) * tsplat::ceil_div(c_in, 16) * 9 * 64 * 16;
+extern "C" size_t tsplat_conv2d_bf16_weight_bytes(int32_t c_out, int32_t c_in, int32_t ksize) {
+    if (c_out <= 0 || c_in <= 0 || !(ksize == 1 || ksize == 3)) return 0;
+    return (size_t)tsplat::ceil_div(c_out, 32) * tsplat::ceil_div(c_in, 16) * ksize * ksize * 64 * 16;
 }
 
-extern "C" int tsplat_conv3x3_bf16_fwd(const void* const* srcs, const int32_t* src_channels, int32_t nsrc,
-                                       int32_t src_f32, const void* w_packed, const float* bias, void* y,
-                                       int32_t batch, int32_t height, int32_t width, int32_t c_out, int32_t act,
-                                       void* stream_) {
+extern "C" int tsplat_conv2d_bf16_fwd(const void* const* srcs, const int32_t* src_channels, int32_t nsrc,
+                                      int32_t src_f32, const void* w_packed, const float* bias, void* y,
+                                      int32_t batch, int32_t height, int32_t width, int32_t c_out, int32_t ksize,
+                                      int32_t upsample, int32_t act, void* stream_) {
     using namespace tsplat::convbf16;
     if (!srcs || !src_channels || nsrc < 1 || nsrc > kMaxSrc || !w_packed || !y) return TSPLAT_EINVAL;
     if (batch <= 0 || height <= 0 || width <= 0 || c_out <= 0 || (width & 7) || act < 0 || act > 3)
+        return TSPLAT_EINVAL;
+    if (!(ksize == 1 || ksize == 3) || !(upsample == 0 || upsample == 1) || (upsample && (height & 1)))
         return TSPLAT_EINVAL;
     Args a{};
     int ci = 0;
@@ -276,11 +348,27 @@ extern "C" int tsplat_conv3x3_bf16_fwd(const void* const* srcs, const int32_t* s
     a.nchunk = tsplat::ceil_div(ci, 16);
     a.co = c_out;
     a.act = act;
+    a.up = upsample;
+    {
+        const char* e = getenv("TSPLAT_CONVBF16_WGS");  // A/B knob: workgroups per launch
+        a.wg_target = e ? std::max(1, atoi(e)) : 256 * 2;
+        const char* o = getenv("TSPLAT_CONVBF16_OCC");
+        a.occ4 = o && !strcmp(o, "4");
+        if (a.occ4 && !e) a.wg_target = 256 * 4;
+    }
     hipStream_t stream = (hipStream_t)stream_;
-    if (c_out <= 32)
-        launch_ct<1>(a, src_f32 != 0, stream);
-    else
-        launch_ct<2>(a, src_f32 != 0, stream);
+    const bool f32 = src_f32 != 0;
+    if (ksize == 3) {
+        if (c_out <= 32)
+            launch_ct<1, 3>(a, f32, stream);
+        else
+            launch_ct<2, 3>(a, f32, stream);
+    } else {
+        if (c_out <= 32)
+            launch_ct<1, 1>(a, f32, stream);
+        else
+            launch_ct<2, 1>(a, f32, stream);
+    }
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }

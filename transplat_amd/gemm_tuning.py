@@ -16,10 +16,11 @@ TUNED_FILE = Path(__file__).resolve().parent / "tuned" / "gemms_gfx950.csv"
 
 
 def use_tuned_gemms(device, dense_dtype: str = "fp32") -> bool:
-    """Enable TunableOp in replay-only mode with the committed results; True if they were loaded."""
+    """Enable TunableOp in replay-only mode with the committed results; True if they were loaded.
+    The file holds fp32 entries (tools/tune_gemms.py) and bf16 ones (tools/tune_gemms_bf16.py: an
+    allow-list of hipBLASLt's heuristic top-k per problem); a GEMM with no entry takes TunableOp's
+    Default op, i.e. the untuned library path."""
     if os.environ.get("TSPLAT_TUNED_GEMMS", "1") == "0" or torch.device(device).type != "cuda":
-        return False
-    if dense_dtype != "fp32":  # only fp32 shapes were tuned (tools/tune_gemms.py)
         return False
     if not TUNED_FILE.exists():
         return False

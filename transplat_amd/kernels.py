@@ -212,8 +212,8 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = "", ext
     if not x.is_cuda:
         raise RuntimeError("transplat HIP ops need device tensors (no CPU path)")
     if (residual is None and act in _ACTS and _NO_CONV_EPI not in ("all", site)
-            and conv3x3_bf16_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra)):
-        return conv3x3_bf16(x, conv.weight, conv.bias, act, extra)  # bf16 autocast: bias + act fused
+            and conv_bf16_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra)):
+        return conv_bf16(x, conv.weight, conv.bias, act, extra)  # bf16 autocast: bias + act fused
     fused = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32 and _NO_CONV_EPI not in ("all", site)
     if (fused and residual is None and act in _WINO_ACT
             and conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra,
@@ -641,8 +641,8 @@ def conv2d_forward(mod, x):
     (stride 1 or 2) ones that conv2d_direct_ok admits on the direct kernel (bias in the epilogue
     instead of MIOpen's separate bias launch), the rest through MIOpen."""
     if mod.padding_mode == "zeros" and mod.groups == 1 and tuple(mod.dilation) == (1, 1):
-        if conv3x3_bf16_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation, mod.groups):
-            return conv3x3_bf16(x, mod.weight, mod.bias)
+        if conv_bf16_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation, mod.groups):
+            return conv_bf16(x, mod.weight, mod.bias)
         if conv3x3_wino_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation, mod.groups, vs_miopen=True):
             return conv3x3_wino(x, mod.weight, mod.bias)
         st = mod.stride[0] if mod.stride[0] == mod.stride[1] else 0
@@ -693,24 +693,25 @@ def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=()):
     return y
 
 
-# bf16 implicit-GEMM 3x3 convolution (tsplat_conv3x3_bf16_fwd) for the convolutions that run under
-# bf16 autocast (config C3); "0" = MIOpen (A/B knob)
+# bf16 implicit-GEMM 3x3 / 1x1 convolution (tsplat_conv2d_bf16_fwd) for the convolutions that run
+# under bf16 autocast (config C3); "0" = MIOpen (A/B knob)
 _CONV_BF16 = os.environ.get("TSPLAT_CONV_BF16", "1") != "0"
 _BF16_PACKED: dict = {}
 
 
-def conv3x3_bf16_pack_weight(weight):
-    """[cout, cin, 3, 3] -> bf16 [ceil(cout / 32)][ceil(cin / 16)][9][64 lanes][8] (lane c + 32 h
-    holds w[32 b + c][16 k + 8 h + 0..7][tap]), the A operand of tsplat_conv3x3_bf16_fwd; cached
-    per weight tensor version."""
+def conv_bf16_pack_weight(weight):
+    """[cout, cin, k, k] (k = 1, 3) -> bf16 [ceil(cout / 32)][ceil(cin / 16)][k * k][64 lanes][8]
+    (lane c + 32 h holds w[32 b + c][16 j + 8 h + 0..7][tap]), the A operand of
+    tsplat_conv2d_bf16_fwd; cached per weight tensor version."""
     hit = _BF16_PACKED.get(id(weight))
     if hit is not None and hit[0]() is weight and hit[1] == weight._version:
         return hit[2]
     co, ci = weight.shape[:2]
+    taps = weight[0, 0].numel()  # [co, ci, k, k] or a Conv1d's [co, ci, 1]
     cob, nk = (co + 31) // 32, (ci + 15) // 16
-    w = torch.zeros((cob * 32, nk * 16, 9), dtype=torch.bfloat16, device=weight.device)
-    w[:co, :ci] = weight.detach().reshape(co, ci, 9).to(torch.bfloat16)
-    packed = w.view(cob, 32, nk, 2, 8, 9).permute(0, 2, 5, 3, 1, 4).contiguous()
+    w = torch.zeros((cob * 32, nk * 16, taps), dtype=torch.bfloat16, device=weight.device)
+    w[:co, :ci] = weight.detach().reshape(co, ci, taps).to(torch.bfloat16)
+    packed = w.view(cob, 32, nk, 2, 8, taps).permute(0, 2, 5, 3, 1, 4).contiguous()
     if len(_BF16_PACKED) > 512:
         for k in [k for k, v in _BF16_PACKED.items() if v[0]() is None]:
             del _BF16_PACKED[k]
@@ -718,10 +719,22 @@ def conv3x3_bf16_pack_weight(weight):
     return packed
 
 
-def conv3x3_bf16_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=()) -> bool:
-    """True when conv2d(cat([x, *extra], 1), weight) runs under bf16 autocast and fits
-    tsplat_conv3x3_bf16_fwd: 3x3 / stride 1 / padding 1, NCHW contiguous sources of one dtype
-    (fp32 or bf16) with channel counts and width multiples of 8, at most 4 sources."""
+def _bf16_rounded_bias(bias):
+    """fp32 copy of the bias rounded to bf16 (autocast's cast), cached per tensor version."""
+    key = ("bias", id(bias))
+    hit = _BF16_PACKED.get(key)
+    if hit is not None and hit[0]() is bias and hit[1] == bias._version:
+        return hit[2]
+    rb = bias.detach().to(torch.bfloat16).float().contiguous()
+    _BF16_PACKED[key] = (weakref.ref(bias), bias._version, rb)
+    return rb
+
+
+def conv_bf16_ok(x, weight, stride=1, padding=None, dilation=1, groups=1, extra=(), upsample: bool = False) -> bool:
+    """True when conv2d(up(cat([x, *extra], 1)), weight) runs under bf16 autocast and fits
+    tsplat_conv2d_bf16_fwd: 3x3 / padding 1 or 1x1 / padding 0, stride 1, NCHW contiguous sources of
+    one dtype (fp32 or bf16) with channel counts and the convolved width multiples of 8, at most 4
+    sources; up = optional nearest 2x upsample read in place."""
     if (not _CONV_BF16 or not x.is_cuda or not torch.is_autocast_enabled("cuda")
             or torch.get_autocast_dtype("cuda") != torch.bfloat16 or len(extra) > 3):
         return False
@@ -730,20 +743,25 @@ def conv3x3_bf16_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=
                 or not t.is_contiguous() or t.device != x.device or t.shape[0] != x.shape[0]
                 or t.shape[2:] != x.shape[2:] or t.shape[1] % 8 or t.numel() >= 2 ** 31):
             return False
-    if weight.dim() != 4 or tuple(weight.shape[2:]) != (3, 3) or groups != 1:
+    # [co, ci, k, k] (k = 1, 3) or a 1x1 Conv1d's [co, ci, 1] (on a [n, c, 1, t] view of its input)
+    if not ((weight.dim() == 4 and weight.shape[2] == weight.shape[3] and weight.shape[2] in (1, 3))
+            or (weight.dim() == 3 and weight.shape[2] == 1)) or groups != 1:
         return False
+    k = weight.shape[2]
     as_int = lambda v: v if isinstance(v, int) else (v[0] if len(set(v)) == 1 else -1)
-    if as_int(stride) != 1 or as_int(padding) != 1 or as_int(dilation) != 1:
+    if as_int(stride) != 1 or as_int(padding if padding is not None else k // 2) != k // 2 or as_int(dilation) != 1:
         return False
     n, _, h, w = x.shape
+    if upsample:
+        h, w = 2 * h, 2 * w
     ci = sum(t.shape[1] for t in (x, *extra))
-    return weight.shape[1] == ci and w % 8 == 0 and n * weight.shape[0] * h * w < 2 ** 31
+    return weight.shape[1] == ci and w % 8 == 0 and n * max(weight.shape[0], ci) * h * w < 2 ** 31
 
 
-def conv3x3_bf16(x, weight, bias=None, act: str = "none", extra=()):
-    """act(conv2d(cat([x, *extra], 1), weight, bias, 1, 1)) as autocast would compute it in bf16
-    (bf16-rounded sources, weights and bias, fp32 accumulation), output bf16 NCHW, in one
-    tsplat_conv3x3_bf16_fwd launch that reads the concatenation in place."""
+def conv_bf16(x, weight, bias=None, act: str = "none", extra=(), upsample: bool = False):
+    """act(conv2d(up(cat([x, *extra], 1)), weight, bias, 1, k // 2)) as autocast would compute it in
+    bf16 (bf16-rounded sources, weights and bias, fp32 accumulation), output bf16 NCHW, in one
+    tsplat_conv2d_bf16_fwd launch that reads the concatenation / nearest upsample in place."""
     import ctypes
 
     if not x.is_cuda:
@@ -751,16 +769,18 @@ def conv3x3_bf16(x, weight, bias=None, act: str = "none", extra=()):
     lib = _lib.load()
     srcs = (x, *extra)
     n, _, h, w = x.shape
-    co = weight.shape[0]
+    if upsample:
+        h, w = 2 * h, 2 * w
+    co, k = weight.shape[0], weight.shape[2]
     y = torch.empty((n, co, h, w), dtype=torch.bfloat16, device=x.device)
-    pb = bias.detach().to(torch.bfloat16).float().contiguous() if bias is not None else None
+    pb = _bf16_rounded_bias(bias) if bias is not None else None
     ptrs = (ctypes.c_void_p * len(srcs))(*[_lib.ptr(t) for t in srcs])
     chans = (ctypes.c_int32 * len(srcs))(*[t.shape[1] for t in srcs])
-    rc = lib.tsplat_conv3x3_bf16_fwd(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p),
-                                     len(srcs), int(x.dtype == torch.float32),
-                                     _lib.ptr(conv3x3_bf16_pack_weight(weight)), _lib.ptr(pb), _lib.ptr(y), n, h, w,
-                                     co, _ACTS[act], _lib.stream_ptr(x.device))
-    _lib.check(rc, "tsplat_conv3x3_bf16_fwd")
+    rc = lib.tsplat_conv2d_bf16_fwd(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p),
+                                    len(srcs), int(x.dtype == torch.float32),
+                                    _lib.ptr(conv_bf16_pack_weight(weight)), _lib.ptr(pb), _lib.ptr(y), n, h, w,
+                                    co, k, int(upsample), _ACTS[act], _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_conv2d_bf16_fwd")
     return y
 
 

@@ -27,9 +27,11 @@ _DPT_CL_WEIGHTS = os.environ.get("TSPLAT_DPT_CL_WEIGHTS", "1") != "0"
 _DPT_DIRECT = os.environ.get("TSPLAT_DPT_DIRECT", "0")
 # conv epilogues (bias + ReLU, bias + residuals) fused after the MIOpen convolutions; "0" = A/B off
 _DPT_EPI = os.environ.get("TSPLAT_DPT_EPI", "1") != "0"
-# reassemble branches of ViT layers 1-3 forked onto a side stream while the later blocks run
-# (needs streams.enabled); "0" = A/B off
-_DPT_HOIST = os.environ.get("TSPLAT_DPT_HOIST", "1") != "0"
+# Opt-in "1": the reassemble branches of ViT layers 1-3 forked onto a side stream while the later
+# blocks run (needs streams.enabled). Measured SLOWER end to end (profiles/r3/ab_r3c: C2 332 vs
+# 356 views/s, C3 849 vs 887): the branches' MIOpen convolutions take CUs from the critical path
+# (DINOv2 blocks and the backbone beside them) rather than filling idle ones.
+_DPT_HOIST = os.environ.get("TSPLAT_DPT_HOIST", "0") == "1"
 
 
 def _resize(x, modifier: dict, align_corners: bool):

@@ -49,9 +49,17 @@ def conv(conv: nn.Module, x, x2=None, upsample: bool = False, bias: bool = True)
     concat / upsample in place (kernels.conv2d_direct); the rest materialise them and run MIOpen."""
     b = conv.bias if bias else None
     extra = (x2,) if x2 is not None else ()
-    if (isinstance(conv, nn.Conv2d) and not upsample
-            and kernels.conv3x3_bf16_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra)):
-        return kernels.conv3x3_bf16(x, conv.weight, b, extra=extra)  # bf16 autocast (C3), concat read in place
+    if (isinstance(conv, nn.Conv2d) and conv.padding_mode == "zeros"
+            and kernels.conv_bf16_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra,
+                                     upsample)):
+        # bf16 autocast (C3): 3x3 / 1x1 on bf16 MFMA, the concat / upsample read in place
+        return kernels.conv_bf16(x, conv.weight, b, extra=extra, upsample=upsample)
+    if (isinstance(conv, nn.Conv1d) and x2 is None and not upsample and conv.kernel_size == (1,)
+            and conv.stride == (1,) and conv.groups == 1 and x.dim() == 3
+            and kernels.conv_bf16_ok(x.unsqueeze(2), conv.weight)):
+        # the attention blocks' qkv / proj_out under bf16 autocast: a 1x1 over [n, c, t] viewed as a
+        # [n, c, 1, t] map (MIOpen ran the 1-D form as im2col + GEMM)
+        return kernels.conv_bf16(x.unsqueeze(2), conv.weight, b).squeeze(2)
     if _direct(conv, x, x2, upsample):
         return kernels.conv2d_direct(x, conv.weight, b, conv.stride[0], x2=x2, upsample=upsample)
     if (isinstance(conv, nn.Conv1d) and x2 is None and not upsample and conv.kernel_size == (1,)
