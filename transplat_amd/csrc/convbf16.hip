@@ -53,7 +53,7 @@ struct Args {
     int up;                              // 1: sources are [h / 2, w_ / 2], nearest-upsampled on load
     int tiles_x, tiles_y;
     int wg_target;  // workgroups per launch (all co blocks): a few per CU
-    int occ4;       // bf16 sources: the occupancy-4 register allocation (TSPLAT_CONVBF16_OCC=4)
+    int occ4;       // bf16 sources: the occupancy-4 register allocation (default; C3 1057 vs 1042 views/s)
 };
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -142,8 +142,9 @@ __device__ __forceinline__ void transpose8(const uint4 (&in)[8], uint4 (&out)[8]
     }
 }
 
-// OCC: waves per SIMD the register allocation targets (2: no spills; 4: more workgroups per CU to
-// hide the staging loads' latency, at the price of a few spilled registers on the 3x3 bf16 variants)
+// OCC: waves per SIMD the register allocation targets (2: no spills; 4, the default for bf16
+// sources: more workgroups per CU to hide the staging loads' latency, at the price of a few
+// spilled registers on the 3x3 variants; same-box C3 1057 vs 1042 views/s, profiles/r3/ab_r3d)
 template <int TW, int CT, int KS, bool F32, int OCC>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(OCC))) conv_bf16_kernel(Args a) {
     constexpr int P = 32 * (4 / CT) * kNT;  // pixels per workgroup
@@ -351,10 +352,9 @@ extern "C" int tsplat_conv2d_bf16_fwd(const void* const* srcs, const int32_t* sr
     a.up = upsample;
     {
         const char* e = getenv("TSPLAT_CONVBF16_WGS");  // A/B knob: workgroups per launch
-        a.wg_target = e ? std::max(1, atoi(e)) : 256 * 2;
-        const char* o = getenv("TSPLAT_CONVBF16_OCC");
-        a.occ4 = o && !strcmp(o, "4");
-        if (a.occ4 && !e) a.wg_target = 256 * 4;
+        const char* o = getenv("TSPLAT_CONVBF16_OCC");  // "2": the spill-free allocation (A/B knob)
+        a.occ4 = !(o && !strcmp(o, "2"));
+        a.wg_target = e ? std::max(1, atoi(e)) : (a.occ4 ? 256 * 4 : 256 * 2);
     }
     hipStream_t stream = (hipStream_t)stream_;
     const bool f32 = src_f32 != 0;
