@@ -396,16 +396,18 @@ int tsplat_conv3x3_wino_cat_f32_fwd(const float* const* srcs, const int32_t* cha
  * unet.py:212-266, Upsample unet.py:105-137, the output blocks' skip concatenation unet.py:1130,
  * the depth predictor's heads depth_predictor_trans.py:110-125), as an implicit GEMM on
  * v_mfma_f32_32x32x16_bf16 with fp32 accumulation: y = act(conv(up(cat(srcs))) + bias) rounded to
- * bf16, act 0 none, 1 SiLU, 2 GELU (erf), 3 ReLU. srcs / src_channels are HOST arrays of n_src
- * (1..4) device pointers [batch, src_channels[s], h_in, w_in] NCHW, bf16 (src_f32 = 0) or fp32
- * rounded to bf16 on load (src_f32 = 1); (h_in, w_in) = (height, width), or (height / 2, width / 2)
- * with upsample = 1 (nearest 2x, read in place). Every src_channels[s] and width a multiple of 8.
+ * bf16, act 0 none, 1 SiLU, 2 GELU (erf), 3 ReLU. srcs / src_channels / src_f32 are HOST arrays of
+ * n_src (1..4) device pointers [batch, src_channels[s], h_in, w_in] NCHW, their channel counts and
+ * dtypes: bf16 (src_f32[s] = 0) or fp32 rounded to bf16 on load (1); (h_in, w_in) = (height, width),
+ * or (height / 2, width / 2) with upsample = 1 (nearest 2x, read in place). width a multiple of 8;
+ * channel counts free (counts that are not multiples of 8, or mixed dtypes, take a per-channel
+ * loader).
  * w_packed = the bf16 weights packed as [ceil(c_out / 32)][ceil(c_in / 16)][ksize^2 taps][64
  * lanes][8] (lane l = c + 32 h holds w[32 b + c][16 k + 8 h + 0..7][tap], zero padded;
  * tsplat_conv2d_bf16_weight_bytes bytes); bias fp32 [c_out] or null; y [batch, c_out, height, width]
  * bf16. */
 size_t tsplat_conv2d_bf16_weight_bytes(int32_t c_out, int32_t c_in, int32_t ksize);
-int tsplat_conv2d_bf16_fwd(const void* const* srcs, const int32_t* src_channels, int32_t n_src, int32_t src_f32,
+int tsplat_conv2d_bf16_fwd(const void* const* srcs, const int32_t* src_channels, int32_t n_src, const int32_t* src_f32,
                            const void* w_packed, const float* bias, void* y, int32_t batch, int32_t height,
                            int32_t width, int32_t c_out, int32_t ksize, int32_t upsample, int32_t act,
                            void* stream);

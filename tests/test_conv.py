@@ -316,6 +316,11 @@ BF16_CASES = [
     (2, (128, 64), 16, 16, 96, 1, False, True, "none", "f32"),      # 1x1 on a concat, co % 64 != 0
     (2, (128,), 32, 32, 128, 3, True, True, "none", "bf16"),        # Upsample: nearest 2x (16^2 -> 32^2) + 3x3
     (1, (32,), 64, 16, 32, 3, True, True, "none", "f32"),           # upsample, fp32 source, TW = 16
+    (2, (32, 3, 128), 64, 64, 96, 3, False, True, "gelu", "mix"),   # to_gaussians head: ragged + mixed dtypes
+    (1, (3, 1, 20, 1, 1), 32, 32, 40, 3, False, False, "none", "mix"),  # 5 ragged sources: rejected (> 4)
+    (2, (5, 12), 16, 16, 32, 3, True, True, "silu", "mix"),         # ragged + upsample
+    (1, (32, 3, 128), 64, 64, 168, 3, False, True, "gelu", "mix"),  # register-blocked form (ci co >= 96^2), co % 64 != 0
+    (2, (128,), 40, 32, 128, 3, False, False, "none", "bf16"),      # register-blocked form, TW = 32, H % TH != 0
 ]
 
 
@@ -357,14 +362,17 @@ def test_conv_bf16_weight_packing_layout(k):
 def test_conv_bf16_kernel(device, n, chans, h, w, cout, k, up, has_bias, act, sdt):
     from transplat_amd import kernels as K
 
-    dt = torch.float32 if sdt == "f32" else torch.bfloat16
     hs, ws = (h // 2, w // 2) if up else (h, w)
-    srcs = [seeded((n, c, hs, ws), 300 + i).to(dt) for i, c in enumerate(chans)]
+    dts = [torch.float32 if (sdt == "f32" or (sdt == "mix" and i % 2)) else torch.bfloat16 for i in range(len(chans))]
+    srcs = [seeded((n, c, hs, ws), 300 + i).to(dts[i]) for i, c in enumerate(chans)]
     wt = seeded((cout, sum(chans), k, k), 310) * 0.1
     b = seeded((cout,), 311) if has_bias else None
     ref = _bf16_ref(srcs, wt, b, act, up)
     dsrc = [s.to(device) for s in srcs]
     with torch.autocast("cuda", dtype=torch.bfloat16):
+        if len(chans) > 4:
+            assert not K.conv_bf16_ok(dsrc[0], wt, extra=tuple(dsrc[1:]), upsample=up)
+            return
         assert K.conv_bf16_ok(dsrc[0], wt, extra=tuple(dsrc[1:]), upsample=up)
         y = K.conv_bf16(dsrc[0], wt.to(device), b.to(device) if b is not None else None, act, extra=tuple(dsrc[1:]),
                         upsample=up)
@@ -412,6 +420,7 @@ def test_conv_bf16_rejects_unsupported(device):
         assert not K.conv_bf16_ok(torch.zeros(1, 32, 16, 12, device=device), w)   # width % 8
         assert not K.conv_bf16_ok(x, w, stride=2)
         assert not K.conv_bf16_ok(x, torch.zeros(32, 32, 5, 5, device=device))
-        assert not K.conv_bf16_ok(torch.zeros(1, 36, 16, 16, device=device), torch.zeros(32, 36, 3, 3, device=device))
+        assert K.conv_bf16_ok(torch.zeros(1, 36, 16, 16, device=device), torch.zeros(32, 36, 3, 3, device=device))
+        assert not K.conv_bf16_ok(torch.zeros(1, 36, 16, 16, device=device), torch.zeros(32, 35, 3, 3, device=device))
         assert not K.conv_bf16_ok(x.contiguous(memory_format=torch.channels_last), w)
         assert not K.conv_bf16_ok(torch.zeros(1, 32, 16, 6, device=device), w, upsample=True)  # 12 % 8

@@ -7,7 +7,7 @@
 // candidate's solution index is printed and flushed BEFORE it runs, so a fault names its solution.
 //
 // Build: hipcc --offload-arch=gfx950 -O2 -shared -fPIC tools/gemm_probe.cpp -lhipblaslt -o
-//        build/tools/libgemm_probe.so
+//        tools/_bin/libgemm_probe.so (git-ignored, travels to the GPU box)
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt-ext.hpp>
 #include <hipblaslt/hipblaslt.h>

@@ -96,7 +96,7 @@ def parse(line):
 def main():
     lines = recorded_lines()
     print(f"recorded {len(lines)} GEMM signatures", flush=True)
-    so = ROOT / "build" / "tools" / "libgemm_probe.so"
+    so = ROOT / "tools" / "_bin" / "libgemm_probe.so"  # hipcc ... -o tools/_bin/libgemm_probe.so (see gemm_probe.cpp)
     lib = ctypes.CDLL(str(so))
     lib.gemm_probe.restype = ctypes.c_int
     lib.gemm_probe.argtypes = [ctypes.c_char, ctypes.c_char] + [ctypes.c_int64] * 6 + [ctypes.c_int32] + \

@@ -85,7 +85,7 @@ SIGNATURES = {
     "tsplat_conv3x3_wino_f32_fwd": (ctypes.c_int, [_P, _P, _P, _P] + [_I32] * 6 + [_P]),
     "tsplat_conv3x3_wino_cat_f32_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P] + [_I32] * 5 + [_P]),
     "tsplat_conv2d_bf16_weight_bytes": (ctypes.c_size_t, [_I32, _I32, _I32]),
-    "tsplat_conv2d_bf16_fwd": (ctypes.c_int, [_P, _P, _I32, _I32, _P, _P, _P] + [_I32] * 7 + [_P]),
+    "tsplat_conv2d_bf16_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P] + [_I32] * 7 + [_P]),
 }
 
 ERRORS = {-1: "invalid argument", -2: "HIP launch error"}

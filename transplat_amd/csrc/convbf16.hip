@@ -40,11 +40,11 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kThreads = 256;
 constexpr int kMaxSrc = 4;
-constexpr int kNT = 2;  // 32-pixel column tiles per wave
 
 struct Args {
     const void* src[kMaxSrc];
     int src_begin[kMaxSrc + 1];  // first concatenated channel of each source (src_begin[nsrc] = ci)
+    int src_f32[kMaxSrc];        // per source: 1 fp32, 0 bf16 (the RAGGED loader reads it per channel)
     int nsrc;
     const uint4* w;  // packed weights
     const float* bias;
@@ -54,6 +54,7 @@ struct Args {
     int tiles_x, tiles_y;
     int wg_target;  // workgroups per launch (all co blocks): a few per CU
     int occ4;       // bf16 sources: the occupancy-4 register allocation (default; C3 1057 vs 1042 views/s)
+    int big;        // 3x3 with c_in * c_out >= TSPLAT_CONVBF16_BIG (default 96 * 96): register-blocked form
 };
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -126,6 +127,54 @@ __device__ __forceinline__ void load_block(const Args& a, int n, int c0, int y, 
     }
 }
 
+// load_block for sources whose channel counts are not multiples of 8 or whose dtypes differ (the
+// full-resolution heads read cat([features, images (3 channels), projection]) in place): each of
+// the 8 channels picks its own source and dtype.
+__device__ __forceinline__ void load_block_ragged(const Args& a, int n, int c0, int y, int x, uint4 (&st)[8]) {
+    const bool inside = y >= 0 && y < a.h && x >= 0 && x < a.w_;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        st[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (!inside || c >= a.ci) continue;
+        const char* base = reinterpret_cast<const char*>(a.src[0]);
+        int cb = 0, ce = a.src_begin[1], f32 = a.src_f32[0];
+#pragma unroll
+        for (int i = 1; i < kMaxSrc; ++i) {
+            if (i < a.nsrc && c >= a.src_begin[i]) {
+                base = reinterpret_cast<const char*>(a.src[i]);
+                cb = a.src_begin[i];
+                ce = a.src_begin[i + 1];
+                f32 = a.src_f32[i];
+            }
+        }
+        const int cs = ce - cb;
+        const int hs = a.up ? a.h >> 1 : a.h, ws = a.up ? a.w_ >> 1 : a.w_;
+        const int ys = a.up ? y >> 1 : y, xs = a.up ? x >> 1 : x;
+        const size_t e = (((size_t)n * cs + (c - cb)) * hs + ys) * ws + xs;
+        if (f32) {
+            const float* p = reinterpret_cast<const float*>(base) + e;
+            if (a.up) {
+                const float4 u = *reinterpret_cast<const float4*>(p);
+                st[j] = make_uint4(pack_bf16x2(u.x, u.x), pack_bf16x2(u.y, u.y), pack_bf16x2(u.z, u.z),
+                                   pack_bf16x2(u.w, u.w));
+            } else {
+                const float4 u = reinterpret_cast<const float4*>(p)[0], v = reinterpret_cast<const float4*>(p)[1];
+                st[j] = make_uint4(pack_bf16x2(u.x, u.y), pack_bf16x2(u.z, u.w), pack_bf16x2(v.x, v.y),
+                                   pack_bf16x2(v.z, v.w));
+            }
+        } else {
+            const __bf16* p = reinterpret_cast<const __bf16*>(base) + e;
+            if (a.up) {
+                const uint2 u = *reinterpret_cast<const uint2*>(p);
+                st[j] = make_uint4(dup_bf16(u.x), dup_bf16(u.x >> 16), dup_bf16(u.y), dup_bf16(u.y >> 16));
+            } else {
+                st[j] = *reinterpret_cast<const uint4*>(p);
+            }
+        }
+    }
+}
+
 // 8 channels (in[j]: channel j, 8 pixels) -> 8 pixels (out[p]: 8 channels of pixel p)
 __device__ __forceinline__ void transpose8(const uint4 (&in)[8], uint4 (&out)[8]) {
 #pragma unroll
@@ -143,11 +192,17 @@ __device__ __forceinline__ void transpose8(const uint4 (&in)[8], uint4 (&out)[8]
 }
 
 // OCC: waves per SIMD the register allocation targets (2: no spills; 4, the default for bf16
-// sources: more workgroups per CU to hide the staging loads' latency, at the price of a few
-// spilled registers on the 3x3 variants; same-box C3 1057 vs 1042 views/s, profiles/r3/ab_r3d)
-template <int TW, int CT, int KS, bool F32, int OCC>
+// sources: more workgroups per CU to hide the staging loads' latency; same-box C3 1057 vs 1042
+// views/s, profiles/r3/ab_r3d)
+// SRC: 0 bf16 sources, 1 fp32 sources, 2 ragged / mixed (load_block_ragged)
+// WCT x NT: 32-channel co tiles x 32-pixel column tiles per wave. (1, 2) = the small form, LDS
+// epilogue; (2, 4) = the register-blocked form for the compute-heavy convolutions (full-resolution
+// heads, 128-channel levels): per tap 2 A + 4 B LDS reads feed 8 MFMAs (the small form: 3 reads for
+// 2), which takes the kernel off the LDS-bandwidth bound; its epilogue stores from registers.
+template <int TW, int CT, int KS, int SRC, int OCC, int WCT, int NT>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(OCC))) conv_bf16_kernel(Args a) {
-    constexpr int P = 32 * (4 / CT) * kNT;  // pixels per workgroup
+    constexpr int WR = CT / WCT;            // wave rows (co direction)
+    constexpr int P = 32 * NT * (4 / WR);   // pixels per workgroup
     constexpr int TH = P / TW;
     constexpr int HY = KS / 2, HX = KS == 3 ? 8 : 0;  // staged halo rows / columns per side
     constexpr int NTAP = KS * KS;
@@ -157,16 +212,20 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(O
     constexpr int kTasks = SR * 2 * G;
     constexpr int kBuf = SR * 2 * LW;  // 16-B words per buffer
     static_assert(kTasks <= kThreads, "one staging task per thread");
-    constexpr int kEpi = 32 * CT * P * 2 / 16;  // bf16 epilogue tile [32 CT][P] in 16-B words
-    __shared__ uint4 s_lds[2 * kBuf + kEpi];
-    __bf16* const tile_out = reinterpret_cast<__bf16*>(s_lds + 2 * kBuf);
+    static_assert(CT % WCT == 0 && 4 % WR == 0, "wave grid");
+    constexpr bool kLdsEpi = WCT == 1;
+    constexpr int kEpi = kLdsEpi ? 32 * CT * P * 2 / 16 : 0;  // bf16 epilogue tile [32 CT][P]
+    constexpr int kW = CT * NTAP * 64;          // one chunk's A fragments of the CT co blocks
+    constexpr int kWPer = (kW + kThreads - 1) / kThreads;
+    __shared__ uint4 s_lds[2 * kBuf + 2 * kW + kEpi];
+    uint4* const s_w = s_lds + 2 * kBuf;
+    __bf16* const tile_out = reinterpret_cast<__bf16*>(s_lds + 2 * kBuf + 2 * kW);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int c = lane & 31, h = lane >> 5;
     const int per_img = a.tiles_x * a.tiles_y;
     const int ntiles = a.n * per_img;
-    const int ct = wid % CT, grp = wid / CT;
-    const int cob = blockIdx.y * CT + ct;  // this wave's 32-channel output block
+    const int ct0 = (wid % WR) * WCT, grp = wid / WR;  // this wave's first co tile, pixel group
     // this workgroup's pixel tiles: blockIdx.x, blockIdx.x + gridDim.x, ... (at least one)
     const int my_tiles = (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
     const int total = my_tiles * a.nchunk;  // flattened (tile, chunk) iterations
@@ -182,14 +241,33 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(O
     const bool task = tid < kTasks;
     const int tg = tid % G, thf = (tid / G) & 1, trow = tid / (2 * G);
     uint4 st[8];
+    // the chunk's weights for all CT co blocks, [ct][tap][lane], staged through LDS with the input
+    // (loaded once per workgroup instead of once per wave, one iteration ahead); a co block past
+    // c_out reads zeros and its outputs are never stored
+    uint4 wst[kWPer];
     auto load_iter = [&](int it) {
-        if (!task) return;
         const int ti = it / a.nchunk, k = it - ti * a.nchunk;
+#pragma unroll
+        for (int i = 0; i < kWPer; ++i) {
+            const int idx = tid + i * kThreads;
+            const int wct = idx / (NTAP * 64), rem = idx - wct * (NTAP * 64);
+            const int wcob = blockIdx.y * CT + wct;
+            wst[i] = (idx < kW && 32 * wcob < a.co)
+                         ? a.w[((size_t)wcob * a.nchunk + k) * NTAP * 64 + rem]
+                         : make_uint4(0u, 0u, 0u, 0u);
+        }
+        if (!task) return;
         int n, y0, x0;
         tile_origin(ti, n, y0, x0);
-        load_block<F32>(a, n, 16 * k + 8 * thf, y0 - HY + trow, x0 - HX + 8 * tg, st);
+        if constexpr (SRC == 2)
+            load_block_ragged(a, n, 16 * k + 8 * thf, y0 - HY + trow, x0 - HX + 8 * tg, st);
+        else
+            load_block<SRC == 1>(a, n, 16 * k + 8 * thf, y0 - HY + trow, x0 - HX + 8 * tg, st);
     };
     auto store_chunk = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < kWPer; ++i)
+            if (tid + i * kThreads < kW) s_w[buf * kW + tid + i * kThreads] = wst[i];
         if (!task) return;
         uint4 px[8];
         transpose8(st, px);
@@ -197,89 +275,104 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(O
 #pragma unroll
         for (int p = 0; p < 8; ++p) dst[p] = px[p];
     };
-    // a wave whose 32-channel block lies past c_out (c_out not a multiple of 32 CT) reads no
-    // weights and multiplies zeros; its outputs are never stored
-    const bool cvalid = 32 * cob < a.co;
-    const uint4* wsrc = a.w + (size_t)(cvalid ? cob : 0) * a.nchunk * NTAP * 64 + lane;
-    uint4 wf[NTAP];
-    auto load_w = [&](int k, uint4 (&dst)[NTAP]) {
-#pragma unroll
-        for (int tap = 0; tap < NTAP; ++tap)
-            dst[tap] = cvalid ? wsrc[((size_t)k * NTAP + tap) * 64] : make_uint4(0u, 0u, 0u, 0u);
-    };
 
     // LDS word of (pixel p of column tile j) at tap (0, 0): staged row p / TW, column p % TW + HX - KS / 2
-    int bbase[kNT];
+    int bbase[NT];
 #pragma unroll
-    for (int k = 0; k < kNT; ++k) {
-        const int p = 32 * (grp * kNT + k) + c;
+    for (int k = 0; k < NT; ++k) {
+        const int p = 32 * (grp * NT + k) + c;
         bbase[k] = ((p / TW) * 2 + h) * LW + (p % TW) + HX - KS / 2;
     }
-    floatx16 acc[kNT];
+    floatx16 acc[WCT][NT];
 
     // software pipeline over the flattened (tile, chunk) sequence: the loads of iteration it + 1
     // (next chunk, or the next tile's first chunk) fly during iteration it's MFMAs, so the
     // workgroup streams tiles instead of paying a memory round trip per tile
-    // weights are loaded per iteration just before the barrier (L2 hits; no register prefetch,
-    // which would cost 4 NTAP VGPRs and an occupancy step)
     load_iter(0);
     for (int it = 0; it < total; ++it) {
         const int ti = it / a.nchunk, k = it - ti * a.nchunk;
         const int buf = it & 1;
         store_chunk(buf);
-        load_w(k, wf);
         __syncthreads();
         if (it + 1 < total) load_iter(it + 1);
         if (k == 0) {
 #pragma unroll
-            for (int j = 0; j < kNT; ++j)
+            for (int wc = 0; wc < WCT; ++wc)
 #pragma unroll
-                for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+                for (int j = 0; j < NT; ++j)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) acc[wc][j][r] = 0.0f;
         }
         const uint4* sb = s_lds + buf * kBuf;
+        const uint4* sw = s_w + buf * kW + ct0 * NTAP * 64 + lane;
 #pragma unroll
         for (int tap = 0; tap < NTAP; ++tap) {
             const int off = (tap / KS) * 2 * LW + (tap % KS);
-            const bf16x8 av = __builtin_bit_cast(bf16x8, wf[tap]);
+            bf16x8 av[WCT], bv[NT];
 #pragma unroll
-            for (int j = 0; j < kNT; ++j) {
-                const bf16x8 bv = __builtin_bit_cast(bf16x8, sb[bbase[j] + off]);
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[j], 0, 0, 0);
-            }
+            for (int wc = 0; wc < WCT; ++wc) av[wc] = __builtin_bit_cast(bf16x8, sw[(wc * NTAP + tap) * 64]);
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bv[j] = __builtin_bit_cast(bf16x8, sb[bbase[j] + off]);
+#pragma unroll
+            for (int wc = 0; wc < WCT; ++wc)
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    acc[wc][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av[wc], bv[j], acc[wc][j], 0, 0, 0);
         }
         if (k + 1 == a.nchunk) {
-            // epilogue of tile ti: bias + act in fp32 -> bf16 [co_local][pixel] in its own LDS
-            // buffer (its previous readers finished before this iteration's barrier) -> 16-B stores
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int col = 32 * ct + 8 * (r >> 2) + 4 * h + (r & 3);
-                const int co = 32 * cob + 8 * (r >> 2) + 4 * h + (r & 3);
-                const float bias = (a.bias && co < a.co) ? a.bias[co] : 0.0f;
-#pragma unroll
-                for (int j = 0; j < kNT; ++j)
-                    tile_out[col * P + 32 * (grp * kNT + j) + c] = (__bf16)act_fn(acc[j][r] + bias, a.act);
-            }
-            __syncthreads();
             int n, y0, x0;
             tile_origin(ti, n, y0, x0);
-            constexpr int kItems = 32 * CT * P / 8;
+            if constexpr (kLdsEpi) {
+                // bias + act in fp32 -> bf16 [co_local][pixel] in its own LDS buffer (its previous
+                // readers finished before this iteration's barrier) -> 16-B row stores
 #pragma unroll
-            for (int i = tid; i < kItems; i += kThreads) {
-                const int col = i / (P / 8), pg = i % (P / 8);
-                const int co = 32 * CT * blockIdx.y + col;
-                const int py = y0 + (8 * pg) / TW, px = x0 + (8 * pg) % TW;
-                if (co < a.co && py < a.h && px < a.w_) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(tile_out + col * P + 8 * pg);
-                    *reinterpret_cast<uint4*>(a.y + (((size_t)n * a.co + co) * a.h + py) * a.w_ + px) = v;
+                for (int r = 0; r < 16; ++r) {
+                    const int col = 32 * ct0 + 8 * (r >> 2) + 4 * h + (r & 3);
+                    const int co = 32 * (blockIdx.y * CT + ct0) + 8 * (r >> 2) + 4 * h + (r & 3);
+                    const float bias = (a.bias && co < a.co) ? a.bias[co] : 0.0f;
+#pragma unroll
+                    for (int j = 0; j < NT; ++j)
+                        tile_out[col * P + 32 * (grp * NT + j) + c] = (__bf16)act_fn(acc[0][j][r] + bias, a.act);
                 }
+                __syncthreads();
+                constexpr int kItems = 32 * CT * P / 8;
+#pragma unroll
+                for (int i = tid; i < kItems; i += kThreads) {
+                    const int col = i / (P / 8), pg = i % (P / 8);
+                    const int co = 32 * CT * blockIdx.y + col;
+                    const int py = y0 + (8 * pg) / TW, px = x0 + (8 * pg) % TW;
+                    if (co < a.co && py < a.h && px < a.w_) {
+                        const uint4 v = *reinterpret_cast<const uint4*>(tile_out + col * P + 8 * pg);
+                        *reinterpret_cast<uint4*>(a.y + (((size_t)n * a.co + co) * a.h + py) * a.w_ + px) = v;
+                    }
+                }
+            } else {
+                // straight from the accumulators: per register, 32 lanes store one co row's 32
+                // consecutive pixels (64-B segments)
+#pragma unroll
+                for (int wc = 0; wc < WCT; ++wc)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int co = 32 * (blockIdx.y * CT + ct0 + wc) + 8 * (r >> 2) + 4 * h + (r & 3);
+                        if (co >= a.co) continue;
+                        const float bias = a.bias ? a.bias[co] : 0.0f;
+#pragma unroll
+                        for (int j = 0; j < NT; ++j) {
+                            const int p = 32 * (grp * NT + j) + c;
+                            const int py = y0 + p / TW, px = x0 + p % TW;
+                            if (py < a.h && px < a.w_)
+                                a.y[(((size_t)n * a.co + co) * a.h + py) * a.w_ + px] =
+                                    (__bf16)act_fn(acc[wc][j][r] + bias, a.act);
+                        }
+                    }
             }
         }
     }
 }
 
-template <int TW, int CT, int KS>
-static void launch_tw(const Args& a, bool f32, hipStream_t stream) {
-    constexpr int P = 32 * (4 / CT) * kNT;
+template <int TW, int CT, int KS, int WCT = 1, int NT = 2>
+static void launch_tw(const Args& a, int src_mode, hipStream_t stream) {
+    constexpr int P = 32 * NT * (4 / (CT / WCT));
     constexpr int TH = P / TW;
     Args b = a;
     b.tiles_x = ceil_div(a.w_, TW);
@@ -288,24 +381,26 @@ static void launch_tw(const Args& a, bool f32, hipStream_t stream) {
     const int ntiles = a.n * b.tiles_x * b.tiles_y, cob = ceil_div(a.co, 32 * CT);
     const int want = std::max(1, a.wg_target / cob);
     dim3 grid(std::min(ntiles, want), cob);
-    if (f32)
-        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, true, 2>), grid, dim3(kThreads), 0, stream, b);
-    else if (a.occ4)
-        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, false, 4>), grid, dim3(kThreads), 0, stream, b);
+    if (src_mode == 2)
+        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, 2, 2, WCT, NT>), grid, dim3(kThreads), 0, stream, b);
+    else if (src_mode == 1)
+        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, 1, 2, WCT, NT>), grid, dim3(kThreads), 0, stream, b);
+    else if (a.occ4 && WCT == 1)
+        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, 0, 4, WCT, NT>), grid, dim3(kThreads), 0, stream, b);
     else
-        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, false, 2>), grid, dim3(kThreads), 0, stream, b);
+        hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, 0, 2, WCT, NT>), grid, dim3(kThreads), 0, stream, b);
 }
 
 template <int CT, int KS>
-static void launch_ct(const Args& a, bool f32, hipStream_t stream) {
+static void launch_ct(const Args& a, int src_mode, hipStream_t stream) {
     if (a.w_ >= 64)
-        launch_tw<64, CT, KS>(a, f32, stream);
+        launch_tw<64, CT, KS>(a, src_mode, stream);
     else if (a.w_ >= 32)
-        launch_tw<32, CT, KS>(a, f32, stream);
+        launch_tw<32, CT, KS>(a, src_mode, stream);
     else if (a.w_ >= 16)
-        launch_tw<16, CT, KS>(a, f32, stream);
+        launch_tw<16, CT, KS>(a, src_mode, stream);
     else
-        launch_tw<8, CT, KS>(a, f32, stream);
+        launch_tw<8, CT, KS>(a, src_mode, stream);
 }
 
 }  // namespace convbf16
@@ -317,20 +412,23 @@ extern "C" size_t tsplat_conv2d_bf16_weight_bytes(int32_t c_out, int32_t c_in, i
 }
 
 extern "C" int tsplat_conv2d_bf16_fwd(const void* const* srcs, const int32_t* src_channels, int32_t nsrc,
-                                      int32_t src_f32, const void* w_packed, const float* bias, void* y,
+                                      const int32_t* src_f32, const void* w_packed, const float* bias, void* y,
                                       int32_t batch, int32_t height, int32_t width, int32_t c_out, int32_t ksize,
                                       int32_t upsample, int32_t act, void* stream_) {
     using namespace tsplat::convbf16;
-    if (!srcs || !src_channels || nsrc < 1 || nsrc > kMaxSrc || !w_packed || !y) return TSPLAT_EINVAL;
+    if (!srcs || !src_channels || !src_f32 || nsrc < 1 || nsrc > kMaxSrc || !w_packed || !y) return TSPLAT_EINVAL;
     if (batch <= 0 || height <= 0 || width <= 0 || c_out <= 0 || (width & 7) || act < 0 || act > 3)
         return TSPLAT_EINVAL;
     if (!(ksize == 1 || ksize == 3) || !(upsample == 0 || upsample == 1) || (upsample && (height & 1)))
         return TSPLAT_EINVAL;
     Args a{};
     int ci = 0;
+    bool ragged = false;
     for (int s = 0; s < nsrc; ++s) {
-        if (!srcs[s] || src_channels[s] <= 0 || (src_channels[s] & 7)) return TSPLAT_EINVAL;
+        if (!srcs[s] || src_channels[s] <= 0 || !(src_f32[s] == 0 || src_f32[s] == 1)) return TSPLAT_EINVAL;
+        ragged = ragged || (src_channels[s] & 7) || src_f32[s] != src_f32[0];
         a.src[s] = srcs[s];
+        a.src_f32[s] = src_f32[s];
         a.src_begin[s] = ci;
         ci += src_channels[s];
         if ((int64_t)batch * src_channels[s] * height * width >= (1ll << 31)) return TSPLAT_EINVAL;
@@ -355,14 +453,24 @@ extern "C" int tsplat_conv2d_bf16_fwd(const void* const* srcs, const int32_t* sr
         const char* o = getenv("TSPLAT_CONVBF16_OCC");  // "2": the spill-free allocation (A/B knob)
         a.occ4 = !(o && !strcmp(o, "2"));
         a.wg_target = e ? std::max(1, atoi(e)) : (a.occ4 ? 256 * 4 : 256 * 2);
+        const char* bg = getenv("TSPLAT_CONVBF16_BIG");  // A/B knob: c_in * c_out threshold, 0 = off
+        const long big_min = bg ? atol(bg) : 96L * 96L;
+        a.big = big_min > 0 && (long)ci * c_out >= big_min;
     }
     hipStream_t stream = (hipStream_t)stream_;
-    const bool f32 = src_f32 != 0;
+    const int f32 = ragged ? 2 : src_f32[0];  // loader mode
     if (ksize == 3) {
-        if (c_out <= 32)
+        if (a.big && c_out > 32 && width >= 32) {
+            // register-blocked form: 64 co x 512 pixels per workgroup
+            if (width >= 64)
+                launch_tw<64, 2, 3, 2, 4>(a, f32, stream);
+            else
+                launch_tw<32, 2, 3, 2, 4>(a, f32, stream);
+        } else if (c_out <= 32) {
             launch_ct<1, 3>(a, f32, stream);
-        else
+        } else {
             launch_ct<2, 3>(a, f32, stream);
+        }
     } else {
         if (c_out <= 32)
             launch_ct<1, 1>(a, f32, stream);

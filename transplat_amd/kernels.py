@@ -732,16 +732,16 @@ def _bf16_rounded_bias(bias):
 
 def conv_bf16_ok(x, weight, stride=1, padding=None, dilation=1, groups=1, extra=(), upsample: bool = False) -> bool:
     """True when conv2d(up(cat([x, *extra], 1)), weight) runs under bf16 autocast and fits
-    tsplat_conv2d_bf16_fwd: 3x3 / padding 1 or 1x1 / padding 0, stride 1, NCHW contiguous sources of
-    one dtype (fp32 or bf16) with channel counts and the convolved width multiples of 8, at most 4
-    sources; up = optional nearest 2x upsample read in place."""
+    tsplat_conv2d_bf16_fwd: 3x3 / padding 1 or 1x1 / padding 0, stride 1, NCHW contiguous fp32 or
+    bf16 sources (any channel counts, dtypes may differ) with the convolved width a multiple of 8, at
+    most 4 sources; up = optional nearest 2x upsample read in place."""
     if (not _CONV_BF16 or not x.is_cuda or not torch.is_autocast_enabled("cuda")
             or torch.get_autocast_dtype("cuda") != torch.bfloat16 or len(extra) > 3):
         return False
     for t in (x, *extra):
-        if (t.dtype not in (torch.float32, torch.bfloat16) or t.dtype != x.dtype or t.dim() != 4
-                or not t.is_contiguous() or t.device != x.device or t.shape[0] != x.shape[0]
-                or t.shape[2:] != x.shape[2:] or t.shape[1] % 8 or t.numel() >= 2 ** 31):
+        if (t.dtype not in (torch.float32, torch.bfloat16) or t.dim() != 4 or not t.is_contiguous()
+                or t.device != x.device or t.shape[0] != x.shape[0] or t.shape[2:] != x.shape[2:]
+                or t.numel() >= 2 ** 31):
             return False
     # [co, ci, k, k] (k = 1, 3) or a 1x1 Conv1d's [co, ci, 1] (on a [n, c, 1, t] view of its input)
     if not ((weight.dim() == 4 and weight.shape[2] == weight.shape[3] and weight.shape[2] in (1, 3))
@@ -776,8 +776,9 @@ def conv_bf16(x, weight, bias=None, act: str = "none", extra=(), upsample: bool 
     pb = _bf16_rounded_bias(bias) if bias is not None else None
     ptrs = (ctypes.c_void_p * len(srcs))(*[_lib.ptr(t) for t in srcs])
     chans = (ctypes.c_int32 * len(srcs))(*[t.shape[1] for t in srcs])
+    f32 = (ctypes.c_int32 * len(srcs))(*[int(t.dtype == torch.float32) for t in srcs])
     rc = lib.tsplat_conv2d_bf16_fwd(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p),
-                                    len(srcs), int(x.dtype == torch.float32),
+                                    len(srcs), ctypes.cast(f32, ctypes.c_void_p),
                                     _lib.ptr(conv_bf16_pack_weight(weight)), _lib.ptr(pb), _lib.ptr(y), n, h, w,
                                     co, k, int(upsample), _ACTS[act], _lib.stream_ptr(x.device))
     _lib.check(rc, "tsplat_conv2d_bf16_fwd")
