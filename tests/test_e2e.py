@@ -197,3 +197,36 @@ def test_tuned_gemms_keep_outputs(device):
     assert rel(tuned[0], ref[0]) < 1e-3 and rel(tuned[1], ref[1]) < 1e-2
     assert (tuned[2] - ref[2]).abs().max().item() < 2e-2
     assert (tuned[2] - ref[2]).abs().mean().item() < 1e-4
+
+
+@pytest.mark.gpu
+def test_tuned_gemms_keep_outputs_bf16(device):
+    """C3's bf16 library GEMMs replay the allow-list choices of tools/tune_gemms_bf16.py from the same
+    file; the bf16 step with and without them must agree within bf16 noise (the worst-view PSNR
+    between the two >= 40 dB; two bf16 runs differ at ~1e-2 mean abs, test_c3_batch8_bf16_step)."""
+    import torch.cuda.tunable as tun
+
+    from transplat_amd.e2e import build_model
+    from transplat_amd.gemm_tuning import use_tuned_gemms
+
+    model = build_model(device, "bf16")
+    data = S.make_batch(2, image_shape=(256, 256), device=device)
+
+    def run():
+        with torch.no_grad():
+            out = model.test_step(data).color.float()
+        torch.cuda.synchronize()
+        return out.clone()
+
+    was = tun.is_enabled()
+    tun.enable(False)
+    try:
+        ref = run()
+        assert use_tuned_gemms(device, "bf16")
+        tuned = run()
+    finally:
+        tun.enable(was)
+    mse = ((tuned.clamp(0, 1) - ref.clamp(0, 1)) ** 2).flatten(2).mean(-1)
+    psnr = (-10 * torch.log10(mse.clamp_min(1e-20))).min().item()
+    print(f"bf16 tuned vs default GEMMs: worst-view PSNR {psnr:.1f} dB")
+    assert torch.isfinite(tuned).all() and psnr >= 40.0

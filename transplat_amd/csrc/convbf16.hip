@@ -54,7 +54,8 @@ struct Args {
     int tiles_x, tiles_y;
     int wg_target;  // workgroups per launch (all co blocks): a few per CU
     int occ4;       // bf16 sources: the occupancy-4 register allocation (default; C3 1057 vs 1042 views/s)
-    int big;        // 3x3 with c_in * c_out >= TSPLAT_CONVBF16_BIG (default 96 * 96): register-blocked form
+    int big;        // 3x3 with c_in * c_out >= TSPLAT_CONVBF16_BIG (default 96 * 96) and >= 192 workgroups:
+                    // the register-blocked form (C3 1019 -> 1062 views/s, profiles/r3/convbf16)
 };
 
 __device__ __forceinline__ float act_fn(float v, int act) {
@@ -455,7 +456,10 @@ extern "C" int tsplat_conv2d_bf16_fwd(const void* const* srcs, const int32_t* sr
         a.wg_target = e ? std::max(1, atoi(e)) : (a.occ4 ? 256 * 4 : 256 * 2);
         const char* bg = getenv("TSPLAT_CONVBF16_BIG");  // A/B knob: c_in * c_out threshold, 0 = off
         const long big_min = bg ? atol(bg) : 96L * 96L;
-        a.big = big_min > 0 && (long)ci * c_out >= big_min;
+        // ... and only with enough 512-pixel tiles to fill the CUs (16 x 128 -> 128 at 32^2: 64
+        // workgroups, 51 vs 25 us in the small form; at 64^2: 256, 79 vs 97 us for 256 -> 128)
+        const long wgs = ((long)batch * height * width + 511) / 512 * ((c_out + 63) / 64);
+        a.big = big_min > 0 && (long)ci * c_out >= big_min && wgs >= 192;
     }
     hipStream_t stream = (hipStream_t)stream_;
     const int f32 = ragged ? 2 : src_f32[0];  // loader mode
