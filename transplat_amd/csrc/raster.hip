@@ -45,7 +45,6 @@ constexpr int kSortCap = 4096;            // tile lists up to this length are so
 constexpr int kPreThreads = 256;
 constexpr int kRecBytes = 64;             // per-(view, Gaussian) record (Workspace::rec)
 constexpr int kRecFields = 9;             // x, y, conic a b c, opacity, r g b
-constexpr int kRecFieldsRel = 10;         // block-relative form: F, D, E, conic a b c, opacity, r g b
 
 __constant__ float kSH_C0 = 0.28209479177387814f;
 __constant__ float kSH_C1 = 0.4886025119029199f;
@@ -100,7 +99,6 @@ struct Params {
     int diag;  // timing diagnostics only (TSPLAT_RASTER_DIAG; output is wrong when != 0)
     int count_sort;  // 1: counting sort for long tile lists (default); 0: bitonic only (A/B)
     int view_rot;    // render: view v's workgroups take tiles rotated by v * view_rot (load balance)
-    int rel;         // render: block-relative power form (render_kernel<true>)
 };
 
 __device__ __forceinline__ void get_rect(float px, float py, int r, int tx, int ty, int& x0,
@@ -657,21 +655,15 @@ __device__ __forceinline__ bool ellipse_meets_block(float mx, float my, float4 c
 // chunk ahead, the entries whose alpha >= 1/255 box can touch the block are compacted in depth
 // order into the wave's LDS slot (conservative, so exact) and blended branch-free; the wave
 // leaves as soon as all its 64 pixels are saturated.
-// REL: the power is evaluated as a quadratic in the pixel's offset (u, v) from its 8x8 block's
-// centre, with the entry's block-dependent coefficients F, D, E computed once per entry and block
-// at compaction: power2 = F + u (D + a' u + b' v) + v (E + c' v), 5 FMAs per (entry, pixel) instead
-// of 2 subtractions + 3 multiplies + 2 FMAs.
-template <bool REL>
 __global__ void __launch_bounds__(kTileThreads)
 render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_color,
               Workspace ws) {
-    constexpr int NF = REL ? kRecFieldsRel : kRecFields;
     __shared__ uint64_t skeys[kSortCap];
     __shared__ uint32_t s_cnt[kBuckets];
     __shared__ uint32_t s_red[4];
     // per-wave compacted records of the current 64-entry chunk (waves progress independently),
     // field-major: one ds_read_b128 of a field gives 4 consecutive entries = 2 packed pairs
-    __shared__ __attribute__((aligned(16))) float s_rec[kTileThreads / kWave][NF][kWave];
+    __shared__ __attribute__((aligned(16))) float s_rec[kTileThreads / kWave][kRecFields][kWave];
 
     const int v = blockIdx.y;
     // Workgroup (tile, v) and (tile, v') share an XCD and a CU slot in dispatch order, and a
@@ -728,11 +720,10 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
     // e^power = 2^power2 is one v_exp_f32, and the quadratic in Horner form (2 FMAs + 3 multiplies).
     // Scalar fp32 on purpose: v_pk_fma_f32 has the same FLOP rate as v_fma_f32 (twice the cycles),
     // and packing the operands costs register moves.
-    // block centre and this lane's offset from it (REL form)
-    const float bcx = wx0 + 3.5f, bcy = wy0 + 3.5f;
-    const float pu = pfx - bcx, pv = pfy - bcy;
-    // blend(f0, f1, ...): plain form (x, y, ca, cb, cc, ...) or REL form (F, D, E, ca, cb, cc, ...)
-    auto blend_p = [&](float power2, float o, float r, float g, float bl) {
+    auto blend = [&](float x, float y, float ca, float cb, float cc, float o, float r, float g, float bl) {
+        // (ca, cb, cc) = log2(e) (-a/2, -b, -c/2): power2 = dy (cc dy + cb dx) + (ca dx) dx
+        const float dx = x - pfx, dy = y - pfy;
+        const float power2 = fmaf(dy, fmaf(cc, dy, cb * dx), (ca * dx) * dx);
         const float alpha = fminf(0.99f, o * __builtin_amdgcn_exp2f(power2));
         const float test_T = fmaf(-alpha, T, T);
         // reference order: skip power > 0, skip alpha < 1/255, stop if test_T < 1e-4
@@ -746,38 +737,20 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
         T = acc ? test_T : T;
         done = done || stop;
     };
-    auto blend = [&](float x, float y, float ca, float cb, float cc, float o, float r, float g, float bl) {
-        // (ca, cb, cc) = log2(e) (-a/2, -b, -c/2): power2 = dy (cc dy + cb dx) + (ca dx) dx
-        const float dx = x - pfx, dy = y - pfy;
-        blend_p(fmaf(dy, fmaf(cc, dy, cb * dx), (ca * dx) * dx), o, r, g, bl);
-    };
-    auto blend_rel = [&](float F, float D, float E, float ca, float cb, float cc, float o, float r, float g,
-                         float bl) {
-        // power2 at (u, v) from the block centre: F + u (D + ca u + cb v) + v (E + cc v)
-        blend_p(fmaf(pv, fmaf(cc, pv, E), fmaf(pu, fmaf(cb, pv, fmaf(ca, pu, D)), F)), o, r, g, bl);
-    };
 
     struct Quad {
-        float4 f[NF];
+        float4 f[kRecFields];
     };
     auto load_quad = [&](int i, Quad& q) {
 #pragma unroll
-        for (int f = 0; f < NF; ++f) q.f[f] = *reinterpret_cast<const float4*>(&w_rec[f][i]);
-    };
-    auto blend_one = [&](const float (&e)[NF]) {
-        if constexpr (REL)
-            blend_rel(e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7], e[8], e[9]);
-        else
-            blend(e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7], e[8]);
+        for (int f = 0; f < kRecFields; ++f) q.f[f] = *reinterpret_cast<const float4*>(&w_rec[f][i]);
     };
     auto blend_quad = [&](const Quad& q) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float e[NF];
-#pragma unroll
-            for (int f = 0; f < NF; ++f) e[f] = (&q.f[f].x)[k];
-            blend_one(e);
-        }
+        const float4* f = q.f;
+        blend(f[0].x, f[1].x, f[2].x, f[3].x, f[4].x, f[5].x, f[6].x, f[7].x, f[8].x);
+        blend(f[0].y, f[1].y, f[2].y, f[3].y, f[4].y, f[5].y, f[6].y, f[7].y, f[8].y);
+        blend(f[0].z, f[1].z, f[2].z, f[3].z, f[4].z, f[5].z, f[6].z, f[7].z, f[8].z);
+        blend(f[0].w, f[1].w, f[2].w, f[3].w, f[4].w, f[5].w, f[6].w, f[7].w, f[8].w);
     };
 
     const uint32_t* sids = reinterpret_cast<const uint32_t*>(skeys);  // sorted ids (n <= kSortCap)
@@ -820,31 +793,15 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
             ++d_chunks;
             if (hit) {
                 const int pos = __popcll(mask & lt_mask);
-                if constexpr (REL) {
-                    // the entry's quadratic about this block's centre: power2(X - u, Y - v) =
-                    // F + u D + v E + ca u^2 + cb u v + cc v^2
-                    const float X = xy.x - bcx, Y = xy.y - bcy;
-                    w_rec[0][pos] = fmaf(X, fmaf(co.x, X, co.y * Y), co.z * Y * Y);
-                    w_rec[1][pos] = -fmaf(2.0f * co.x, X, co.y * Y);
-                    w_rec[2][pos] = -fmaf(co.y, X, 2.0f * co.z * Y);
-                    w_rec[3][pos] = co.x;
-                    w_rec[4][pos] = co.y;
-                    w_rec[5][pos] = co.z;
-                    w_rec[6][pos] = co.w;
-                    w_rec[7][pos] = rgb.x;
-                    w_rec[8][pos] = rgb.y;
-                    w_rec[9][pos] = rgb.z;
-                } else {
-                    w_rec[0][pos] = xy.x;
-                    w_rec[1][pos] = xy.y;
-                    w_rec[2][pos] = co.x;
-                    w_rec[3][pos] = co.y;
-                    w_rec[4][pos] = co.z;
-                    w_rec[5][pos] = co.w;
-                    w_rec[6][pos] = rgb.x;
-                    w_rec[7][pos] = rgb.y;
-                    w_rec[8][pos] = rgb.z;
-                }
+                w_rec[0][pos] = xy.x;
+                w_rec[1][pos] = xy.y;
+                w_rec[2][pos] = co.x;
+                w_rec[3][pos] = co.y;
+                w_rec[4][pos] = co.z;
+                w_rec[5][pos] = co.w;
+                w_rec[6][pos] = rgb.x;
+                w_rec[7][pos] = rgb.y;
+                w_rec[8][pos] = rgb.z;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -856,12 +813,9 @@ render_kernel(Params p, const float* __restrict__ bg, float* __restrict__ out_co
                 load_quad(i, q);
                 blend_quad(q);
             }
-            for (int i = m4; i < m; ++i) {
-                float e[NF];
-#pragma unroll
-                for (int f = 0; f < NF; ++f) e[f] = w_rec[f][i];
-                blend_one(e);
-            }
+            for (int i = m4; i < m; ++i)
+                blend(w_rec[0][i], w_rec[1][i], w_rec[2][i], w_rec[3][i], w_rec[4][i], w_rec[5][i], w_rec[6][i],
+                      w_rec[7][i], w_rec[8][i]);
             __builtin_amdgcn_wave_barrier();  // reads of this chunk's records precede the next writes
         }
     };
@@ -941,8 +895,6 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
         const char* r = getenv("TSPLAT_RASTER_ROT");
         const int rows = (p.tiles_y + 1) / 3;
         p.view_rot = (r && !strcmp(r, "0")) ? 0 : rows * p.tiles_x;
-        const char* rl = getenv("TSPLAT_RASTER_REL");  // block-relative power form (A/B knob)
-        p.rel = !(rl && !strcmp(rl, "0"));
     }
     if ((size_t)p.T * 2 * sizeof(uint32_t) > 64 * 1024) return TSPLAT_EINVAL;  // LDS histogram
     Workspace ws = carve(workspace, p.G, p.V, p.T, p.capacity, nullptr);
@@ -973,12 +925,8 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
     TSPLAT_PROF_END(prof::kRasterScatter, stream);
     TSPLAT_CHECK_LAUNCH();
     TSPLAT_PROF_BEGIN(prof::kRasterRender, stream);
-    if (p.rel)
-        hipLaunchKernelGGL(render_kernel<true>, dim3(p.T, p.V), dim3(kTileThreads), 0, stream, p, bg,
-                           out_color, ws);
-    else
-        hipLaunchKernelGGL(render_kernel<false>, dim3(p.T, p.V), dim3(kTileThreads), 0, stream, p, bg,
-                           out_color, ws);
+    hipLaunchKernelGGL(render_kernel, dim3(p.T, p.V), dim3(kTileThreads), 0, stream, p, bg,
+                       out_color, ws);
     TSPLAT_PROF_END(prof::kRasterRender, stream);
     TSPLAT_PROF_END(prof::kRasterAll, stream);
     TSPLAT_CHECK_LAUNCH();
