@@ -79,18 +79,26 @@ class TransformerLayer(nn.Module):
         # source [B, L, C]; target [B, L, C] (self) or [B, V-1, L, C] (cross)
         if source.dtype == torch.float32 and self.dim == 128 and not torch.is_autocast_enabled(source.device.type):
             return self._forward_fused(source, target, height, width, attn_num_splits)
-        query = self.q_proj(source)
-        key = self.k_proj(target)
-        value = self.v_proj(target)
+        ln128 = self._ln128_ok(source)
+        if ln128:
+            # bf16 dense mode: the fp32 residual stream is cast once per layer (autocast would cast
+            # it again for every projection that reads it, and for the FFN's concat)
+            source16 = source.to(torch.bfloat16)
+            target16 = source16 if target is source else target.to(torch.bfloat16)
+        else:
+            source16, target16 = source, target
+        query = self.q_proj(source16)
+        key = self.k_proj(target16)
+        value = self.v_proj(target16)
         message = kernels.window_attention(query, key, value, height, width, attn_num_splits, self.with_shift)
-        if self._ln128_ok(source):
+        if ln128:
             # bf16 dense mode: each LayerNorm (+ the `source + message` residual) as one kernel on
             # the bf16 linear output (autocast would run PyTorch's LayerNorm in fp32 between casts)
             if self.no_ffn:
                 return kernels.layer_norm128(self.merge(message), self.norm1, residual=source,
                                              out_dtype=torch.float32)
             message = kernels.layer_norm128(self.merge(message), self.norm1, out_dtype=torch.bfloat16)
-            hidden = self.mlp(torch.cat([source.to(torch.bfloat16), message], dim=-1))
+            hidden = self.mlp(torch.cat([source16, message], dim=-1))
             return kernels.layer_norm128(hidden, self.norm2, residual=source, out_dtype=torch.float32)
         message = self.norm1(self.merge(message))
         if not self.no_ffn:

@@ -186,10 +186,13 @@ class QKVAttentionLegacy(nn.Module):
 
     def forward(self, qkv):
         width = qkv.shape[1]
-        if (qkv.dtype == torch.float32 and width // (3 * self.n_heads) == 32
-                and not torch.is_autocast_enabled("cuda")):
-            # one kernel reading / writing the (v b) layout in place (kernels.qkv_attention_cf)
-            return kernels.qkv_attention_cf(qkv, self.n_heads, self.n_frames if self.use_cross_view_self_attn else 1)
+        if qkv.is_cuda and width // (3 * self.n_heads) == 32 and (
+                qkv.dtype == torch.float32 or torch.is_autocast_enabled("cuda")):
+            # one kernel reading / writing the (v b) layout in place (kernels.qkv_attention_cf); under
+            # bf16 autocast the qkv projection's bf16 output is widened once and the attention runs in
+            # fp32 (the reference's einsum path: bf16 products, fp32 softmax; 8 launches)
+            return kernels.qkv_attention_cf(qkv.float(), self.n_heads,
+                                            self.n_frames if self.use_cross_view_self_attn else 1)
         if self.use_cross_view_self_attn:
             qkv = rearrange(qkv, "(v b) n t -> b n (v t)", v=self.n_frames)
         bs, width, length = qkv.shape
