@@ -257,23 +257,31 @@ uv_coarse_dedup_kernel(Geo g, int nw, const float* __restrict__ feat, const floa
     __syncthreads();
     if (diag == 1) { if (active) out[((size_t)n * HW + p) * g.D + lane] = (float)bm[lane] + key[0].x; return; }
 
-    // 2. rank the distinct corners. Lane l tests word w0 + (l >> 5), bit l & 31; only non-empty
-    //    words are visited (a uniform loop over the ballot of non-empty words).
+    // 2. rank the distinct corners. Lane l holds word wb + l; the non-empty words are visited two
+    //    at a time (a uniform loop over the ballot of non-empty words): half-wave h takes the h-th
+    //    of the pair, lane l & 31 tests its bit. The words come from their owner lanes by
+    //    v_readlane (a uniform index), not by an LDS read per iteration.
     int total = 0;
     for (int wb = 0; wb < nw; wb += 64) {
         const int wl = wb + lane;
         const unsigned mine = wl < nw ? bm[wl] : 0u;
         unsigned long long nz = __ballot(mine != 0u);
         while (nz) {
-            const int w = wb + __ffsll((long long)nz) - 1;
+            const int i0 = __ffsll((long long)nz) - 1;
             nz &= nz - 1ull;
-            const unsigned bits = bm[w];
-            const int l = lane & 31;
-            if (lane < 32) {
-                if ((bits >> l) & 1u) list[total + __popc(bits & ((1u << l) - 1u))] = w * 32 + l;
-                if (lane == 0) pre[w] = (unsigned)total;
+            const int i1 = nz ? __ffsll((long long)nz) - 1 : -1;
+            if (nz) nz &= nz - 1ull;
+            const unsigned b0 = (unsigned)__builtin_amdgcn_readlane((int)mine, i0);
+            const unsigned b1 = i1 >= 0 ? (unsigned)__builtin_amdgcn_readlane((int)mine, i1) : 0u;
+            const int h = lane >> 5, l = lane & 31;
+            if (h == 0 || i1 >= 0) {
+                const unsigned bits = h ? b1 : b0;
+                const int w = wb + (h ? i1 : i0);
+                const int base = total + (h ? __popc(b0) : 0);
+                if ((bits >> l) & 1u) list[base + __popc(bits & ((1u << l) - 1u))] = w * 32 + l;
+                if (l == 0) pre[w] = (unsigned)base;
             }
-            total += __popc(bits);
+            total += __popc(b0) + __popc(b1);
         }
     }
     __syncthreads();
