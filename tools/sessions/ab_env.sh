@@ -1,4 +1,4 @@
-# Same-box A/B of one environment knob on the C2 bench: bash tools/ab_env.sh VAR NEW OLD [bench args]
+# Same-box A/B of one environment knob on the C2 bench: bash tools/sessions/ab_env.sh VAR NEW OLD [bench args]
 export PYTHONPATH=$PWD
 VAR=$1; NEW=$2; OLD=$3; shift 3
 O=gpurun_out/abenv; mkdir -p $O

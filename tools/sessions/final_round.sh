@@ -39,6 +39,6 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats -d $OUT/prof_c3 -o run --outp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof_raster -o run --output-format csv -- python3 $R/bench.py --workload raster --steps 10 --warmup 2 --no-cpu-baseline > $OUT/prof_raster.log 2>&1 || exit 1
 if [ "${NO_PMC:-0}" != "1" ]; then
 step pmc
-cd $R && bash tools/pmc_round.sh || exit 1
+cd $R && bash tools/sessions/pmc_round.sh || exit 1
 fi
 echo done

@@ -2059,7 +2059,7 @@ static bool env_is(const char* name, const char* val) {
 }
 
 // 128-query blocks as 8 x 16-query waves (win_attn_f32x16_kernel) with TSPLAT_WA16=1; default the
-// 4 x 32-query kernel. Same-box A/B (round 3, tools/ab_r3.sh): x16 47.5 vs x32 50.0 us per launch at
+// 4 x 32-query kernel. Same-box A/B (round 3, tools/sessions/ab_r3.sh): x16 47.5 vs x32 50.0 us per launch at
 // the C2 shape, but the C2 step 355.9 / 357.1 vs 360.8 views/s with the concurrent encoder branches
 // (its 138 KB of LDS leaves no room on a CU for the other branch's workgroups).
 static bool use_x16() { return env_is("TSPLAT_WA16", "1"); }
