@@ -46,7 +46,12 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", choices=["e2e", "raster", "selftest"], default="e2e")
-    ap.add_argument("--dense-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--dense-dtype", choices=["bf16x3", "fp32", "bf16"], default="bf16x3",
+                    help="dense convs / GEMMs: bf16x3 = split-bf16 products with fp32 accumulation (the "
+                         "stand-in for the reference's TF32, src/main.py:15; more precise than it), fp32 = "
+                         "exact fp32, bf16 = autocast (narrower than the reference)")
+    ap.add_argument("--attn-dtype", choices=["auto", "fp32", "bf16"], default="auto",
+                    help="window attention: auto = bf16 under bf16 dense layers, else exact fp32")
     ap.add_argument("--dominant", default=None, help="kernel timed for the roofline object")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
     ap.add_argument("--batch", type=int, default=1, help="scenes per step per GPU")
@@ -169,7 +174,7 @@ def committed_traffic(kernel: str, dense_dtype: str, batch: int):
     return None, None
 
 
-def e2e_roofline_info(kernel: str, batch: int, dense_dtype: str = "fp32") -> dict:
+def e2e_roofline_info(kernel: str, batch: int, attn_dtype: str = "fp32") -> dict:
     """Algorithmic HBM bytes (or FLOPs) per launch of the hand-written encoder kernels at 256x256,
     2 views, D = 128, C = 128, per SURVEY §8d (units per launch = `batch` scenes)."""
     hw, c, d, p = 64 * 64, 128, 128, 4
@@ -187,9 +192,9 @@ def e2e_roofline_info(kernel: str, batch: int, dense_dtype: str = "fp32") -> dic
         return {"dominant": kernel, "alg_bytes_per_launch": per, "bound": "hbm"}
     if kernel == "win_attn":
         # 4 L S d FLOPs per window, 8 windows per scene-call (v = 2), fp32 MFMA
-        # bf16 dense mode runs the bf16-MFMA kernel (priced against the dense bf16 peak)
+        # bf16 attention runs the bf16-MFMA kernel (priced against the dense bf16 peak)
         return {"dominant": kernel, "alg_flops_per_launch": 4 * 1024 * 1024 * 128 * 8 * batch, "bound": "mfma",
-                "peak_tflops": BF16_MFMA_PEAK_TFS if dense_dtype == "bf16" else FP32_MFMA_PEAK_TFS}
+                "peak_tflops": BF16_MFMA_PEAK_TFS if attn_dtype == "bf16" else FP32_MFMA_PEAK_TFS}
     if kernel == "raster":
         return {"dominant": kernel, "alg_bytes_per_launch": raster_bytes_per_view(131072, 25, 256, 256) * 3 * batch,
                 "bound": "hbm"}
@@ -336,6 +341,13 @@ def main():
         return selftest_main(args, world, rank)
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
+    attn_dtype = args.attn_dtype if args.attn_dtype != "auto" else ("bf16" if args.dense_dtype == "bf16" else "fp32")
+    if args.workload == "raster":
+        dtype_label = "fp32"
+    else:
+        dtype_label = {"bf16x3": "fp32 (bf16x3 dense, >= TF32)", "fp32": "fp32",
+                       "bf16": "bf16 dense (narrower than the reference's TF32)"}[args.dense_dtype]
+        dtype_label += f" + {attn_dtype} attention + fp32 raster"
     if not args.no_conv_search:
         torch.backends.cudnn.benchmark = True
     from transplat_amd import _lib
@@ -348,8 +360,9 @@ def main():
         from transplat_amd.e2e import build_e2e_workload
 
         step, info, model = build_e2e_workload(args.batch, device, scene_offset=rank * args.batch,
-                                               dense_dtype=args.dense_dtype, graph=not args.no_graph)
-        info.update(e2e_roofline_info(args.dominant or "win_attn", args.batch, args.dense_dtype))
+                                               dense_dtype=args.dense_dtype, graph=not args.no_graph,
+                                               attn_dtype=args.attn_dtype)
+        info.update(e2e_roofline_info(args.dominant or "win_attn", args.batch, attn_dtype))
         cpu_inputs = ("e2e", model)
     if args.dominant and args.workload == "raster":
         info["dominant"] = args.dominant
@@ -388,12 +401,13 @@ def main():
         achieved = info["alg_bytes_per_launch"] / (avg_ms * 1e-3) / 1e9
         peak, unit = HBM_PEAK_GBS, "GB/s"
 
-    traffic, traffic_src = committed_traffic(info["dominant"], args.dense_dtype, args.batch)
+    traffic, traffic_src = committed_traffic(info["dominant"], attn_dtype if info["dominant"] == "win_attn" else "fp32",
+                                             args.batch)
 
     # the step's largest hand-written kernel by time (SURVEY §8d's kernel #1 above stays the
     # headline roofline): the Winograd convolution launches of one step, timed the same way
     conv_roofline = None
-    if args.workload == "e2e" and args.dense_dtype == "fp32":
+    if args.workload == "e2e" and args.dense_dtype in ("fp32", "bf16x3"):
         from transplat_amd import kernels as K
 
         K.WINO_FLOP_LOG = []
@@ -406,11 +420,19 @@ def main():
         if claunches and cms > 0 and len(log) == claunches:
             gemm = sum(f for f, _ in log) / (cms * 1e-3) / 1e12
             direct = sum(f for _, f in log) / (cms * 1e-3) / 1e12
+            if args.dense_dtype == "bf16x3":
+                # three bf16 MFMA products per fp32 product, priced against the dense bf16 peak
+                achieved, peak = 3 * gemm, BF16_MFMA_PEAK_TFS
+                flops = ("bf16 MFMA products 3 * 2*16*ci*co*tiles (hi*hi + hi*lo + lo*hi of the 16 F(2x2,3x3) "
+                         "GEMMs, unpadded)")
+            else:
+                achieved, peak = gemm, FP32_MFMA_PEAK_TFS
+                flops = "Winograd GEMM products 2*16*ci*co*tiles (the 16 F(2x2,3x3) GEMMs, unpadded)"
             conv_roofline = {
-                "kernel": "wino_conv", "bound": "mfma", "achieved": gemm, "peak": FP32_MFMA_PEAK_TFS,
-                "unit": "TFLOP/s", "frac": gemm / FP32_MFMA_PEAK_TFS,
-                "flops": "Winograd GEMM products 2*16*ci*co*tiles (the 16 F(2x2,3x3) GEMMs, unpadded)",
-                "direct_equivalent_achieved": direct, "launches_per_step": claunches / n_prof,
+                "kernel": "wino_conv" if args.dense_dtype == "fp32" else "wino_conv_bf16x3", "bound": "mfma",
+                "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "flops": flops,
+                "fp32_gemm_equivalent_achieved": gemm, "direct_equivalent_achieved": direct,
+                "launches_per_step": claunches / n_prof,
                 "ms_per_step": cms / n_prof, "share_of_step": cms / n_prof / (elapsed / args.steps * 1e3),
             }
 
@@ -427,7 +449,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32" if args.workload == "raster" or args.dense_dtype == "fp32" else "bf16+fp32",
+        "dtype": dtype_label,
         "data": "synthetic",
         "config": {
             "workload": info["workload"],

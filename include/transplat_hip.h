@@ -39,6 +39,14 @@ extern "C" {
 /* Library version / build identification (for the smoke check and the loader). */
 int tsplat_version(void);
 
+/* Debug mode (the upstream rasterizer's `debug` setting, GaussianRasterizationSettings.debug as
+ * passed by src/model/decoder/cuda_splatting.py:120, whose CHECK_CUDA synchronises and checks
+ * after every kernel): with on != 0 every launch of every entry point is followed by a device
+ * synchronisation and an error check, and a failure prints the failing source line to stderr and
+ * returns TSPLAT_EHIP from the entry point that launched it. Not usable inside hipGraph capture
+ * (the Python side refuses). Returns the previous setting. */
+int tsplat_set_debug(int32_t on);
+
 /* Per-kernel timing with HIP events recorded on the launch stream around every launch of ONE
  * kernel (ids: 1 raster preprocess, 2 raster scan, 3 raster scatter, 4 raster render,
  * 5 uv coarse correlation, 6 uv cross correlation, 7 msda, 8 window attention, 9 the whole
@@ -390,6 +398,31 @@ int tsplat_conv3x3_wino_f32_fwd(const float* x, const float* w_packed, const flo
 int tsplat_conv3x3_wino_cat_f32_fwd(const float* const* srcs, const int32_t* chans, int32_t n_src,
                                     const float* w_packed, const float* bias, float* y, int32_t batch,
                                     int32_t height, int32_t width, int32_t c_out, int32_t act, void* stream);
+
+/* The same Winograd convolutions in split-bf16 ("bf16x3") precision, the C2 step's dense-layer
+ * mode standing in for the reference's TF32 (src/main.py:15 + cuDNN's TF32 convolutions; gfx950
+ * has no xf32 MFMA): every operand x = hi + lo (two bf16), every product hi*hi + hi*lo + lo*hi on
+ * v_mfma_f32_32x32x16_bf16 with fp32 accumulation (<= 3 * 2^-18 relative per product, TF32 2^-11).
+ * Same arguments and semantics as tsplat_conv3x3_wino_{,cat_}f32_fwd except w_packed =
+ * tsplat_wino_weight_bf16x3(weight): G g G^T split into hi / lo bf16 and packed as
+ * [16][cobs][ceil(c_in / 16)][hi, lo][64 lanes][8] (tsplat_wino_weight_bf16x3_bytes bytes). */
+size_t tsplat_wino_weight_bf16x3_bytes(int32_t c_out, int32_t c_in);
+int tsplat_wino_weight_bf16x3(const float* weight, void* w_packed, int32_t c_out, int32_t c_in, void* stream);
+int tsplat_conv3x3_wino_bf16x3_fwd(const float* x, const void* w_packed, const float* bias, float* y, int32_t batch,
+                                   int32_t c_in, int32_t height, int32_t width, int32_t c_out, int32_t act,
+                                   void* stream);
+int tsplat_conv3x3_wino_bf16x3_cat_fwd(const float* const* srcs, const int32_t* chans, int32_t n_src,
+                                       const void* w_packed, const float* bias, float* y, int32_t batch,
+                                       int32_t height, int32_t width, int32_t c_out, int32_t act, void* stream);
+
+/* Split-bf16 operands for ONE library bf16 GEMM that computes an fp32 linear layer in bf16x3
+ * precision (the nn.Linear layers of the fp32 path -- DINOv2 qkv / proj / fc1 / fc2,
+ * src/depth_anything_v2/dinov2_layers/{attention,mlp}.py, the transformer FFN's mlp[0],
+ * multiview_transformer.py:327-407 -- in the stand-in for the reference's TF32 matmuls): x [rows, k]
+ * fp32 (k % 4 == 0) -> out [rows, 3k] bf16 = [hi | hi | lo] (weight_order = 0, activations) or
+ * [hi | lo | hi] (weight_order = 1, weights), hi = bf16(x), lo = bf16(x - hi); then
+ * [x_hi | x_hi | x_lo] [W_hi | W_lo | W_hi]^T = x_hi W_hi^T + x_hi W_lo^T + x_lo W_hi^T. */
+int tsplat_split_bf16x3(const float* x, void* out, int64_t rows, int32_t k, int32_t weight_order, void* stream);
 
 /* bf16 3x3 / 1x1 convolution (stride 1, padding ksize / 2) for config C3 (bf16 autocast of the same
  * reference nn.Conv2d layers: ldm_unet/unet.py ResBlock in/out convolutions and 1x1 skips

@@ -219,6 +219,68 @@ def test_conv3x3_wino_kernel(device, monkeypatch, wg, n, ci, co, h, w, bias, act
     assert err < 2e-5, err
 
 
+def tf32_round(t: torch.Tensor) -> torch.Tensor:
+    """fp32 -> TF32 (10 explicit mantissa bits, round to nearest even), as the reference's TF32
+    convolutions / matmuls (src/main.py:15) see their operands."""
+    i = t.float().contiguous().view(torch.int32)
+    r = (i + 0xFFF + ((i >> 13) & 1)) & ~0x1FFF
+    return r.view(torch.float32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", ["auto", "1", "2", "3", "4"])
+@pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES)
+def test_conv3x3_wino_bf16x3_kernel(device, monkeypatch, form, n, ci, co, h, w, bias, act):
+    """Winograd F(2x2, 3x3) in split-bf16 precision (tsplat_conv3x3_wino_bf16x3_fwd: hi*hi + hi*lo +
+    lo*hi on bf16 MFMA, fp32 accumulation) against torch's conv2d in float64, with the launch's own
+    workgroup form and each form forced (TSPLAT_WINO3_FORM: 32 co x 32 tiles, the same with two
+    k-groups, 32 x 64, 64 x 64). Bounds (written here): the same 2e-5 of max |y| as the exact-fp32
+    kernel, and at most 1/8 of the error of the reference's own precision -- TF32 operands
+    (float64 conv of TF32-rounded x and w, TF32's best case: exact accumulation)."""
+    from transplat_amd import kernels as K
+
+    if form != "auto":
+        monkeypatch.setenv("TSPLAT_WINO3_FORM", form)
+    x = seeded((n, ci, h, w), 41)
+    wt = seeded((co, ci, 3, 3), 42) * (1.0 / (9 * ci) ** 0.5)
+    b = seeded((co,), 43) if bias else None
+    fn = {"none": lambda t: t, "relu": torch.relu, "gelu": torch.nn.functional.gelu}[act]
+    bd = b.double() if bias else None
+    ref = fn(torch.nn.functional.conv2d(x.double(), wt.double(), bd, padding=1))
+    ref_tf32 = fn(torch.nn.functional.conv2d(tf32_round(x).double(), tf32_round(wt).double(), bd, padding=1))
+    args = (x.to(device), wt.to(device), b.to(device) if bias else None, act)
+    out3 = K.conv3x3_wino(*args, precision="bf16x3").cpu().double()
+    out32 = K.conv3x3_wino(*args, precision="fp32").cpu().double()
+    scale = ref.abs().max().item()
+    e3, e32, etf = ((o - ref).abs().max().item() / scale for o in (out3, out32, ref_tf32))
+    print(f"wino bf16x3 form {form} {(n, ci, co, h, w)}: rel err {e3:.2e} (exact fp32 kernel {e32:.2e}, "
+          f"TF32 operands {etf:.2e}; ratio to fp32 {e3 / max(e32, 1e-12):.1f}, to TF32 {e3 / etf:.3f})")
+    assert e3 < 2e-5, e3
+    assert e3 <= etf / 8, (e3, etf)
+
+
+@pytest.mark.gpu
+def test_conv3x3_wino_bf16x3_concat_and_production_size(device):
+    """bf16x3 Winograd on the to_gaussians head's three sources at 256^2 (2 x 163 -> 168, the
+    64 x 64 workgroup form) equals the kernel on the materialised concatenation bit for bit, and
+    stays within 2e-5 of MIOpen's fp32 conv2d; the weight cache follows in-place updates."""
+    from transplat_amd import kernels as K
+
+    parts = [seeded((2, c, 256, 256), 60 + c).to(device) for c in (32, 3, 128)]
+    wt = (seeded((168, 163, 3, 3), 63) * (1.0 / (9 * 163) ** 0.5)).to(device)
+    b = seeded((168,), 64).to(device)
+    y = K.conv3x3_wino(parts[0], wt, b, extra=tuple(parts[1:]), precision="bf16x3")
+    cat = torch.cat(parts, 1)
+    assert torch.equal(y, K.conv3x3_wino(cat, wt, b, precision="bf16x3"))
+    ref = torch.nn.functional.conv2d(cat, wt, b, padding=1)
+    assert ((y - ref).abs().max() / ref.abs().max()).item() < 2e-5
+    with torch.no_grad():
+        wt.mul_(2.0)
+    y2 = K.conv3x3_wino(cat, wt, None, precision="bf16x3")
+    ref2 = torch.nn.functional.conv2d(cat, wt, None, padding=1)
+    assert ((y2 - ref2).abs().max() / ref2.abs().max()).item() < 2e-5
+
+
 @pytest.mark.gpu
 def test_conv3x3_wino_weight_cache_tracks_updates(device):
     """The transformed-filter cache is keyed on the live weight tensor and its version: an in-place

@@ -122,12 +122,16 @@ def test_uv_coarse_kernel(device, monkeypatch, hw, b, variant):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("hw,b,variant", [(16, 1, "table"), (24, 2, "table"), (64, 1, "table"), (16, 1, "direct"),
-                                          (24, 2, "direct"), (24, 2, "table_bf16"), (64, 1, "table_bf16")])
+                                          (24, 2, "direct"), (24, 2, "table_bf16"), (64, 1, "table_bf16"),
+                                          (24, 2, "table_bf16x3"), (64, 1, "table_bf16x3")])
 def test_uv_cross_kernel(device, hw, b, variant):
     """Both forms of the fine cross correlation: the correlation-table gather (default) and the
     direct feature-row sampling kernel; table_bf16: a bf16 value (bf16 dense mode, the value_proj
     output) takes the split-bf16 table GEMM (key = hi + lo bf16 halves, fp32 accumulate), checked
-    against the fp32 restatement on the same bf16-exact values."""
+    against the fp32 restatement on the same bf16-exact values; table_bf16x3: fp32 key and value in
+    the bf16x3 dense mode (both split, one K = 3C bf16 GEMM), at the same 1e-4 bound."""
+    import contextlib
+
     from transplat_amd import kernels as K
 
     op = K.uv_cross if variant != "direct" else K.uv_cross_direct
@@ -139,7 +143,9 @@ def test_uv_cross_kernel(device, hw, b, variant):
     offsets = seeded((b * 2, hw * hw, 128 * 4 * 2), 43, 2.0)
     logits = seeded((b * 2, hw * hw, 128 * 4), 44)
     ref = E.uv_cross(value.float(), key, intr, pose, disp, offsets, logits, hw, hw)
-    out = op(*(t.to(device) for t in (value, key, intr, pose, disp, offsets, logits)), hw, hw).cpu()
+    mode = K.dense_precision("bf16x3") if variant == "table_bf16x3" else contextlib.nullcontext()
+    with mode:
+        out = op(*(t.to(device) for t in (value, key, intr, pose, disp, offsets, logits)), hw, hw).cpu()
     assert (out - ref).abs().max().item() < 1e-4
 
 
@@ -333,6 +339,14 @@ def test_group_norm_kernel(device, shape, groups, act, res, pb):
     assert out_b.dtype == torch.bfloat16
     # one bf16 rounding of the output (2^-8 relative) on top of fp32 arithmetic
     assert (out_b.float().cpu() - ref_b).abs().max().item() < 8e-3 * max(1.0, ref_b.abs().max().item())
+    if res:
+        # an fp32 residual beside a bf16 x (an identity skip of an fp32 stream): the module path's
+        # bf16(norm) + fp32 residual, promoted to fp32 -- the residual is not narrowed to bf16
+        out_m = K.group_norm(xb.to(device), groups, w.to(device), b.to(device), 1e-5, act, r.to(device),
+                             bias.to(device) if pb else None)
+        assert out_m.dtype == torch.float32
+        ref_m = E.group_norm(xb.float(), groups, w, b, 1e-5, act, None, bias).bfloat16().float() + r
+        assert (out_m.cpu() - ref_m).abs().max().item() < 8e-3 * max(1.0, ref_m.abs().max().item())
 
 
 @pytest.mark.gpu

@@ -26,6 +26,13 @@ from transplat_amd.model.decoder.hip_splatting import RasterCameras, prepare_cam
 
 ATOL = 1e-4
 MAX_FLAGGED = 0.01  # fraction of pixels the threshold flags may exclude
+# flagged pixels are not exempt from every bound: a flipped decision moves a pixel by at most about
+# alpha * T of the entry it decides, so their L-inf is capped too (measured worst: 1.8e-3 on the
+# DTU stress scene), at most MAX_ABOVE of the image may exceed ATOL at all, and at most
+# MAX_AMBIGUOUS_RADII of the (view, Gaussian) radii may be excused by the ambiguity flags
+FLAGGED_CAP = 2e-2
+MAX_ABOVE = 1e-3
+MAX_AMBIGUOUS_RADII = 1e-3
 
 
 def _cams(ext, K, near, far, bg):
@@ -147,10 +154,16 @@ def parity_report(color, radii, ref, atol=ATOL, max_flagged=MAX_FLAGGED, tag="")
           f"power {int(((pflag & oracle_raster.FLAG_POWER) > 0).sum())}, alpha {int(((pflag & oracle_raster.FLAG_ALPHA) > 0).sum())}, "
           f"T {int(((pflag & oracle_raster.FLAG_T) > 0).sum())}), L-inf incl. flagged {float(err.max()):.3e}; "
           f"ambiguous radii {int(gflag.sum())}")
+    n_above = int((err > atol).sum())
+    print(f"  pixels above {atol:g}: {n_above} ({n_above / err.size:.4%}); radii excused as ambiguous: "
+          f"{int(gflag.sum())} of {gflag.size}")
     bad = (radii != radii_ref) & ~gflag
     assert not bad.any(), f"{int(bad.sum())} radii differ (first at {np.argwhere(bad)[0]})"
+    assert gflag.sum() <= MAX_AMBIGUOUS_RADII * gflag.size, f"{int(gflag.sum())} ambiguous radii"
     assert linf <= atol, f"L-inf {linf:.3e} > {atol} on unflagged pixels"
     assert n_flag <= max_flagged * clear.size, f"{n_flag} flagged pixels > {max_flagged:.1%}"
+    assert float(err.max()) <= FLAGGED_CAP, f"L-inf {float(err.max()):.3e} > {FLAGGED_CAP} on flagged pixels"
+    assert n_above <= MAX_ABOVE * err.size, f"{n_above} pixels above {atol} > {MAX_ABOVE:.1%} of the image"
     return linf, n_flag, clear.size, float(err.max())
 
 

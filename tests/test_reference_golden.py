@@ -249,6 +249,9 @@ def test_hip_render_depth_vs_reference_inputs(device, mode):
           f"{int((~clear).sum())} of {clear.numel()} pixels flagged")
     assert float(err[clear].max()) <= 1e-4 * scale
     assert int((~clear).sum()) <= 0.01 * clear.numel()
+    # flagged pixels too: every pixel within 2e-2 of the depth scale, at most 1e-3 of them above 1e-4
+    assert float(err.max()) <= 2e-2 * scale
+    assert int((err > 1e-4 * scale).sum()) <= 1e-3 * err.numel()
     assert n == depth.shape[0] * depth.shape[1]
 
 

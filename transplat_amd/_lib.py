@@ -36,6 +36,7 @@ _I32 = ctypes.c_int32
 # name -> (restype, argtypes); must match include/transplat_hip.h exactly
 SIGNATURES = {
     "tsplat_version": (ctypes.c_int, []),
+    "tsplat_set_debug": (ctypes.c_int, [_I32]),
     "tsplat_prof_enable": (ctypes.c_int, [_I32]),
     "tsplat_prof_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I32)]),
     "tsplat_raster_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, _I32, _I32, _I32]),
@@ -84,6 +85,11 @@ SIGNATURES = {
     "tsplat_wino_weight_f32": (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     "tsplat_conv3x3_wino_f32_fwd": (ctypes.c_int, [_P, _P, _P, _P] + [_I32] * 6 + [_P]),
     "tsplat_conv3x3_wino_cat_f32_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P] + [_I32] * 5 + [_P]),
+    "tsplat_wino_weight_bf16x3_bytes": (ctypes.c_size_t, [_I32, _I32]),
+    "tsplat_wino_weight_bf16x3": (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
+    "tsplat_conv3x3_wino_bf16x3_fwd": (ctypes.c_int, [_P, _P, _P, _P] + [_I32] * 6 + [_P]),
+    "tsplat_conv3x3_wino_bf16x3_cat_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P] + [_I32] * 5 + [_P]),
+    "tsplat_split_bf16x3": (ctypes.c_int, [_P, _P, ctypes.c_int64, _I32, _I32, _P]),
     "tsplat_conv2d_bf16_weight_bytes": (ctypes.c_size_t, [_I32, _I32, _I32]),
     "tsplat_conv2d_bf16_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P] + [_I32] * 7 + [_P]),
 }
@@ -114,6 +120,8 @@ def load(build_if_missing: bool = False):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if os.environ.get("TSPLAT_DEBUG", "0") == "1":  # every entry point: sync + check per launch
+        lib.tsplat_set_debug(1)
     _lib = lib
     return lib
 

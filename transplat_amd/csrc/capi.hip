@@ -1,4 +1,6 @@
 // Library identification + the kernel-timing facility of the C-ABI (include/transplat_hip.h).
+#include <stdio.h>
+
 #include <vector>
 
 #include "prof.h"
@@ -54,7 +56,25 @@ ExtEvents ext_events(int kid) {
 }  // namespace prof
 }  // namespace tsplat
 
+namespace tsplat {
+int g_debug = 0;
+
+int debug_check(const char* file, int line) {
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipGetLastError();
+    if (e == hipSuccess) return 0;
+    fprintf(stderr, "[tsplat debug] %s:%d: %s\n", file, line, hipGetErrorString(e));
+    return -1;
+}
+}  // namespace tsplat
+
 extern "C" int tsplat_version(void) { return 1; }
+
+extern "C" int tsplat_set_debug(int32_t on) {
+    const int was = tsplat::g_debug;
+    tsplat::g_debug = on != 0;
+    return was;
+}
 
 extern "C" int tsplat_prof_enable(int32_t kernel_id) {
     using namespace tsplat::prof;

@@ -8,10 +8,18 @@
 
 #include "../../include/transplat_hip.h"
 
-#define TSPLAT_CHECK_LAUNCH()                                        \
-    do {                                                             \
-        hipError_t _e = hipGetLastError();                           \
-        if (_e != hipSuccess) return TSPLAT_EHIP;                    \
+namespace tsplat {
+// tsplat_set_debug (capi.hip): synchronise + check after every launch
+extern int g_debug;
+int debug_check(const char* file, int line);
+}  // namespace tsplat
+
+#define TSPLAT_CHECK_LAUNCH()                                                      \
+    do {                                                                           \
+        hipError_t _e = hipGetLastError();                                         \
+        if (_e != hipSuccess) return TSPLAT_EHIP;                                  \
+        if (tsplat::g_debug && tsplat::debug_check(__FILE__, __LINE__) != 0)       \
+            return TSPLAT_EHIP;                                                    \
     } while (0)
 
 #define TSPLAT_CHECK(expr)                                           \

@@ -1,0 +1,454 @@
+// 3x3 / stride 1 / pad 1 convolution as Winograd F(2x2, 3x3) on split-bf16 ("bf16x3") MFMA: the
+// fp32 dense-layer precision mode of the C2 step (the reference runs these convolutions in TF32,
+// src/main.py:15 + cuDNN's default; gfx950 has no xf32 MFMA). Same convolutions as winoconv.hip
+// (depth_predictor_trans.py:110-125 heads, ldm_unet/unet.py ResBlocks, the UniMatch CNN 3x3s).
+//
+// Every fp32 GEMM operand x is split as x = xh + xl (xh = bf16(x), xl = bf16(x - xh); x - xh is
+// exact in fp32), and each product as xh yh + xh yl + xl yh -- three v_mfma_f32_32x32x16_bf16 with
+// fp32 accumulation. The dropped xl yl term and xl's rounding leave <= 3 * 2^-18 relative per
+// product (TF32 rounds each operand to 2^-11), at 3 / 16 of the exact-fp32 MFMA cycles.
+//
+// Winograd as in winoconv.hip: M[xi][co][t] = sum_ci U[xi][co][ci] V[xi][ci][t], V = B^T d B of the
+// 4x4 input patch of output tile t, U = G g G^T (fp32, split once per weight version), y = A^T M A.
+// Workgroup: 4 * CB * KS waves; CB 32-channel output blocks x T = 32 * NB output tiles; wave
+// (k-group kg, co block hh, transform row r) owns the 4 GEMMs xi = 4 r + s of its co block for all
+// NB tile blocks (4 * NB accumulator tiles). Per 16-channel chunk every thread transforms PP
+// channel pairs of one tile (lanes = consecutive tiles: coalesced loads, conflict-free LDS writes),
+// splits each V value into hi / lo bf16 and stores the pair as one dword of
+//   sV[hl][xi][pair 8][tile T]   (pair p = channels 2p, 2p + 1 of the chunk),
+// so a B fragment (lane = tile n, half h: channels 8h .. 8h + 7) is 4 dwords at stride T (two
+// ds_read2 instructions). A = the packed U fragment, one 16-B load per (xi, hi / lo) and lane.
+// Double-buffered sV, one barrier per chunk; the next chunk's patch loads and A fragments are in
+// flight during the current MFMAs. KS = 2 splits the chunks of one output block over two k-groups
+// (few-workgroup grids of the 32^2-64^2 maps); their Z slabs are summed in the epilogue.
+#include <stdlib.h>
+
+#include "common.h"
+#include "prof.h"
+
+namespace tsplat {
+namespace wino3 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kMaxSrc = 6;
+constexpr int kMaxCiPad = 1024;
+
+struct Args {
+    const float* src[kMaxSrc];
+    int cs[kMaxSrc];
+    int nsrc;
+    const uint4* u;      // packed U: [16 xi][cobs][nchunk][2 hl][64 lanes][8 bf16]
+    const float* bias;   // [co] or null
+    float* y;            // [n][co][h][w]
+    int n, ci, h, w, co, ci_pad, cobs, nchunk;  // cobs: 32-channel blocks in the packing
+    int th, tw, tbx, tby, bx, by;
+    int act;             // 0 none, 1 ReLU, 2 GELU (erf)
+    int cob_base;        // first 32-channel output block of this launch
+};
+
+__device__ __forceinline__ float act_fn(float v, int act) {
+    if (act == 1) return fmaxf(v, 0.0f);
+    if (act == 2) return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f));
+    return v;
+}
+
+__device__ __forceinline__ uint32_t bf16_bits(float v) { return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v); }
+
+// hi / lo halves of the channel pair (a, b) as two packed dwords (channel a in the low half)
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
+    hi = bf16_bits(a) | (bf16_bits(b) << 16);
+    const float ah = __builtin_bit_cast(float, hi << 16), bh = __builtin_bit_cast(float, hi & 0xffff0000u);
+    lo = bf16_bits(a - ah) | (bf16_bits(b - bh) << 16);
+}
+
+// U = G g G^T (as winoconv.hip's weight_kernel), split into hi / lo bf16 and packed as the A operand
+// of v_mfma_f32_32x32x16_bf16: lane l (co = 32 b + (l & 31), h = l >> 5), element j <- ci = 16 k + 8 h + j
+__global__ void __launch_bounds__(256) weight_kernel(const float* __restrict__ g, __bf16* __restrict__ u, int co,
+                                                     int ci, int ci_pad, int cobs) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;  // over cobs * 32 * ci_pad
+    if (idx >= cobs * 32 * ci_pad) return;
+    const int c = idx % ci_pad, o = idx / ci_pad;
+    float k[3][3];
+    const bool ok = o < co && c < ci;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) k[i][j] = ok ? g[((size_t)o * ci + c) * 9 + 3 * i + j] : 0.0f;
+    float t[4][3];  // G g
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        t[0][j] = k[0][j];
+        t[1][j] = 0.5f * (k[0][j] + k[1][j] + k[2][j]);
+        t[2][j] = 0.5f * (k[0][j] - k[1][j] + k[2][j]);
+        t[3][j] = k[2][j];
+    }
+    const int b = o / 32, ol = o % 32;
+    const int chunk = c / 16, h = (c >> 3) & 1, j = c & 7;
+    const int nchunk = ci_pad / 16;
+    const size_t lane = 32 * h + ol;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float uu[4] = {t[r][0], 0.5f * (t[r][0] + t[r][1] + t[r][2]), 0.5f * (t[r][0] - t[r][1] + t[r][2]),
+                             t[r][2]};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const size_t base = ((((size_t)(4 * r + s) * cobs + b) * nchunk + chunk) * 2) * 64;
+            const __bf16 hi = (__bf16)uu[s];
+            const __bf16 lo = (__bf16)(uu[s] - (float)hi);
+            u[((base + lane) * 8) + j] = hi;
+            u[((base + 64 + lane) * 8) + j] = lo;
+        }
+    }
+}
+
+template <int T>
+struct Patch {
+    int img, y0, x0;
+    bool rok[4], cok[4];
+
+    __device__ __forceinline__ Patch(const Args& a, int blk_linear, int t) {
+        const int blocks_per_img = a.bx * a.by;
+        img = blk_linear / blocks_per_img;
+        const int blk = blk_linear % blocks_per_img;
+        const int ty = (blk / a.bx) * a.tby + t / a.tbx, tx = (blk % a.bx) * a.tbx + t % a.tbx;
+        const bool tile_ok = ty < a.th && tx < a.tw;
+        y0 = 2 * ty - 1;
+        x0 = 2 * tx - 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            rok[i] = tile_ok && y0 + i >= 0 && y0 + i < a.h;
+            cok[i] = x0 + i >= 0 && x0 + i < a.w;
+        }
+    }
+
+    __device__ __forceinline__ void load(const Args& a, const float* const* planes, int c, float (&d)[16]) const {
+        const __attribute__((address_space(1))) float* src =
+            (const __attribute__((address_space(1))) float*)planes[min(c, a.ci_pad - 1)];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool ok = c < a.ci && rok[i] && cok[j];
+                d[4 * i + j] = ok ? src[(size_t)(y0 + i) * a.w + (x0 + j)] : 0.0f;
+            }
+    }
+};
+
+// V = B^T d B of the channel pair (da, db) -> hi / lo dwords of every xi into sV (this thread's tile
+// and pair; xi stride 8 * T dwords, hl stride 16 * 8 * T)
+template <int T>
+__device__ __forceinline__ void transform_pair(const float (&da)[16], const float (&db)[16], uint32_t* sV) {
+    float ta[16], tb[16];  // B^T d
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        ta[0 + j] = da[0 + j] - da[8 + j];
+        ta[4 + j] = da[4 + j] + da[8 + j];
+        ta[8 + j] = da[8 + j] - da[4 + j];
+        ta[12 + j] = da[4 + j] - da[12 + j];
+        tb[0 + j] = db[0 + j] - db[8 + j];
+        tb[4 + j] = db[4 + j] + db[8 + j];
+        tb[8 + j] = db[8 + j] - db[4 + j];
+        tb[12 + j] = db[4 + j] - db[12 + j];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const float va[4] = {ta[4 * r] - ta[4 * r + 2], ta[4 * r + 1] + ta[4 * r + 2], ta[4 * r + 2] - ta[4 * r + 1],
+                             ta[4 * r + 1] - ta[4 * r + 3]};
+        const float vb[4] = {tb[4 * r] - tb[4 * r + 2], tb[4 * r + 1] + tb[4 * r + 2], tb[4 * r + 2] - tb[4 * r + 1],
+                             tb[4 * r + 1] - tb[4 * r + 3]};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            uint32_t hi, lo;
+            split_pair(va[s], vb[s], hi, lo);
+            sV[(4 * r + s) * 8 * T] = hi;
+            sV[(16 + 4 * r + s) * 8 * T] = lo;
+        }
+    }
+}
+
+template <int CB, int NB, int KS>
+__global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
+    constexpr int T = 32 * NB;                 // tiles per workgroup
+    constexpr int GT = 256 * CB;               // threads per k-group
+    constexpr int ROWS = GT / T;               // pair rows per pass
+    constexpr int PP = 8 / ROWS;               // channel pairs per thread per chunk
+    static_assert(ROWS * PP == 8, "pairs per chunk");
+    constexpr int BUF = 2 * 16 * 8 * T;        // dwords per sV buffer (hi + lo)
+    constexpr int CO = 32 * CB;
+    __shared__ __attribute__((aligned(16))) uint32_t smem[KS * 2 * BUF];
+    __shared__ const float* planes[kMaxCiPad];
+
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int kg = wid / (4 * CB), wg = wid % (4 * CB);
+    const int hh = wg >> 2, rr = wg & 3;
+    const int gtid = tid % GT;
+    const int t = gtid % T, prow = gtid / T;
+    const Patch<T> pt(a, blockIdx.x, t);
+
+    for (int c = tid; c < a.ci_pad; c += 256 * CB * KS) {
+        const float* src = nullptr;
+        int rem = min(c, a.ci - 1);
+        for (int q = 0; q < a.nsrc && !src; ++q) {
+            if (rem < a.cs[q])
+                src = a.src[q] + ((size_t)pt.img * a.cs[q] + rem) * ((size_t)a.h * a.w);
+            else
+                rem -= a.cs[q];
+        }
+        planes[c] = src;
+    }
+    __syncthreads();
+
+    const int cob = a.cob_base + blockIdx.y * CB + hh;
+    const bool co_ok = cob < a.cobs;
+    // A fragments: [xi][cob][chunk][hl][lane] uint4
+    const uint4* ub = a.u + ((size_t)(4 * rr) * a.cobs + (co_ok ? cob : 0)) * a.nchunk * 128 + lane;
+    const size_t xi_stride = (size_t)a.cobs * a.nchunk * 128;
+    uint4 af[4][2];
+    auto load_a = [&](int chunk, int s0, int s1) {
+        const bool ok = co_ok && chunk < a.nchunk;
+#pragma unroll
+        for (int s = s0; s < s1; ++s)
+#pragma unroll
+            for (int hl = 0; hl < 2; ++hl)
+                af[s][hl] = ok ? ub[s * xi_stride + (size_t)chunk * 128 + hl * 64] : make_uint4(0u, 0u, 0u, 0u);
+    };
+
+    floatx16 acc[4][NB];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[s][nb][e] = 0.0f;
+
+    float d[PP][2][16];
+    auto load_patches = [&](int chunk) {
+#pragma unroll
+        for (int q = 0; q < PP; ++q) {
+            const int c0 = chunk * 16 + 2 * (prow + q * ROWS);
+            pt.load(a, planes, c0, d[q][0]);
+            pt.load(a, planes, c0 + 1, d[q][1]);
+        }
+    };
+    uint32_t* sG = smem + kg * 2 * BUF;
+    auto transform = [&](uint32_t* sV) {
+#pragma unroll
+        for (int q = 0; q < PP; ++q) transform_pair<T>(d[q][0], d[q][1], sV + (prow + q * ROWS) * T + t);
+    };
+    // MFMAs of xi s0 .. s1 - 1 on buffer sV: B fragment of lane (n, h) = dwords [hl][xi][4 h + c][32 nb + n]
+    auto mfma = [&](const uint32_t* sV, int s0, int s1) {
+        const uint32_t* bb = sV + (4 * (lane >> 5)) * T + (lane & 31);
+#pragma unroll
+        for (int s = s0; s < s1; ++s) {
+            const int xi = 4 * rr + s;
+            const bf16x8 ah = __builtin_bit_cast(bf16x8, af[s][0]);
+            const bf16x8 al = __builtin_bit_cast(bf16x8, af[s][1]);
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) {
+                const uint32_t* ph = bb + xi * 8 * T + 32 * nb;
+                const uint32_t* pl = ph + 16 * 8 * T;
+                const uint4 vh = make_uint4(ph[0], ph[T], ph[2 * T], ph[3 * T]);
+                const uint4 vl = make_uint4(pl[0], pl[T], pl[2 * T], pl[3 * T]);
+                const bf16x8 bh = __builtin_bit_cast(bf16x8, vh);
+                const bf16x8 bl = __builtin_bit_cast(bf16x8, vl);
+                acc[s][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[s][nb], 0, 0, 0);
+                acc[s][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[s][nb], 0, 0, 0);
+                acc[s][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[s][nb], 0, 0, 0);
+            }
+        }
+    };
+
+    // k-group kg takes chunks kg, kg + KS, ...; every group runs the same iteration count (a chunk
+    // past the last one is all zeros) so the groups meet at every barrier
+    const int iters = (a.nchunk + KS - 1) / KS;
+    load_patches(kg);
+    load_a(kg, 0, 4);
+    transform(sG);
+    if (iters > 1) load_patches(kg + KS);
+    __syncthreads();
+    for (int it = 0; it < iters; ++it) {
+        const int ch = kg + it * KS;
+        const uint32_t* sV = sG + (it & 1) * BUF;
+        const bool more = it + 1 < iters;
+        mfma(sV, 0, 2);
+        if (more) load_a(ch + KS, 0, 2);  // the first two xi's registers are free again
+        if (more) {
+            transform(sG + ((it + 1) & 1) * BUF);
+            if (it + 2 < iters) load_patches(ch + 2 * KS);
+        }
+        mfma(sV, 2, 4);
+        if (more) {
+            load_a(ch + KS, 2, 4);
+            __syncthreads();  // sV(it + 1) complete; every wave is done reading sV(it)
+        }
+    }
+    __syncthreads();  // all MFMAs' LDS reads done: smem becomes Z[kg][r][j][co CO][tile T]
+    float* zs = reinterpret_cast<float*>(smem) + kg * (8 * CO * T);
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int col = 32 * hh + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            const int tt = 32 * nb + (lane & 31);
+            zs[((rr * 2 + 0) * CO + col) * T + tt] = acc[0][nb][e] + acc[1][nb][e] + acc[2][nb][e];
+            zs[((rr * 2 + 1) * CO + col) * T + tt] = acc[1][nb][e] - acc[2][nb][e] - acc[3][nb][e];
+        }
+    __syncthreads();
+    const float* z0 = reinterpret_cast<const float*>(smem);
+    if (KS > 1) {
+        float* zw = reinterpret_cast<float*>(smem);
+        for (int i = tid; i < 8 * CO * T; i += 256 * CB * KS) {
+            float z = zw[i];
+#pragma unroll
+            for (int g2 = 1; g2 < KS; ++g2) z += zw[g2 * (8 * CO * T) + i];
+            zw[i] = z;
+        }
+        __syncthreads();
+    }
+    const int blocks_per_img = a.bx * a.by;
+    const int blk = blockIdx.x % blocks_per_img;
+    const size_t hw = (size_t)a.h * a.w;
+    for (int pidx = tid; pidx < CO * T; pidx += 256 * CB * KS) {
+        const int col = pidx / T, t2 = pidx % T;
+        const int o = (a.cob_base + blockIdx.y * CB) * 32 + col;
+        const int oty = (blk / a.bx) * a.tby + t2 / a.tbx, otx = (blk % a.bx) * a.tbx + t2 % a.tbx;
+        if (o >= a.co || oty >= a.th || otx >= a.tw) continue;
+        const float bv = a.bias ? a.bias[o] : 0.0f;
+        float z[4][2];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) z[r][j] = z0[((r * 2 + j) * CO + col) * T + t2];
+        float* dst = a.y + ((size_t)pt.img * a.co + o) * hw;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int py = 2 * oty + i;
+            if (py >= a.h) continue;
+            const float y0v = i == 0 ? z[0][0] + z[1][0] + z[2][0] : z[1][0] - z[2][0] - z[3][0];
+            const float y1v = i == 0 ? z[0][1] + z[1][1] + z[2][1] : z[1][1] - z[2][1] - z[3][1];
+            const float r0 = act_fn(y0v + bv, a.act), r1 = act_fn(y1v + bv, a.act);
+            const int px = 2 * otx;
+            float* p = dst + (size_t)py * a.w + px;
+            if (px + 1 < a.w && ((reinterpret_cast<uintptr_t>(p) & 7) == 0)) {
+                *reinterpret_cast<float2*>(p) = make_float2(r0, r1);
+            } else {
+                p[0] = r0;
+                if (px + 1 < a.w) p[1] = r1;
+            }
+        }
+    }
+}
+
+}  // namespace wino3
+}  // namespace tsplat
+
+using namespace tsplat;
+
+static int wino3_ci_pad(int ci) { return (ci + 15) / 16 * 16; }
+static int wino3_cobs(int co) { return (co + 63) / 64 * 2; }
+
+extern "C" size_t tsplat_wino_weight_bf16x3_bytes(int32_t co, int32_t ci) {
+    if (co <= 0 || ci <= 0) return 0;
+    return (size_t)16 * wino3_cobs(co) * wino3_ci_pad(ci) * 32 * 2 * 2;  // hi + lo bf16
+}
+
+extern "C" int tsplat_wino_weight_bf16x3(const float* weight, void* packed, int32_t co, int32_t ci, void* stream_) {
+    if (!weight || !packed || co <= 0 || ci <= 0) return TSPLAT_EINVAL;
+    const int ci_pad = wino3_ci_pad(ci);
+    const int cobs = wino3_cobs(co);
+    const int total = cobs * 32 * ci_pad;
+    hipLaunchKernelGGL(wino3::weight_kernel, dim3((total + 255) / 256), dim3(256), 0, (hipStream_t)stream_, weight,
+                       (__bf16*)packed, co, ci, ci_pad, cobs);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+// workgroup forms: 0 = auto, 1 = 32 co x 32 tiles (KS 1), 2 = 32 x 32 with two k-groups,
+// 3 = 32 co x 64 tiles, 4 = 64 co x 64 tiles
+static int pick_form(int n, int th, int tw, int co) {
+    if (const char* e = getenv("TSPLAT_WINO3_FORM")) {
+        const int f = atoi(e);
+        if (f >= 1 && f <= 4) return f;
+    }
+    const long tiles = (long)n * th * tw;
+    const int cob32 = (co + 31) / 32;
+    const long wg64 = (tiles + 63) / 64 * ((co + 63) / 64);
+    const long wg32 = (tiles + 31) / 32 * cob32;
+    if (co > 32 && wg64 >= 256) return 4;
+    if (co <= 32 && (tiles + 63) / 64 * cob32 >= 256) return 3;
+    return wg32 <= 256 ? 2 : 1;
+}
+
+template <int CB, int NB, int KS>
+static void launch(wino3::Args a, int blocks, hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
+    const int coblocks = (a.co + 32 * CB - 1) / (32 * CB);
+    hipExtLaunchKernelGGL(wino3::conv_kernel<CB, NB, KS>, dim3(blocks, coblocks), dim3(256 * CB * KS), 0, stream,
+                          start, stop, 0, a);
+}
+
+extern "C" int tsplat_conv3x3_wino_bf16x3_cat_fwd(const float* const* srcs, const int32_t* chans, int32_t nsrc,
+                                                  const void* packed, const float* bias, float* y, int32_t n,
+                                                  int32_t h, int32_t w, int32_t co, int32_t act, void* stream_) {
+    if (!srcs || !chans || nsrc <= 0 || nsrc > wino3::kMaxSrc || !packed || !y || n <= 0 || h <= 0 || w <= 0 ||
+        co <= 0 || act < 0 || act > 2)
+        return TSPLAT_EINVAL;
+    wino3::Args a;
+    int ci = 0;
+    for (int q = 0; q < wino3::kMaxSrc; ++q) {
+        a.src[q] = q < nsrc ? srcs[q] : nullptr;
+        a.cs[q] = q < nsrc ? chans[q] : 0;
+        if (q < nsrc && (!srcs[q] || chans[q] <= 0)) return TSPLAT_EINVAL;
+        ci += a.cs[q];
+    }
+    a.nsrc = nsrc;
+    a.u = (const uint4*)packed;
+    a.bias = bias;
+    a.y = y;
+    a.n = n;
+    a.ci = ci;
+    a.h = h;
+    a.w = w;
+    a.co = co;
+    a.ci_pad = wino3_ci_pad(ci);
+    if (a.ci_pad > wino3::kMaxCiPad) return TSPLAT_EINVAL;
+    a.cobs = wino3_cobs(co);
+    a.nchunk = a.ci_pad / 16;
+    a.th = (h + 1) / 2;
+    a.tw = (w + 1) / 2;
+    a.act = act;
+    a.cob_base = 0;
+    const int form = pick_form(n, a.th, a.tw, co);
+    const int ttiles = form >= 3 ? 64 : 32;
+    // tile block: the widest of T x 1, T/2 x 2, T/4 x 4, T/8 x 8 with the fewest padded tiles
+    long best = -1;
+    for (int tbx = ttiles; tbx >= ttiles / 8; tbx /= 2) {
+        const int tby = ttiles / tbx;
+        const long padded = (long)((a.tw + tbx - 1) / tbx) * tbx * ((a.th + tby - 1) / tby) * tby;
+        if (best < 0 || padded < best) {
+            best = padded;
+            a.tbx = tbx;
+        }
+    }
+    a.tby = ttiles / a.tbx;
+    a.bx = (a.tw + a.tbx - 1) / a.tbx;
+    a.by = (a.th + a.tby - 1) / a.tby;
+    const int blocks = n * a.bx * a.by;
+    hipStream_t stream = (hipStream_t)stream_;
+    const prof::ExtEvents ev = prof::ext_events(prof::kWinoConv);
+    switch (form) {
+        case 4: launch<2, 2, 1>(a, blocks, stream, ev.start, ev.stop); break;
+        case 3: launch<1, 2, 1>(a, blocks, stream, ev.start, ev.stop); break;
+        case 2: launch<1, 1, 2>(a, blocks, stream, ev.start, ev.stop); break;
+        default: launch<1, 1, 1>(a, blocks, stream, ev.start, ev.stop); break;
+    }
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_conv3x3_wino_bf16x3_fwd(const float* x, const void* packed, const float* bias, float* y,
+                                              int32_t n, int32_t ci, int32_t h, int32_t w, int32_t co, int32_t act,
+                                              void* stream_) {
+    return tsplat_conv3x3_wino_bf16x3_cat_fwd(&x, &ci, 1, packed, bias, y, n, h, w, co, act, stream_);
+}

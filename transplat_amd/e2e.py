@@ -47,9 +47,10 @@ class TransplatModel(torch.nn.Module):
         return missing, unexpected
 
 
-def build_model(device, dense_dtype: str = "fp32", seed: int = 0, num_context_views: int = 2) -> TransplatModel:
+def build_model(device, dense_dtype: str = "fp32", seed: int = 0, num_context_views: int = 2,
+                attn_dtype: str = "auto") -> TransplatModel:
     torch.manual_seed(seed)
-    cfg = EncoderTransCfg(dense_dtype=dense_dtype, num_context_views=num_context_views)
+    cfg = EncoderTransCfg(dense_dtype=dense_dtype, num_context_views=num_context_views, attn_dtype=attn_dtype)
     model = TransplatModel(cfg, DecoderSplattingHIPCfg(check_overflow=False))
     S.init_synthetic_weights(model.encoder, seed)
     model = model.eval().to(device)
@@ -143,11 +144,21 @@ def _copy_batch(dst, src):
             dst[k].copy_(v, non_blocking=True)
 
 
-def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: str = "fp32", graph: bool = True):
+def precision_label(dense_dtype: str, attn_dtype: str = "auto") -> str:
+    """What runs in which arithmetic, for the bench line's workload string."""
+    attn = attn_dtype if attn_dtype != "auto" else ("bf16" if dense_dtype == "bf16" else "fp32")
+    dense = {"fp32": "exact fp32", "bf16x3": "bf16x3 (split-bf16 products, fp32 accumulation; >= TF32)",
+             "bf16": "bf16 (autocast)"}[dense_dtype]
+    return (f"dense convs/GEMMs {dense}, window attention {attn}, correlation / norms / adapter / raster fp32"
+            + ("; DPT-head / stem / transposed convs on MIOpen exact fp32" if dense_dtype == "bf16x3" else ""))
+
+
+def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: str = "fp32", graph: bool = True,
+                       attn_dtype: str = "auto"):
     from .gemm_tuning import use_tuned_gemms
 
     use_tuned_gemms(device, dense_dtype)  # recorded library GEMM solutions (replay only), before any capture
-    model = build_model(device, dense_dtype)
+    model = build_model(device, dense_dtype, attn_dtype=attn_dtype)
     data = S.make_batch(batch, image_shape=(256, 256), scene_offset=scene_offset, device=device)
     if graph:
         graphed = GraphedStep(model, data)
@@ -161,7 +172,7 @@ def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: s
     info = {
         "eager_step": lambda: model.test_step(data),
         "views_per_step": batch * data["target"]["near"].shape[1],
-        "workload": f"e2e TranSplat test_step: {batch} scene(s) x (2 ctx -> 3 tgt) 256x256, "
-                    f"dense layers {dense_dtype}, correlation/attention/raster fp32",
+        "workload": f"e2e TranSplat test_step: {batch} scene(s) x (2 ctx -> 3 tgt) 256x256; "
+                    + precision_label(dense_dtype, attn_dtype),
     }
     return step, info, model

@@ -145,7 +145,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--index", required=True)
     ap.add_argument("--checkpoint", default=None, help="reference Lightning checkpoint (loaded weights_only)")
-    ap.add_argument("--dense-dtype", choices=["fp32", "bf16"], default="fp32")
+    ap.add_argument("--dense-dtype", choices=["fp32", "bf16x3", "bf16"], default="fp32")
     ap.add_argument("--limit", type=int, default=None, help="first N scenes of the index")
     ap.add_argument("--data-root", action="append", default=None,
                     help="dataset root holding test/*.torch chunks (repeatable); real frames instead of synthetic")

@@ -110,6 +110,15 @@ def uv_cross(value, key, intr, pose, disp, offsets, logits, h: int, w: int):
             table = torch.bmm(k2, torch.cat((vb, vb), dim=-1).transpose(1, 2), out_dtype=torch.float32)
         value = None
         key, offsets, logits, disp = map(_f32, (key, offsets, logits, disp))
+    elif _DENSE == "bf16x3" and value.is_cuda and c % 4 == 0:
+        # bf16x3 dense mode: the table in split-bf16 precision as ONE bf16 GEMM with K = 3C,
+        # [key_hi | key_hi | key_lo] x [val_hi | val_lo | val_hi]^T, fp32 output (47 vs 86 us for
+        # the fp32 bmm at b = 1, tools/bench_split_gemm.py; <= 3 * 2^-18 relative per product)
+        value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
+        k3 = split_bf16x3(key.reshape(b * 2, hw, c))
+        v3 = split_bf16x3(torch.flip(value, dims=[1]).reshape(b * 2, hw, c), weight_order=True)
+        with torch.autocast("cuda", enabled=False):
+            table = torch.bmm(k3, v3.transpose(1, 2), out_dtype=torch.float32)
     else:
         value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
         with torch.autocast("cuda", enabled=False):
@@ -212,9 +221,11 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = "", ext
     if not x.is_cuda:
         raise RuntimeError("transplat HIP ops need device tensors (no CPU path)")
     if (residual is None and act in _ACTS and _NO_CONV_EPI not in ("all", site)
+            and getattr(conv, "padding_mode", "zeros") == "zeros"
             and conv_bf16_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra)):
         return conv_bf16(x, conv.weight, conv.bias, act, extra)  # bf16 autocast: bias + act fused
-    fused = not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32 and _NO_CONV_EPI not in ("all", site)
+    fused = (not torch.is_autocast_enabled("cuda") and x.dtype == torch.float32 and _NO_CONV_EPI not in ("all", site)
+             and getattr(conv, "padding_mode", "zeros") == "zeros")
     if (fused and residual is None and act in _WINO_ACT
             and conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, extra,
                                 vs_miopen=True)):
@@ -273,8 +284,12 @@ def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", 
     n, c = x.shape[:2]
     hw = x[0, 0].numel()
     if x.dtype == torch.bfloat16 and x.is_cuda and _BF16_NORMS:
+        if residual is not None and residual.dtype != torch.bfloat16:
+            # the module path rounds the norm's output to bf16 (GroupNorm32 casts back to x's dtype)
+            # and then promotes bf16 + fp32 to fp32: keep the fp32 residual stream un-narrowed
+            return group_norm(x, num_groups, weight, bias, eps, act, None, pre_bias).float() + residual
         xb = x.contiguous()
-        res = residual.to(torch.bfloat16).contiguous() if residual is not None else None
+        res = residual.contiguous() if residual is not None else None
         if res is not None and res.shape != x.shape:
             raise ValueError(f"residual {tuple(res.shape)} != input {tuple(x.shape)}")
         y = torch.empty_like(xb)
@@ -360,6 +375,15 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     b, l, c = q.shape
     m = 1 if k.dim() == 3 else k.shape[1]
     fp32 = q.dtype == k.dtype == v.dtype == torch.float32
+    wl = (h // num_splits) * (w // num_splits)
+    if _ATTN == "bf16" and wl % 128 == 0:
+        # bf16 attention (config C3): the projections' fp32 outputs rounded to bf16 once, the bf16
+        # MFMA kernel, the bf16 message widened by the merge projection's operand load
+        qb, kb, vb = q.to(torch.bfloat16), k.to(torch.bfloat16), v.to(torch.bfloat16)
+        if kv_shift:
+            kb, vb = torch.roll(kb, -kv_shift, dims=0), torch.roll(vb, -kv_shift, dims=0)
+        msg = window_attention(qb, kb, vb, h, w, num_splits, with_shift)
+        return fused_linear(msg, merge_weight, ln=ln, residual=residual)
     ks = int(lib.tsplat_win_attn_split(b, h, w, m, num_splits)) if fp32 and c == 128 else 0
     if ks <= 1:
         if kv_shift:
@@ -665,17 +689,175 @@ def install_conv2d_dispatch(module) -> int:
     return n
 
 
+# Dense-layer precision of the fp32 path (set by the encoder around its dense regions,
+# EncoderTransCfg.dense_dtype): "fp32" = exact fp32 MFMA / library SGEMM; "bf16x3" = split-bf16
+# products (x = hi + lo, hi*hi + hi*lo + lo*hi on bf16 MFMA, fp32 accumulation: <= 3 * 2^-18
+# relative per product, the stand-in for the reference's TF32, src/main.py:15).
+_DENSE = "fp32"
+_DENSE_MODES = ("fp32", "bf16x3")
+
+
+class dense_precision:
+    """Context manager: the dense-layer precision mode inside the block (see _DENSE)."""
+
+    def __init__(self, mode: str):
+        if mode not in _DENSE_MODES:
+            raise ValueError(f"dense precision {mode!r} not in {_DENSE_MODES}")
+        self.mode, self.prev = mode, None
+
+    def __enter__(self):
+        global _DENSE
+        self.prev, _DENSE = _DENSE, self.mode
+        return self
+
+    def __exit__(self, *exc):
+        global _DENSE
+        _DENSE = self.prev
+        return False
+
+
+def split_mode() -> bool:
+    """True inside dense_precision("bf16x3")."""
+    return _DENSE == "bf16x3"
+
+
+# Window-attention precision of the fp32 transformer path: "fp32" (exact fp32 MFMA) or "bf16"
+# (q / k / v rounded to bf16, bf16 MFMA with fp32 softmax and accumulation: config C3's "bf16
+# attention" beside fp32-class dense layers). Under bf16 autocast the attention is bf16 regardless.
+_ATTN = "fp32"
+
+
+class attention_precision:
+    """Context manager: the window-attention precision inside the block (see _ATTN)."""
+
+    def __init__(self, mode: str):
+        if mode not in ("fp32", "bf16"):
+            raise ValueError(f"attention precision {mode!r}")
+        self.mode, self.prev = mode, None
+
+    def __enter__(self):
+        global _ATTN
+        self.prev, _ATTN = _ATTN, self.mode
+        return self
+
+    def __exit__(self, *exc):
+        global _ATTN
+        _ATTN = self.prev
+        return False
+
+
+_SPLIT_W: dict = {}
+
+
+def split_bf16x3(x: torch.Tensor, weight_order: bool = False) -> torch.Tensor:
+    """[..., k] fp32 -> [..., 3k] bf16: [hi | hi | lo] (activations) or [hi | lo | hi] (weights_order),
+    hi = bf16(x), lo = bf16(x - hi) (tsplat_split_bf16x3)."""
+    lib = _lib.load()
+    xf = _f32(x)
+    k = xf.shape[-1]
+    out = torch.empty((*xf.shape[:-1], 3 * k), dtype=torch.bfloat16, device=xf.device)
+    _lib.check(lib.tsplat_split_bf16x3(_lib.ptr(xf), _lib.ptr(out), xf.numel() // k, k, int(weight_order),
+                                       _lib.stream_ptr(xf.device)), "tsplat_split_bf16x3")
+    return out
+
+
+def _split_weight(weight):
+    """[n, k] -> [n, 3k] bf16 [hi | lo | hi], cached per weight tensor version."""
+    hit = _SPLIT_W.get(id(weight))
+    if hit is not None and hit[0]() is weight and hit[1] == weight._version:
+        return hit[2]
+    packed = split_bf16x3(weight.detach(), weight_order=True)
+    if len(_SPLIT_W) > 512:
+        for k in [k for k, v in _SPLIT_W.items() if v[0]() is None]:
+            del _SPLIT_W[k]
+    _SPLIT_W[id(weight)] = (weakref.ref(weight), weight._version, packed)
+    return packed
+
+
+def linear_bf16x3(x, weight, bias=None):
+    """F.linear(x, weight, bias) in split-bf16 precision: ONE hipBLASLt bf16 GEMM with K' = 3K on
+    [x_hi | x_hi | x_lo] and the cached [W_hi | W_lo | W_hi], fp32 accumulation and fp32 output
+    (torch.mm / addmm with out_dtype=float32), <= 3 * 2^-18 relative per product."""
+    k = x.shape[-1]
+    x3 = split_bf16x3(x).reshape(-1, 3 * k)
+    w3 = _split_weight(weight)
+    with torch.autocast("cuda", enabled=False):
+        if bias is not None:
+            y = torch.addmm(_f32(bias), x3, w3.t(), out_dtype=torch.float32)
+        else:
+            y = torch.mm(x3, w3.t(), out_dtype=torch.float32)
+    return y.reshape(*x.shape[:-1], weight.shape[0])
+
+
+# nn.Linear in bf16x3 mode: OFF by default (TSPLAT_LIN3=1 enables). Measured (tools/bench_split_gemm.py,
+# profiles/r4/split_gemm.log): hipBLASLt's bf16 GEMM at K' = 3K is no faster than its fp32 GEMM on the
+# step's linears (DINOv2 qkv 23.4 vs 28.8 us, proj 23.3 vs 18.7, fc1 27.8 vs 31.1, fc2 30.3 vs 29.2,
+# MVT fc1 50.7 vs 39.9 at M = 650 / 8192): the small-M shapes are not MFMA-bound in the library, and
+# the activation split is another launch. Only the correlation table gains (uv_cross: 47 vs 86 us).
+_LIN3 = os.environ.get("TSPLAT_LIN3", "0") == "1"
+_LIN3_MIN_FLOP = float(os.environ.get("TSPLAT_LIN3_MIN_FLOP", "2e8"))  # smaller linears stay exact fp32
+
+
+def linear_forward(mod, x):
+    """nn.Linear.forward (installed by install_linear_dispatch): in dense_precision("bf16x3") the
+    fp32 linears of at least _LIN3_MIN_FLOP run as linear_bf16x3; everything else is F.linear."""
+    import torch.nn.functional as F
+
+    if (_LIN3 and _DENSE == "bf16x3" and x.is_cuda and x.dtype == torch.float32 and mod.weight.dtype == torch.float32
+            and not torch.is_autocast_enabled("cuda") and x.shape[-1] % 4 == 0
+            and 2.0 * x.numel() * mod.weight.shape[0] >= _LIN3_MIN_FLOP):
+        return linear_bf16x3(x, mod.weight, mod.bias)
+    return F.linear(x, mod.weight, mod.bias)
+
+
+def install_linear_dispatch(module) -> int:
+    """Route every nn.Linear under `module` through linear_forward (same parameters and state dict)."""
+    import functools
+
+    n = 0
+    for m in module.modules():
+        if type(m) is torch.nn.Linear:
+            m.forward = functools.partial(linear_forward, m)
+            n += 1
+    return n
+
+
 # bench.py's roofline pass sets a list here: one (Winograd GEMM FLOPs, direct-equivalent FLOPs) pair
 # per launch (GEMM FLOPs = 2 * 16 * ci * co * output tiles, the products the 16 MFMA GEMMs compute)
 WINO_FLOP_LOG = None
 
 
-def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=()):
-    """act(conv2d(cat([x, *extra], 1), weight, bias, stride 1, padding 1)) via Winograd F(2x2, 3x3)
-    on fp32 MFMA; the concatenation is read in place (tsplat_conv3x3_wino_cat_f32_fwd)."""
+_WINO3_PACKED: dict = {}
+
+
+def wino_pack_weight_bf16x3(weight):
+    """[cout, cin, 3, 3] -> G g G^T split into hi / lo bf16 in the A-operand order of
+    tsplat_conv3x3_wino_bf16x3_fwd, cached per weight tensor version."""
+    hit = _WINO3_PACKED.get(id(weight))
+    if hit is not None and hit[0]() is weight and hit[1] == weight._version:
+        return hit[2]
+    lib = _lib.load()
+    co, ci = weight.shape[:2]
+    packed = torch.empty(int(lib.tsplat_wino_weight_bf16x3_bytes(co, ci)), dtype=torch.uint8, device=weight.device)
+    w = weight.detach().float().contiguous()
+    _lib.check(lib.tsplat_wino_weight_bf16x3(_lib.ptr(w), _lib.ptr(packed), co, ci, _lib.stream_ptr(weight.device)),
+               "tsplat_wino_weight_bf16x3")
+    if len(_WINO3_PACKED) > 512:
+        for k in [k for k, v in _WINO3_PACKED.items() if v[0]() is None]:
+            del _WINO3_PACKED[k]
+    _WINO3_PACKED[id(weight)] = (weakref.ref(weight), weight._version, packed)
+    return packed
+
+
+def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=(), precision: str | None = None):
+    """act(conv2d(cat([x, *extra], 1), weight, bias, stride 1, padding 1)) via Winograd F(2x2, 3x3);
+    the concatenation is read in place. precision "fp32" (tsplat_conv3x3_wino_cat_f32_fwd, exact fp32
+    MFMA) or "bf16x3" (tsplat_conv3x3_wino_bf16x3_cat_fwd, split-bf16 MFMA); default: the current
+    dense_precision mode."""
     import ctypes
 
     lib = _lib.load()
+    precision = precision or _DENSE
     srcs = [_f32(t) for t in (x, *extra)]
     n, _, h, w = srcs[0].shape
     co = weight.shape[0]
@@ -686,10 +868,13 @@ def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=()):
     pb = _f32(bias) if bias is not None else None
     ptrs = (ctypes.c_void_p * len(srcs))(*[_lib.ptr(t) for t in srcs])
     chans = (ctypes.c_int32 * len(srcs))(*[t.shape[1] for t in srcs])
-    rc = lib.tsplat_conv3x3_wino_cat_f32_fwd(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p),
-                                             len(srcs), _lib.ptr(wino_pack_weight(weight)), _lib.ptr(pb),
-                                             _lib.ptr(y), n, h, w, co, _WINO_ACT[act], _lib.stream_ptr(x.device))
-    _lib.check(rc, "tsplat_conv3x3_wino_cat_f32_fwd")
+    if precision == "bf16x3":
+        fn, packed, name = lib.tsplat_conv3x3_wino_bf16x3_cat_fwd, wino_pack_weight_bf16x3(weight), "bf16x3"
+    else:
+        fn, packed, name = lib.tsplat_conv3x3_wino_cat_f32_fwd, wino_pack_weight(weight), "f32"
+    rc = fn(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p), len(srcs), _lib.ptr(packed),
+            _lib.ptr(pb), _lib.ptr(y), n, h, w, co, _WINO_ACT[act], _lib.stream_ptr(x.device))
+    _lib.check(rc, f"tsplat_conv3x3_wino_{name}_cat_fwd")
     return y
 
 

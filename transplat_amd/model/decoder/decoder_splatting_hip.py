@@ -23,6 +23,7 @@ class DecoderSplattingHIPCfg:
     name: Literal["splatting_hip", "splatting_cuda"] = "splatting_hip"
     sh_eval_degree: Optional[int] = None  # None: min(isqrt(d_sh) - 1, 3), the upstream behaviour
     check_overflow: bool = True  # sync after each call to surface capacity overflow
+    debug: bool = False  # upstream GaussianRasterizationSettings.debug: sync + check after every launch
 
 
 def depth_fake_color(extrinsics: Tensor, means: Tensor, near: Tensor, far: Tensor,
@@ -82,6 +83,7 @@ class DecoderSplattingHIP(Decoder[DecoderSplattingHIPCfg]):
             views_per_scene=v,
             sh_degree=self.cfg.sh_eval_degree,
             check=self.cfg.check_overflow,
+            debug=self.cfg.debug,
         )
         color = rearrange(color, "(b v) c h w -> b v c h w", b=b, v=v)
         depth = None
@@ -118,6 +120,7 @@ class DecoderSplattingHIP(Decoder[DecoderSplattingHIPCfg]):
             views_per_scene=1,
             sh_degree=0,
             check=self.cfg.check_overflow,
+            debug=self.cfg.debug,
         )
         return rearrange(color.mean(dim=1), "(b v) h w -> b v h w", b=b, v=v)
 

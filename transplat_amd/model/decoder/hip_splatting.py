@@ -155,8 +155,13 @@ def rasterize(
     sh_degree: int | None = None,
     capacity: int | None = None,
     check: bool = True,
+    debug: bool = False,
 ) -> tuple[Tensor, Tensor]:
     """Render V = scenes * views_per_scene views.
+
+    debug=True mirrors the upstream rasterizer's `debug` setting (cuda_splatting.py:120): every
+    launch of the call is followed by a device synchronisation and an error check
+    (tsplat_set_debug), so a faulting kernel is named; it cannot run inside hipGraph capture.
 
     means [S, G, 3], covariances [S, G, 3, 3], harmonics [S, G, 3, M], opacities [S, G]
     -> color [V, 3, H, W], radii [V, G] int32.
@@ -189,16 +194,23 @@ def rasterize(
     for t in cams:
         if t.device != dev:
             raise ValueError("camera tensors must be on the Gaussians' device")
-    rc = lib.tsplat_raster_fwd(
-        desc,
-        *(_lib.ptr(t) for t in (means, covariances, harmonics, opacities)),
-        *(_lib.ptr(t) for t in cams),
-        _lib.ptr(color),
-        _lib.ptr(radii),
-        _lib.ptr(ws),
-        _lib.ptr(status),
-        _lib.stream_ptr(dev),
-    )
+    if debug and torch.cuda.is_current_stream_capturing():
+        raise RuntimeError("rasterize(debug=True) synchronises after every launch: not inside hipGraph capture")
+    was = lib.tsplat_set_debug(1) if debug else None
+    try:
+        rc = lib.tsplat_raster_fwd(
+            desc,
+            *(_lib.ptr(t) for t in (means, covariances, harmonics, opacities)),
+            *(_lib.ptr(t) for t in cams),
+            _lib.ptr(color),
+            _lib.ptr(radii),
+            _lib.ptr(ws),
+            _lib.ptr(status),
+            _lib.stream_ptr(dev),
+        )
+    finally:
+        if was is not None:
+            lib.tsplat_set_debug(was)
     _lib.check(rc, "tsplat_raster_fwd")
     _STATE.last[(dev.type, dev.index)] = (ws, int(lib.tsplat_raster_num_rendered_offset(g, v, h, w)))
     if check:

@@ -51,9 +51,9 @@ def _resize(x, modifier: dict, align_corners: bool):
             sf = modifier["scale_factor"]
             size = (int(x.shape[-2] * sf), int(x.shape[-1] * sf))
         return kernels.resize_bilinear_nhwc(x, size)
-    if align_corners and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous():
-        # NCHW fp32 (the head's final resize in bf16 mode): PyTorch's generic NCHW kernel took
-        # 0.87 ms per call at C3's batch 8
+    if _DPT_EPI and align_corners and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.is_contiguous():
+        # NCHW fp32 (the head's final resize; every config, fp32 included -- test_depth_anything_gpu
+        # covers it in fp32): PyTorch's generic NCHW kernel took 0.87 ms per call at C3's batch 8
         if "size" in modifier:
             size = modifier["size"]
         else:

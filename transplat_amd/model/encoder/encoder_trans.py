@@ -68,9 +68,14 @@ class EncoderTransCfg:
     num_context_views: int = 2  # the reference reads it from the global dataset config
     da_encoder: str = "vitb"
     # Arithmetic of the conv / GEMM layers around the hand-written kernels (CNN, cam encoders,
-    # DA-V2, U-Nets, heads): "fp32" (parity mode) or "bf16" (autocast). Correlation and the
-    # rasterizer always run fp32.
+    # DA-V2, U-Nets, heads): "fp32" (exact fp32, parity mode), "bf16x3" (split-bf16 products with
+    # fp32 accumulation -- the stand-in for the reference's TF32, src/main.py:15, more precise than
+    # it; kernels.dense_precision) or "bf16" (autocast). Correlation and the rasterizer always run
+    # fp32.
     dense_dtype: str = "fp32"
+    # Window attention (T2): "auto" (bf16 MFMA under bf16 dense layers, else exact fp32), "fp32" or
+    # "bf16" (config C3 as BASELINE.json states it: bf16 attention beside fp32-class dense layers).
+    attn_dtype: str = "auto"
 
 
 class EncoderTrans(Encoder[EncoderTransCfg]):
@@ -97,6 +102,8 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         # every plain Conv2d: the large 3x3s on the Winograd fp32 MFMA kernel, the rest unchanged
         # (kernels.conv2d_forward; CPU tensors and bf16 autocast keep the module's own conv)
         kernels.install_conv2d_dispatch(self)
+        # every plain Linear: split-bf16 GEMMs in dense_dtype "bf16x3" (kernels.linear_forward)
+        kernels.install_linear_dispatch(self)
 
     def map_pdf_to_opacity(self, pdf, global_step: int):
         """(reference :139-152)"""
@@ -112,6 +119,10 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
     def _dense(self):
         if self.cfg.dense_dtype == "bf16":
             return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
+        if self.cfg.dense_dtype == "bf16x3":
+            return kernels.dense_precision("bf16x3")
+        if self.cfg.dense_dtype != "fp32":
+            raise ValueError(f"dense_dtype {self.cfg.dense_dtype!r}")
         return nullcontext()
 
     def forward(self, context: dict, global_step: int = 0, deterministic: bool = False,
@@ -150,9 +161,13 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
                 da_depth = ((da_depth - da_min) / (da_max - da_min)).reshape(b, v, 1, h, w)
                 return da_depth, out_feature.float()
 
-        def backbone():
-            with bench("encoder_2_backbone"), self._dense():
-                tf, cf = self.backbone(context["image"], attn_splits=self.cfg.multiview_trans_attn_split,
+        attn = self.cfg.attn_dtype
+        if attn == "auto":
+            attn = "bf16" if self.cfg.dense_dtype == "bf16" else "fp32"
+
+        def backbone(images, img2world):
+            with bench("encoder_2_backbone"), self._dense(), kernels.attention_precision(attn):
+                tf, cf = self.backbone(images, attn_splits=self.cfg.multiview_trans_attn_split,
                                        return_cnn_features=True, img2world=img2world)
             return tf.float(), cf.float()
 
@@ -162,7 +177,7 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         # the MVT's 256-workgroup kernels) that leave CUs idle on their own. Depth-Anything stays on
         # the current stream because it forks again (its DPT reassemble branches, dpt.py): a fork
         # from a side stream inside hipGraph capture crashed HIP's capture_end.
-        bb = streams.fork(device, backbone)
+        bb = streams.fork(device, backbone, context["image"], img2world)  # inputs marked for the side stream
         da_depth, out_feature = depth_anything()
         trans_features, cnn_features = streams.join(bb)
         dino_feature = out_feature.view(b, v, *out_feature.shape[1:])

@@ -14,6 +14,15 @@ far; `join(pending)` makes the current stream wait for it and returns fn's resul
 marked as used by the side stream and outputs as used by the current one (record_stream), so the
 caching allocator never hands their memory to the other stream while it is still in flight.
 `serial()` turns forking off (the reference's serial order), e.g. to time one kernel alone.
+
+Tensors a branch reads must reach it as fork arguments (tuples, lists and dict values are walked)
+so that they are marked; a tensor the branch only captures through a closure is not marked and must
+stay referenced by the caller until join.
+
+Forks nest only from the current stream: a fork issued while a side stream is current (inside a
+forked branch) during hipGraph capture raises. ROCm 7.2's capture_end segfaults on a graph whose
+side-stream branch forks onto a second side stream (tools/graph_fork_repro.py nested_once,
+profiles/r3/hoist_dbg/); a flat fork from the capturing stream is fine.
 """
 from __future__ import annotations
 
@@ -54,6 +63,9 @@ def _tensors(x):
     elif isinstance(x, (tuple, list)):
         for y in x:
             yield from _tensors(y)
+    elif isinstance(x, dict):
+        for y in x.values():
+            yield from _tensors(y)
 
 
 class _Pending:
@@ -61,10 +73,21 @@ class _Pending:
         self.out, self.main, self.side = out, main, side
 
 
+class NestedForkError(RuntimeError):
+    """A fork from a side stream during hipGraph capture (see the module docstring)."""
+
+
+def _is_side(stream) -> bool:
+    return any(stream == s for s in _SIDE.values())
+
+
 def fork(device, fn, *args, slot: int = 0) -> _Pending:
     if not enabled(device):
         return _Pending(fn(*args))
     main = torch.cuda.current_stream(device)
+    if _is_side(main) and torch.cuda.is_current_stream_capturing():
+        raise NestedForkError("streams.fork from a side stream inside hipGraph capture: HIP's capture_end "
+                              "crashes on nested side-stream forks (fork from the capturing stream instead)")
     side = side_stream(device, slot)
     side.wait_stream(main)
     for t in _tensors(args):
