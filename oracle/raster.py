@@ -14,6 +14,7 @@ ambiguous. Parity tests exclude exactly the flagged pixels (and radii) and repor
 from __future__ import annotations
 
 import ctypes
+import os
 import subprocess
 from pathlib import Path
 
@@ -22,11 +23,14 @@ import numpy as np
 FLAG_RECT, FLAG_POWER, FLAG_ALPHA, FLAG_T = 1, 2, 4, 8
 
 HERE = Path(__file__).resolve().parent
-LIB = HERE / "build" / "libtsplat_oracle.so"
+# TSPLAT_ORACLE_LIB: an alternative build of the same restatement (the ASan / UBSan one, `make asan`)
+LIB = Path(os.environ.get("TSPLAT_ORACLE_LIB") or HERE / "build" / "libtsplat_oracle.so")
 _lib = None
 
 
 def build() -> Path:
+    if os.environ.get("TSPLAT_ORACLE_LIB"):
+        return LIB
     if not LIB.exists() or LIB.stat().st_mtime < (HERE / "raster_ref.c").stat().st_mtime:
         subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
     return LIB

@@ -228,19 +228,25 @@ def tf32_round(t: torch.Tensor) -> torch.Tensor:
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("stage", ["auto", "0"])
 @pytest.mark.parametrize("form", ["auto", "1", "2", "3", "4"])
-@pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES)
-def test_conv3x3_wino_bf16x3_kernel(device, monkeypatch, form, n, ci, co, h, w, bias, act):
+@pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES + [(1, 24, 48, 10, 96, True, "relu"),
+                                                               (2, 40, 64, 22, 136, False, "none")])
+def test_conv3x3_wino_bf16x3_kernel(device, monkeypatch, stage, form, n, ci, co, h, w, bias, act):
     """Winograd F(2x2, 3x3) in split-bf16 precision (tsplat_conv3x3_wino_bf16x3_fwd: hi*hi + hi*lo +
     lo*hi on bf16 MFMA, fp32 accumulation) against torch's conv2d in float64, with the launch's own
     workgroup form and each form forced (TSPLAT_WINO3_FORM: 32 co x 32 tiles, the same with two
-    k-groups, 32 x 64, 64 x 64). Bounds (written here): the same 2e-5 of max |y| as the exact-fp32
+    k-groups, 32 x 64, 64 x 64), with the staged input (coalesced region loads through LDS, maps
+    whose width is a multiple of 4: tile blocks 32 / 16 / 8 wide) and without it
+    (TSPLAT_WINO3_STAGE=0). Bounds (written here): the same 2e-5 of max |y| as the exact-fp32
     kernel, and at most 1/8 of the error of the reference's own precision -- TF32 operands
     (float64 conv of TF32-rounded x and w, TF32's best case: exact accumulation)."""
     from transplat_amd import kernels as K
 
     if form != "auto":
         monkeypatch.setenv("TSPLAT_WINO3_FORM", form)
+    if stage != "auto":
+        monkeypatch.setenv("TSPLAT_WINO3_STAGE", stage)
     x = seeded((n, ci, h, w), 41)
     wt = seeded((co, ci, 3, 3), 42) * (1.0 / (9 * ci) ** 0.5)
     b = seeded((co,), 43) if bias else None

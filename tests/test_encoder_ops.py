@@ -64,20 +64,17 @@ def test_camera_prep_matches_reference_golden():
 
 # ------------------------------------------------------------------ HIP kernels vs oracle
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", ["auto", "x16", "quad"])
+@pytest.mark.parametrize("variant", ["auto", "16"])
 @pytest.mark.parametrize("hw,m,shift,b", [(16, 1, False, 2), (16, 1, True, 2), (16, 2, True, 2), (64, 1, False, 2),
                                           (64, 1, True, 2), (64, 2, True, 2), (32, 2, False, 2), (64, 1, True, 8),
                                           (64, 1, True, 1), (64, 1, False, 1)])
 def test_window_attention_kernel(device, monkeypatch, hw, m, shift, b, variant):
     """auto: 128-query blocks as 4 waves x 32 queries (32x32x2) with the global key split + combine
     (b = 1 / 2 at 64x64), without split at b = 8, the 64-query 16x16x4 kernel for 8x8 windows;
-    "x16": the same blocks as 8 waves x 16 queries (16x16x4, TSPLAT_WA16=1); "quad": the opt-in
-    split-free kernel (4 waves x key quarters on 32 queries) where its shapes allow."""
+    "16": the 64-query 16x16x4 kernel forced (TSPLAT_WINATTN=16) at every shape."""
     from transplat_amd import kernels as K
 
-    if variant == "x16":
-        monkeypatch.setenv("TSPLAT_WA16", "1")
-    elif variant != "auto":
+    if variant != "auto":
         monkeypatch.setenv("TSPLAT_WINATTN", variant)
     q = seeded((b, hw * hw, 128), 11)
     k = seeded((b, m, hw * hw, 128), 12) if m > 1 else seeded((b, hw * hw, 128), 12)
@@ -455,21 +452,18 @@ def test_fused_linear_kernel(device, m, k1, k2, n, gelu, ln, res, split, bias, g
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("x16", [False, True])
 @pytest.mark.parametrize("hw,m,shift,b,res,kvs", [(64, 1, True, 2, True, 0), (64, 1, False, 2, False, 0),
                                                   (64, 2, True, 3, True, 0), (32, 1, True, 2, False, 0),
                                                   (64, 1, True, 8, True, 0), (64, 1, True, 2, True, 1),
                                                   (64, 1, False, 4, False, 2), (64, 1, True, 8, False, 4),
                                                   (64, 1, True, 1, True, 0)])
-def test_attention_merge_kernel(device, monkeypatch, hw, m, shift, b, res, kvs, x16):
+def test_attention_merge_kernel(device, monkeypatch, hw, m, shift, b, res, kvs):
     """Window attention + merge Linear + LayerNorm (+ residual) with the split-key combine folded
     into the merge kernel (tsplat_win_attn_partials_fwd + tsplat_linear_f32_attn_merge_fwd; key
     splits 4 / 8 here, b = 8 takes the unsplit path) vs the CPU restatement."""
     from transplat_amd import _lib
     from transplat_amd import kernels as K
 
-    if x16:  # the 16-query-wave kernel writes the same partial layout (TSPLAT_WA16=1)
-        monkeypatch.setenv("TSPLAT_WA16", "1")
     q = seeded((b, hw * hw, 128), 41)
     k = seeded((b, m, hw * hw, 128), 42) if m > 1 else seeded((b, hw * hw, 128), 42)
     v = seeded(k.shape, 43)

@@ -45,6 +45,16 @@ def _run(dev, fn):
         return fn(dev)
 
 
+@pytest.fixture(params=["fp32", "bf16x3"])
+def dense(request):
+    """GPU module goldens in both dense-layer precisions (kernels.dense_precision: exact fp32, or
+    the bf16x3 split-bf16 convolutions / correlation-table GEMM), at the same tolerances."""
+    from transplat_amd import kernels
+
+    with kernels.dense_precision(request.param):
+        yield request.param
+
+
 # ------------------------------------------------------------------ multi-view transformer
 def _mvt(dev, nv):
     from transplat_amd.model.encoder.backbone.multiview_transformer import MultiViewFeatureTransformer
@@ -62,7 +72,7 @@ def test_mvt_cpu(cpu_ops, nv):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nv", [2, 3])
-def test_mvt_gpu(device, nv):
+def test_mvt_gpu(device, dense, nv):
     _close(_run(device, lambda d: _mvt(d, nv)), np.load(GOLD / f"mvt_v{nv}.npz")["out"], 1e-3)
 
 
@@ -92,7 +102,7 @@ def test_backbone_cpu(cpu_ops):
 
 
 @pytest.mark.gpu
-def test_backbone_gpu(device):
+def test_backbone_gpu(device, dense):
     g = np.load(GOLD / "backbone_64.npz")
     trans, cnn = _run(device, _backbone)
     _close(cnn, g["cnn"], 1e-3)
@@ -127,7 +137,7 @@ def test_uv_transformers_cpu(cpu_ops):
 
 
 @pytest.mark.gpu
-def test_uv_transformers_gpu(device):
+def test_uv_transformers_gpu(device, dense):
     g = np.load(GOLD / "uv_16.npz")
     c, f = _run(device, _uv)
     _close(c, g["coarse"], 1e-4)
@@ -152,7 +162,7 @@ def test_unet_cpu(cpu_ops, tag, ch, mult, attn, hw):
 @pytest.mark.gpu
 @pytest.mark.parametrize("tag,ch,mult,attn,hw", [("cv", 128, (1, 1, 1), (4,), 16),
                                                  ("depth", 32, (1, 1, 1, 1, 1), (16,), 32)])
-def test_unet_gpu(device, tag, ch, mult, attn, hw):
+def test_unet_gpu(device, dense, tag, ch, mult, attn, hw):
     """The U-Nets with the fused GroupNorm(+SiLU, +residual) kernels vs the reference golden."""
     from transplat_amd.model.encoder.matching.ldm_unet import UNetModel
 
@@ -201,14 +211,14 @@ def _check_depth_predictor(out, rel, nv=2):
     _close(raw[torch.tensor(g["raw_idx"])], g["raw_rows"], rel)
 
 
-@pytest.mark.parametrize("nv", [2, 3])
+@pytest.mark.parametrize("nv", [2, 3, 4])
 def test_depth_predictor_cpu(cpu_ops, nv):
     _check_depth_predictor(_run(cpu_ops, lambda d: _depth_predictor(d, nv)), 1e-3, nv)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nv", [2, 3, 4])
-def test_depth_predictor_gpu(device, nv):
+def test_depth_predictor_gpu(device, dense, nv):
     _check_depth_predictor(_run(device, lambda d: _depth_predictor(d, nv)), 2e-3, nv)
 
 
@@ -244,7 +254,7 @@ def test_encoder_state_dict_matches_reference_keys():
 
 
 @pytest.mark.gpu
-def test_depth_anything_gpu(device):
+def test_depth_anything_gpu(device, dense):
     """DA-V2 ViT-B + DPT on the gfx950 path with its default settings (patch-embed GEMM,
     tsplat_mha_f32_fwd attention, tsplat_residual_ln_fwd, channels-last DPT weights, NHWC conv
     epilogues and bilinear resizes) against the reference golden (reference dpt.py:177-184)."""

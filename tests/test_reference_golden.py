@@ -292,33 +292,45 @@ def test_adapter_kernel_vs_reference(device):
 
 
 # --------------------------------------------------------------------------- whole encoder
-def _encoder(dev):
+def _encoder(dev, dense="fp32"):
     from transplat_amd import synthetic as S
     from transplat_amd.model.encoder import EncoderTrans, EncoderTransCfg
 
-    enc = canonical_init(EncoderTrans(EncoderTransCfg()), seed=61).eval().to(dev)
+    enc = canonical_init(EncoderTrans(EncoderTransCfg(dense_dtype=dense)), seed=61).eval().to(dev)
     ctx = {k: t.to(dev) for k, t in S.make_batch(1, image_shape=(256, 256))["context"].items()}
     with torch.no_grad():
         gs = enc(ctx, global_step=0, deterministic=True)
     return gs
 
 
-def _check_encoder(gs, tol):
+def _check_encoder(gs, tol, tag=""):
+    """tol: a float for every output, or a dict per output (relative errors as _rel / _rel_sh)."""
     g = np.load(GOLD / "encoder_256.npz")
     idx = torch.from_numpy(g["idx"])
+    errs = {}
     for k in ("means", "covariances", "harmonics", "opacities"):
         rel = _rel_sh if k == "harmonics" else _rel
-        err = rel(getattr(gs, k)[0].cpu()[idx], g[k])
-        assert err < tol, f"{k}: {err:.3e}"
+        errs[k] = rel(getattr(gs, k)[0].cpu()[idx], g[k])
+    print(f"encoder vs reference{tag}: " + ", ".join(f"{k} {e:.2e}" for k, e in errs.items()))
+    for k, err in errs.items():
+        t = tol[k] if isinstance(tol, dict) else tol
+        assert err < t, f"{k}: {err:.3e} (tol {t})"
 
 
 def test_encoder_cpu_vs_reference(cpu_ops):
-    _check_encoder(_encoder(cpu_ops), 1e-4)
+    _check_encoder(_encoder(cpu_ops), 1e-4, " (CPU oracle ops)")
 
 
 @pytest.mark.gpu
-def test_encoder_gpu_vs_reference(device):
-    _check_encoder(_encoder(device), 3e-3)
+@pytest.mark.parametrize("dense", ["fp32", "bf16x3"])
+def test_encoder_gpu_vs_reference(device, dense):
+    """The whole encoder on the GPU against the reference golden, in exact-fp32 and bf16x3 dense
+    precision. The achieved errors are printed; the bounds are 2x the measured ones (rounded up)."""
+    _check_encoder(_encoder(device, dense), ENCODER_GPU_TOL[dense], f" (GPU, dense {dense})")
+
+
+# measured on MI355X (profiles/r4/): 2x the achieved relative errors, rounded up
+ENCODER_GPU_TOL = {"fp32": 3e-3, "bf16x3": 3e-3}
 
 
 # --------------------------------------------------------------------------- .ply export

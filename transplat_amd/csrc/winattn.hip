@@ -31,42 +31,12 @@
 namespace tsplat {
 namespace winattn {
 
-// TSPLAT_WA_ABL (diagnostic builds only, never the shipped library): removes one phase of the
-// key-pair kernel's tile loop to attribute its time (results are wrong in such a build)
-#ifndef TSPLAT_WA_ABL
-#define TSPLAT_WA_ABL 0
-#endif
-constexpr int kAbl = TSPLAT_WA_ABL;
 // TSPLAT_WA2_ABL (diagnostic builds only): removes one phase of the bf16 v2 loop -- 1 softmax,
 // 2 PV MFMAs, 3 QK MFMAs, 4 next-tile gather + staging (results are wrong in such a build)
 #ifndef TSPLAT_WA2_ABL
 #define TSPLAT_WA2_ABL 0
 #endif
 constexpr int kAbl2 = TSPLAT_WA2_ABL;
-
-// TSPLAT_WA_STAMP (diagnostic builds only): per-wave s_memtime sums of the key-pair kernel's loop
-// segments, read back with tsplat_diag_wa_stamps(); shares are meaningful, the build's time is not
-#ifndef TSPLAT_WA_STAMP
-#define TSPLAT_WA_STAMP 0
-#endif
-constexpr int kStampSegs = 10;
-constexpr int kStampWaves = 8192;
-#if TSPLAT_WA_STAMP
-__device__ unsigned long long g_wa_stamp[kStampWaves][kStampSegs];
-#define WA_STAMP(seg)                                                                        \
-    do {                                                                                     \
-        __builtin_amdgcn_sched_barrier(0);                                                   \
-        unsigned long long _t;                                                               \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");           \
-        stamp_acc[seg] += _t - stamp_prev;                                                   \
-        stamp_prev = _t;                                                                     \
-        __builtin_amdgcn_sched_barrier(0);                                                   \
-    } while (0)
-#else
-#define WA_STAMP(seg) \
-    do {              \
-    } while (0)
-#endif
 
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
@@ -655,903 +625,13 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
 
 
 // ============================================================================================
-// 16-query waves (v_mfma_f32_16x16x4_f32) over the same 128-query block: 8 waves per workgroup,
-// so the launch that gives the 32-query kernel ONE wave per SIMD (b = 1: 64 query blocks x 4 key
-// splits = 256 workgroups on 256 CUs) runs TWO per SIMD here, with the same key split and the
-// same partial slabs: one wave's softmax, LDS waits and barrier run under the other's MFMAs.
-// 16x16x4 f32 does 2,048 FLOP in 32 cycles, the 32x32x2 rate.
-//   S^T = K Q^T per 16-key subtile: A = K[key 16 sub + (l & 15)][d], B = Q[q = l & 15][d], the k
-//     index of lane group g = l >> 4 at step s mapped to d = 32 g + s (a lane's 32 dims are
-//     contiguous: Q in 32 registers, K as one ds_read_b128 per 4 steps); lane l then holds
-//     S^T[key 16 sub + 4 g + i][q = l & 15] in s[sub][i].
-//   O^T += V^T P^T: step (sub, i) contracts keys 16 sub + 4 g + i, so B = s[sub][i] itself and
-//     A = V^T[d = 16 dt + (l & 15)][that key]: one ds_read_b128 of the transposed V tile gives
-//     the 4 steps i of a (sub, dt).
-//   K and V^T double-buffered in LDS (2 x (33.8 + 34.8) KB): tile t + 1 is loaded into registers
-//     at the start of tile t and stored into the other buffer after QK(t); one barrier per tile.
-//     Staging thread: key row = lane, 16-dim segment = wave.
-//   Row sums stay lane-partial (the running max is uniform over a query's 4 lanes) and are
-//   reduced once at the end. Partials go out in the 32-query kernel's lane-contiguous layout
-//   (lane_tile_base), so the merge projection and the combine read them unchanged.
-// ============================================================================================
-constexpr int kWaves16 = 8;
-constexpr int kThreads16 = 64 * kWaves16;
-constexpr int kKRow16 = kC + 4;    // padded K row (floats)
-constexpr int kVtRow16 = kBK + 4;  // padded transposed-V row (floats)
-
-// lanes l and l ^ 16 (v_permlane16_swap exchanges 16-lane rows 0 <-> 1 and 2 <-> 3, VALU only)
-__device__ __forceinline__ float rows_max(float x) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float rows_sum(float x) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
-__global__ void __launch_bounds__(kThreads16, 1)
-win_attn_f32x16_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
-                       const float* __restrict__ v, float* __restrict__ out, Partials part) {
-    __shared__ __attribute__((aligned(16))) float sK[2][kBK * kKRow16];
-    __shared__ __attribute__((aligned(16))) float sVt[2][kC * kVtRow16];
-    __shared__ __attribute__((aligned(16))) int sReg[2][kBK];
-
-    int qblk, wi, bz;
-    xcd_block_coords(qblk, wi, bz);
-    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int n16 = lane & 15, g = lane >> 4;
-    const size_t HW = (size_t)p.H * p.W;
-    const float* qb = q + (size_t)b * HW * kC;
-    const int bkv = p.kv_shift ? (b + p.kv_shift) % p.nbatch : b;
-    const float* kb = k + (size_t)bkv * p.m * HW * kC;
-    const float* vb = v + (size_t)bkv * p.m * HW * kC;
-    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
-
-    floatx4 sk[4], sv[4];
-    int s_region = 0;
-    auto load_tile = [&](int k0) {
-        size_t off;
-        key_row(p, wi, HW, k0 + lane, off, s_region);
-        const floatx4* ksrc = reinterpret_cast<const floatx4*>(kb + off * kC + 16 * wid);
-        const floatx4* vsrc = reinterpret_cast<const floatx4*>(vb + off * kC + 16 * wid);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            sk[i] = ksrc[i];
-            sv[i] = vsrc[i];
-        }
-    };
-    auto store_tile = [&](int buf) {
-        float* dk = &sK[buf][lane * kKRow16 + 16 * wid];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) *reinterpret_cast<floatx4*>(dk + 4 * i) = sk[i];
-        float* dv = &sVt[buf][(16 * wid) * kVtRow16 + lane];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) dv[(4 * i + j) * kVtRow16] = sv[i][j];
-        if (wid == 0 && p.shift) sReg[buf][lane] = s_region;
-    };
-
-    const int tq = qblk * kBQ3 + wid * 16 + n16;
-    const int qpix = win_pixel(p, wi, tq);
-    const int qreg = p.shift ? win_region(p, wi, tq) : 0;
-    const float qscale = p.scale * kLog2e;  // log2-domain scores, bare v_exp_f32
-    float qr[32];
-    load_tile(kbeg);
-    {
-        const float4* src = reinterpret_cast<const float4*>(qb + (size_t)qpix * kC + 32 * g);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float4 t4 = src[i];
-            qr[4 * i] = t4.x * qscale;
-            qr[4 * i + 1] = t4.y * qscale;
-            qr[4 * i + 2] = t4.z * qscale;
-            qr[4 * i + 3] = t4.w * qscale;
-        }
-    }
-    floatx4 o[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (floatx4)(0.f);
-    float m_run = -INFINITY, l_run = 0.f;
-
-    store_tile(0);
-    __syncthreads();
-    int buf = 0;
-    for (int k0 = kbeg; k0 < kend; k0 += kBK, buf ^= 1) {
-        const bool has_next = k0 + kBK < kend;
-        // unconditional (the last tile reloads itself, unused): a conditional load of the staging
-        // registers made the compiler keep them in scratch
-        load_tile(has_next ? k0 + kBK : k0);
-
-        // ---- S^T = K Q^T: four 16-key subtiles, their chains interleaved
-        floatx4 s[4];
-#pragma unroll
-        for (int sub = 0; sub < 4; ++sub) s[sub] = (floatx4)(0.f);
-        const float* kt = &sK[buf][n16 * kKRow16 + 32 * g];
-#pragma unroll
-        for (int s4 = 0; s4 < 8; ++s4) {
-            float4 kk[4];
-#pragma unroll
-            for (int sub = 0; sub < 4; ++sub)
-                kk[sub] = *reinterpret_cast<const float4*>(kt + 16 * sub * kKRow16 + 4 * s4);
-#pragma unroll
-            for (int sub = 0; sub < 4; ++sub) s[sub] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[sub].x, qr[4 * s4 + 0], s[sub], 0, 0, 0);
-#pragma unroll
-            for (int sub = 0; sub < 4; ++sub) s[sub] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[sub].y, qr[4 * s4 + 1], s[sub], 0, 0, 0);
-#pragma unroll
-            for (int sub = 0; sub < 4; ++sub) s[sub] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[sub].z, qr[4 * s4 + 2], s[sub], 0, 0, 0);
-#pragma unroll
-            for (int sub = 0; sub < 4; ++sub) s[sub] = __builtin_amdgcn_mfma_f32_16x16x4f32(kk[sub].w, qr[4 * s4 + 3], s[sub], 0, 0, 0);
-        }
-        // ---- shifted-window mask (region ids of the lane's keys 16 sub + 4 g + i)
-        if (p.shift) {
-#pragma unroll
-            for (int sub = 0; sub < 4; ++sub) {
-                const int4 rg = *reinterpret_cast<const int4*>(&sReg[buf][16 * sub + 4 * g]);
-                s[sub][0] += rg.x == qreg ? 0.0f : kMaskLog2;
-                s[sub][1] += rg.y == qreg ? 0.0f : kMaskLog2;
-                s[sub][2] += rg.z == qreg ? 0.0f : kMaskLog2;
-                s[sub][3] += rg.w == qreg ? 0.0f : kMaskLog2;
-            }
-        }
-        // ---- online softmax (a query's 64 keys live in its 4 lanes l & 15 + 16 g)
-        float bmax = -INFINITY;
-#pragma unroll
-        for (int sub = 0; sub < 4; ++sub)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) bmax = fmaxf(bmax, s[sub][i]);
-        bmax = halves_max(rows_max(bmax));
-        const float m_new = fmaxf(m_run, bmax);
-        if (__any(m_new > m_run)) {  // exact: corr == 1 for every lane otherwise
-            const float corr = fast_exp2(m_run - m_new);
-            l_run *= corr;
-#pragma unroll
-            for (int dt = 0; dt < 8; ++dt) o[dt] *= corr;
-            m_run = m_new;
-        }
-#pragma unroll
-        for (int sub = 0; sub < 4; ++sub)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const float e = fast_exp2(s[sub][i] - m_run);
-                s[sub][i] = e;
-                l_run += e;
-            }
-        // the other buffer's last readers (tile t - 1) passed the previous barrier
-        if (has_next) store_tile(buf ^ 1);
-
-        // ---- O^T += V^T P^T: 8 d tiles' chains interleaved over the 16 key steps
-        const float* vt = &sVt[buf][n16 * kVtRow16 + 4 * g];
-#pragma unroll
-        for (int sub = 0; sub < 4; ++sub) {
-            float4 vv[8];
-#pragma unroll
-            for (int dt = 0; dt < 8; ++dt) vv[dt] = *reinterpret_cast<const float4*>(vt + 16 * dt * kVtRow16 + 16 * sub);
-#pragma unroll
-            for (int dt = 0; dt < 8; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt].x, s[sub][0], o[dt], 0, 0, 0);
-#pragma unroll
-            for (int dt = 0; dt < 8; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt].y, s[sub][1], o[dt], 0, 0, 0);
-#pragma unroll
-            for (int dt = 0; dt < 8; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt].z, s[sub][2], o[dt], 0, 0, 0);
-#pragma unroll
-            for (int dt = 0; dt < 8; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(vv[dt].w, s[sub][3], o[dt], 0, 0, 0);
-        }
-        __syncthreads();  // tile t's buffers are free; tile t + 1's are visible
-    }
-    l_run = halves_sum(rows_sum(l_run));
-
-    // O^T[d = 16 dt + 4 g + i][q] in o[dt][i]
-    if (p.ksplit == 1) {
-        const float inv = 1.0f / l_run;
-        float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * g;
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt)
-            *reinterpret_cast<float4*>(dst + 16 * dt) =
-                make_float4(o[dt][0] * inv, o[dt][1] * inv, o[dt][2] * inv, o[dt][3] * inv);
-    } else {
-        // the 32-query kernel's lane-contiguous partial layout: query t of the block sits in wave
-        // slot t >> 5, lane c = t & 31 (+ 32 for dims with bit 2 set); d = D .. D + 3 at float4
-        // ((D >> 5) * 4 + ((D >> 3) & 3)) * 64 + c + 32 ((D >> 2) & 1)
-        const int t = wid * 16 + n16;
-        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, t >> 5)) + (t & 31);
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-            const int D = 16 * dt + 4 * g;
-            dst[((D >> 5) * 4 + ((D >> 3) & 3)) * 64 + 32 * ((D >> 2) & 1)] =
-                make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]);
-        }
-        if (g == 0) {
-            const size_t row = pidx(p, b, wi, ks, tq);
-            part.m[row] = m_run * kLn2;  // natural-log domain for the combine
-            part.l[row] = l_run;
-        }
-    }
-}
-
-// ============================================================================================
-// Key-pair variant of the 32x32x2 kernel (for launches that need a key split): a workgroup of
-// 4 waves owns 64 queries; waves (2g, 2g + 1) share query group g and take the low / high 32 keys
-// of every 64-key tile, so each workgroup covers twice the keys of the 128-query kernel at the
-// same work. The two halves merge their (max, sum, O) in LDS at the end, which halves the
-// global split (and its partial traffic and combine) for the same number of workgroups.
-// Partials use the 128-query lane-contiguous layout (wave slot = 2 (qblk & 1) + g), so the same
-// combine kernel applies.
-// ============================================================================================
-__global__ void __launch_bounds__(kThreads, 2)
-win_attn_f32_pair_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
-                         const float* __restrict__ v, float* __restrict__ out, Partials part) {
-    __shared__ __attribute__((aligned(16))) float sK[kBK * kC];
-    __shared__ __attribute__((aligned(16))) float sVt[kC * kVtStride];
-    __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
-
-#if TSPLAT_WA_STAMP
-    unsigned long long stamp_acc[kStampSegs] = {}, stamp_prev;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_prev)::"memory");
-#endif
-    int qblk, wi, bz;  // qblk: 64-query block
-    xcd_block_coords(qblk, wi, bz);
-    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int qg = wid >> 1, kh = wid & 1;
-    const int c = lane & 31, h = lane >> 5;
-    const size_t HW = (size_t)p.H * p.W;
-    const float* qb = q + (size_t)b * HW * kC;
-    const int bkv = p.kv_shift ? (b + p.kv_shift) % p.nbatch : b;
-    const float* kb = k + (size_t)bkv * p.m * HW * kC;
-    const float* vb = v + (size_t)bkv * p.m * HW * kC;
-
-    const int tq = qblk * 64 + qg * 32 + c;
-    const int qpix = win_pixel(p, wi, tq);
-    const int qreg = p.shift ? win_region(p, wi, tq) : 0;
-    // scores are kept in the log2 domain (Q pre-scaled by log2(e) / sqrt(C), mask -100 log2(e)) so
-    // the softmax exponentials are bare v_exp_f32; m is converted back to natural log for partials
-    const float qscale = p.scale * kLog2e;
-    float qr[64];
-    {
-        const float4* src = reinterpret_cast<const float4*>(qb + (size_t)qpix * kC + 64 * h);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float4 t4 = src[i];
-            qr[4 * i] = t4.x * qscale;
-            qr[4 * i + 1] = t4.y * qscale;
-            qr[4 * i + 2] = t4.z * qscale;
-            qr[4 * i + 3] = t4.w * qscale;
-        }
-    }
-    floatx16 o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
-    float m_run = -INFINITY, l_run = 0.f;
-
-    // staging (T14 split): the next tile's K rows are loaded into registers during this tile's
-    // QK^T and written to LDS after the barrier that retires K(t); the same registers then carry
-    // V(t+1) during PV(t). One 8 x float4 register set, two barriers per tile: V(t+1) is stored
-    // after the second and first read after the next tile's first.
-    const int grow = tid & 63, gpart = tid >> 6;
-    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
-    const int row = 32 * kh + c;  // this lane's key row (A operand) within the tile
-    float4 stg[8];
-    int stg_region = 0;
-    size_t stg_off = 0;  // row offset of this thread's key in the tile being staged (K, then V)
-    auto load_k = [&](int k0) {
-        key_row(p, wi, HW, k0 + grow, stg_off, stg_region);
-        const float4* src = reinterpret_cast<const float4*>(kb + stg_off * kC + 32 * gpart);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) stg[i] = src[i];
-    };
-    auto load_v = [&]() {
-        const float4* src = reinterpret_cast<const float4*>(vb + stg_off * kC + 32 * gpart);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) stg[i] = src[i];
-    };
-    auto store_k = [&]() {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int chunk = 8 * gpart + i;
-            *reinterpret_cast<float4*>(&sK[grow * kC + ((chunk ^ (grow & 15)) * 4)]) = stg[i];
-        }
-        if (gpart == 0 && p.shift) sKeyRegion[grow] = stg_region;
-    };
-    auto store_v = [&]() {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int chunk = 8 * gpart + i;
-            sVt[(4 * chunk + 0) * kVtStride + grow] = stg[i].x;
-            sVt[(4 * chunk + 1) * kVtStride + grow] = stg[i].y;
-            sVt[(4 * chunk + 2) * kVtStride + grow] = stg[i].z;
-            sVt[(4 * chunk + 3) * kVtStride + grow] = stg[i].w;
-        }
-    };
-    load_k(kbeg);
-    store_k();
-    load_v();
-    store_v();
-    __syncthreads();
-    WA_STAMP(0);  // prologue
-    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
-        const bool has_next = k0 + kBK < kend;
-        if (has_next && kAbl != 3) load_k(k0 + kBK);
-
-        // ---- S^T for this wave's 32 keys (one chain: 32x32x2 issue interval = dependent latency;
-        // the next K chunk is read before the current chunk's MFMAs)
-        floatx16 s;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] = 0.f;
-        {
-            auto kread = [&](int i4) {
-                return *reinterpret_cast<const float4*>(&sK[row * kC + (((16 * h + i4) ^ (row & 15)) * 4)]);
-            };
-            float4 ka = kread(0);
-#pragma unroll
-            for (int i4 = 0; i4 < 16; ++i4) {
-                const float4 nk = i4 + 1 < 16 ? kread(i4 + 1) : ka;
-                if (kAbl == 6) { s[i4] += ka.x * qr[4 * i4]; ka = nk; continue; }
-                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.x, qr[4 * i4 + 0], s, 0, 0, 0);
-                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.y, qr[4 * i4 + 1], s, 0, 0, 0);
-                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.z, qr[4 * i4 + 2], s, 0, 0, 0);
-                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.w, qr[4 * i4 + 3], s, 0, 0, 0);
-                ka = nk;
-            }
-        }
-        WA_STAMP(1);  // QK issue
-        if (p.shift) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int4 rg = *reinterpret_cast<const int4*>(&sKeyRegion[32 * kh + 8 * u + 4 * h]);
-                s[4 * u + 0] += rg.x == qreg ? 0.0f : kMaskLog2;
-                s[4 * u + 1] += rg.y == qreg ? 0.0f : kMaskLog2;
-                s[4 * u + 2] += rg.z == qreg ? 0.0f : kMaskLog2;
-                s[4 * u + 3] += rg.w == qreg ? 0.0f : kMaskLog2;
-            }
-        }
-        if (kAbl != 1) {
-            float bmax = -INFINITY;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[r]);
-            bmax = halves_max(bmax);
-            const float m_new = fmaxf(m_run, bmax);
-            // rescale only when some query's running max moved (corr is exactly 1 otherwise)
-            if (__any(m_new > m_run)) {
-                const float corr = fast_exp2(m_run - m_new);
-                l_run *= corr;
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
-                m_run = m_new;
-            }
-            float bsum = 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float e = fast_exp2(s[r] - m_run);
-                s[r] = e;
-                bsum += e;
-            }
-            bsum = halves_sum(bsum);
-            l_run += bsum;
-        }
-
-        WA_STAMP(2);  // mask + softmax (waits for the QK MFMAs)
-        if (kAbl != 2) __syncthreads();  // every wave is done with K(t) / regions(t)
-        WA_STAMP(3);  // barrier 1
-        if (has_next) {
-            if (kAbl != 4) store_k();
-            if (kAbl != 3) load_v();
-        }
-        WA_STAMP(4);  // store K(t+1) (waits for its loads), issue V(t+1) loads
-
-        // ---- O^T += V^T P^T over this wave's 32 keys, the four d tiles' chains interleaved
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int dp = 0; dp < 4; dp += 2) {
-                if (kAbl == 5) break;
-                const float4 v0 = *reinterpret_cast<const float4*>(&sVt[(32 * dp + c) * kVtStride + 32 * kh + 8 * u + 4 * h]);
-                const float4 v1 = *reinterpret_cast<const float4*>(&sVt[(32 * dp + 32 + c) * kVtStride + 32 * kh + 8 * u + 4 * h]);
-                o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.x, s[4 * u + 0], o[dp], 0, 0, 0);
-                o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.x, s[4 * u + 0], o[dp + 1], 0, 0, 0);
-                o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.y, s[4 * u + 1], o[dp], 0, 0, 0);
-                o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.y, s[4 * u + 1], o[dp + 1], 0, 0, 0);
-                o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.z, s[4 * u + 2], o[dp], 0, 0, 0);
-                o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.z, s[4 * u + 2], o[dp + 1], 0, 0, 0);
-                o[dp] = __builtin_amdgcn_mfma_f32_32x32x2f32(v0.w, s[4 * u + 3], o[dp], 0, 0, 0);
-                o[dp + 1] = __builtin_amdgcn_mfma_f32_32x32x2f32(v1.w, s[4 * u + 3], o[dp + 1], 0, 0, 0);
-            }
-        WA_STAMP(5);  // PV issue
-        if (kAbl != 2) __syncthreads();  // every wave is done with V(t); K(t+1) is visible
-        WA_STAMP(6);  // barrier 2 (waits for the PV MFMAs)
-        // V(t+1) becomes visible at the next tile's first barrier, before its PV reads
-        if (has_next && kAbl != 4) store_v();
-        WA_STAMP(7);  // store V(t+1)
-    }
-
-    // ---- merge the two key halves of each query group through LDS (sK / sVt are free now)
-    float* so = sK + qg * 64 * 64;          // [16 regs x 4 dt][64 lanes] of the high-key wave
-    float* sml = sVt + qg * 128;            // [64 lanes] m, [64 lanes] l
-    if (kh == 1) {
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) so[(dt * 16 + r) * 64 + lane] = o[dt][r];
-        sml[lane] = m_run;
-        sml[64 + lane] = l_run;
-    }
-    __syncthreads();
-#if TSPLAT_WA_STAMP
-    WA_STAMP(8);  // merge
-    {
-        const int wave_id = (blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 4 + wid;
-        if (lane == 0 && wave_id < kStampWaves)
-            for (int i = 0; i < kStampSegs; ++i) g_wa_stamp[wave_id][i] = stamp_acc[i];
-    }
-#endif
-    if (kh == 1) return;
-    {
-        const float m1 = sml[lane], l1 = sml[64 + lane];
-        const float M = fmaxf(m_run, m1);
-        const float a0 = fast_exp2(m_run - M), a1 = fast_exp2(m1 - M);
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) o[dt][r] = o[dt][r] * a0 + so[(dt * 16 + r) * 64 + lane] * a1;
-        l_run = l_run * a0 + l1 * a1;
-        m_run = M;
-    }
-
-    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
-    if (p.ksplit == 1) {
-        const float inv = 1.0f / l_run;
-        float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                *reinterpret_cast<float4*>(dst + 32 * dt + 8 * u) =
-                    make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv, o[dt][4 * u + 2] * inv,
-                                o[dt][4 * u + 3] * inv);
-    } else {
-        const size_t prow = pidx(p, b, wi, ks, tq);
-        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk >> 1, 2 * (qblk & 1) + qg)) + lane;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
-        if (h == 0) {
-            part.m[prow] = m_run * kLn2;
-            part.l[prow] = l_run;
-        }
-    }
-}
-
-// ============================================================================================
-// Quad kernel (launches whose 128-query blocks cannot fill the chip, e.g. the 2-view 64x64 map
-// at batch 1: 64 blocks): one workgroup = 4 INDEPENDENT waves on the same 32 queries, wave w
-// taking the w-th quarter of the window's keys, merged once through LDS at the end. No global
-// key split: no partial slabs in HBM and no combine launch; 256 workgroups of 32 queries fill
-// the 256 CUs once. Each wave stages its own 32-key K / V tiles (no workgroup barrier in the
-// loop): tile t+1's rows are loaded into registers during tile t's MFMAs and stored after them.
-//   loads: instruction i covers 8 key rows x 128 B (rows 8 (i & 3) + (lane >> 3), 128-B segment
-//          i >> 2), i.e. whole cache lines; a lane holds 4 rows' pieces.
-//   K: row-major, 16-B chunks XOR-swizzled by row (the x32 kernel's S^T = K Q^T reads, 1 subtile).
-//   V: row-major, rows padded to 136 floats: the O^T += V^T P^T A operand of lane (c, h) is
-//      V[key 8u + 4h + j][32 dt + c], one ds_read_b32 per MFMA, the two half-waves (key + 4)
-//      on disjoint banks.
-// ============================================================================================
-constexpr int kQT = 32;             // keys per wave tile
-constexpr int kVRow = kC + 8;       // padded V row (floats)
-constexpr int kQuadWave = kQT * kC + kQT * kVRow + kQT;  // floats of one wave's LDS region
-
-__global__ void __launch_bounds__(kThreads, 1)
-win_attn_f32_quad_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
-                         const float* __restrict__ v, float* __restrict__ out) {
-    __shared__ __attribute__((aligned(16))) float smem[4 * kQuadWave];
-    __shared__ float sML[4][2][kQW];
-
-    int qblk, wi, b;
-    xcd_block_coords(qblk, wi, b);
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int c = lane & 31, h = lane >> 5;
-    const size_t HW = (size_t)p.H * p.W;
-    const float* qb = q + (size_t)b * HW * kC;
-    const int bkv = p.kv_shift ? (b + p.kv_shift) % p.nbatch : b;
-    const float* kb = k + (size_t)bkv * p.m * HW * kC;
-    const float* vb = v + (size_t)bkv * p.m * HW * kC;
-    float* sK = smem + wid * kQuadWave;
-    float* sV = sK + kQT * kC;
-    int* sReg = reinterpret_cast<int*>(sV + kQT * kVRow);
-
-    const int nkeys = p.L * p.m / 4;
-    const int kbeg = wid * nkeys, kend = kbeg + nkeys;
-    const int lrow = lane >> 3, lseg = lane & 7;  // row within an 8-row group, 16-B piece of a 128-B segment
-    floatx4 stk[16], stv[16];  // vector types: plain loads, no memcpy (which stays in scratch)
-    int rreg[4];
-#define QUAD_LOAD_TILE(k0_)                                                                      \
-    {                                                                                            \
-        size_t roff[4];                                                                          \
-        _Pragma("unroll") for (int g = 0; g < 4; ++g)                                            \
-            key_row(p, wi, HW, (k0_) + 8 * g + lrow, roff[g], rreg[g]);                          \
-        _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                         \
-            const size_t o_ = roff[i & 3] * kC + 32 * (i >> 2) + 4 * lseg;                       \
-            stk[i] = *reinterpret_cast<const floatx4*>(kb + o_);                                  \
-            stv[i] = *reinterpret_cast<const floatx4*>(vb + o_);                                  \
-        }                                                                                        \
-    }
-#define QUAD_STORE_TILE()                                                                        \
-    {                                                                                            \
-        _Pragma("unroll") for (int i = 0; i < 16; ++i) {                                         \
-            const int row = 8 * (i & 3) + lrow, chunk = 8 * (i >> 2) + lseg;                    \
-            *reinterpret_cast<floatx4*>(&sK[row * kC + ((chunk ^ (row & 15)) * 4)]) = stk[i];     \
-            *reinterpret_cast<floatx4*>(&sV[row * kVRow + chunk * 4]) = stv[i];                 \
-        }                                                                                        \
-        if (p.shift && lseg == 0) {                                                              \
-            _Pragma("unroll") for (int g = 0; g < 4; ++g) sReg[8 * g + lrow] = rreg[g];          \
-        }                                                                                        \
-    }
-
-    const int tq = qblk * kQW + c;
-    const int qpix = win_pixel(p, wi, tq);
-    const int qreg = p.shift ? win_region(p, wi, tq) : 0;
-    const float qscale = p.scale * kLog2e;  // log2-domain scores (see the key-pair kernel)
-    float qr[64];
-    QUAD_LOAD_TILE(kbeg);
-    {
-        const float4* src = reinterpret_cast<const float4*>(qb + (size_t)qpix * kC + 64 * h);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float4 t4 = src[i];
-            qr[4 * i] = t4.x * qscale;
-            qr[4 * i + 1] = t4.y * qscale;
-            qr[4 * i + 2] = t4.z * qscale;
-            qr[4 * i + 3] = t4.w * qscale;
-        }
-    }
-    floatx16 o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
-    float m_run = -INFINITY, l_run = 0.f;
-    QUAD_STORE_TILE();
-
-    for (int k0 = kbeg; k0 < kend; k0 += kQT) {
-        // this wave's LDS stores of tile t are complete before any lane reads them
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const bool has_next = k0 + kQT < kend;
-        if (has_next) QUAD_LOAD_TILE(k0 + kQT);
-
-        // ---- S^T = K Q^T over the tile's 32 keys (lane = query c; keys 8(r >> 2) + 4h + (r & 3))
-        floatx16 s;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] = 0.f;
-        {
-            auto kread = [&](int i4) {
-                return *reinterpret_cast<const float4*>(&sK[c * kC + (((16 * h + i4) ^ (c & 15)) * 4)]);
-            };
-            float4 ka = kread(0);
-#pragma unroll
-            for (int i4 = 0; i4 < 16; ++i4) {
-                const float4 nk = i4 + 1 < 16 ? kread(i4 + 1) : ka;
-                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.x, qr[4 * i4 + 0], s, 0, 0, 0);
-                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.y, qr[4 * i4 + 1], s, 0, 0, 0);
-                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.z, qr[4 * i4 + 2], s, 0, 0, 0);
-                s = __builtin_amdgcn_mfma_f32_32x32x2f32(ka.w, qr[4 * i4 + 3], s, 0, 0, 0);
-                ka = nk;
-            }
-        }
-        if (p.shift) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int4 rg = *reinterpret_cast<const int4*>(&sReg[8 * u + 4 * h]);
-                s[4 * u + 0] += rg.x == qreg ? 0.0f : kMaskLog2;
-                s[4 * u + 1] += rg.y == qreg ? 0.0f : kMaskLog2;
-                s[4 * u + 2] += rg.z == qreg ? 0.0f : kMaskLog2;
-                s[4 * u + 3] += rg.w == qreg ? 0.0f : kMaskLog2;
-            }
-        }
-        float bmax = -INFINITY;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[r]);
-        bmax = halves_max(bmax);
-        const float m_new = fmaxf(m_run, bmax);
-        if (__any(m_new > m_run)) {  // exact: corr == 1 for every lane otherwise
-            const float corr = fast_exp2(m_run - m_new);
-            l_run *= corr;
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
-            m_run = m_new;
-        }
-        float bsum = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const float e = fast_exp2(s[r] - m_run);
-            s[r] = e;
-            bsum += e;
-        }
-        l_run += halves_sum(bsum);
-
-        // ---- O^T += V^T P^T: k-step (u, j) contracts keys {8u + j, 8u + 4 + j} (lane halves)
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float* vrow = &sV[(8 * u + 4 * h + j) * kVRow + c];
-                const float a0 = vrow[0], a1 = vrow[32], a2 = vrow[64], a3 = vrow[96];
-                o[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, s[4 * u + j], o[0], 0, 0, 0);
-                o[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, s[4 * u + j], o[1], 0, 0, 0);
-                o[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a2, s[4 * u + j], o[2], 0, 0, 0);
-                o[3] = __builtin_amdgcn_mfma_f32_32x32x2f32(a3, s[4 * u + j], o[3], 0, 0, 0);
-            }
-        if (has_next) QUAD_STORE_TILE();  // waits for tile t+1's loads; every lane's reads of tile t are done
-    }
-
-    // ---- merge the four key quarters: wave w finishes output d tile w.
-    // Own region, own (finished) loop: park the three d tiles other waves finish, then one barrier.
-    if (h == 0) {
-        sML[wid][0][c] = m_run;
-        sML[wid][1][c] = l_run;
-    }
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-        if (dt == wid) continue;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sK[(dt * 16 + r) * 64 + lane] = o[dt][r];
-    }
-    __syncthreads();
-    float mw[4], M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        mw[w] = sML[w][0][c];
-        M = fmaxf(M, mw[w]);
-    }
-    float a[4], L = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        a[w] = fast_exp2(mw[w] - M);
-        L += a[w] * sML[w][1][c];
-    }
-    const float inv = 1.0f / L;
-    floatx16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        if (w == wid) {
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)  // compile-time register index (o[wid] would spill)
-                if (dt == wid)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) acc[r] += a[w] * o[dt][r];
-        } else {
-            const float* src = smem + w * kQuadWave + wid * 16 * 64 + lane;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] += a[w] * src[r * 64];
-        }
-    }
-    // O^T[d = 32 wid + 8u + 4h + j][q = c] in acc[4u + j]
-    float* dst = out + ((size_t)b * HW + qpix) * kC + 32 * wid + 4 * h;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-        *reinterpret_cast<float4*>(dst + 8 * u) =
-            make_float4(acc[4 * u] * inv, acc[4 * u + 1] * inv, acc[4 * u + 2] * inv, acc[4 * u + 3] * inv);
-#undef QUAD_LOAD_TILE
-#undef QUAD_STORE_TILE
-}
-
-// ============================================================================================
-// bf16 variant (config C3: bf16 attention): v_mfma_f32_32x32x16_bf16, fp32 accumulation and
-// fp32 softmax, bf16 in/out. One workgroup = 4 waves x 32 queries, 64-key tiles in LDS as bf16
-// (K rows XOR-swizzled per 16-B chunk, V transposed). Operand maps (lane l, c = l & 31,
-// h = l >> 5, fragment element j = 0..7):
-//   QK step i (0..7): A = K[key c][16i + 8h + j], B = Q[query c][16i + 8h + j] (registers).
-//   S^T tile: lane holds query c, keys 8(r >> 2) + 4h + (r & 3) in register r.
-//   PV k-step s (16 keys) takes the S^T registers 8s..8s+7 packed to bf16 as the B operand
-//   (element j <-> key 16s + 8(j >> 2) + 4h + (j & 3)); A = V^T[d][same keys] from LDS.
-// ============================================================================================
+// bf16 operand types (the v2 / v3 kernels below)
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 constexpr int kVtStrideH = kBK + 8;  // transposed V row (bf16 elements)
 
-__global__ void __launch_bounds__(kThreads, 2)
-win_attn_bf16_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __restrict__ k,
-                     const __bf16* __restrict__ v, __bf16* __restrict__ out, Partials part) {
-    __shared__ __attribute__((aligned(16))) __bf16 sK[kBK * kC];
-    __shared__ __attribute__((aligned(16))) __bf16 sVt[kC * kVtStrideH];
-    __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
-
-    int qblk, wi, bz;
-    xcd_block_coords(qblk, wi, bz);
-    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int c = lane & 31, h = lane >> 5;
-    const size_t HW = (size_t)p.H * p.W;
-    const __bf16* qb = q + (size_t)b * HW * kC;
-    const __bf16* kb = k + (size_t)b * p.m * HW * kC;
-    const __bf16* vb = v + (size_t)b * p.m * HW * kC;
-
-    const int tq = qblk * kBQ3 + wid * kQW + c;
-    const int qpix = win_pixel(p, wi, tq);
-    const int qreg = p.shift ? win_region(p, wi, tq) : 0;
-    bf16x8 qf[8];
-    {
-        const bf16x8* src = reinterpret_cast<const bf16x8*>(qb + (size_t)qpix * kC + 8 * h);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) qf[i] = src[2 * i];
-    }
-    floatx16 o[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
-    float m_run = -INFINITY, l_run = 0.f;
-
-    // gather: thread = (key row grow, 32-channel quarter gpart). The next tile's rows are loaded
-    // into registers right after this tile's barrier and written to LDS after the end-of-tile
-    // barrier (issue early / write late). V is transposed in the write: lanes 2r and 2r + 1 (keys
-    // 2r, 2r + 1) swap half their channels so each writes 32-bit (key pair) words.
-    const int grow = tid & 63, gpart = tid >> 6;
-    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
-    bf16x8 kv[4], vv[4];
-    int kreg = 0;
-    auto gather = [&](int k0) {
-        const int j = k0 + grow;
-        const int tk = j / p.m, vi = j - tk * p.m;
-        const int kpix = win_pixel(p, wi, tk);
-        const bf16x8* ksrc = reinterpret_cast<const bf16x8*>(kb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
-        const bf16x8* vsrc = reinterpret_cast<const bf16x8*>(vb + ((size_t)vi * HW + kpix) * kC + 32 * gpart);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            kv[i] = ksrc[i];
-            vv[i] = vsrc[i];
-        }
-        kreg = p.shift ? win_region(p, wi, j % p.L) : 0;
-    };
-    auto stage = [&]() {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int chunk = 4 * gpart + i;  // 16-B chunk (8 channels) of the 256-B row
-            *reinterpret_cast<bf16x8*>(&sK[grow * kC + ((chunk ^ (grow & 15)) * 8)]) = kv[i];
-        }
-        // V^T: lane pair (even key e, odd key e + 1); even lane writes channels 0..15 of the
-        // quarter, odd lane 16..31, each as (V[e][d], V[e+1][d]) words
-        const bool odd = grow & 1;
-        const int key0 = grow & ~1;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            // give away the half the partner writes, receive the partner's half of mine
-            const bf16x8 mine = odd ? vv[2 + i] : vv[i];
-            const bf16x8 give = odd ? vv[i] : vv[2 + i];
-            typedef int intx4 __attribute__((ext_vector_type(4)));
-            const intx4 gi = __builtin_bit_cast(intx4, give);
-            intx4 ri;
-#pragma unroll
-            for (int w = 0; w < 4; ++w) ri[w] = __shfl_xor(gi[w], 1);
-            const bf16x8 other = __builtin_bit_cast(bf16x8, ri);
-            const int c0 = 32 * gpart + 16 * (odd ? 1 : 0) + 8 * i;  // first channel of this 8-run
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-                const bf16x2 pr = odd ? bf16x2{other[e], mine[e]} : bf16x2{mine[e], other[e]};
-                *reinterpret_cast<bf16x2*>(&sVt[(c0 + e) * kVtStrideH + key0]) = pr;
-            }
-        }
-        if (gpart == 0 && p.shift) sKeyRegion[grow] = kreg;
-    };
-    gather(kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += kBK) {
-        stage();
-        __syncthreads();
-        if (k0 + kBK < kend) gather(k0 + kBK);
-
-        // ---- S^T = K Q^T (two 32-key subtiles, interleaved chains), scaled in fp32
-        floatx16 s[2];
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[0][r] = s[1][r] = 0.f;
-        {
-            bf16x8 kk[2][8];
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int row = 32 * sub + c, chunk = 2 * i + h;
-                    kk[sub][i] = *reinterpret_cast<const bf16x8*>(&sK[row * kC + ((chunk ^ (row & 15)) * 8)]);
-                }
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                s[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk[0][i], qf[i], s[0], 0, 0, 0);
-                s[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kk[1][i], qf[i], s[1], 0, 0, 0);
-            }
-        }
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) s[sub][r] *= p.scale;
-        // ---- mask (int4 region reads, branch-free) + online softmax (fp32)
-        if (p.shift) {
-#pragma unroll
-            for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int4 rg = *reinterpret_cast<const int4*>(&sKeyRegion[32 * sub + 8 * u + 4 * h]);
-                    s[sub][4 * u + 0] += rg.x == qreg ? 0.0f : -100.0f;
-                    s[sub][4 * u + 1] += rg.y == qreg ? 0.0f : -100.0f;
-                    s[sub][4 * u + 2] += rg.z == qreg ? 0.0f : -100.0f;
-                    s[sub][4 * u + 3] += rg.w == qreg ? 0.0f : -100.0f;
-                }
-        }
-        float bmax = -INFINITY;
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[sub][r]);
-        bmax = halves_max(bmax);
-        const float m_new = fmaxf(m_run, bmax);
-        const float corr = __expf(m_run - m_new);
-        float bsum = 0.f;
-#pragma unroll
-        for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float e = __expf(s[sub][r] - m_new);
-                s[sub][r] = e;
-                bsum += e;
-            }
-        bsum = halves_sum(bsum);
-        l_run = l_run * corr + bsum;
-        m_run = m_new;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
-
-        // ---- O^T += V^T P^T: 4 k-steps of 16 keys
-#pragma unroll
-        for (int ksx = 0; ksx < 4; ++ksx) {
-            const int sub = ksx >> 1, st = ksx & 1;
-            bf16x8 pf;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) pf[e] = (__bf16)s[sub][8 * st + e];
-            const int key0 = 16 * ksx + 4 * h;  // keys key0 + 0..3 and key0 + 8 + 0..3
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-                const __bf16* vrow = &sVt[(32 * dt + c) * kVtStrideH];
-                const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vrow + key0);
-                const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vrow + key0 + 8);
-                const bf16x8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[dt], 0, 0, 0);
-            }
-        }
-        __syncthreads();
-    }
-
-    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
-    if (p.ksplit == 1) {
-        const float inv = 1.0f / l_run;
-        __bf16* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                store4(dst + 32 * dt + 8 * u, make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv,
-                                                          o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
-    } else {
-        // lane-contiguous partial tile: each store instruction writes one 1-KB run
-        const size_t row = pidx(p, b, wi, ks, tq);
-        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, wid)) + lane;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
-        if (h == 0) {
-            part.m[row] = m_run;
-            part.l[row] = l_run;
-        }
-    }
-}
-
 // ============================================================================================
-// bf16 v2 (default for bf16): the same operand maps as win_attn_bf16_kernel, re-cut for the
+// bf16 v2 (bf16 launches that need a key split): the round-1 bf16 kernel's operand maps, re-cut for the
 // VALU budget beside 2.5 PF of matrix cores (one 32x32x16 MFMA = 32 cycles, of which 24 are free
 // for vector issue):
 //   * K / V / mask tiles double-buffered in LDS, one barrier per key tile (the next tile's rows,
@@ -2047,8 +1127,10 @@ static int choose_ksplit(int base_wgs, int key_tiles, int target) {
     return ks;
 }
 
-// Tuning knobs (benchmarking only): TSPLAT_WINATTN=16 forces the 16x16x4 kernel, =32 the 128-query
-// 32x32x2 kernel, =pair the key-pair kernel; TSPLAT_WINATTN_KSPLIT forces the key split.
+// Tuning knobs (benchmarking only): TSPLAT_WINATTN=16 forces the 16x16x4 kernel;
+// TSPLAT_WINATTN_KSPLIT forces the key split. (Round 4: the opt-in variants measured slower than the
+// defaults -- the 16-query-wave x16 kernel, the key-pair kernel, the split-free quad kernel and the
+// round-1 bf16 kernel -- were removed; DESIGN.md §3 keeps their measurements.)
 static int env_int(const char* name, int dflt) {
     const char* e = getenv(name);
     return e ? atoi(e) : dflt;
@@ -2057,12 +1139,6 @@ static bool env_is(const char* name, const char* val) {
     const char* e = getenv(name);
     return e && !strcmp(e, val);
 }
-
-// 128-query blocks as 8 x 16-query waves (win_attn_f32x16_kernel) with TSPLAT_WA16=1; default the
-// 4 x 32-query kernel. Same-box A/B (round 3, tools/sessions/ab_r3.sh): x16 47.5 vs x32 50.0 us per launch at
-// the C2 shape, but the C2 step 355.9 / 357.1 vs 360.8 views/s with the concurrent encoder branches
-// (its 138 KB of LDS leaves no room on a CU for the other branch's workgroups).
-static bool use_x16() { return env_is("TSPLAT_WA16", "1"); }
 
 // query-block size of the kernel used for window size L (128: 32x32x2 kernel, 64: 16x16x4)
 static int query_block(int L) {
@@ -2077,17 +1153,6 @@ static int pick_ksplit(int base, int key_tiles, int qb) {
     return choose_ksplit(base, key_tiles, qb == tsplat::winattn::kBQ3 ? 256 : 512);
 }
 
-// quad kernel (no global key split): opt-in with TSPLAT_WINATTN=quad where its shape constraints
-// hold. Measured on MI355X (2-view 64x64 map, b = 2, shifted): 59.7 us vs 56.9 us for the 128-query
-// kernel with its 4-way key split + combine, and 115 vs 96.5 us at b = 4, so the split kernels stay
-// the default: one wave per SIMD re-reading a quarter of the window's K/V per 32 queries (1 MB per
-// workgroup through L2) costs more than the partial slabs it avoids.
-static bool use_quad(int L, int m, int base128) {
-    (void)base128;
-    if (L % tsplat::winattn::kQW || (L * m) % (4 * tsplat::winattn::kQT)) return false;
-    return env_is("TSPLAT_WINATTN", "quad");
-}
-
 extern "C" size_t tsplat_win_attn_workspace_bytes(int32_t batch, int32_t height, int32_t width,
                                                   int32_t key_views, int32_t splits) {
     using namespace tsplat::winattn;
@@ -2095,7 +1160,6 @@ extern "C" size_t tsplat_win_attn_workspace_bytes(int32_t batch, int32_t height,
     const int L = (height / splits) * (width / splits);
     if (L % kBQ || (L * key_views) % kBK) return 0;
     const int base = (L / query_block(L)) * splits * splits * batch;
-    if (use_quad(L, key_views, (L / kBQ3) * splits * splits * batch)) return 0;
     const int ks = pick_ksplit(base, L * key_views / kBK, query_block(L));
     if (ks == 1) return 0;
     return (size_t)batch * splits * splits * ks * L * (kC + 2) * sizeof(float);
@@ -2127,22 +1191,9 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     if (p.L % kBQ || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
     hipStream_t stream = (hipStream_t)stream_;
-    if (use_quad(p.L, p.m, (p.L / kBQ3) * splits * splits * batch)) {
-        p.ksplit = 1;
-        p.keys_per_split = p.L * p.m;
-        TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
-        hipLaunchKernelGGL(win_attn_f32_quad_kernel, dim3(p.L / kQW, splits * splits, batch), dim3(kThreads), 0,
-                           stream, p, q, k, v, out);
-        TSPLAT_PROF_END(prof::kWinAttn, stream);
-        TSPLAT_CHECK_LAUNCH();
-        return TSPLAT_OK;
-    }
     const int qb = query_block(p.L);
     const int base = (p.L / qb) * splits * splits * batch;
     p.ksplit = pick_ksplit(base, p.L * p.m / kBK, qb);
-    // key-pair kernel: 64-query workgroups (twice the blocks), half the global key split
-    const bool pair = qb == kBQ3 && env_is("TSPLAT_WINATTN", "pair");
-    if (pair) p.ksplit = std::max(1, p.ksplit / 2);
     p.keys_per_split = p.L * p.m / p.ksplit;
     Partials part{nullptr, nullptr, nullptr};
     if (p.ksplit > 1) {
@@ -2154,12 +1205,7 @@ extern "C" int tsplat_win_attn_fwd(const float* q, const float* k, const float* 
     }
     const dim3 grid(p.L / qb, splits * splits, batch * p.ksplit);
     TSPLAT_PROF_BEGIN(prof::kWinAttn, stream);
-    if (pair)
-        hipLaunchKernelGGL(win_attn_f32_pair_kernel, dim3(p.L / 64, splits * splits, batch * p.ksplit),
-                           dim3(kThreads), 0, stream, p, q, k, v, out, part);
-    else if (qb == kBQ3 && use_x16())
-        hipLaunchKernelGGL(win_attn_f32x16_kernel, grid, dim3(kThreads16), 0, stream, p, q, k, v, out, part);
-    else if (qb == kBQ3)
+    if (qb == kBQ3)
         hipLaunchKernelGGL(win_attn_f32x32_kernel, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
     else
         hipLaunchKernelGGL(win_attn_f32_kernel, grid, dim3(kThreads), 0, stream, p, q, k, v, out, part);
@@ -2224,11 +1270,7 @@ extern "C" int tsplat_win_attn_partials_fwd(const float* q, const float* k, cons
     part.l = part.m + n;
     hipStream_t stream = (hipStream_t)stream_;
     const prof::ExtEvents ev = prof::ext_events(prof::kWinAttn);  // kernel timestamps when timed
-    if (use_x16())
-        hipExtLaunchKernelGGL(win_attn_f32x16_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
-                              dim3(kThreads16), 0, stream, ev.start, ev.stop, 0, p, q, k, v, (float*)nullptr, part);
-    else
-        hipExtLaunchKernelGGL(win_attn_f32x32_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
+    hipExtLaunchKernelGGL(win_attn_f32x32_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
                               dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p, q, k, v, (float*)nullptr, part);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
@@ -2272,7 +1314,7 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     if (p.L % kBQ3 || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
     p.scale = 1.0f / sqrtf((float)kC);
     // v3 (8 staggered waves, 256 queries per workgroup, no key split) where the launch gives
-    // >= 1 workgroup per CU without splitting keys; TSPLAT_WINATTN_BF16=v1 / v2 / v3 selects
+    // >= 1 workgroup per CU without splitting keys; TSPLAT_WINATTN_BF16=v2 / v3 selects
     const bool v3 = p.L % kBQ8 == 0 &&
                     (env_is("TSPLAT_WINATTN_BF16", "v3") ||
                      (!getenv("TSPLAT_WINATTN_BF16") && (p.L / kBQ8) * splits * splits * batch >= 256));
@@ -2291,10 +1333,7 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     // the main kernel's own dispatch timestamps when timed (the split path's combine is not in it)
     const prof::ExtEvents ev = prof::ext_events(prof::kWinAttn);
     const __bf16 *qh = (const __bf16*)q, *kh = (const __bf16*)k, *vh = (const __bf16*)v;
-    if (env_is("TSPLAT_WINATTN_BF16", "v1"))
-        hipExtLaunchKernelGGL(win_attn_bf16_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit),
-                              dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p, qh, kh, vh, (__bf16*)out, part);
-    else if (v3)
+    if (v3)
         hipExtLaunchKernelGGL(win_attn_bf16_v3_kernel, dim3(p.L / kBQ8, splits * splits, batch), dim3(kThreads8), 0,
                               stream, ev.start, ev.stop, 0, p, qh, kh, vh, (__bf16*)out);
     else
@@ -2307,13 +1346,3 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     return TSPLAT_OK;
 }
 
-#if TSPLAT_WA_STAMP
-extern "C" int tsplat_diag_wa_stamps(unsigned long long* host, int waves) {
-    using namespace tsplat::winattn;
-    if (waves > kStampWaves) waves = kStampWaves;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wa_stamp), sizeof(unsigned long long) * kStampSegs * waves, 0,
-                               hipMemcpyDeviceToHost) == hipSuccess
-               ? waves
-               : -1;
-}
-#endif

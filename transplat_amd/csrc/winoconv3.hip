@@ -26,6 +26,10 @@
 #include "common.h"
 #include "prof.h"
 
+#ifndef TSPLAT_W3_ABL
+#define TSPLAT_W3_ABL 0  // diagnostic ablation builds only (tools/build_ablation_w3.sh)
+#endif
+
 namespace tsplat {
 namespace wino3 {
 
@@ -124,6 +128,11 @@ struct Patch {
     }
 
     __device__ __forceinline__ void load(const Args& a, const float* const* planes, int c, float (&d)[16]) const {
+#if TSPLAT_W3_ABL == 1  // diagnostic build: no patch loads
+#pragma unroll
+        for (int i = 0; i < 16; ++i) d[i] = (float)(c + i + x0) * 1e-3f;
+        return;
+#endif
         const __attribute__((address_space(1))) float* src =
             (const __attribute__((address_space(1))) float*)planes[min(c, a.ci_pad - 1)];
 #pragma unroll
@@ -168,7 +177,17 @@ __device__ __forceinline__ void transform_pair(const float (&da)[16], const floa
     }
 }
 
-template <int CB, int NB, int KS>
+// Staged input (ST): per 16-channel chunk the tile block's input region -- rows 2 ty0 - 1 ..
+// 2 (ty0 + TBY), columns from the 16-B-aligned 2 tx0 - 4, TBX / 2 + 2 float4 per row -- is loaded
+// with coalesced float4 loads (a chunk ahead, in registers) into an LDS slot sIn[ch][row][col], and
+// each thread reads its 4x4 patches from there: ~5 float4 loads per thread and chunk instead of 32
+// predicated scalar ones (the map width must be a multiple of 4 and the sources 16-B aligned).
+template <int T>
+struct Region {
+    static constexpr int kMaxFloats = T == 32 ? 16 * 4 * 72 : 16 * 4 * 136;  // largest [16][R][RP] over TBX
+};
+
+template <int CB, int NB, int KS, bool ST>
 __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     constexpr int T = 32 * NB;                 // tiles per workgroup
     constexpr int GT = 256 * CB;               // threads per k-group
@@ -177,7 +196,12 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     static_assert(ROWS * PP == 8, "pairs per chunk");
     constexpr int BUF = 2 * 16 * 8 * T;        // dwords per sV buffer (hi + lo)
     constexpr int CO = 32 * CB;
-    __shared__ __attribute__((aligned(16))) uint32_t smem[KS * 2 * BUF];
+    constexpr int NSV = ST ? 1 : 2;            // sV buffers per k-group
+    constexpr int RGN = Region<T>::kMaxFloats; // floats per sIn slot
+    constexpr int NL = (RGN / 4 + GT - 1) / GT;  // float4 region loads per thread and chunk
+    constexpr int SMEM = KS * (NSV * BUF + (ST ? 2 * RGN : 0));
+    static_assert(8 * CO * T * KS <= SMEM, "Z slabs fit");
+    __shared__ __attribute__((aligned(16))) uint32_t smem[SMEM];
     __shared__ const float* planes[kMaxCiPad];
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -212,7 +236,11 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
         for (int s = s0; s < s1; ++s)
 #pragma unroll
             for (int hl = 0; hl < 2; ++hl)
+#if TSPLAT_W3_ABL == 3  // diagnostic build: no A loads
+                af[s][hl] = make_uint4(chunk, s, hl, lane);
+#else
                 af[s][hl] = ok ? ub[s * xi_stride + (size_t)chunk * 128 + hl * 64] : make_uint4(0u, 0u, 0u, 0u);
+#endif
     };
 
     floatx16 acc[4][NB];
@@ -232,13 +260,60 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
             pt.load(a, planes, c0 + 1, d[q][1]);
         }
     };
-    uint32_t* sG = smem + kg * 2 * BUF;
+    uint32_t* sG = smem + kg * (NSV * BUF + (ST ? 2 * RGN : 0));
     auto transform = [&](uint32_t* sV) {
 #pragma unroll
         for (int q = 0; q < PP; ++q) transform_pair<T>(d[q][0], d[q][1], sV + (prow + q * ROWS) * T + t);
     };
+    // staged region of the chunk: R rows x C4 float4 per channel, origin (ry0, rx0)
+    const int blk = blockIdx.x % (a.bx * a.by);
+    const int R = 2 * a.tby + 2, C4 = a.tbx / 2 + 2, RP = 4 * C4;
+    const int ry0 = 2 * (blk / a.bx) * a.tby - 1, rx0 = 2 * (blk % a.bx) * a.tbx - 4;
+    float* sIn = reinterpret_cast<float*>(sG + NSV * BUF);
+    float4 gr[ST ? NL : 1];
+    auto gload = [&](int chunk) {
+        const int total = 16 * R * C4;
+#pragma unroll
+        for (int k = 0; k < (ST ? NL : 0); ++k) {
+            const int idx = gtid + GT * k;
+            const int ch = idx / (R * C4), rem = idx - ch * (R * C4);
+            const int row = rem / C4, c4 = rem - row * C4;
+            const int c = chunk * 16 + ch, y = ry0 + row, x = rx0 + 4 * c4;
+            const bool ok = idx < total && c < a.ci && y >= 0 && y < a.h && x >= 0 && x < a.w;
+            const float4* src = reinterpret_cast<const float4*>(planes[min(c, a.ci_pad - 1)] + (size_t)y * a.w + x);
+            gr[k] = ok ? *src : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto sstore = [&](int slot) {
+        const int total = 16 * R * C4;
+        float4* dst = reinterpret_cast<float4*>(sIn + slot * RGN);
+#pragma unroll
+        for (int k = 0; k < (ST ? NL : 0); ++k) {
+            const int idx = gtid + GT * k;
+            if (idx < total) dst[idx] = gr[k];  // [ch][row][c4]: idx is already that order
+        }
+    };
+    auto read_patches = [&](int slot) {  // this thread's PP channel pairs of tile t from sIn
+        const int tyl = t / a.tbx, txl = t - tyl * a.tbx;
+        const float* base = sIn + slot * RGN + 2 * tyl * RP + 2 * txl + 3;
+#pragma unroll
+        for (int q = 0; q < PP; ++q)
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float* b = base + (2 * (prow + q * ROWS) + e) * R * RP;
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) d[q][e][4 * i + j] = b[i * RP + j];
+            }
+    };
     // MFMAs of xi s0 .. s1 - 1 on buffer sV: B fragment of lane (n, h) = dwords [hl][xi][4 h + c][32 nb + n]
     auto mfma = [&](const uint32_t* sV, int s0, int s1) {
+#if TSPLAT_W3_ABL == 2  // diagnostic build: no MFMAs (the B reads stay)
+        const uint32_t* bq = sV + (4 * (lane >> 5)) * T + (lane & 31);
+        for (int s = s0; s < s1; ++s) acc[s][0][0] += __builtin_bit_cast(float, bq[(4 * rr + s) * 8 * T]);
+        return;
+#endif
         const uint32_t* bb = sV + (4 * (lane >> 5)) * T + (lane & 31);
 #pragma unroll
         for (int s = s0; s < s1; ++s) {
@@ -263,6 +338,29 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     // k-group kg takes chunks kg, kg + KS, ...; every group runs the same iteration count (a chunk
     // past the last one is all zeros) so the groups meet at every barrier
     const int iters = (a.nchunk + KS - 1) / KS;
+    if constexpr (ST) {
+        // single sV: transform(it) | barrier | MFMAs(it) | barrier; the region of chunk it + 1 is
+        // stored to the other sIn slot during transform(it) and chunk it + 2's loads fly meanwhile
+        gload(kg);
+        sstore(0);
+        if (iters > 1) gload(kg + KS);
+        load_a(kg, 0, 4);
+        __syncthreads();
+        for (int it = 0; it < iters; ++it) {
+            const int ch = kg + it * KS;
+            const bool more = it + 1 < iters;
+            read_patches(it & 1);
+            transform(sG);
+            if (more) {
+                sstore((it + 1) & 1);
+                if (it + 2 < iters) gload(ch + 2 * KS);
+            }
+            __syncthreads();  // sV(it) complete
+            mfma(sG, 0, 4);
+            if (more) load_a(ch + KS, 0, 4);
+            __syncthreads();  // every wave is done with sV(it) and with sIn slot it & 1
+        }
+    } else {
     load_patches(kg);
     load_a(kg, 0, 4);
     transform(sG);
@@ -283,6 +381,7 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
             load_a(ch + KS, 2, 4);
             __syncthreads();  // sV(it + 1) complete; every wave is done reading sV(it)
         }
+    }
     }
     __syncthreads();  // all MFMAs' LDS reads done: smem becomes Z[kg][r][j][co CO][tile T]
     float* zs = reinterpret_cast<float*>(smem) + kg * (8 * CO * T);
@@ -307,8 +406,6 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
         }
         __syncthreads();
     }
-    const int blocks_per_img = a.bx * a.by;
-    const int blk = blockIdx.x % blocks_per_img;
     const size_t hw = (size_t)a.h * a.w;
     for (int pidx = tid; pidx < CO * T; pidx += 256 * CB * KS) {
         const int col = pidx / T, t2 = pidx % T;
@@ -366,7 +463,7 @@ extern "C" int tsplat_wino_weight_bf16x3(const float* weight, void* packed, int3
 }
 
 // workgroup forms: 0 = auto, 1 = 32 co x 32 tiles (KS 1), 2 = 32 x 32 with two k-groups,
-// 3 = 32 co x 64 tiles, 4 = 64 co x 64 tiles
+// 3 = 32 co x 64 tiles, 4 = 64 co x 64 tiles; staged input (Region) on top where the map allows it
 static int pick_form(int n, int th, int tw, int co) {
     if (const char* e = getenv("TSPLAT_WINO3_FORM")) {
         const int f = atoi(e);
@@ -382,10 +479,14 @@ static int pick_form(int n, int th, int tw, int co) {
 }
 
 template <int CB, int NB, int KS>
-static void launch(wino3::Args a, int blocks, hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
+static void launch(wino3::Args a, int blocks, bool staged, hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
     const int coblocks = (a.co + 32 * CB - 1) / (32 * CB);
-    hipExtLaunchKernelGGL(wino3::conv_kernel<CB, NB, KS>, dim3(blocks, coblocks), dim3(256 * CB * KS), 0, stream,
-                          start, stop, 0, a);
+    if (staged)
+        hipExtLaunchKernelGGL((wino3::conv_kernel<CB, NB, KS, true>), dim3(blocks, coblocks), dim3(256 * CB * KS), 0,
+                              stream, start, stop, 0, a);
+    else
+        hipExtLaunchKernelGGL((wino3::conv_kernel<CB, NB, KS, false>), dim3(blocks, coblocks), dim3(256 * CB * KS),
+                              0, stream, start, stop, 0, a);
 }
 
 extern "C" int tsplat_conv3x3_wino_bf16x3_cat_fwd(const float* const* srcs, const int32_t* chans, int32_t nsrc,
@@ -435,13 +536,17 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_cat_fwd(const float* const* srcs, cons
     a.bx = (a.tw + a.tbx - 1) / a.tbx;
     a.by = (a.th + a.tby - 1) / a.tby;
     const int blocks = n * a.bx * a.by;
+    // staged input: float4 rows need a width that is a multiple of 4 and 16-B aligned sources
+    bool staged = w % 4 == 0;
+    for (int q = 0; q < nsrc; ++q) staged = staged && (reinterpret_cast<uintptr_t>(srcs[q]) & 15) == 0;
+    if (const char* e = getenv("TSPLAT_WINO3_STAGE")) staged = staged && atoi(e) != 0;
     hipStream_t stream = (hipStream_t)stream_;
     const prof::ExtEvents ev = prof::ext_events(prof::kWinoConv);
     switch (form) {
-        case 4: launch<2, 2, 1>(a, blocks, stream, ev.start, ev.stop); break;
-        case 3: launch<1, 2, 1>(a, blocks, stream, ev.start, ev.stop); break;
-        case 2: launch<1, 1, 2>(a, blocks, stream, ev.start, ev.stop); break;
-        default: launch<1, 1, 1>(a, blocks, stream, ev.start, ev.stop); break;
+        case 4: launch<2, 2, 1>(a, blocks, staged, stream, ev.start, ev.stop); break;
+        case 3: launch<1, 2, 1>(a, blocks, staged, stream, ev.start, ev.stop); break;
+        case 2: launch<1, 1, 2>(a, blocks, staged, stream, ev.start, ev.stop); break;
+        default: launch<1, 1, 1>(a, blocks, staged, stream, ev.start, ev.stop); break;
     }
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
