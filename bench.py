@@ -229,6 +229,10 @@ def cpu_baseline_e2e(model, seconds: float, one_thread: bool = False):
         setattr(kernels, n, getattr(E, n))
     threads = torch.get_num_threads()
 
+    from transplat_amd.misc.benchmarker import Benchmarker
+
+    bm = Benchmarker()  # the reference's stage tags, wall time per stage (CPU: no device sync)
+
     def run(budget, nthreads):
         torch.set_num_threads(nthreads)
         oracle_raster.set_threads(nthreads)
@@ -236,7 +240,7 @@ def cpu_baseline_e2e(model, seconds: float, one_thread: bool = False):
         while True:
             batch = S.make_batch(1, image_shape=(256, 256))
             with torch.no_grad():
-                g = enc(batch["context"], 0, deterministic=True)
+                g = enc(batch["context"], 0, deterministic=True, benchmarker=bm)
             t = batch["target"]
             cams = prepare_cameras(t["extrinsics"][0], t["intrinsics"][0], t["near"][0], t["far"][0], torch.zeros(3, 3))
             tr = time.perf_counter()
@@ -250,7 +254,9 @@ def cpu_baseline_e2e(model, seconds: float, one_thread: bool = False):
     try:
         enc = copy.deepcopy(model.encoder).float().cpu()
         enc.cfg.dense_dtype = "fp32"
+        enc.cfg.attn_dtype = "fp32"
         n_views, el, t_raster = run(seconds, threads)
+        stages = {tag: sum(ts) / len(ts) for tag, ts in bm.execution_times.items()}
         one = run(0.0, 1) if one_thread else None  # one full scene on one thread
     finally:
         torch.set_num_threads(threads)
@@ -263,6 +269,22 @@ def cpu_baseline_e2e(model, seconds: float, one_thread: bool = False):
                   f"{threads} threads) with oracle/encoder_ops.py restatements for the HIP kernels + "
                   f"oracle/raster_ref.c (literal mode; OpenMP, {threads} threads; raster "
                   f"{t_raster / n_views * 1e3:.0f} ms/view), {el:.1f} s, host {cpu_model()}, nproc={os.cpu_count()}",
+    }
+    # per-stage seconds per scene of the port, and the like-for-like comparison with the reference's
+    # own CPU path as measured in the survey container (backbone + depth predictor
+    # only -- DA-V2, the e3nn adapter and the CUDA-only rasterizer do not run on the reference's CPU path)
+    keep = ("encoder_2_backbone", "encoder_3_depth_anything", "encoder_4_depth_predictor", "encoder_5_gaussian_adapter",
+            "encoder_4b_cost_volume_matching")
+    res["stages_s_per_scene"] = {k: round(stages[k], 3) for k in keep if k in stages}
+    res["stages_s_per_scene"]["raster_3_views"] = round(t_raster / (n_views // 3), 3)
+    bb_dp = stages.get("encoder_2_backbone", 0.0) + stages.get("encoder_4_depth_predictor", 0.0)
+    res["reference_cpu"] = {
+        "backbone_plus_depth_predictor_s_per_scene": 5.24, "port_same_stages_s_per_scene": round(bb_dp, 3),
+        "cores": 8, "kind": "reference",
+        "sample": "the reference's own BackboneMultiview + DepthPredictorTrans, b = 1, 256x256, fp32, 8 torch "
+                  "threads on the survey container's 8 Xeon vCPUs (BASELINE.md §2; reference code cannot run on "
+                  "the GPU box). DA-V2 (weights / cv2 absent), the e3nn adapter and the rasterizer (CUDA-only "
+                  "fork) have no runnable reference CPU path, so the full-step CPU figure is the port's.",
     }
     if one is not None:
         res["value_1thread"] = one[0] / one[1]

@@ -288,6 +288,30 @@ def test_conv3x3_wino_bf16x3_concat_and_production_size(device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("m,k,n,bias,act", [(650, 768, 2304, True, "none"), (650, 768, 3072, True, "gelu"),
+                                           (650, 3072, 768, True, "none"), (100, 256, 128, False, "none"),
+                                           (8192, 256, 1024, False, "none"), (33, 64, 64, True, "gelu")])
+def test_linear_bf16x3_kernel(device, m, k, n, bias, act):
+    """tsplat_linear_bf16x3_fwd (DINOv2's linears in the bf16x3 dense mode: x split while staged, W
+    packed [hi | lo | hi]) against float64 F.linear (+ exact GELU): within 2e-5 of max |y| and at
+    most 1/8 of the TF32-operand error (tolerances written here); 64- and 32-row workgroups, M not
+    a multiple of the block."""
+    from transplat_amd import kernels as K
+
+    x = seeded((m, k), 81)
+    w = seeded((n, k), 82) / k ** 0.5
+    b = seeded((n,), 83) if bias else None
+    fn = torch.nn.functional.gelu if act == "gelu" else (lambda t: t)
+    ref = fn(torch.nn.functional.linear(x.double(), w.double(), b.double() if bias else None))
+    ref_tf = fn(torch.nn.functional.linear(tf32_round(x).double(), tf32_round(w).double(), b.double() if bias else None))
+    out = K.linear_bf16x3(x.to(device), w.to(device), b.to(device) if bias else None, act=act).cpu().double()
+    scale = ref.abs().max().item()
+    e3, etf = (out - ref).abs().max().item() / scale, (ref_tf - ref).abs().max().item() / scale
+    print(f"linear bf16x3 {(m, k, n)} {act}: rel err {e3:.2e}, TF32 operands {etf:.2e}")
+    assert e3 < 2e-5 and e3 <= etf / 8, (e3, etf)
+
+
+@pytest.mark.gpu
 def test_conv3x3_wino_weight_cache_tracks_updates(device):
     """The transformed-filter cache is keyed on the live weight tensor and its version: an in-place
     update of the weight is picked up."""

@@ -260,9 +260,12 @@ def test_depth_anything_gpu(device, dense):
     epilogues and bilinear resizes) against the reference golden (reference dpt.py:177-184)."""
     from transplat_amd.model.depth_anything.dpt import DepthAnythingV2
 
+    from transplat_amd import kernels
+
     g = np.load(GOLD / "depth_anything.npz")
     m = canonical_init(DepthAnythingV2(encoder="vitb", features=128, out_channels=[96, 192, 384, 768]),
                        seed=51).eval().to(device)
+    kernels.install_linear_dispatch(m)  # as EncoderTrans installs it: bf16x3 linears in that mode
     with torch.no_grad():
         depth, feat = m(seeded((1, 3, 252, 252), 701).to(device))
     depth, feat = depth.float().cpu(), feat.float().cpu()

@@ -9,6 +9,8 @@ max error of both against float64 (relative to max |y|), next to a TF32-rounded 
 import torch
 import torch.nn.functional as F
 
+from transplat_amd import kernels as K
+
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 
@@ -56,13 +58,16 @@ for name, m, k, n in cases:
     t_f32 = timeit(lambda: F.linear(x, w, b))
     t_s = timeit(lambda: torch.addmm(b, x3, w3.t(), out_dtype=torch.float32))
     t_split = timeit(lambda: split3_act(x))
+    t_ours = timeit(lambda: K.linear_bf16x3(x, w, b))
+    e_ours = ((K.linear_bf16x3(x, w, b).double() - ref).abs().max() / scale).item()
     y3 = torch.addmm(b, x3, w3.t(), out_dtype=torch.float32)
     e_f32 = ((F.linear(x, w, b).double() - ref).abs().max() / scale).item()
     e_s = ((y3.double() - ref).abs().max() / scale).item()
     e_tf = (((tf32(x).double() @ tf32(w).double().t() + b.double()) - ref).abs().max() / scale).item()
     fl = 2.0 * m * k * n
     print(f"{name:10s} M={m:5d} K={k:5d} N={n:5d}: fp32 {t_f32:7.1f} us ({fl / t_f32 / 1e6:6.1f} TF)  "
-          f"bf16x3 gemm {t_s:7.1f} us  split(x) {t_split:6.1f} us | err fp32 {e_f32:.1e} bf16x3 {e_s:.1e} "
+          f"bf16x3 gemm {t_s:7.1f} us  split(x) {t_split:6.1f} us  tsplat_linear_bf16x3 {t_ours:6.1f} us | "
+          f"err fp32 {e_f32:.1e} bf16x3 {e_s:.1e} ours {e_ours:.1e} "
           f"tf32-emul {e_tf:.1e}", flush=True)
 
 # correlation table: [2, 4096, 128] x [2, 128, 4096]

@@ -774,38 +774,54 @@ def _split_weight(weight):
     return packed
 
 
-def linear_bf16x3(x, weight, bias=None):
-    """F.linear(x, weight, bias) in split-bf16 precision: ONE hipBLASLt bf16 GEMM with K' = 3K on
-    [x_hi | x_hi | x_lo] and the cached [W_hi | W_lo | W_hi], fp32 accumulation and fp32 output
-    (torch.mm / addmm with out_dtype=float32), <= 3 * 2^-18 relative per product."""
-    k = x.shape[-1]
-    x3 = split_bf16x3(x).reshape(-1, 3 * k)
+def linear_bf16x3(x, weight, bias=None, act: str = "none"):
+    """act(F.linear(x, weight, bias)) in split-bf16 precision (act "none" or "gelu", exact erf):
+    tsplat_linear_bf16x3_fwd where the shape fits (N % 64 == 0, K % 32 == 0: x split while it is
+    staged, W packed once per version), else ONE hipBLASLt bf16 GEMM with K' = 3K on
+    [x_hi | x_hi | x_lo] and [W_hi | W_lo | W_hi] (fp32 accumulation and output)."""
+    lib = _lib.load()
+    k, n = x.shape[-1], weight.shape[0]
     w3 = _split_weight(weight)
+    if n % 64 == 0 and k % 32 == 0:
+        xf = _f32(x).reshape(-1, k)
+        y = torch.empty((xf.shape[0], n), dtype=torch.float32, device=x.device)
+        bb = _f32(bias) if bias is not None else None
+        _lib.check(lib.tsplat_linear_bf16x3_fwd(_lib.ptr(xf), _lib.ptr(w3), _lib.ptr(bb), _lib.ptr(y), xf.shape[0], n, k,
+                                                _ACTS[act], _lib.stream_ptr(x.device)), "tsplat_linear_bf16x3_fwd")
+        return y.reshape(*x.shape[:-1], n)
+    x3 = split_bf16x3(x).reshape(-1, 3 * k)
     with torch.autocast("cuda", enabled=False):
         if bias is not None:
             y = torch.addmm(_f32(bias), x3, w3.t(), out_dtype=torch.float32)
         else:
             y = torch.mm(x3, w3.t(), out_dtype=torch.float32)
-    return y.reshape(*x.shape[:-1], weight.shape[0])
+    y = y.reshape(*x.shape[:-1], n)
+    if act == "gelu":
+        y = torch.nn.functional.gelu(y)
+    return y
 
 
-# nn.Linear in bf16x3 mode: OFF by default (TSPLAT_LIN3=1 enables). Measured (tools/bench_split_gemm.py,
-# profiles/r4/split_gemm.log): hipBLASLt's bf16 GEMM at K' = 3K is no faster than its fp32 GEMM on the
-# step's linears (DINOv2 qkv 23.4 vs 28.8 us, proj 23.3 vs 18.7, fc1 27.8 vs 31.1, fc2 30.3 vs 29.2,
-# MVT fc1 50.7 vs 39.9 at M = 650 / 8192): the small-M shapes are not MFMA-bound in the library, and
-# the activation split is another launch. Only the correlation table gains (uv_cross: 47 vs 86 us).
-_LIN3 = os.environ.get("TSPLAT_LIN3", "0") == "1"
-_LIN3_MIN_FLOP = float(os.environ.get("TSPLAT_LIN3_MIN_FLOP", "2e8"))  # smaller linears stay exact fp32
+# nn.Linear in bf16x3 mode (TSPLAT_LIN3=0 turns it off). hipBLASLt's own bf16 GEMM at K' = 3K is no
+# faster than its fp32 GEMM on the step's linears (tools/bench_split_gemm.py, profiles/r4/split_gemm.log:
+# DINOv2 qkv 23.4 vs 28.8 us, proj 23.3 vs 18.7, fc1 27.8 vs 31.1, fc2 30.3 vs 29.2), so the dispatch
+# takes the hand-written tsplat_linear_bf16x3_fwd; linears below _LIN3_MIN_FLOP stay exact fp32.
+_LIN3 = os.environ.get("TSPLAT_LIN3", "1") == "1"
+_LIN3_MIN_FLOP = float(os.environ.get("TSPLAT_LIN3_MIN_FLOP", "2e8"))
+
+
+def linear_ok(x, weight) -> bool:
+    """True when linear_forward takes the bf16x3 kernel for F.linear(x, weight) in the current mode."""
+    return (_LIN3 and _DENSE == "bf16x3" and x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32
+            and not torch.is_autocast_enabled("cuda") and weight.shape[0] % 64 == 0 and x.shape[-1] % 32 == 0
+            and 2.0 * x.numel() * weight.shape[0] >= _LIN3_MIN_FLOP)
 
 
 def linear_forward(mod, x):
     """nn.Linear.forward (installed by install_linear_dispatch): in dense_precision("bf16x3") the
-    fp32 linears of at least _LIN3_MIN_FLOP run as linear_bf16x3; everything else is F.linear."""
+    fp32 linears that linear_ok admits run as linear_bf16x3; everything else is F.linear."""
     import torch.nn.functional as F
 
-    if (_LIN3 and _DENSE == "bf16x3" and x.is_cuda and x.dtype == torch.float32 and mod.weight.dtype == torch.float32
-            and not torch.is_autocast_enabled("cuda") and x.shape[-1] % 4 == 0
-            and 2.0 * x.numel() * mod.weight.shape[0] >= _LIN3_MIN_FLOP):
+    if linear_ok(x, mod.weight):
         return linear_bf16x3(x, mod.weight, mod.bias)
     return F.linear(x, mod.weight, mod.bias)
 
