@@ -414,6 +414,14 @@ int tsplat_conv3x3_wino_bf16x3_fwd(const float* x, const void* w_packed, const f
 int tsplat_conv3x3_wino_bf16x3_cat_fwd(const float* const* srcs, const int32_t* chans, int32_t n_src,
                                        const void* w_packed, const float* bias, float* y, int32_t batch,
                                        int32_t height, int32_t width, int32_t c_out, int32_t act, void* stream);
+/* The same with the Depth-Anything DPT ResidualConvUnit's glue fused (src/depth_anything_v2/util/
+ * blocks.py ResidualConvUnit.forward: conv(relu(x)) ... + x, FeatureFusionBlock's + skip):
+ * relu_in != 0 applies ReLU to the input as it is loaded; y = act(conv + bias) + residual +
+ * residual2 (each [batch, c_out, height, width] NCHW fp32, or null). */
+int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const int32_t* chans, int32_t n_src,
+                                      const void* w_packed, const float* bias, const float* residual,
+                                      const float* residual2, float* y, int32_t batch, int32_t height, int32_t width,
+                                      int32_t c_out, int32_t act, int32_t relu_in, void* stream);
 
 /* Split-bf16 operands for ONE library bf16 GEMM that computes an fp32 linear layer in bf16x3
  * precision (the nn.Linear layers of the fp32 path -- DINOv2 qkv / proj / fc1 / fc2,

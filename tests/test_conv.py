@@ -266,6 +266,30 @@ def test_conv3x3_wino_bf16x3_kernel(device, monkeypatch, stage, form, n, ci, co,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("stage", ["auto", "0"])
+@pytest.mark.parametrize("n,c,h,w,skip", [(2, 128, 72, 72, True), (2, 128, 36, 36, False), (2, 128, 9, 9, True),
+                                          (1, 64, 30, 52, True)])
+def test_conv3x3_wino_bf16x3_relu_in_residual(device, monkeypatch, stage, n, c, h, w, skip):
+    """The DPT ResidualConvUnit's fused form (tsplat_conv3x3_wino_bf16x3_ex_fwd): conv(relu(x)) +
+    bias + x (+ the fusion block's skip) against float64, within 2e-5 of max |y|."""
+    from transplat_amd import kernels as K
+
+    if stage != "auto":
+        monkeypatch.setenv("TSPLAT_WINO3_STAGE", stage)
+    x = seeded((n, c, h, w), 91)
+    wt = seeded((c, c, 3, 3), 92) * (1.0 / (9 * c) ** 0.5)
+    b = seeded((c,), 93)
+    sk = seeded((n, c, h, w), 94) if skip else None
+    ref = torch.nn.functional.conv2d(torch.relu(x).double(), wt.double(), b.double(), padding=1) + x.double()
+    if skip:
+        ref = ref + sk.double()
+    out = K.conv3x3_wino(x.to(device), wt.to(device), b.to(device), precision="bf16x3", residual=x.to(device),
+                         residual2=sk.to(device) if skip else None, relu_in=True).cpu().double()
+    err = ((out - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-5, err
+
+
+@pytest.mark.gpu
 def test_conv3x3_wino_bf16x3_concat_and_production_size(device):
     """bf16x3 Winograd on the to_gaussians head's three sources at 256^2 (2 x 163 -> 168, the
     64 x 64 workgroup form) equals the kernel on the materialised concatenation bit for bit, and

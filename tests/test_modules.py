@@ -265,7 +265,8 @@ def test_depth_anything_gpu(device, dense):
     g = np.load(GOLD / "depth_anything.npz")
     m = canonical_init(DepthAnythingV2(encoder="vitb", features=128, out_channels=[96, 192, 384, 768]),
                        seed=51).eval().to(device)
-    kernels.install_linear_dispatch(m)  # as EncoderTrans installs it: bf16x3 linears in that mode
+    kernels.install_linear_dispatch(m)  # as EncoderTrans installs them: bf16x3 linears / convs in that mode
+    kernels.install_conv2d_dispatch(m)
     with torch.no_grad():
         depth, feat = m(seeded((1, 3, 252, 252), 701).to(device))
     depth, feat = depth.float().cpu(), feat.float().cpu()

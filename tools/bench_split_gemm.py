@@ -81,5 +81,15 @@ t_s = timeit(lambda: torch.bmm(k3, v3.transpose(1, 2), out_dtype=torch.float32))
 t_split = timeit(lambda: (split3_act(k_), split3_w(v_)))
 e_s = ((torch.bmm(k3, v3.transpose(1, 2), out_dtype=torch.float32).double() - ref).abs().max() / scale).item()
 e_f = ((torch.bmm(k_, v_.transpose(1, 2)).double() - ref).abs().max() / scale).item()
-print(f"corr table 2x4096x4096x128: fp32 {t_f32:.1f} us  bf16x3 {t_s:.1f} us  split {t_split:.1f} us | "
-      f"err fp32 {e_f:.1e} bf16x3 {e_s:.1e}", flush=True)
+tab = torch.empty(2, 4096, 4096, device=dev)
+
+
+def ours():
+    for i in range(2):
+        K.linear_bf16x3(k_[i], v_[i], out=tab[i], cache=False)
+
+
+t_o = timeit(ours)
+e_o = ((tab.double() - ref).abs().max() / scale).item()
+print(f"corr table 2x4096x4096x128: fp32 {t_f32:.1f} us  bf16x3 {t_s:.1f} us  split {t_split:.1f} us  "
+      f"tsplat_linear_bf16x3 x2 {t_o:.1f} us | err fp32 {e_f:.1e} bf16x3 {e_s:.1e} ours {e_o:.1e}", flush=True)

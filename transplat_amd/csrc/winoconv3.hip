@@ -49,6 +49,9 @@ struct Args {
     int n, ci, h, w, co, ci_pad, cobs, nchunk;  // cobs: 32-channel blocks in the packing
     int th, tw, tbx, tby, bx, by;
     int act;             // 0 none, 1 ReLU, 2 GELU (erf)
+    int relu_in;         // ReLU applied to the input as it is loaded (a pre-activation unit)
+    const float* res;    // [n][co][h][w] added after the activation, or null
+    const float* res2;   // a second such addend (the fusion block's skip), or null
     int cob_base;        // first 32-channel output block of this launch
 };
 
@@ -141,6 +144,7 @@ struct Patch {
             for (int j = 0; j < 4; ++j) {
                 const bool ok = c < a.ci && rok[i] && cok[j];
                 d[4 * i + j] = ok ? src[(size_t)(y0 + i) * a.w + (x0 + j)] : 0.0f;
+                if (a.relu_in) d[4 * i + j] = fmaxf(d[4 * i + j], 0.0f);
             }
     }
 };
@@ -290,7 +294,9 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
 #pragma unroll
         for (int k = 0; k < (ST ? NL : 0); ++k) {
             const int idx = gtid + GT * k;
-            if (idx < total) dst[idx] = gr[k];  // [ch][row][c4]: idx is already that order
+            float4 v = gr[k];
+            if (a.relu_in) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+            if (idx < total) dst[idx] = v;  // [ch][row][c4]: idx is already that order
         }
     };
     auto read_patches = [&](int slot) {  // this thread's PP channel pairs of tile t from sIn
@@ -425,9 +431,18 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
             if (py >= a.h) continue;
             const float y0v = i == 0 ? z[0][0] + z[1][0] + z[2][0] : z[1][0] - z[2][0] - z[3][0];
             const float y1v = i == 0 ? z[0][1] + z[1][1] + z[2][1] : z[1][1] - z[2][1] - z[3][1];
-            const float r0 = act_fn(y0v + bv, a.act), r1 = act_fn(y1v + bv, a.act);
+            float r0 = act_fn(y0v + bv, a.act), r1 = act_fn(y1v + bv, a.act);
             const int px = 2 * otx;
             float* p = dst + (size_t)py * a.w + px;
+            const size_t off = ((size_t)pt.img * a.co + o) * hw + (size_t)py * a.w + px;
+            if (a.res) {
+                r0 += a.res[off];
+                if (px + 1 < a.w) r1 += a.res[off + 1];
+            }
+            if (a.res2) {
+                r0 += a.res2[off];
+                if (px + 1 < a.w) r1 += a.res2[off + 1];
+            }
             if (px + 1 < a.w && ((reinterpret_cast<uintptr_t>(p) & 7) == 0)) {
                 *reinterpret_cast<float2*>(p) = make_float2(r0, r1);
             } else {
@@ -489,9 +504,10 @@ static void launch(wino3::Args a, int blocks, bool staged, hipStream_t stream, h
                               0, stream, start, stop, 0, a);
 }
 
-extern "C" int tsplat_conv3x3_wino_bf16x3_cat_fwd(const float* const* srcs, const int32_t* chans, int32_t nsrc,
-                                                  const void* packed, const float* bias, float* y, int32_t n,
-                                                  int32_t h, int32_t w, int32_t co, int32_t act, void* stream_) {
+extern "C" int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const int32_t* chans, int32_t nsrc,
+                                                 const void* packed, const float* bias, const float* residual,
+                                                 const float* residual2, float* y, int32_t n, int32_t h, int32_t w,
+                                                 int32_t co, int32_t act, int32_t relu_in, void* stream_) {
     if (!srcs || !chans || nsrc <= 0 || nsrc > wino3::kMaxSrc || !packed || !y || n <= 0 || h <= 0 || w <= 0 ||
         co <= 0 || act < 0 || act > 2)
         return TSPLAT_EINVAL;
@@ -519,6 +535,9 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_cat_fwd(const float* const* srcs, cons
     a.th = (h + 1) / 2;
     a.tw = (w + 1) / 2;
     a.act = act;
+    a.relu_in = relu_in != 0;
+    a.res = residual;
+    a.res2 = residual2;
     a.cob_base = 0;
     const int form = pick_form(n, a.th, a.tw, co);
     const int ttiles = form >= 3 ? 64 : 32;
@@ -550,6 +569,13 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_cat_fwd(const float* const* srcs, cons
     }
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
+}
+
+extern "C" int tsplat_conv3x3_wino_bf16x3_cat_fwd(const float* const* srcs, const int32_t* chans, int32_t nsrc,
+                                                  const void* packed, const float* bias, float* y, int32_t n,
+                                                  int32_t h, int32_t w, int32_t co, int32_t act, void* stream_) {
+    return tsplat_conv3x3_wino_bf16x3_ex_fwd(srcs, chans, nsrc, packed, bias, nullptr, nullptr, y, n, h, w, co, act, 0,
+                                             stream_);
 }
 
 extern "C" int tsplat_conv3x3_wino_bf16x3_fwd(const float* x, const void* packed, const float* bias, float* y,

@@ -110,15 +110,16 @@ def uv_cross(value, key, intr, pose, disp, offsets, logits, h: int, w: int):
             table = torch.bmm(k2, torch.cat((vb, vb), dim=-1).transpose(1, 2), out_dtype=torch.float32)
         value = None
         key, offsets, logits, disp = map(_f32, (key, offsets, logits, disp))
-    elif _DENSE == "bf16x3" and value.is_cuda and c % 4 == 0:
-        # bf16x3 dense mode: the table in split-bf16 precision as ONE bf16 GEMM with K = 3C,
-        # [key_hi | key_hi | key_lo] x [val_hi | val_lo | val_hi]^T, fp32 output (47 vs 86 us for
-        # the fp32 bmm at b = 1, tools/bench_split_gemm.py; <= 3 * 2^-18 relative per product)
+    elif _DENSE == "bf16x3" and value.is_cuda and c % 32 == 0 and hw % 64 == 0:
+        # bf16x3 dense mode: the table G[i] = key[i] value_other[i]^T in split-bf16 precision on
+        # tsplat_linear_bf16x3_fwd (value_other as the [HW, C] "weight", split per call), written
+        # straight into the [2b, HW, HW] table (<= 3 * 2^-18 relative per product)
         value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
-        k3 = split_bf16x3(key.reshape(b * 2, hw, c))
-        v3 = split_bf16x3(torch.flip(value, dims=[1]).reshape(b * 2, hw, c), weight_order=True)
-        with torch.autocast("cuda", enabled=False):
-            table = torch.bmm(k3, v3.transpose(1, 2), out_dtype=torch.float32)
+        kf = key.reshape(b * 2, hw, c)
+        vo = torch.flip(value, dims=[1]).reshape(b * 2, hw, c)
+        table = torch.empty((b * 2, hw, hw), dtype=torch.float32, device=value.device)
+        for i in range(b * 2):
+            linear_bf16x3(kf[i], vo[i], out=table[i], cache=False)
     else:
         value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
         with torch.autocast("cuda", enabled=False):
@@ -774,17 +775,20 @@ def _split_weight(weight):
     return packed
 
 
-def linear_bf16x3(x, weight, bias=None, act: str = "none"):
+def linear_bf16x3(x, weight, bias=None, act: str = "none", out=None, cache: bool = True):
     """act(F.linear(x, weight, bias)) in split-bf16 precision (act "none" or "gelu", exact erf):
     tsplat_linear_bf16x3_fwd where the shape fits (N % 64 == 0, K % 32 == 0: x split while it is
-    staged, W packed once per version), else ONE hipBLASLt bf16 GEMM with K' = 3K on
-    [x_hi | x_hi | x_lo] and [W_hi | W_lo | W_hi] (fp32 accumulation and output)."""
+    staged, W packed once per version -- cache=False packs it for this call only, for a weight that
+    is an activation), else ONE hipBLASLt bf16 GEMM with K' = 3K on [x_hi | x_hi | x_lo] and
+    [W_hi | W_lo | W_hi] (fp32 accumulation and output). out: a contiguous [M, N] fp32 destination."""
     lib = _lib.load()
     k, n = x.shape[-1], weight.shape[0]
-    w3 = _split_weight(weight)
+    w3 = _split_weight(weight) if cache else split_bf16x3(weight, weight_order=True)
     if n % 64 == 0 and k % 32 == 0:
         xf = _f32(x).reshape(-1, k)
-        y = torch.empty((xf.shape[0], n), dtype=torch.float32, device=x.device)
+        y = out if out is not None else torch.empty((xf.shape[0], n), dtype=torch.float32, device=x.device)
+        if y.dtype != torch.float32 or not y.is_contiguous() or y.numel() != xf.shape[0] * n:
+            raise ValueError("linear_bf16x3: out must be a contiguous fp32 [M, N] tensor")
         bb = _f32(bias) if bias is not None else None
         _lib.check(lib.tsplat_linear_bf16x3_fwd(_lib.ptr(xf), _lib.ptr(w3), _lib.ptr(bb), _lib.ptr(y), xf.shape[0], n, k,
                                                 _ACTS[act], _lib.stream_ptr(x.device)), "tsplat_linear_bf16x3_fwd")
@@ -865,15 +869,24 @@ def wino_pack_weight_bf16x3(weight):
     return packed
 
 
-def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=(), precision: str | None = None):
-    """act(conv2d(cat([x, *extra], 1), weight, bias, stride 1, padding 1)) via Winograd F(2x2, 3x3);
-    the concatenation is read in place. precision "fp32" (tsplat_conv3x3_wino_cat_f32_fwd, exact fp32
-    MFMA) or "bf16x3" (tsplat_conv3x3_wino_bf16x3_cat_fwd, split-bf16 MFMA); default: the current
-    dense_precision mode."""
+def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=(), precision: str | None = None, residual=None,
+                 residual2=None, relu_in: bool = False):
+    """act(conv2d(cat([x, *extra], 1), weight, bias, stride 1, padding 1)) (+ residual + residual2)
+    via Winograd F(2x2, 3x3); the concatenation is read in place; relu_in: ReLU on the input as it
+    is loaded. precision "fp32" (tsplat_conv3x3_wino_cat_f32_fwd, exact fp32 MFMA; relu_in /
+    residuals as separate launches) or "bf16x3" (tsplat_conv3x3_wino_bf16x3_ex_fwd, split-bf16
+    MFMA, all fused); default: the current dense_precision mode."""
     import ctypes
 
     lib = _lib.load()
     precision = precision or _DENSE
+    if precision != "bf16x3" and (relu_in or residual is not None or residual2 is not None):
+        y = conv3x3_wino(torch.relu(x) if relu_in else x, weight, bias, act,
+                         tuple(torch.relu(t) for t in extra) if relu_in else extra, precision)
+        for r in (residual, residual2):
+            if r is not None:
+                y = y + r
+        return y
     srcs = [_f32(t) for t in (x, *extra)]
     n, _, h, w = srcs[0].shape
     co = weight.shape[0]
@@ -885,12 +898,20 @@ def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=(), precision: s
     ptrs = (ctypes.c_void_p * len(srcs))(*[_lib.ptr(t) for t in srcs])
     chans = (ctypes.c_int32 * len(srcs))(*[t.shape[1] for t in srcs])
     if precision == "bf16x3":
-        fn, packed, name = lib.tsplat_conv3x3_wino_bf16x3_cat_fwd, wino_pack_weight_bf16x3(weight), "bf16x3"
-    else:
-        fn, packed, name = lib.tsplat_conv3x3_wino_cat_f32_fwd, wino_pack_weight(weight), "f32"
-    rc = fn(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p), len(srcs), _lib.ptr(packed),
-            _lib.ptr(pb), _lib.ptr(y), n, h, w, co, _WINO_ACT[act], _lib.stream_ptr(x.device))
-    _lib.check(rc, f"tsplat_conv3x3_wino_{name}_cat_fwd")
+        res = [_f32(r) if r is not None else None for r in (residual, residual2)]
+        for r in res:
+            if r is not None and tuple(r.shape) != tuple(y.shape):
+                raise ValueError(f"residual {tuple(r.shape)} != output {tuple(y.shape)}")
+        rc = lib.tsplat_conv3x3_wino_bf16x3_ex_fwd(
+            ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p), len(srcs),
+            _lib.ptr(wino_pack_weight_bf16x3(weight)), _lib.ptr(pb), _lib.ptr(res[0]), _lib.ptr(res[1]), _lib.ptr(y),
+            n, h, w, co, _WINO_ACT[act], int(relu_in), _lib.stream_ptr(x.device))
+        _lib.check(rc, "tsplat_conv3x3_wino_bf16x3_ex_fwd")
+        return y
+    rc = lib.tsplat_conv3x3_wino_cat_f32_fwd(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p),
+                                             len(srcs), _lib.ptr(wino_pack_weight(weight)), _lib.ptr(pb),
+                                             _lib.ptr(y), n, h, w, co, _WINO_ACT[act], _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_conv3x3_wino_f32_cat_fwd")
     return y
 
 

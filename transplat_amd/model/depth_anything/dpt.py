@@ -32,6 +32,15 @@ _DPT_EPI = os.environ.get("TSPLAT_DPT_EPI", "1") != "0"
 # 356 views/s, C3 849 vs 887): the branches' MIOpen convolutions take CUs from the critical path
 # (DINOv2 blocks and the backbone beside them) rather than filling idle ones.
 _DPT_HOIST = os.environ.get("TSPLAT_DPT_HOIST", "0") == "1"
+# bf16x3 dense mode (kernels.dense_precision): the head runs on NCHW maps instead, so its 3x3
+# convolutions take the bf16x3 Winograd kernel with the ResidualConvUnit glue fused (ReLU on load,
+# bias, + x, + the fusion block's skip: two launches per unit) and the 1x1s the direct kernel;
+# "0" = the channels-last MIOpen chain in that mode too (A/B knob).
+_DPT_NCHW3 = os.environ.get("TSPLAT_DPT_NCHW3", "1") != "0"
+
+
+def _nchw3() -> bool:
+    return _DPT_NCHW3 and kernels.split_mode()
 
 
 def _resize(x, modifier: dict, align_corners: bool):
@@ -81,6 +90,13 @@ class ResidualConvUnit(nn.Module):
 
     def forward(self, x, skip=None):
         """out(x) + x (+ skip: the FeatureFusionBlock's other input, added in the same pass)."""
+        if (_nchw3() and not self.bn and isinstance(self.activation, nn.ReLU) and x.is_cuda and x.is_contiguous()
+                and kernels.conv3x3_wino_ok(x, self.conv1.weight, vs_miopen=True)
+                and (skip is None or skip.is_contiguous())):
+            # bf16x3 mode, NCHW: relu -> conv1 + bias, relu -> conv2 + bias + x (+ skip), two launches
+            out = kernels.conv3x3_wino(x, self.conv1.weight, self.conv1.bias, relu_in=True)
+            return kernels.conv3x3_wino(out, self.conv2.weight, self.conv2.bias, relu_in=True, residual=x,
+                                        residual2=skip)
         if _DPT_DIRECT == "0" and self._epilogue_ok(x):
             # bias-free MIOpen convs with bias + ReLU / bias + residual(s) fused after each:
             # 3 glue launches per unit instead of 5 (6 with the fusion block's add)
@@ -170,13 +186,16 @@ class DPTHead(nn.Module):
         self._cl_done = True
 
     def prepare(self, is_cuda: bool):
-        if _DPT_CL_WEIGHTS and not getattr(self, "_cl_done", False) and is_cuda:
+        if _DPT_CL_WEIGHTS and not getattr(self, "_cl_done", False) and is_cuda and not _nchw3():
             self._channels_last_weights()
 
     def reassemble(self, i, x, patch_h, patch_w):
         """Branch i of the head up to layer{i+1}_rn (reference dpt.py:121-140): tokens [B, N, C] ->
         project (1x1) -> resize (convT / identity / strided conv) -> 3x3 layer_rn."""
         x = x.permute(0, 2, 1).reshape((x.shape[0], x.shape[-1], patch_h, patch_w))
+        if _nchw3():  # NCHW maps for the bf16x3 kernels (the permuted view is channels-last)
+            x = self.resize_layers[i](self.projects[i](x.contiguous())).contiguous()
+            return getattr(self.scratch, f"layer{i + 1}_rn")(x).contiguous()
         x = self.resize_layers[i](self.projects[i](x))
         return getattr(self.scratch, f"layer{i + 1}_rn")(x)
 
@@ -198,6 +217,9 @@ class DPTHead(nn.Module):
         out_feature = final_out.clone().detach()
         final_out = _resize(final_out, {"size": (int(patch_h * 14), int(patch_w * 14))}, True)
         oc = s.output_conv2
+        if _nchw3() and final_out.is_contiguous() and kernels.conv3x3_wino_ok(final_out, oc[0].weight, vs_miopen=True):
+            h = kernels.conv3x3_wino(final_out, oc[0].weight, oc[0].bias, act="relu")
+            return oc[4](oc[3](oc[2](h))), out_feature
         if (_DPT_EPI and final_out.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")
                 and final_out.is_cuda and final_out.is_contiguous(memory_format=torch.channels_last)):
             # conv -> ReLU as conv + (bias, ReLU) epilogue; the 1-channel tail stays on the modules
