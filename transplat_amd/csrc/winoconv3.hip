@@ -484,12 +484,15 @@ static int pick_form(int n, int th, int tw, int co) {
         const int f = atoi(e);
         if (f >= 1 && f <= 4) return f;
     }
+    // measured per census shape (tools/bench_wino3.py, profiles/r4/bench_wino3_*.log): the 64 x 64
+    // form from 128 workgroups up (2 x 128 -> 64 at 144^2: 53.9 vs 69.6 us for 32 x 32), two
+    // k-groups where 32 x 32 workgroups would leave CUs idle, the 32 x 64 form never (32 -> 32 at
+    // 256^2: 37.6 vs 30.1 us for 32 x 32)
     const long tiles = (long)n * th * tw;
     const int cob32 = (co + 31) / 32;
     const long wg64 = (tiles + 63) / 64 * ((co + 63) / 64);
     const long wg32 = (tiles + 31) / 32 * cob32;
-    if (co > 32 && wg64 >= 256) return 4;
-    if (co <= 32 && (tiles + 63) / 64 * cob32 >= 256) return 3;
+    if (co > 32 && wg64 >= 128) return 4;
     return wg32 <= 256 ? 2 : 1;
 }
 

@@ -110,16 +110,16 @@ def uv_cross(value, key, intr, pose, disp, offsets, logits, h: int, w: int):
             table = torch.bmm(k2, torch.cat((vb, vb), dim=-1).transpose(1, 2), out_dtype=torch.float32)
         value = None
         key, offsets, logits, disp = map(_f32, (key, offsets, logits, disp))
-    elif _DENSE == "bf16x3" and value.is_cuda and c % 32 == 0 and hw % 64 == 0:
-        # bf16x3 dense mode: the table G[i] = key[i] value_other[i]^T in split-bf16 precision on
-        # tsplat_linear_bf16x3_fwd (value_other as the [HW, C] "weight", split per call), written
-        # straight into the [2b, HW, HW] table (<= 3 * 2^-18 relative per product)
+    elif _DENSE == "bf16x3" and value.is_cuda and c % 4 == 0:
+        # bf16x3 dense mode: the table in split-bf16 precision as ONE hipBLASLt bf16 GEMM with K = 3C,
+        # [key_hi | key_hi | key_lo] x [val_hi | val_lo | val_hi]^T, fp32 output (47 vs 83 us for the
+        # fp32 bmm at b = 1, and vs 104 us on tsplat_linear_bf16x3_fwd, profiles/r4/split_gemm2.log;
+        # <= 3 * 2^-18 relative per product)
         value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
-        kf = key.reshape(b * 2, hw, c)
-        vo = torch.flip(value, dims=[1]).reshape(b * 2, hw, c)
-        table = torch.empty((b * 2, hw, hw), dtype=torch.float32, device=value.device)
-        for i in range(b * 2):
-            linear_bf16x3(kf[i], vo[i], out=table[i], cache=False)
+        k3 = split_bf16x3(key.reshape(b * 2, hw, c))
+        v3 = split_bf16x3(torch.flip(value, dims=[1]).reshape(b * 2, hw, c), weight_order=True)
+        with torch.autocast("cuda", enabled=False):
+            table = torch.bmm(k3, v3.transpose(1, 2), out_dtype=torch.float32)
     else:
         value, key, offsets, logits, disp = map(_f32, (value, key, offsets, logits, disp))
         with torch.autocast("cuda", enabled=False):
@@ -805,11 +805,13 @@ def linear_bf16x3(x, weight, bias=None, act: str = "none", out=None, cache: bool
     return y
 
 
-# nn.Linear in bf16x3 mode (TSPLAT_LIN3=0 turns it off). hipBLASLt's own bf16 GEMM at K' = 3K is no
-# faster than its fp32 GEMM on the step's linears (tools/bench_split_gemm.py, profiles/r4/split_gemm.log:
-# DINOv2 qkv 23.4 vs 28.8 us, proj 23.3 vs 18.7, fc1 27.8 vs 31.1, fc2 30.3 vs 29.2), so the dispatch
-# takes the hand-written tsplat_linear_bf16x3_fwd; linears below _LIN3_MIN_FLOP stay exact fp32.
-_LIN3 = os.environ.get("TSPLAT_LIN3", "1") == "1"
+# nn.Linear in bf16x3 mode: OFF by default (TSPLAT_LIN3=1 turns it on). Measured on the step's linears
+# (tools/bench_split_gemm.py; profiles/r4/split_gemm.log, split_gemm2.log): neither hipBLASLt's bf16 GEMM
+# at K' = 3K (DINOv2 qkv 23.9 vs 29.0 us fp32, proj 23.9 vs 19.0, fc1 27.3 vs 30.4, fc2 29.3 vs 27.8)
+# nor the first tsplat_linear_bf16x3_fwd (37.3 / 24.8 / 51.9 / 83.6 us: at M = 650 a 64 x 64 tile per
+# workgroup gives 132-528 workgroups whose 32-wide K chunks serialise on load latency) beats the
+# library's fp32 SGEMM; the M = 650 shapes stay exact fp32 until the kernel is pipelined deeper.
+_LIN3 = os.environ.get("TSPLAT_LIN3", "0") == "1"
 _LIN3_MIN_FLOP = float(os.environ.get("TSPLAT_LIN3_MIN_FLOP", "2e8"))
 
 
