@@ -13,11 +13,11 @@
 // Workgroup: 4 * CB * KS waves; CB 32-channel output blocks x T = 32 * NB output tiles; wave
 // (k-group kg, co block hh, transform row r) owns the 4 GEMMs xi = 4 r + s of its co block for all
 // NB tile blocks (4 * NB accumulator tiles). Per 16-channel chunk every thread transforms PP
-// channel pairs of one tile (lanes = consecutive tiles: coalesced loads, conflict-free LDS writes),
-// splits each V value into hi / lo bf16 and stores the pair as one dword of
-//   sV[hl][xi][pair 8][tile T]   (pair p = channels 2p, 2p + 1 of the chunk),
-// so a B fragment (lane = tile n, half h: channels 8h .. 8h + 7) is 4 dwords at stride T (two
-// ds_read2 instructions). A = the packed U fragment, one 16-B load per (xi, hi / lo) and lane.
+// channel pairs of one tile, splits each V value into hi / lo bf16 and stores the pair as one dword of
+//   sV[hl][xi][half 2][tile T][pair 4]   (pair 4 half + p = channels 8 half + 2p, + 1),
+// so a B fragment (lane = tile n, half h: channels 8h .. 8h + 7) is one ds_read_b128, and a wave's
+// stores (lanes = 16 tiles x 4 pairs) are 64 consecutive dwords. A = the packed U fragment, one
+// 16-B load per (xi, hi / lo) and lane.
 // Double-buffered sV, one barrier per chunk; the next chunk's patch loads and A fragments are in
 // flight during the current MFMAs. KS = 2 splits the chunks of one output block over two k-groups
 // (few-workgroup grids of the 32^2-64^2 maps); their Z slabs are summed in the epilogue.
@@ -38,6 +38,10 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxSrc = 6;
 constexpr int kMaxCiPad = 1024;
+
+// 16 zero bytes every masked load reads instead (loads stay unconditional: a select of the address
+// instead of an exec-masked branch with zero-initialised destinations per load)
+__device__ uint4 g_zero16 = {0u, 0u, 0u, 0u};
 
 struct Args {
     const float* src[kMaxSrc];
@@ -61,13 +65,20 @@ __device__ __forceinline__ float act_fn(float v, int act) {
     return v;
 }
 
-__device__ __forceinline__ uint32_t bf16_bits(float v) { return (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v); }
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 
-// hi / lo halves of the channel pair (a, b) as two packed dwords (channel a in the low half)
+// (a, b) rounded to bf16 and packed (a in the low half): one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((floatx2){a, b}, bf16x2));
+}
+
+// hi / lo halves of the channel pair (a, b) as two packed dwords (channel a in the low half):
+// cvt_pk, shift, and, two subtractions, cvt_pk
 __device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
-    hi = bf16_bits(a) | (bf16_bits(b) << 16);
+    hi = pack_bf16(a, b);
     const float ah = __builtin_bit_cast(float, hi << 16), bh = __builtin_bit_cast(float, hi & 0xffff0000u);
-    lo = bf16_bits(a - ah) | (bf16_bits(b - bh) << 16);
+    lo = pack_bf16(a - ah, b - bh);
 }
 
 // U = G g G^T (as winoconv.hip's weight_kernel), split into hi / lo bf16 and packed as the A operand
@@ -195,9 +206,9 @@ template <int CB, int NB, int KS, bool ST>
 __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     constexpr int T = 32 * NB;                 // tiles per workgroup
     constexpr int GT = 256 * CB;               // threads per k-group
-    constexpr int ROWS = GT / T;               // pair rows per pass
-    constexpr int PP = 8 / ROWS;               // channel pairs per thread per chunk
-    static_assert(ROWS * PP == 8, "pairs per chunk");
+    constexpr int PHR = GT / (4 * T);          // pair halves (4 pairs each) covered per pass
+    constexpr int PP = 2 / PHR;                // channel pairs per thread per chunk
+    static_assert(PHR * PP == 2, "pairs per chunk");
     constexpr int BUF = 2 * 16 * 8 * T;        // dwords per sV buffer (hi + lo)
     constexpr int CO = 32 * CB;
     constexpr int NSV = ST ? 1 : 2;            // sV buffers per k-group
@@ -211,8 +222,10 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int kg = wid / (4 * CB), wg = wid % (4 * CB);
     const int hh = wg >> 2, rr = wg & 3;
+    // transform slot: lane bits 0-1 = pair within a half (pl), then the tile, then the half (ph):
+    // a wave's 64 lanes are 16 tiles x 4 pairs, so its sV dword stores are 64 consecutive dwords
     const int gtid = tid % GT;
-    const int t = gtid % T, prow = gtid / T;
+    const int pl = gtid & 3, t = (gtid >> 2) % T, ph0 = (gtid >> 2) / T;
     const Patch<T> pt(a, blockIdx.x, t);
 
     for (int c = tid; c < a.ci_pad; c += 256 * CB * KS) {
@@ -239,12 +252,14 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
 #pragma unroll
         for (int s = s0; s < s1; ++s)
 #pragma unroll
-            for (int hl = 0; hl < 2; ++hl)
+            for (int hl = 0; hl < 2; ++hl) {
 #if TSPLAT_W3_ABL == 3  // diagnostic build: no A loads
                 af[s][hl] = make_uint4(chunk, s, hl, lane);
 #else
-                af[s][hl] = ok ? ub[s * xi_stride + (size_t)chunk * 128 + hl * 64] : make_uint4(0u, 0u, 0u, 0u);
+                const uint4* src = ok ? ub + s * xi_stride + (size_t)chunk * 128 + hl * 64 : &g_zero16;
+                af[s][hl] = *src;
 #endif
+            }
     };
 
     floatx16 acc[4][NB];
@@ -259,7 +274,7 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     auto load_patches = [&](int chunk) {
 #pragma unroll
         for (int q = 0; q < PP; ++q) {
-            const int c0 = chunk * 16 + 2 * (prow + q * ROWS);
+            const int c0 = chunk * 16 + 2 * (4 * (ph0 + q * PHR) + pl);
             pt.load(a, planes, c0, d[q][0]);
             pt.load(a, planes, c0 + 1, d[q][1]);
         }
@@ -267,7 +282,7 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     uint32_t* sG = smem + kg * (NSV * BUF + (ST ? 2 * RGN : 0));
     auto transform = [&](uint32_t* sV) {
 #pragma unroll
-        for (int q = 0; q < PP; ++q) transform_pair<T>(d[q][0], d[q][1], sV + (prow + q * ROWS) * T + t);
+        for (int q = 0; q < PP; ++q) transform_pair<T>(d[q][0], d[q][1], sV + ((ph0 + q * PHR) * T + t) * 4 + pl);
     };
     // staged region of the chunk: R rows x C4 float4 per channel, origin (ry0, rx0)
     const int blk = blockIdx.x % (a.bx * a.by);
@@ -275,17 +290,30 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     const int ry0 = 2 * (blk / a.bx) * a.tby - 1, rx0 = 2 * (blk % a.bx) * a.tbx - 4;
     float* sIn = reinterpret_cast<float*>(sG + NSV * BUF);
     float4 gr[ST ? NL : 1];
+    // this thread's region elements (channel in the chunk, in-plane offset, in-map) do not depend on
+    // the chunk: decomposed once (the runtime divisions by R C4 and C4 stay out of the loop)
+    // packed as (in-plane float offset << 4) | channel-in-chunk, -1 outside the map / region
+    int g_code[ST ? NL : 1];
+#pragma unroll
+    for (int k = 0; k < (ST ? NL : 0); ++k) {
+        const int idx = gtid + GT * k;
+        const int ch = idx / (R * C4), rem = idx - ch * (R * C4);
+        const int row = rem / C4, c4 = rem - row * C4;
+        const int y = ry0 + row, x = rx0 + 4 * c4;
+        const bool ok = idx < 16 * R * C4 && y >= 0 && y < a.h && x >= 0 && x < a.w;
+        g_code[k] = ok ? ((y * a.w + x) << 4) | ch : -1;
+    }
     auto gload = [&](int chunk) {
-        const int total = 16 * R * C4;
 #pragma unroll
         for (int k = 0; k < (ST ? NL : 0); ++k) {
-            const int idx = gtid + GT * k;
-            const int ch = idx / (R * C4), rem = idx - ch * (R * C4);
-            const int row = rem / C4, c4 = rem - row * C4;
-            const int c = chunk * 16 + ch, y = ry0 + row, x = rx0 + 4 * c4;
-            const bool ok = idx < total && c < a.ci && y >= 0 && y < a.h && x >= 0 && x < a.w;
-            const float4* src = reinterpret_cast<const float4*>(planes[min(c, a.ci_pad - 1)] + (size_t)y * a.w + x);
-            gr[k] = ok ? *src : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int c = chunk * 16 + (g_code[k] & 15);
+            const bool ok = g_code[k] >= 0 && c < a.ci;
+            // global address space: a plain pointer read from LDS would make this a flat load, which
+            // counts against the LDS counter too and waits on it
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const float* addr = ok ? planes[c] + (g_code[k] >> 4) : reinterpret_cast<const float*>(&g_zero16);
+            const f4v v = *(const __attribute__((address_space(1))) f4v*)addr;
+            gr[k] = make_float4(v.x, v.y, v.z, v.w);
         }
     };
     auto sstore = [&](int slot) {
@@ -306,21 +334,22 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
         for (int q = 0; q < PP; ++q)
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const float* b = base + (2 * (prow + q * ROWS) + e) * R * RP;
+                const float* b = base + (2 * (4 * (ph0 + q * PHR) + pl) + e) * R * RP;
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
                     for (int j = 0; j < 4; ++j) d[q][e][4 * i + j] = b[i * RP + j];
             }
     };
-    // MFMAs of xi s0 .. s1 - 1 on buffer sV: B fragment of lane (n, h) = dwords [hl][xi][4 h + c][32 nb + n]
+    // MFMAs of xi s0 .. s1 - 1 on buffer sV: B fragment of lane (n, h) = the 16 B of
+    // [hl][xi][half h][tile 32 nb + n][4 pairs] (channels 8 h .. 8 h + 7), one ds_read_b128
     auto mfma = [&](const uint32_t* sV, int s0, int s1) {
 #if TSPLAT_W3_ABL == 2  // diagnostic build: no MFMAs (the B reads stay)
-        const uint32_t* bq = sV + (4 * (lane >> 5)) * T + (lane & 31);
+        const uint32_t* bq = sV + ((lane >> 5) * T + (lane & 31)) * 4;
         for (int s = s0; s < s1; ++s) acc[s][0][0] += __builtin_bit_cast(float, bq[(4 * rr + s) * 8 * T]);
         return;
 #endif
-        const uint32_t* bb = sV + (4 * (lane >> 5)) * T + (lane & 31);
+        const uint32_t* bb = sV + ((lane >> 5) * T + (lane & 31)) * 4;
 #pragma unroll
         for (int s = s0; s < s1; ++s) {
             const int xi = 4 * rr + s;
@@ -328,12 +357,9 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
             const bf16x8 al = __builtin_bit_cast(bf16x8, af[s][1]);
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb) {
-                const uint32_t* ph = bb + xi * 8 * T + 32 * nb;
-                const uint32_t* pl = ph + 16 * 8 * T;
-                const uint4 vh = make_uint4(ph[0], ph[T], ph[2 * T], ph[3 * T]);
-                const uint4 vl = make_uint4(pl[0], pl[T], pl[2 * T], pl[3 * T]);
-                const bf16x8 bh = __builtin_bit_cast(bf16x8, vh);
-                const bf16x8 bl = __builtin_bit_cast(bf16x8, vl);
+                const uint32_t* ph = bb + xi * 8 * T + 32 * nb * 4;
+                const bf16x8 bh = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ph));
+                const bf16x8 bl = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ph + 16 * 8 * T));
                 acc[s][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[s][nb], 0, 0, 0);
                 acc[s][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[s][nb], 0, 0, 0);
                 acc[s][nb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[s][nb], 0, 0, 0);
