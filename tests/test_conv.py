@@ -229,14 +229,16 @@ def tf32_round(t: torch.Tensor) -> torch.Tensor:
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("stage", ["auto", "0"])
-@pytest.mark.parametrize("form", ["auto", "1", "2", "3", "4"])
+@pytest.mark.parametrize("form", ["auto", "1", "2", "3", "4", "5"])
 @pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES + [(1, 24, 48, 10, 96, True, "relu"),
-                                                               (2, 40, 64, 22, 136, False, "none")])
+                                                               (2, 40, 64, 22, 136, False, "none"),
+                                                               (3, 32, 40, 36, 64, True, "gelu")])
 def test_conv3x3_wino_bf16x3_kernel(device, monkeypatch, stage, form, n, ci, co, h, w, bias, act):
     """Winograd F(2x2, 3x3) in split-bf16 precision (tsplat_conv3x3_wino_bf16x3_fwd: hi*hi + hi*lo +
     lo*hi on bf16 MFMA, fp32 accumulation) against torch's conv2d in float64, with the launch's own
     workgroup form and each form forced (TSPLAT_WINO3_FORM: 32 co x 32 tiles, the same with two
-    k-groups, 32 x 64, 64 x 64), with the staged input (coalesced region loads through LDS, maps
+    k-groups, 32 x 64, 64 x 64, the persistent 32 x 32 form walking several tile blocks per workgroup
+    across images -- staged maps only, else form 1), with the staged input (coalesced region loads through LDS, maps
     whose width is a multiple of 4: tile blocks 32 / 16 / 8 wide) and without it
     (TSPLAT_WINO3_STAGE=0). Bounds (written here): the same 2e-5 of max |y| as the exact-fp32
     kernel, and at most 1/8 of the error of the reference's own precision -- TF32 operands
@@ -286,6 +288,29 @@ def test_conv3x3_wino_bf16x3_relu_in_residual(device, monkeypatch, stage, n, c, 
     out = K.conv3x3_wino(x.to(device), wt.to(device), b.to(device), precision="bf16x3", residual=x.to(device),
                          residual2=sk.to(device) if skip else None, relu_in=True).cpu().double()
     err = ((out - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-5, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wgs", ["3", "7", "512"])
+def test_conv3x3_wino_bf16x3_persistent_walk(device, monkeypatch, wgs):
+    """The persistent form (TSPLAT_WINO3_FORM=5) with 3 / 7 / 512 workgroups per output block
+    (TSPLAT_WINO3_PWG): each workgroup's flat (tile block, chunk) sequence crosses image and
+    concatenation-source boundaries; ReLU-on-load and both residuals in the epilogue; against float64."""
+    from transplat_amd import kernels as K
+
+    monkeypatch.setenv("TSPLAT_WINO3_FORM", "5")
+    monkeypatch.setenv("TSPLAT_WINO3_PWG", wgs)
+    parts = [seeded((3, c, 40, 72), 120 + c) for c in (24, 16)]
+    wt = seeded((48, 40, 3, 3), 131) * (1.0 / (9 * 40) ** 0.5)
+    b = seeded((48,), 132)
+    r1, r2 = seeded((3, 48, 40, 72), 133), seeded((3, 48, 40, 72), 134)
+    x = torch.cat(parts, 1)
+    ref = torch.nn.functional.conv2d(torch.relu(x).double(), wt.double(), b.double(), padding=1)
+    ref = torch.nn.functional.gelu(ref) + r1.double() + r2.double()
+    out = K.conv3x3_wino(parts[0].to(device), wt.to(device), b.to(device), "gelu", extra=(parts[1].to(device),),
+                         precision="bf16x3", residual=r1.to(device), residual2=r2.to(device), relu_in=True)
+    err = ((out.cpu().double() - ref).abs().max() / ref.abs().max()).item()
     assert err < 2e-5, err
 
 

@@ -371,8 +371,8 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     // past the last one is all zeros) so the groups meet at every barrier
     const int iters = (a.nchunk + KS - 1) / KS;
     if constexpr (ST) {
-        // single sV: transform(it) | barrier | MFMAs(it) | barrier; the region of chunk it + 1 is
-        // stored to the other sIn slot during transform(it) and chunk it + 2's loads fly meanwhile
+        // single sV: store region(it + 1) | transform(it) | loads of region(it + 2) | barrier |
+        // MFMAs(it) | barrier
         gload(kg);
         sstore(0);
         if (iters > 1) gload(kg + KS);
@@ -381,12 +381,13 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
         for (int it = 0; it < iters; ++it) {
             const int ch = kg + it * KS;
             const bool more = it + 1 < iters;
+            // the region of chunk it + 1 (its loads flew during the last MFMA phase) goes to LDS first,
+            // so its registers are free again during the transform; slot (it + 1) & 1 was last read
+            // by read_patches(it - 1), before the last barrier
+            if (more) sstore((it + 1) & 1);
             read_patches(it & 1);
             transform(sG);
-            if (more) {
-                sstore((it + 1) & 1);
-                if (it + 2 < iters) gload(ch + 2 * KS);
-            }
+            if (more && it + 2 < iters) gload(ch + 2 * KS);
             __syncthreads();  // sV(it) complete
             mfma(sG, 0, 4);
             if (more) load_a(ch + KS, 0, 4);
@@ -479,6 +480,199 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     }
 }
 
+// Persistent 32 co x 32 tile form for large maps with few input channels (the refine U-Net's
+// 32-channel 256^2 levels: 2-4 chunks per output block, so a one-block workgroup was mostly its
+// own prologue and epilogue -- region loads, planes, A fragments, Z fold, stores -- at ~12 us per
+// workgroup round). Each workgroup walks tile blocks blockIdx.x, + gridDim.x, ... of output block
+// blockIdx.y as one flat (block, chunk) sequence: the staged pipeline of conv_kernel<1, 1, 1, true>
+// runs straight across block boundaries (the next block's regions load during this block's last
+// MFMAs and its epilogue), and each block ends with the Z fold and the stores.
+__global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblocks) {
+    constexpr int T = 32, GT = 256;
+    constexpr int BUF = 2 * 16 * 8 * T;
+    constexpr int RGN = Region<T>::kMaxFloats;
+    constexpr int NL = (RGN / 4 + GT - 1) / GT;
+    constexpr int CO = 32;
+    __shared__ __attribute__((aligned(16))) uint32_t smem[BUF + 2 * RGN];
+    __shared__ const float* planes[kMaxCiPad];  // image 0's plane of each input channel
+    __shared__ int cstride[kMaxCiPad];           // floats from one image's plane to the next's
+
+    const int tid = threadIdx.x, lane = tid & 63, rr = tid >> 6;
+    const int pl = tid & 3, t = (tid >> 2) % T, ph0 = (tid >> 2) / T;  // one channel pair per thread
+    const size_t hw = (size_t)a.h * a.w;
+    for (int c = tid; c < a.ci_pad; c += GT) {
+        const float* src = nullptr;
+        int rem = min(c, a.ci - 1), cs = 0;
+        for (int q = 0; q < a.nsrc && !src; ++q) {
+            if (rem < a.cs[q]) {
+                src = a.src[q] + (size_t)rem * hw;
+                cs = a.cs[q];
+            } else {
+                rem -= a.cs[q];
+            }
+        }
+        planes[c] = src;
+        cstride[c] = (int)(cs * hw);
+    }
+
+    const int cob = a.cob_base + blockIdx.y;
+    const uint4* ub = a.u + ((size_t)(4 * rr) * a.cobs + cob) * a.nchunk * 128 + lane;
+    const size_t xi_stride = (size_t)a.cobs * a.nchunk * 128;
+    uint4 af[4][2];
+    auto load_a = [&](int chunk) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int hl = 0; hl < 2; ++hl) af[s][hl] = ub[s * xi_stride + (size_t)chunk * 128 + hl * 64];
+    };
+    floatx16 acc[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[s][e] = 0.0f;
+
+    const int R = 2 * a.tby + 2, C4 = a.tbx / 2 + 2, RP = 4 * C4;
+    const int bpi = a.bx * a.by;  // tile blocks per image
+    float* sIn = reinterpret_cast<float*>(smem + BUF);
+    // block-independent part of this thread's region elements: (channel << 24) | (row << 12) | c4
+    int g_pos[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+        const int idx = tid + GT * k;
+        const int ch = idx / (R * C4), rem = idx - ch * (R * C4);
+        const int row = rem / C4, c4 = rem - row * C4;
+        g_pos[k] = idx < 16 * R * C4 ? (ch << 24) | (row << 12) | c4 : -1;
+    }
+    float4 gr[NL];
+    // region loads of chunk `chunk` of the workgroup's j-th tile block
+    auto gload = [&](int j, int chunk) {
+        const int bl = blockIdx.x + j * gridDim.x;
+        const int img = bl / bpi, blk = bl - img * bpi;
+        const int ry0 = 2 * (blk / a.bx) * a.tby - 1, rx0 = 2 * (blk % a.bx) * a.tbx - 4;
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            const int code = g_pos[k];
+            const int c = chunk * 16 + ((code >> 24) & 15);
+            const int y = ry0 + ((code >> 12) & 4095), x = rx0 + 4 * (code & 4095);
+            const bool ok = code >= 0 && c < a.ci && y >= 0 && y < a.h && x >= 0 && x < a.w;
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const float* addr = ok ? planes[c] + (size_t)img * cstride[c] + (size_t)y * a.w + x
+                                   : reinterpret_cast<const float*>(&g_zero16);
+            const f4v v = *(const __attribute__((address_space(1))) f4v*)addr;
+            gr[k] = make_float4(v.x, v.y, v.z, v.w);
+        }
+    };
+    auto sstore = [&](int slot) {
+        float4* dst = reinterpret_cast<float4*>(sIn + slot * RGN);
+#pragma unroll
+        for (int k = 0; k < NL; ++k) {
+            float4 v = gr[k];
+            if (a.relu_in) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
+            if (g_pos[k] >= 0) dst[tid + GT * k] = v;
+        }
+    };
+    float d[2][16];
+    auto read_transform = [&](int slot) {
+        const int tyl = t / a.tbx, txl = t - tyl * a.tbx;
+        const float* base = sIn + slot * RGN + 2 * tyl * RP + 2 * txl + 3;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const float* b = base + (2 * (4 * ph0 + pl) + e) * R * RP;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) d[e][4 * i + j] = b[i * RP + j];
+        }
+        transform_pair<T>(d[0], d[1], smem + (ph0 * T + t) * 4 + pl);
+    };
+
+    const int nmine = (nblocks - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int G = nmine * a.nchunk;  // flat (block, chunk) steps of this workgroup
+    if (G <= 0) return;              // uniform: no barrier below is reached by part of the group
+    __syncthreads();                 // planes / cstride
+    gload(0, 0);
+    sstore(0);
+    if (G > 1) gload(1 / a.nchunk, 1 % a.nchunk);
+    load_a(0);
+    __syncthreads();
+    int j = 0, c = 0;
+    for (int g = 0; g < G; ++g) {
+        if (g + 1 < G) sstore((g + 1) & 1);
+        read_transform(g & 1);
+        if (g + 2 < G) gload((g + 2) / a.nchunk, (g + 2) % a.nchunk);
+        __syncthreads();  // sV(g) complete
+        const uint32_t* bb = smem + ((lane >> 5) * T + (lane & 31)) * 4;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int xi = 4 * rr + s;
+            const bf16x8 ah = __builtin_bit_cast(bf16x8, af[s][0]);
+            const bf16x8 al = __builtin_bit_cast(bf16x8, af[s][1]);
+            const uint32_t* ph = bb + xi * 8 * T;
+            const bf16x8 bh = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ph));
+            const bf16x8 bl = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ph + 16 * 8 * T));
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[s], 0, 0, 0);
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[s], 0, 0, 0);
+        }
+        if (g + 1 < G) load_a((c + 1) % a.nchunk);
+        __syncthreads();  // every wave is done with sV(g) and with sIn slot g & 1
+        if (++c < a.nchunk) continue;
+        // block j done: Z = M A through LDS (aliasing sV), then Y = A^T Z + bias (+ act, + residuals)
+        float* zs = reinterpret_cast<float*>(smem);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int col = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5), tt = lane & 31;
+            zs[((rr * 2 + 0) * CO + col) * T + tt] = acc[0][e] + acc[1][e] + acc[2][e];
+            zs[((rr * 2 + 1) * CO + col) * T + tt] = acc[1][e] - acc[2][e] - acc[3][e];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) acc[s][e] = 0.0f;
+        }
+        __syncthreads();
+        const int bl = blockIdx.x + j * gridDim.x;
+        const int img = bl / bpi, blk = bl - img * bpi;
+        for (int pidx = tid; pidx < CO * T; pidx += GT) {
+            const int col = pidx / T, t2 = pidx % T;
+            const int o = cob * 32 + col;
+            const int oty = (blk / a.bx) * a.tby + t2 / a.tbx, otx = (blk % a.bx) * a.tbx + t2 % a.tbx;
+            if (o >= a.co || oty >= a.th || otx >= a.tw) continue;
+            const float bv = a.bias ? a.bias[o] : 0.0f;
+            float z[4][2];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int q = 0; q < 2; ++q) z[r][q] = zs[((r * 2 + q) * CO + col) * T + t2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int py = 2 * oty + i;
+                if (py >= a.h) continue;
+                const float y0v = i == 0 ? z[0][0] + z[1][0] + z[2][0] : z[1][0] - z[2][0] - z[3][0];
+                const float y1v = i == 0 ? z[0][1] + z[1][1] + z[2][1] : z[1][1] - z[2][1] - z[3][1];
+                float r0 = act_fn(y0v + bv, a.act), r1 = act_fn(y1v + bv, a.act);
+                const int px = 2 * otx;
+                const size_t off = ((size_t)img * a.co + o) * hw + (size_t)py * a.w + px;
+                if (a.res) {
+                    r0 += a.res[off];
+                    if (px + 1 < a.w) r1 += a.res[off + 1];
+                }
+                if (a.res2) {
+                    r0 += a.res2[off];
+                    if (px + 1 < a.w) r1 += a.res2[off + 1];
+                }
+                float* p = a.y + off;
+                if (px + 1 < a.w && ((reinterpret_cast<uintptr_t>(p) & 7) == 0)) {
+                    *reinterpret_cast<float2*>(p) = make_float2(r0, r1);
+                } else {
+                    p[0] = r0;
+                    if (px + 1 < a.w) p[1] = r1;
+                }
+            }
+        }
+        __syncthreads();  // Z read before the next block's transform overwrites it
+        c = 0;
+        ++j;
+    }
+}
+
 }  // namespace wino3
 }  // namespace tsplat
 
@@ -504,11 +698,12 @@ extern "C" int tsplat_wino_weight_bf16x3(const float* weight, void* packed, int3
 }
 
 // workgroup forms: 0 = auto, 1 = 32 co x 32 tiles (KS 1), 2 = 32 x 32 with two k-groups,
-// 3 = 32 co x 64 tiles, 4 = 64 co x 64 tiles; staged input (Region) on top where the map allows it
+// 3 = 32 co x 64 tiles, 4 = 64 co x 64 tiles, 5 = persistent 32 x 32 (staged maps only); staged
+// input (Region) on top where the map allows it
 static int pick_form(int n, int th, int tw, int co) {
     if (const char* e = getenv("TSPLAT_WINO3_FORM")) {
         const int f = atoi(e);
-        if (f >= 1 && f <= 4) return f;
+        if (f >= 1 && f <= 5) return f;
     }
     // measured per census shape (tools/bench_wino3.py, profiles/r4/bench_wino3_*.log): the 64 x 64
     // form from 128 workgroups up (2 x 128 -> 64 at 144^2: 53.9 vs 69.6 us for 32 x 32), two
@@ -568,8 +763,8 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const
     a.res = residual;
     a.res2 = residual2;
     a.cob_base = 0;
-    const int form = pick_form(n, a.th, a.tw, co);
-    const int ttiles = form >= 3 ? 64 : 32;
+    int form = pick_form(n, a.th, a.tw, co);
+    const int ttiles = form == 3 || form == 4 ? 64 : 32;
     // tile block: the widest of T x 1, T/2 x 2, T/4 x 4, T/8 x 8 with the fewest padded tiles
     long best = -1;
     for (int tbx = ttiles; tbx >= ttiles / 8; tbx /= 2) {
@@ -588,8 +783,20 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const
     bool staged = w % 4 == 0;
     for (int q = 0; q < nsrc; ++q) staged = staged && (reinterpret_cast<uintptr_t>(srcs[q]) & 15) == 0;
     if (const char* e = getenv("TSPLAT_WINO3_STAGE")) staged = staged && atoi(e) != 0;
+    if (form == 5 && !staged) form = 1;
     hipStream_t stream = (hipStream_t)stream_;
     const prof::ExtEvents ev = prof::ext_events(prof::kWinoConv);
+    if (form == 5) {
+        // about two workgroups per CU (68 KB of LDS each), each walking its share of the blocks
+        int wgs = 512;
+        if (const char* e = getenv("TSPLAT_WINO3_PWG")) wgs = std::max(1, atoi(e));
+        const int cob32 = (co + 31) / 32;
+        const int gx = std::max(1, std::min(blocks, (wgs + cob32 - 1) / cob32));
+        hipExtLaunchKernelGGL(wino3::conv_persist_kernel, dim3(gx, cob32), dim3(256), 0, stream, ev.start, ev.stop, 0,
+                              a, blocks);
+        TSPLAT_CHECK_LAUNCH();
+        return TSPLAT_OK;
+    }
     switch (form) {
         case 4: launch<2, 2, 1>(a, blocks, staged, stream, ev.start, ev.stop); break;
         case 3: launch<1, 2, 1>(a, blocks, staged, stream, ev.start, ev.stop); break;
