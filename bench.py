@@ -444,15 +444,16 @@ def main():
             direct = sum(f for _, f in log) / (cms * 1e-3) / 1e12
             if args.dense_dtype == "bf16x3":
                 # three bf16 MFMA products per fp32 product, priced against the dense bf16 peak
-                achieved, peak = 3 * gemm, BF16_MFMA_PEAK_TFS
+                c_achieved, c_peak = 3 * gemm, BF16_MFMA_PEAK_TFS
                 flops = ("bf16 MFMA products 3 * 2*16*ci*co*tiles (hi*hi + hi*lo + lo*hi of the 16 F(2x2,3x3) "
                          "GEMMs, unpadded)")
             else:
-                achieved, peak = gemm, FP32_MFMA_PEAK_TFS
+                c_achieved, c_peak = gemm, FP32_MFMA_PEAK_TFS
                 flops = "Winograd GEMM products 2*16*ci*co*tiles (the 16 F(2x2,3x3) GEMMs, unpadded)"
             conv_roofline = {
                 "kernel": "wino_conv" if args.dense_dtype == "fp32" else "wino_conv_bf16x3", "bound": "mfma",
-                "achieved": achieved, "peak": peak, "unit": "TFLOP/s", "frac": achieved / peak, "flops": flops,
+                "achieved": c_achieved, "peak": c_peak, "unit": "TFLOP/s", "frac": c_achieved / c_peak,
+                "flops": flops,
                 "fp32_gemm_equivalent_achieved": gemm, "direct_equivalent_achieved": direct,
                 "launches_per_step": claunches / n_prof,
                 "ms_per_step": cms / n_prof, "share_of_step": cms / n_prof / (elapsed / args.steps * 1e3),

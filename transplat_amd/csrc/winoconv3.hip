@@ -38,6 +38,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kMaxSrc = 6;
 constexpr int kMaxCiPad = 1024;
+constexpr int kPersistCiPad = 512;  // the persistent form's plane table (keeps it at 2 workgroups / CU)
 
 // 16 zero bytes every masked load reads instead (loads stay unconditional: a select of the address
 // instead of an exec-masked branch with zero-initialised destinations per load)
@@ -197,9 +198,14 @@ __device__ __forceinline__ void transform_pair(const float (&da)[16], const floa
 // with coalesced float4 loads (a chunk ahead, in registers) into an LDS slot sIn[ch][row][col], and
 // each thread reads its 4x4 patches from there: ~5 float4 loads per thread and chunk instead of 32
 // predicated scalar ones (the map width must be a multiple of 4 and the sources 16-B aligned).
+// sIn holds [16 channels][R rows][RP floats] with the channel stride padded by 8 floats (CS =
+// R RP + 8, R RP being a multiple of 16 for every tile-block shape): a wave's patch reads (16 tiles
+// x 4 channel pairs, pair p at channel stride 2 CS) then hit 2 distinct banks per tile column
+// instead of one (2-way instead of 4-way conflicts)
 template <int T>
 struct Region {
-    static constexpr int kMaxFloats = T == 32 ? 16 * 4 * 72 : 16 * 4 * 136;  // largest [16][R][RP] over TBX
+    static constexpr int kPad = 8;
+    static constexpr int kMaxFloats = T == 32 ? 16 * (4 * 72 + 8) : 16 * (4 * 136 + 8);  // largest [16][CS]
 };
 
 template <int CB, int NB, int KS, bool ST>
@@ -213,7 +219,9 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     constexpr int CO = 32 * CB;
     constexpr int NSV = ST ? 1 : 2;            // sV buffers per k-group
     constexpr int RGN = Region<T>::kMaxFloats; // floats per sIn slot
-    constexpr int NL = (RGN / 4 + GT - 1) / GT;  // float4 region loads per thread and chunk
+    // float4 region loads per thread and chunk: the largest R x C4 (72 for 32-tile blocks, 136 for
+    // 64-tile ones) over the GT / 16 threads of a channel
+    constexpr int NL = ((T == 32 ? 72 : 136) + GT / 16 - 1) / (GT / 16);
     constexpr int SMEM = KS * (NSV * BUF + (ST ? 2 * RGN : 0));
     static_assert(8 * CO * T * KS <= SMEM, "Z slabs fit");
     __shared__ __attribute__((aligned(16))) uint32_t smem[SMEM];
@@ -290,41 +298,44 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     const int ry0 = 2 * (blk / a.bx) * a.tby - 1, rx0 = 2 * (blk % a.bx) * a.tbx - 4;
     float* sIn = reinterpret_cast<float*>(sG + NSV * BUF);
     float4 gr[ST ? NL : 1];
-    // this thread's region elements (channel in the chunk, in-plane offset, in-map) do not depend on
-    // the chunk: decomposed once (the runtime divisions by R C4 and C4 stay out of the loop)
-    // packed as (in-plane float offset << 4) | channel-in-chunk, -1 outside the map / region
+    // region loads: thread gtid stages channel gch = gtid / TPC of the chunk (one plane pointer per
+    // chunk) and its elements j = sub + TPC k of that channel's R x C4 float4 ([row][c4] order). The
+    // in-plane offset of element k (-1 outside the map or the region) does not depend on the chunk:
+    // decomposed once, out of the loop (runtime divisions by C4)
+    constexpr int TPC = GT / 16;
+    const int gch = gtid / TPC, sub = gtid % TPC;
     int g_code[ST ? NL : 1];
 #pragma unroll
     for (int k = 0; k < (ST ? NL : 0); ++k) {
-        const int idx = gtid + GT * k;
-        const int ch = idx / (R * C4), rem = idx - ch * (R * C4);
-        const int row = rem / C4, c4 = rem - row * C4;
+        const int j = sub + TPC * k;
+        const int row = j / C4, c4 = j - row * C4;
         const int y = ry0 + row, x = rx0 + 4 * c4;
-        const bool ok = idx < 16 * R * C4 && y >= 0 && y < a.h && x >= 0 && x < a.w;
-        g_code[k] = ok ? ((y * a.w + x) << 4) | ch : -1;
+        const bool ok = j < R * C4 && y >= 0 && y < a.h && x >= 0 && x < a.w;
+        g_code[k] = ok ? y * a.w + x : -1;
     }
     auto gload = [&](int chunk) {
+        const int c = chunk * 16 + gch;
+        // global address space: a plain pointer read from LDS would make these flat loads, which
+        // count against the LDS counter too and wait on it
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        typedef const __attribute__((address_space(1))) f4v* gptr;
+        const float* plane = planes[min(c, a.ci_pad - 1)];
+        const bool cok = c < a.ci;
 #pragma unroll
         for (int k = 0; k < (ST ? NL : 0); ++k) {
-            const int c = chunk * 16 + (g_code[k] & 15);
-            const bool ok = g_code[k] >= 0 && c < a.ci;
-            // global address space: a plain pointer read from LDS would make this a flat load, which
-            // counts against the LDS counter too and waits on it
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            const float* addr = ok ? planes[c] + (g_code[k] >> 4) : reinterpret_cast<const float*>(&g_zero16);
-            const f4v v = *(const __attribute__((address_space(1))) f4v*)addr;
+            const float* addr = cok && g_code[k] >= 0 ? plane + g_code[k] : reinterpret_cast<const float*>(&g_zero16);
+            const f4v v = *(gptr)addr;
             gr[k] = make_float4(v.x, v.y, v.z, v.w);
         }
     };
     auto sstore = [&](int slot) {
-        const int total = 16 * R * C4;
-        float4* dst = reinterpret_cast<float4*>(sIn + slot * RGN);
+        float4* dst = reinterpret_cast<float4*>(sIn + slot * RGN) + gch * ((R * RP + Region<T>::kPad) / 4);
 #pragma unroll
         for (int k = 0; k < (ST ? NL : 0); ++k) {
-            const int idx = gtid + GT * k;
+            const int j = sub + TPC * k;
             float4 v = gr[k];
             if (a.relu_in) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
-            if (idx < total) dst[idx] = v;  // [ch][row][c4]: idx is already that order
+            if (j < R * C4) dst[j] = v;  // [ch][row][c4] with the padded channel stride
         }
     };
     auto read_patches = [&](int slot) {  // this thread's PP channel pairs of tile t from sIn
@@ -334,7 +345,7 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
         for (int q = 0; q < PP; ++q)
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const float* b = base + (2 * (4 * (ph0 + q * PHR) + pl) + e) * R * RP;
+                const float* b = base + (2 * (4 * (ph0 + q * PHR) + pl) + e) * (R * RP + Region<T>::kPad);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -491,11 +502,11 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
     constexpr int T = 32, GT = 256;
     constexpr int BUF = 2 * 16 * 8 * T;
     constexpr int RGN = Region<T>::kMaxFloats;
-    constexpr int NL = (RGN / 4 + GT - 1) / GT;
+    constexpr int NL = (72 + 15) / 16;  // float4 region loads per thread (R C4 <= 72 over 16 threads)
     constexpr int CO = 32;
     __shared__ __attribute__((aligned(16))) uint32_t smem[BUF + 2 * RGN];
-    __shared__ const float* planes[kMaxCiPad];  // image 0's plane of each input channel
-    __shared__ int cstride[kMaxCiPad];           // floats from one image's plane to the next's
+    __shared__ const float* planes[kPersistCiPad];  // image 0's plane of each input channel
+    __shared__ int cstride[kPersistCiPad];           // floats from one image's plane to the next's
 
     const int tid = threadIdx.x, lane = tid & 63, rr = tid >> 6;
     const int pl = tid & 3, t = (tid >> 2) % T, ph0 = (tid >> 2) / T;  // one channel pair per thread
@@ -534,41 +545,44 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
     const int R = 2 * a.tby + 2, C4 = a.tbx / 2 + 2, RP = 4 * C4;
     const int bpi = a.bx * a.by;  // tile blocks per image
     float* sIn = reinterpret_cast<float*>(smem + BUF);
-    // block-independent part of this thread's region elements: (channel << 24) | (row << 12) | c4
+    // region elements as in conv_kernel: channel gch = tid / 16 of the chunk, elements j = sub + 16 k
+    // of its R x C4 float4; block-independent part (row << 12) | c4, -1 past the region
+    const int gch = tid >> 4, sub = tid & 15;
     int g_pos[NL];
 #pragma unroll
     for (int k = 0; k < NL; ++k) {
-        const int idx = tid + GT * k;
-        const int ch = idx / (R * C4), rem = idx - ch * (R * C4);
-        const int row = rem / C4, c4 = rem - row * C4;
-        g_pos[k] = idx < 16 * R * C4 ? (ch << 24) | (row << 12) | c4 : -1;
+        const int j = sub + 16 * k;
+        const int row = j / C4, c4 = j - row * C4;
+        g_pos[k] = j < R * C4 ? (row << 12) | c4 : -1;
     }
     float4 gr[NL];
     // region loads of chunk `chunk` of the workgroup's j-th tile block
-    auto gload = [&](int j, int chunk) {
-        const int bl = blockIdx.x + j * gridDim.x;
+    auto gload = [&](int jb, int chunk) {
+        const int bl = blockIdx.x + jb * gridDim.x;
         const int img = bl / bpi, blk = bl - img * bpi;
         const int ry0 = 2 * (blk / a.bx) * a.tby - 1, rx0 = 2 * (blk % a.bx) * a.tbx - 4;
+        const int c = chunk * 16 + gch;
+        const bool cok = c < a.ci;
+        const int cc = min(c, a.ci_pad - 1);
+        const float* plane = planes[cc] + (size_t)img * cstride[cc];
+        typedef float f4v __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int k = 0; k < NL; ++k) {
             const int code = g_pos[k];
-            const int c = chunk * 16 + ((code >> 24) & 15);
             const int y = ry0 + ((code >> 12) & 4095), x = rx0 + 4 * (code & 4095);
-            const bool ok = code >= 0 && c < a.ci && y >= 0 && y < a.h && x >= 0 && x < a.w;
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            const float* addr = ok ? planes[c] + (size_t)img * cstride[c] + (size_t)y * a.w + x
-                                   : reinterpret_cast<const float*>(&g_zero16);
+            const bool ok = cok && code >= 0 && y >= 0 && y < a.h && x >= 0 && x < a.w;
+            const float* addr = ok ? plane + (size_t)y * a.w + x : reinterpret_cast<const float*>(&g_zero16);
             const f4v v = *(const __attribute__((address_space(1))) f4v*)addr;
             gr[k] = make_float4(v.x, v.y, v.z, v.w);
         }
     };
     auto sstore = [&](int slot) {
-        float4* dst = reinterpret_cast<float4*>(sIn + slot * RGN);
+        float4* dst = reinterpret_cast<float4*>(sIn + slot * RGN) + gch * ((R * RP + Region<T>::kPad) / 4);
 #pragma unroll
         for (int k = 0; k < NL; ++k) {
             float4 v = gr[k];
             if (a.relu_in) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
-            if (g_pos[k] >= 0) dst[tid + GT * k] = v;
+            if (g_pos[k] >= 0) dst[sub + 16 * k] = v;
         }
     };
     float d[2][16];
@@ -577,7 +591,7 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
         const float* base = sIn + slot * RGN + 2 * tyl * RP + 2 * txl + 3;
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-            const float* b = base + (2 * (4 * ph0 + pl) + e) * R * RP;
+            const float* b = base + (2 * (4 * ph0 + pl) + e) * (R * RP + Region<T>::kPad);
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -705,16 +719,19 @@ static int pick_form(int n, int th, int tw, int co) {
         const int f = atoi(e);
         if (f >= 1 && f <= 5) return f;
     }
-    // measured per census shape (tools/bench_wino3.py, profiles/r4/bench_wino3_*.log): the 64 x 64
-    // form from 128 workgroups up (2 x 128 -> 64 at 144^2: 53.9 vs 69.6 us for 32 x 32), two
-    // k-groups where 32 x 32 workgroups would leave CUs idle, the 32 x 64 form never (32 -> 32 at
-    // 256^2: 37.6 vs 30.1 us for 32 x 32)
+    // measured per census shape (tools/bench_wino3.py, profiles/r4/g9/bench_wino3.log): the 64 x 64
+    // form above 128 workgroups (2 x 128 -> 64 at 144^2, 162 of them: 34.9 vs 47.8 us for 32 x 32;
+    // at 128 -- 64 -> 64 at 128^2, 128 -> 256 at 64^2 -- half the CUs idle and 32 x 32 wins, 17.3
+    // vs 20.7 us), the persistent form for one 32-channel output block over more than 256 blocks
+    // (32 -> 32 at 256^2: 24.0 vs 26.9 us), two k-groups where 32 x 32 workgroups would leave CUs
+    // idle, the 32 x 64 form never
     const long tiles = (long)n * th * tw;
     const int cob32 = (co + 31) / 32;
     const long wg64 = (tiles + 63) / 64 * ((co + 63) / 64);
     const long wg32 = (tiles + 31) / 32 * cob32;
-    if (co > 32 && wg64 >= 128) return 4;
-    return wg32 <= 256 ? 2 : 1;
+    if (co > 32 && wg64 > 128) return 4;
+    if (wg32 <= 256) return 2;
+    return co <= 32 ? 5 : 1;
 }
 
 template <int CB, int NB, int KS>
@@ -776,6 +793,8 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const
         }
     }
     a.tby = ttiles / a.tbx;
+    // the staged region loads assume R x C4 <= 72 (32-tile blocks) / 136 (64-tile blocks) float4 rows
+    if ((2 * a.tby + 2) * (a.tbx / 2 + 2) > (ttiles == 32 ? 72 : 136)) return TSPLAT_EINVAL;
     a.bx = (a.tw + a.tbx - 1) / a.tbx;
     a.by = (a.th + a.tby - 1) / a.tby;
     const int blocks = n * a.bx * a.by;
@@ -783,7 +802,7 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const
     bool staged = w % 4 == 0;
     for (int q = 0; q < nsrc; ++q) staged = staged && (reinterpret_cast<uintptr_t>(srcs[q]) & 15) == 0;
     if (const char* e = getenv("TSPLAT_WINO3_STAGE")) staged = staged && atoi(e) != 0;
-    if (form == 5 && !staged) form = 1;
+    if (form == 5 && (!staged || a.ci_pad > wino3::kPersistCiPad)) form = 1;
     hipStream_t stream = (hipStream_t)stream_;
     const prof::ExtEvents ev = prof::ext_events(prof::kWinoConv);
     if (form == 5) {
