@@ -44,6 +44,21 @@ constexpr int kPersistCiPad = 512;  // the persistent form's plane table (keeps 
 // instead of an exec-masked branch with zero-initialised destinations per load)
 __device__ uint4 g_zero16 = {0u, 0u, 0u, 0u};
 
+#ifndef TSPLAT_W3_STAMP
+#define TSPLAT_W3_STAMP 0  // diagnostic builds only (tools/build_stamp_w3.sh): per-workgroup phase clocks
+#endif
+#if TSPLAT_W3_STAMP
+// [workgroup][8] 100-MHz wall clock at the phase boundaries, written by thread 0 (vector stores)
+__device__ unsigned long long* g_w3_stamps = nullptr;
+#define W3_STAMP(slot)                                                                                  \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && g_w3_stamps)                                                            \
+            g_w3_stamps[(size_t)(blockIdx.y * gridDim.x + blockIdx.x) * 8 + (slot)] = wall_clock64();   \
+    } while (0)
+#else
+#define W3_STAMP(slot) do {} while (0)
+#endif
+
 struct Args {
     const float* src[kMaxSrc];
     int cs[kMaxSrc];
@@ -227,6 +242,7 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t smem[SMEM];
     __shared__ const float* planes[kMaxCiPad];
 
+    W3_STAMP(0);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int kg = wid / (4 * CB), wg = wid % (4 * CB);
     const int hh = wg >> 2, rr = wg & 3;
@@ -389,6 +405,7 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
         if (iters > 1) gload(kg + KS);
         load_a(kg, 0, 4);
         __syncthreads();
+        W3_STAMP(1);
         for (int it = 0; it < iters; ++it) {
             const int ch = kg + it * KS;
             const bool more = it + 1 < iters;
@@ -428,6 +445,7 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     }
     }
     __syncthreads();  // all MFMAs' LDS reads done: smem becomes Z[kg][r][j][co CO][tile T]
+    W3_STAMP(2);
     float* zs = reinterpret_cast<float*>(smem) + kg * (8 * CO * T);
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
@@ -489,6 +507,7 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
             }
         }
     }
+    W3_STAMP(3);
 }
 
 // Persistent 32 co x 32 tile form for large maps with few input channels (the refine U-Net's
@@ -603,12 +622,14 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
     const int nmine = (nblocks - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
     const int G = nmine * a.nchunk;  // flat (block, chunk) steps of this workgroup
     if (G <= 0) return;              // uniform: no barrier below is reached by part of the group
+    W3_STAMP(0);
     __syncthreads();                 // planes / cstride
     gload(0, 0);
     sstore(0);
     if (G > 1) gload(1 / a.nchunk, 1 % a.nchunk);
     load_a(0);
     __syncthreads();
+    W3_STAMP(1);
     int j = 0, c = 0;
     for (int g = 0; g < G; ++g) {
         if (g + 1 < G) sstore((g + 1) & 1);
@@ -632,6 +653,7 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
         __syncthreads();  // every wave is done with sV(g) and with sIn slot g & 1
         if (++c < a.nchunk) continue;
         // block j done: Z = M A through LDS (aliasing sV), then Y = A^T Z + bias (+ act, + residuals)
+        if (j == 0) W3_STAMP(2);
         float* zs = reinterpret_cast<float*>(smem);
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -682,15 +704,25 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
             }
         }
         __syncthreads();  // Z read before the next block's transform overwrites it
+        if (j == 0) W3_STAMP(3);
         c = 0;
         ++j;
     }
+    W3_STAMP(4);
 }
 
 }  // namespace wino3
 }  // namespace tsplat
 
 using namespace tsplat;
+
+#if TSPLAT_W3_STAMP
+// diagnostic builds only: buffer of [workgroups][8] uint64 the next launches stamp (null = off)
+extern "C" int tsplat_wino3_stamps(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(wino3::g_w3_stamps), &buf, sizeof(buf)) == hipSuccess ? TSPLAT_OK
+                                                                                             : TSPLAT_EINVAL;
+}
+#endif
 
 static int wino3_ci_pad(int ci) { return (ci + 15) / 16 * 16; }
 static int wino3_cobs(int co) { return (co + 63) / 64 * 2; }
