@@ -23,3 +23,11 @@ python3 tools/prof_steps.py $OUT/prof_c2_x3/run_kernel_trace.csv > $OUT/c2_x3_pe
 head -30 $OUT/c2_x3_per_step.txt | cut -c1-150
 TSPLAT_LIB=tools/_bin/w3stamp.so timeout -k 10 120 python -u tools/w3_stamps.py > $OUT/w3_stamps.log 2>&1 || { tail -5 $OUT/w3_stamps.log; exit 6; }
 grep -v amdgpu $OUT/w3_stamps.log
+for m in plain xf32 tf32; do
+  case $m in
+    plain) timeout -k 10 120 python -u tools/bench_xf32.py > $OUT/xf32_$m.log 2>&1 ;;
+    xf32) HIPBLASLT_OVERRIDE_COMPUTE_TYPE_XF32=1 timeout -k 10 120 python -u tools/bench_xf32.py > $OUT/xf32_$m.log 2>&1 ;;
+    tf32) timeout -k 10 120 python -u tools/bench_xf32.py --allow-tf32 > $OUT/xf32_$m.log 2>&1 ;;
+  esac || { tail -5 $OUT/xf32_$m.log; exit 7; }
+  grep -v amdgpu $OUT/xf32_$m.log
+done

@@ -576,10 +576,17 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
     }
     float4 gr[NL];
     // region loads of chunk `chunk` of the workgroup's j-th tile block
+    // origin of the tile block the loads are for, recomputed (scalar divisions) only when it changes
+    int o_jb = -1, img = 0, ry0 = 0, rx0 = 0;
     auto gload = [&](int jb, int chunk) {
-        const int bl = blockIdx.x + jb * gridDim.x;
-        const int img = bl / bpi, blk = bl - img * bpi;
-        const int ry0 = 2 * (blk / a.bx) * a.tby - 1, rx0 = 2 * (blk % a.bx) * a.tbx - 4;
+        if (jb != o_jb) {  // uniform
+            const int bl = blockIdx.x + jb * gridDim.x;
+            img = bl / bpi;
+            const int blk = bl - img * bpi;
+            ry0 = 2 * (blk / a.bx) * a.tby - 1;
+            rx0 = 2 * (blk % a.bx) * a.tbx - 4;
+            o_jb = jb;
+        }
         const int c = chunk * 16 + gch;
         const bool cok = c < a.ci;
         const int cc = min(c, a.ci_pad - 1);
@@ -631,10 +638,17 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
     __syncthreads();
     W3_STAMP(1);
     int j = 0, c = 0;
+    int nj = 2 / a.nchunk, nc = 2 % a.nchunk;  // (block, chunk) of step g + 2
     for (int g = 0; g < G; ++g) {
         if (g + 1 < G) sstore((g + 1) & 1);
         read_transform(g & 1);
-        if (g + 2 < G) gload((g + 2) / a.nchunk, (g + 2) % a.nchunk);
+        if (g + 2 < G) {
+            gload(nj, nc);
+            if (++nc == a.nchunk) {
+                nc = 0;
+                ++nj;
+            }
+        }
         __syncthreads();  // sV(g) complete
         const uint32_t* bb = smem + ((lane >> 5) * T + (lane & 31)) * 4;
 #pragma unroll
