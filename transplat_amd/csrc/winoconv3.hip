@@ -224,7 +224,7 @@ struct Region {
 };
 
 template <int CB, int NB, int KS, bool ST>
-__global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
+__global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Args a) {
     constexpr int T = 32 * NB;                 // tiles per workgroup
     constexpr int GT = 256 * CB;               // threads per k-group
     constexpr int PHR = GT / (4 * T);          // pair halves (4 pairs each) covered per pass
@@ -271,8 +271,11 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     const uint4* ub = a.u + ((size_t)(4 * rr) * a.cobs + (co_ok ? cob : 0)) * a.nchunk * 128 + lane;
     const size_t xi_stride = (size_t)a.cobs * a.nchunk * 128;
     uint4 af[4][2];
+    // unconditional loads (a chunk past the last reads the last one's weights again: its B operand is
+    // all zeros): a branch around them would make every later wait a vmcnt(0), draining the region
+    // prefetch before the MFMAs
     auto load_a = [&](int chunk, int s0, int s1) {
-        const bool ok = co_ok && chunk < a.nchunk;
+        const size_t cofs = (size_t)min(chunk, a.nchunk - 1) * 128;
 #pragma unroll
         for (int s = s0; s < s1; ++s)
 #pragma unroll
@@ -280,8 +283,7 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
 #if TSPLAT_W3_ABL == 3  // diagnostic build: no A loads
                 af[s][hl] = make_uint4(chunk, s, hl, lane);
 #else
-                const uint4* src = ok ? ub + s * xi_stride + (size_t)chunk * 128 + hl * 64 : &g_zero16;
-                af[s][hl] = *src;
+                af[s][hl] = ub[s * xi_stride + cofs + hl * 64];
 #endif
             }
     };
@@ -313,7 +315,10 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     const int R = 2 * a.tby + 2, C4 = a.tbx / 2 + 2, RP = 4 * C4;
     const int ry0 = 2 * (blk / a.bx) * a.tby - 1, rx0 = 2 * (blk % a.bx) * a.tbx - 4;
     float* sIn = reinterpret_cast<float*>(sG + NSV * BUF);
-    float4 gr[ST ? NL : 1];
+    // DS: two register sets for the region loads (the 32-co forms have the registers): the loads of
+    // chunk it + 3 are issued at iteration it and stored at it + 2, a whole iteration in flight
+    constexpr bool DS = ST && CB == 1 && NB == 1;
+    float4 gr[DS ? 2 : 1][ST ? NL : 1];
     // region loads: thread gtid stages channel gch = gtid / TPC of the chunk (one plane pointer per
     // chunk) and its elements j = sub + TPC k of that channel's R x C4 float4 ([row][c4] order). The
     // in-plane offset of element k (-1 outside the map or the region) does not depend on the chunk:
@@ -329,7 +334,8 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
         const bool ok = j < R * C4 && y >= 0 && y < a.h && x >= 0 && x < a.w;
         g_code[k] = ok ? y * a.w + x : -1;
     }
-    auto gload = [&](int chunk) {
+    // (S: register set, a compile-time constant -- std::integral_constant -- so the arrays stay in VGPRs)
+    auto gload = [&](int chunk, auto S) {
         const int c = chunk * 16 + gch;
         // global address space: a plain pointer read from LDS would make these flat loads, which
         // count against the LDS counter too and wait on it
@@ -341,15 +347,15 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
         for (int k = 0; k < (ST ? NL : 0); ++k) {
             const float* addr = cok && g_code[k] >= 0 ? plane + g_code[k] : reinterpret_cast<const float*>(&g_zero16);
             const f4v v = *(gptr)addr;
-            gr[k] = make_float4(v.x, v.y, v.z, v.w);
+            gr[decltype(S)::value][k] = make_float4(v.x, v.y, v.z, v.w);
         }
     };
-    auto sstore = [&](int slot) {
+    auto sstore = [&](int slot, auto S) {
         float4* dst = reinterpret_cast<float4*>(sIn + slot * RGN) + gch * ((R * RP + Region<T>::kPad) / 4);
 #pragma unroll
         for (int k = 0; k < (ST ? NL : 0); ++k) {
             const int j = sub + TPC * k;
-            float4 v = gr[k];
+            float4 v = gr[decltype(S)::value][k];
             if (a.relu_in) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
             if (j < R * C4) dst[j] = v;  // [ch][row][c4] with the padded channel stride
         }
@@ -397,29 +403,42 @@ __global__ void __launch_bounds__(256 * CB * KS) conv_kernel(Args a) {
     // k-group kg takes chunks kg, kg + KS, ...; every group runs the same iteration count (a chunk
     // past the last one is all zeros) so the groups meet at every barrier
     const int iters = (a.nchunk + KS - 1) / KS;
+    const std::integral_constant<int, 0> I0;
+    const std::integral_constant<int, DS ? 1 : 0> I1;
     if constexpr (ST) {
-        // single sV: store region(it + 1) | transform(it) | loads of region(it + 2) | barrier |
-        // MFMAs(it) | barrier
-        gload(kg);
-        sstore(0);
-        if (iters > 1) gload(kg + KS);
+        // single sV: store region(it + 1) | transform(it) | loads of region(it + 3) (DS) or it + 2 |
+        // barrier | MFMAs(it) | barrier. Region r lives in register set r & 1 (DS) or set 0.
+        gload(kg, I0);
+        sstore(0, I0);
+        gload(kg + KS, I1);
+        if (DS) gload(kg + 2 * KS, I0);
         load_a(kg, 0, 4);
         __syncthreads();
         W3_STAMP(1);
-        for (int it = 0; it < iters; ++it) {
+        // S = the register set of region it + 1
+        auto step = [&](int it, auto S) {
             const int ch = kg + it * KS;
             const bool more = it + 1 < iters;
-            // the region of chunk it + 1 (its loads flew during the last MFMA phase) goes to LDS first,
-            // so its registers are free again during the transform; slot (it + 1) & 1 was last read
-            // by read_patches(it - 1), before the last barrier
-            if (more) sstore((it + 1) & 1);
+            // the region of chunk it + 1 (its loads flew during the last iteration(s)) goes to LDS
+            // first, so its registers are free again during the transform; slot (it + 1) & 1 was last
+            // read by read_patches(it - 1), before the last barrier
+            if (more) sstore((it + 1) & 1, S);
             read_patches(it & 1);
             transform(sG);
-            if (more && it + 2 < iters) gload(ch + 2 * KS);
+            // unconditional (past the last chunk: zero-page loads), see load_a
+            gload(ch + (DS ? 3 : 2) * KS, S);
             __syncthreads();  // sV(it) complete
             mfma(sG, 0, 4);
-            if (more) load_a(ch + KS, 0, 4);
+            load_a(ch + KS, 0, 4);
             __syncthreads();  // every wave is done with sV(it) and with sIn slot it & 1
+        };
+        if constexpr (DS) {
+            for (int it = 0; it < iters; it += 2) {
+                step(it, I1);
+                if (it + 1 < iters) step(it + 1, I0);
+            }
+        } else {
+            for (int it = 0; it < iters; ++it) step(it, I0);
         }
     } else {
     load_patches(kg);
@@ -546,6 +565,14 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
     }
 
     const int cob = a.cob_base + blockIdx.y;
+    // the epilogue's bias values (output channel cob * 32 + (tid + GT i) / T), loaded once: a load in
+    // the per-block epilogue would wait vmcnt(0), draining the next block's region loads
+    float bias_r[CO * T / GT];
+#pragma unroll
+    for (int i = 0; i < CO * T / GT; ++i) {
+        const int o = cob * 32 + (tid + GT * i) / T;
+        bias_r[i] = a.bias && o < a.co ? a.bias[o] : 0.0f;
+    }
     const uint4* ub = a.u + ((size_t)(4 * rr) * a.cobs + cob) * a.nchunk * 128 + lane;
     const size_t xi_stride = (size_t)a.cobs * a.nchunk * 128;
     uint4 af[4][2];
@@ -574,11 +601,14 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
         const int row = j / C4, c4 = j - row * C4;
         g_pos[k] = j < R * C4 ? (row << 12) | c4 : -1;
     }
-    float4 gr[NL];
-    // region loads of chunk `chunk` of the workgroup's j-th tile block
-    // origin of the tile block the loads are for, recomputed (scalar divisions) only when it changes
+    // two register sets: the region of step g + 3 is loaded at step g and stored at step g + 2
+    float4 gr[2][NL];
+    // region loads of chunk `chunk` of the workgroup's jb-th tile block; origin of the tile block the
+    // loads are for, recomputed (scalar divisions) only when it changes
     int o_jb = -1, img = 0, ry0 = 0, rx0 = 0;
-    auto gload = [&](int jb, int chunk) {
+    // (valid: a step of this workgroup; past its last one the loads read the zero page -- they stay
+    // unconditional, see conv_kernel's load_a. S: register set, a compile-time constant)
+    auto gload = [&](int jb, int chunk, bool valid, auto S) {
         if (jb != o_jb) {  // uniform
             const int bl = blockIdx.x + jb * gridDim.x;
             img = bl / bpi;
@@ -588,7 +618,7 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
             o_jb = jb;
         }
         const int c = chunk * 16 + gch;
-        const bool cok = c < a.ci;
+        const bool cok = valid && c < a.ci;
         const int cc = min(c, a.ci_pad - 1);
         const float* plane = planes[cc] + (size_t)img * cstride[cc];
         typedef float f4v __attribute__((ext_vector_type(4)));
@@ -599,14 +629,14 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
             const bool ok = cok && code >= 0 && y >= 0 && y < a.h && x >= 0 && x < a.w;
             const float* addr = ok ? plane + (size_t)y * a.w + x : reinterpret_cast<const float*>(&g_zero16);
             const f4v v = *(const __attribute__((address_space(1))) f4v*)addr;
-            gr[k] = make_float4(v.x, v.y, v.z, v.w);
+            gr[decltype(S)::value][k] = make_float4(v.x, v.y, v.z, v.w);
         }
     };
-    auto sstore = [&](int slot) {
+    auto sstore = [&](int slot, auto S) {
         float4* dst = reinterpret_cast<float4*>(sIn + slot * RGN) + gch * ((R * RP + Region<T>::kPad) / 4);
 #pragma unroll
         for (int k = 0; k < NL; ++k) {
-            float4 v = gr[k];
+            float4 v = gr[decltype(S)::value][k];
             if (a.relu_in) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
             if (g_pos[k] >= 0) dst[sub + 16 * k] = v;
         }
@@ -631,23 +661,25 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
     if (G <= 0) return;              // uniform: no barrier below is reached by part of the group
     W3_STAMP(0);
     __syncthreads();                 // planes / cstride
-    gload(0, 0);
-    sstore(0);
-    if (G > 1) gload(1 / a.nchunk, 1 % a.nchunk);
+    const std::integral_constant<int, 0> I0;
+    const std::integral_constant<int, 1> I1;
+    gload(0, 0, true, I0);
+    sstore(0, I0);
+    gload(1 / a.nchunk, 1 % a.nchunk, G > 1, I1);
+    gload(2 / a.nchunk, 2 % a.nchunk, G > 2, I0);
     load_a(0);
     __syncthreads();
     W3_STAMP(1);
     int j = 0, c = 0;
-    int nj = 2 / a.nchunk, nc = 2 % a.nchunk;  // (block, chunk) of step g + 2
-    for (int g = 0; g < G; ++g) {
-        if (g + 1 < G) sstore((g + 1) & 1);
+    int nj = 3 / a.nchunk, nc = 3 % a.nchunk;  // (block, chunk) of step g + 3
+    // S = the register set of step g + 1's region
+    auto step = [&](int g, auto S) {
+        if (g + 1 < G) sstore((g + 1) & 1, S);
         read_transform(g & 1);
-        if (g + 2 < G) {
-            gload(nj, nc);
-            if (++nc == a.nchunk) {
-                nc = 0;
-                ++nj;
-            }
+        gload(nj, nc, g + 3 < G, S);
+        if (++nc == a.nchunk) {
+            nc = 0;
+            ++nj;
         }
         __syncthreads();  // sV(g) complete
         const uint32_t* bb = smem + ((lane >> 5) * T + (lane & 31)) * 4;
@@ -663,9 +695,9 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
             acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[s], 0, 0, 0);
             acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[s], 0, 0, 0);
         }
-        if (g + 1 < G) load_a((c + 1) % a.nchunk);
+        load_a(c + 1 < a.nchunk ? c + 1 : 0);  // unconditional (the last step's reload is unused)
         __syncthreads();  // every wave is done with sV(g) and with sIn slot g & 1
-        if (++c < a.nchunk) continue;
+        if (++c < a.nchunk) return;
         // block j done: Z = M A through LDS (aliasing sV), then Y = A^T Z + bias (+ act, + residuals)
         if (j == 0) W3_STAMP(2);
         float* zs = reinterpret_cast<float*>(smem);
@@ -680,12 +712,14 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
         __syncthreads();
         const int bl = blockIdx.x + j * gridDim.x;
         const int img = bl / bpi, blk = bl - img * bpi;
-        for (int pidx = tid; pidx < CO * T; pidx += GT) {
+#pragma unroll
+        for (int i = 0; i < CO * T / GT; ++i) {
+            const int pidx = tid + GT * i;
             const int col = pidx / T, t2 = pidx % T;
             const int o = cob * 32 + col;
             const int oty = (blk / a.bx) * a.tby + t2 / a.tbx, otx = (blk % a.bx) * a.tbx + t2 % a.tbx;
             if (o >= a.co || oty >= a.th || otx >= a.tw) continue;
-            const float bv = a.bias ? a.bias[o] : 0.0f;
+            const float bv = bias_r[i];
             float z[4][2];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
@@ -717,10 +751,18 @@ __global__ void __launch_bounds__(256, 2) conv_persist_kernel(Args a, int nblock
                 }
             }
         }
-        __syncthreads();  // Z read before the next block's transform overwrites it
+        // Z read before the next block's transform overwrites it: LDS order only, a raw barrier (a
+        // __syncthreads fence would wait for this block's output stores, vmcnt(0), and with them for
+        // the next block's region loads already in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
         if (j == 0) W3_STAMP(3);
         c = 0;
         ++j;
+    };
+    for (int g = 0; g < G; g += 2) {
+        step(g, I1);
+        if (g + 1 < G) step(g + 1, I0);
     }
     W3_STAMP(4);
 }

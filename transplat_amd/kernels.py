@@ -698,22 +698,31 @@ _DENSE = "fp32"
 _DENSE_MODES = ("fp32", "bf16x3")
 
 
+# bf16x3 mode's library fp32 GEMMs (F.linear / matmul on hipBLASLt): with TSPLAT_XF32=1 they run
+# with torch's allow_tf32, which on gfx950 selects hipBLASLt's emulated-xf32 kernels (fp32 in / out,
+# bf16 MFMA; tools/bench_xf32.py measures their error next to the split kernels')
+_XF32 = os.environ.get("TSPLAT_XF32", "0") == "1"
+
+
 class dense_precision:
     """Context manager: the dense-layer precision mode inside the block (see _DENSE)."""
 
     def __init__(self, mode: str):
         if mode not in _DENSE_MODES:
             raise ValueError(f"dense precision {mode!r} not in {_DENSE_MODES}")
-        self.mode, self.prev = mode, None
+        self.mode, self.prev, self.prev_tf32 = mode, None, None
 
     def __enter__(self):
         global _DENSE
         self.prev, _DENSE = _DENSE, self.mode
+        self.prev_tf32 = torch.backends.cuda.matmul.allow_tf32
+        torch.backends.cuda.matmul.allow_tf32 = _XF32 and self.mode == "bf16x3"
         return self
 
     def __exit__(self, *exc):
         global _DENSE
         _DENSE = self.prev
+        torch.backends.cuda.matmul.allow_tf32 = self.prev_tf32
         return False
 
 
