@@ -339,7 +339,8 @@ def test_conv3x3_wino_bf16x3_concat_and_production_size(device):
 @pytest.mark.gpu
 @pytest.mark.parametrize("m,k,n,bias,act", [(650, 768, 2304, True, "none"), (650, 768, 3072, True, "gelu"),
                                            (650, 3072, 768, True, "none"), (100, 256, 128, False, "none"),
-                                           (8192, 256, 1024, False, "none"), (33, 64, 64, True, "gelu")])
+                                           (8192, 256, 1024, False, "none"), (33, 64, 64, True, "gelu"),
+                                           (20, 64, 128, True, "gelu")])
 def test_linear_bf16x3_kernel(device, m, k, n, bias, act):
     """tsplat_linear_bf16x3_fwd (DINOv2's linears in the bf16x3 dense mode: x split while staged, W
     packed [hi | lo | hi]) against float64 F.linear (+ exact GELU): within 2e-5 of max |y| and at

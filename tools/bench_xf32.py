@@ -54,9 +54,19 @@ with torch.no_grad():
         t = timeit(lambda: F.linear(x, w, b))
         e = ((F.linear(x, w, b).double() - ref).abs().max() / sc).item()
         etf = (((tf32(x).double() @ tf32(w).double().t() + b.double()) - ref).abs().max() / sc).item()
+        # the same product without the bias epilogue: mm, and a 3-D matmul (bmm path)
+        ref0 = x.double() @ w.double().t()
+        sc0 = ref0.abs().max().item()
+        wt = w.t()
+        t_mm = timeit(lambda: torch.mm(x, wt))
+        e_mm = ((torch.mm(x, wt).double() - ref0).abs().max() / sc0).item()
+        x3 = x.unsqueeze(0)
+        t_bmm = timeit(lambda: torch.matmul(x3, wt))
+        e_bmm = ((torch.matmul(x3, wt)[0].double() - ref0).abs().max() / sc0).item()
         tot += t * (12 if name.startswith("dino") else 0)
-        print(f"{name:10s} M={m:5d} K={k:5d} N={n:5d}: {t:7.1f} us ({2.0 * m * k * n / t / 1e6:6.1f} TF)  "
-              f"err {e:.1e}  (tf32-emul {etf:.1e})", flush=True)
+        print(f"{name:10s} M={m:5d} K={k:5d} N={n:5d}: linear {t:6.1f} us ({2.0 * m * k * n / t / 1e6:6.1f} TF) "
+              f"err {e:.1e} | mm {t_mm:6.1f} us err {e_mm:.1e} | matmul3d {t_bmm:6.1f} us err {e_bmm:.1e} "
+              f"(tf32-emul {etf:.1e})", flush=True)
     a = torch.randn(2, 4096, 128, device=dev, generator=g)
     v = torch.randn(2, 4096, 128, device=dev, generator=g)
     ref = a.double() @ v.double().transpose(1, 2)

@@ -827,7 +827,7 @@ _LIN3_MIN_FLOP = float(os.environ.get("TSPLAT_LIN3_MIN_FLOP", "2e8"))
 def linear_ok(x, weight) -> bool:
     """True when linear_forward takes the bf16x3 kernel for F.linear(x, weight) in the current mode."""
     return (_LIN3 and _DENSE == "bf16x3" and x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32
-            and not torch.is_autocast_enabled("cuda") and weight.shape[0] % 64 == 0 and x.shape[-1] % 32 == 0
+            and not torch.is_autocast_enabled("cuda") and weight.shape[0] % 128 == 0 and x.shape[-1] % 64 == 0
             and 2.0 * x.numel() * weight.shape[0] >= _LIN3_MIN_FLOP)
 
 
