@@ -105,7 +105,23 @@ def calculate_grid(intr, pose, disp, h: int, w: int):
 
 def bilinear_zero(img, x, y):
     """Sample img [HW... as H, W, C] at pixel coords (x, y) with zero padding (mmcv MSDA /
-    grid_sample(align_corners=False) after loc * size - 0.5). x, y: [...] -> [..., C]."""
+    grid_sample(align_corners=False) after loc * size - 0.5). x, y: [...] -> [..., C].
+
+    Runs as F.grid_sample (bilinear, zeros, align_corners=False) -- the operator the reference's own
+    CPU path calls for these samplings (mmcv's pytorch MSDA fallback and UVCoarseAttention) -- on
+    grid = (pixel + 0.5) / size * 2 - 1; `bilinear_zero_corners` is the explicit four-corner form
+    it is checked against (tests/test_encoder_ops.py)."""
+    import torch.nn.functional as F
+
+    hh, ww, c = img.shape
+    grid = torch.stack(((x + 0.5) * (2.0 / ww) - 1.0, (y + 0.5) * (2.0 / hh) - 1.0), -1).reshape(1, -1, 1, 2)
+    out = F.grid_sample(img.permute(2, 0, 1).unsqueeze(0), grid.to(img.dtype), mode="bilinear",
+                        padding_mode="zeros", align_corners=False)  # [1, C, N, 1]
+    return out[0, :, :, 0].t().reshape(*x.shape, c)
+
+
+def bilinear_zero_corners(img, x, y):
+    """bilinear_zero written out: the four corners' weights and zero padding per sample."""
     hh, ww, c = img.shape
     x0 = torch.floor(x)
     y0 = torch.floor(y)

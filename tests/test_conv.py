@@ -362,6 +362,32 @@ def test_linear_bf16x3_kernel(device, m, k, n, bias, act):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("m,k,n,bias,act", [(650, 768, 2304, True, "none"), (650, 768, 3072, True, "gelu"),
+                                           (8192, 256, 1024, True, "none"), (8192, 128, 512, False, "none")])
+def test_linear_xf32_library_path(device, m, k, n, bias, act):
+    """kernels.linear_xf32 (bf16x3 mode's library linears: hipBLASLt's emulated-xf32 GEMM under
+    allow_tf32, then bias (+ exact GELU) in one pass) against float64: within 2e-5 of max |y| and at
+    most 1/8 of the TF32-operand error -- the same bar as the split kernels; the shapes are the ones
+    linear_xf32_ok admits (DINOv2 qkv / fc1, the transformer MLP input GEMMs)."""
+    from transplat_amd import kernels as K
+
+    x = seeded((m, k), 91)
+    w = seeded((n, k), 92) / k ** 0.5
+    b = seeded((n,), 93) if bias else None
+    fn = torch.nn.functional.gelu if act == "gelu" else (lambda t: t)
+    ref = fn(torch.nn.functional.linear(x.double(), w.double(), b.double() if bias else None))
+    ref_tf = fn(torch.nn.functional.linear(tf32_round(x).double(), tf32_round(w).double(), b.double() if bias else None))
+    with K.dense_precision("bf16x3"):
+        assert K.linear_xf32_ok(x.to(device), w.to(device))
+        out = K.linear_xf32(x.to(device), w.to(device), b.to(device) if bias else None, act=act).cpu().double()
+    assert not torch.backends.cuda.matmul.allow_tf32  # restored
+    scale = ref.abs().max().item()
+    e3, etf = (out - ref).abs().max().item() / scale, (ref_tf - ref).abs().max().item() / scale
+    print(f"linear xf32 {(m, k, n)} {act}: rel err {e3:.2e}, TF32 operands {etf:.2e}")
+    assert e3 < 2e-5 and e3 <= etf / 8, (e3, etf)
+
+
+@pytest.mark.gpu
 def test_conv3x3_wino_weight_cache_tracks_updates(device):
     """The transformed-filter cache is keyed on the live weight tensor and its version: an in-place
     update of the weight is picked up."""

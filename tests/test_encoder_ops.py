@@ -684,3 +684,17 @@ def test_layer_norm128_kernel(device, y_bf16, out_bf16, res):
     assert out.dtype == (torch.bfloat16 if out_bf16 else torch.float32)
     tol = 8e-3 * ref.abs().max().item() if out_bf16 else 2e-5 * max(1.0, ref.abs().max().item())
     assert (out.float().cpu() - ref).abs().max().item() < tol
+
+
+def test_oracle_bilinear_zero_grid_sample_matches_corners():
+    """The oracle's sampler (F.grid_sample, the reference CPU path's operator) against the explicit
+    four-corner zero-padded bilinear form, including out-of-map and edge samples."""
+    g = torch.Generator().manual_seed(5)
+    img = torch.randn(16, 20, 8, generator=g)
+    x = torch.rand(300, 5, generator=g) * 26 - 3
+    y = torch.rand(300, 5, generator=g) * 22 - 3
+    a, b = E.bilinear_zero(img, x, y), E.bilinear_zero_corners(img, x, y)
+    assert a.shape == b.shape == (300, 5, 8)
+    # coordinates are rounded differently (grid_sample unnormalises (g + 1) W / 2 - 1 / 2): a few ulps
+    # of a coordinate times the map's slope
+    assert (a - b).abs().max().item() < 2e-5

@@ -831,11 +831,54 @@ def linear_ok(x, weight) -> bool:
             and 2.0 * x.numel() * weight.shape[0] >= _LIN3_MIN_FLOP)
 
 
+# Library fp32 GEMMs in bf16x3 mode: hipBLASLt's emulated-xf32 kernels (fp32 in / out on bf16 MFMA;
+# selected by torch's allow_tf32 for a plain matmul, not for addmm with a bias epilogue) measured
+# 4.4-5.6e-6 of max |y| against float64 -- the bf16x3 class, TF32-emulated operands 2.0-2.4e-4 -- and
+# faster where N >= 1024 or M >= 4096 (tools/bench_xf32.py, profiles/r4/g12/xf32_tf32.log: DINOv2
+# qkv 20.7 vs 29.6 us, fc1 25.7 vs 30.5, MVT fc1 22.8 vs 39.2; proj / fc2 at N = 768 slower: they stay
+# exact fp32). The bias (+ exact GELU) then runs as one pass (tsplat_bias_act_nhwc_fwd on [rows, N]).
+# TSPLAT_LINX=0 keeps every linear on exact fp32 F.linear in bf16x3 mode.
+_LINX = os.environ.get("TSPLAT_LINX", "1") == "1"
+
+
+def linear_xf32_ok(x, weight) -> bool:
+    """True when linear_forward takes linear_xf32 for F.linear(x, weight) in the current mode."""
+    if not (_LINX and _DENSE == "bf16x3" and x.is_cuda and x.dtype == torch.float32
+            and weight.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")):
+        return False
+    n, k = weight.shape
+    m = x.numel() // max(k, 1)
+    return n % 4 == 0 and ((n >= 1024 and m >= 512) or (m >= 4096 and n >= 512))
+
+
+def linear_xf32(x, weight, bias=None, act: str = "none"):
+    """act(x W^T + bias) with the product on hipBLASLt's emulated-xf32 kernels (see _LINX) and the
+    bias / activation in one tsplat_bias_act_nhwc_fwd pass."""
+    prev = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = True
+    try:
+        y = torch.matmul(x, weight.t())
+    finally:
+        torch.backends.cuda.matmul.allow_tf32 = prev
+    if bias is None and act == "none":
+        return y
+    y = y.contiguous()
+    bb = _f32(bias) if bias is not None else None
+    lib = _lib.load()
+    rc = lib.tsplat_bias_act_nhwc_fwd(_lib.ptr(y), _lib.ptr(bb), None, None, _lib.ptr(y), y.numel() // y.shape[-1],
+                                      y.shape[-1], _ACTS[act], _lib.stream_ptr(y.device))
+    _lib.check(rc, "tsplat_bias_act_nhwc_fwd")
+    return y
+
+
 def linear_forward(mod, x):
     """nn.Linear.forward (installed by install_linear_dispatch): in dense_precision("bf16x3") the
-    fp32 linears that linear_ok admits run as linear_bf16x3; everything else is F.linear."""
+    fp32 linears that linear_xf32_ok admits run as linear_xf32, those linear_ok admits as
+    linear_bf16x3; everything else is F.linear."""
     import torch.nn.functional as F
 
+    if linear_xf32_ok(x, mod.weight):
+        return linear_xf32(x, mod.weight, mod.bias)
     if linear_ok(x, mod.weight):
         return linear_bf16x3(x, mod.weight, mod.bias)
     return F.linear(x, mod.weight, mod.bias)

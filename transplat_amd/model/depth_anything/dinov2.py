@@ -53,9 +53,13 @@ class Mlp(nn.Module):
         self.fc2 = nn.Linear(hidden_features, out_features, bias=bias)
 
     def forward(self, x):
-        if type(self.act) is nn.GELU and self.act.approximate == "none" and kernels.linear_ok(x, self.fc1.weight):
-            # bf16x3 dense mode: fc1 + bias + exact GELU in one tsplat_linear_bf16x3_fwd launch
-            return self.fc2(kernels.linear_bf16x3(x, self.fc1.weight, self.fc1.bias, act="gelu"))
+        if type(self.act) is nn.GELU and self.act.approximate == "none":
+            # bf16x3 dense mode: fc1 on hipBLASLt's emulated-xf32 GEMM + bias + exact GELU in one pass
+            # (kernels.linear_xf32), or fc1 + bias + GELU in one tsplat_linear_bf16x3_fwd launch
+            if kernels.linear_xf32_ok(x, self.fc1.weight):
+                return self.fc2(kernels.linear_xf32(x, self.fc1.weight, self.fc1.bias, act="gelu"))
+            if kernels.linear_ok(x, self.fc1.weight):
+                return self.fc2(kernels.linear_bf16x3(x, self.fc1.weight, self.fc1.bias, act="gelu"))
         return self.fc2(self.act(self.fc1(x)))
 
 
