@@ -324,7 +324,10 @@ int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void* v, void* 
  *   8 split: column block j of 128 is written to out + j * split_stride as its own [M, 128]
  *   matrix (not with 4); 32 GELU of the INPUT: exact-erf GELU applied to [x1 | x2] as it is
  *   loaded (the producing layer's activation; N must be 128); 128 ReLU of the input (same rule);
- *   64 with 4: the residual is added BEFORE the LayerNorm (post-norm layers: LN(x W^T + b + r)).
+ *   64 with 4: the residual is added BEFORE the LayerNorm (post-norm layers: LN(x W^T + b + r));
+ *   256 bf16x3 products: x and w split as hi + lo bf16 while staged, hi*hi + hi*lo + lo*hi on
+ *   v_mfma_f32_32x32x16_bf16 with fp32 accumulation (<= 3 * 2^-18 relative per product, the
+ *   stand-in for the reference's TF32, src/main.py:15); default exact fp32.
  *   Epilogues applied in that order.
  * ---------------------------------------------------------------------------------------- */
 int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x2, int32_t k2, const float* w,
@@ -337,7 +340,7 @@ int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x2, int32_t 
  * sum_s e^(m_s - M) l_s per query (the combine launch of tsplat_win_attn_fwd, moved into this
  * kernel's operand staging). partials as left by tsplat_win_attn_partials_fwd for the same
  * (batch, height, width, key_views, splits, with_shift); out [batch, height*width, N] in pixel
- * order; w [N, 128]; flags as tsplat_linear_f32_fwd (2 LayerNorm, 4 residual; no 8/16/32). */
+ * order; w [N, 128]; flags as tsplat_linear_f32_fwd (2 LayerNorm, 4 residual, 256 bf16x3; no 8/16/32). */
 int tsplat_linear_f32_attn_merge_fwd(const float* partials, int32_t batch, int32_t height, int32_t width,
                                      int32_t key_views, int32_t splits, int32_t with_shift, const float* w,
                                      const float* ln_gamma, const float* ln_beta, float ln_eps,

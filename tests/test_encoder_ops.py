@@ -428,9 +428,12 @@ def test_window_attention_bf16_growing_scores(device, monkeypatch, kern, shift, 
     (8192, 1024, 0, 128, False, True, True, False, False, True),     # GELU(h) mlp[2] + norm2 + res
     (96, 64, 0, 256, True, False, False, False, True, False),        # bias path, tiny M
 ])
-def test_fused_linear_kernel(device, m, k1, k2, n, gelu, ln, res, split, bias, gin):
+@pytest.mark.parametrize("dense", ["fp32", "bf16x3"])
+def test_fused_linear_kernel(device, m, k1, k2, n, gelu, ln, res, split, bias, gin, dense):
     """tsplat_linear_f32_fwd vs the CPU restatement of the reference TransformerLayer chain
-    (exact fp32 MFMA; only the summation order differs)."""
+    (exact fp32 MFMA: only the summation order differs; bf16x3 mode, flag 256: split-bf16 products,
+    <= 3 * 2^-18 relative each -- the same 2e-4 bound, which the TF32 rounding of the reference's
+    own GPU run would not meet at these K)."""
     from transplat_amd import kernels as K
 
     x1 = seeded((m, k1), 31)
@@ -441,9 +444,10 @@ def test_fused_linear_kernel(device, m, k1, k2, n, gelu, ln, res, split, bias, g
     r = seeded((m, n), 37) if res else None
     ref = E.fused_linear(x1, w, x2=x2, bias=b, gelu=gelu, ln=lnp, residual=r, split=split, gelu_in=gin)
     d = lambda t: t.to(device) if t is not None else None
-    out = K.fused_linear(d(x1), d(w), x2=d(x2), bias=d(b), gelu=gelu,
-                         ln=(d(lnp[0]), d(lnp[1]), lnp[2]) if ln else None, residual=d(r), split=split,
-                         gelu_in=gin)
+    with K.dense_precision(dense):
+        out = K.fused_linear(d(x1), d(w), x2=d(x2), bias=d(b), gelu=gelu,
+                             ln=(d(lnp[0]), d(lnp[1]), lnp[2]) if ln else None, residual=d(r), split=split,
+                             gelu_in=gin)
     if split:
         assert len(out) == n // 128 and all(o.is_contiguous() and o.shape == (m, 128) for o in out)
         out, ref = torch.cat(out, -1), torch.cat(ref, -1)
@@ -457,10 +461,12 @@ def test_fused_linear_kernel(device, m, k1, k2, n, gelu, ln, res, split, bias, g
                                                   (64, 1, True, 8, True, 0), (64, 1, True, 2, True, 1),
                                                   (64, 1, False, 4, False, 2), (64, 1, True, 8, False, 4),
                                                   (64, 1, True, 1, True, 0)])
-def test_attention_merge_kernel(device, monkeypatch, hw, m, shift, b, res, kvs):
+@pytest.mark.parametrize("dense", ["fp32", "bf16x3"])
+def test_attention_merge_kernel(device, monkeypatch, hw, m, shift, b, res, kvs, dense):
     """Window attention + merge Linear + LayerNorm (+ residual) with the split-key combine folded
     into the merge kernel (tsplat_win_attn_partials_fwd + tsplat_linear_f32_attn_merge_fwd; key
-    splits 4 / 8 here, b = 8 takes the unsplit path) vs the CPU restatement."""
+    splits 4 / 8 here, b = 8 takes the unsplit path) vs the CPU restatement; the merge's products
+    exact fp32 or bf16x3 (dense mode)."""
     from transplat_amd import _lib
     from transplat_amd import kernels as K
 
@@ -474,8 +480,9 @@ def test_attention_merge_kernel(device, monkeypatch, hw, m, shift, b, res, kvs):
     assert (ks > 1) == (b < 8)
     ref = E.attention_merge(q, k, v, hw, hw, 2, shift, wm, ln, residual=r, kv_shift=kvs)
     d = lambda t: t.to(device) if t is not None else None
-    out = K.attention_merge(d(q), d(k), d(v), hw, hw, 2, shift, d(wm), (d(ln[0]), d(ln[1]), ln[2]), residual=d(r),
-                            kv_shift=kvs)
+    with K.dense_precision(dense):
+        out = K.attention_merge(d(q), d(k), d(v), hw, hw, 2, shift, d(wm), (d(ln[0]), d(ln[1]), ln[2]),
+                                residual=d(r), kv_shift=kvs)
     err = (out.cpu() - ref).abs().max().item()
     assert err < 1e-3, err
 

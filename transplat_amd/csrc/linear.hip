@@ -32,6 +32,7 @@ enum Flags : int {
     kGelu = 1, kLayerNorm = 2, kResidual = 4, kSplit = 8, kBias = 16, kGeluIn = 32,
     kResPreLN = 64,  // with kResidual: the residual is added BEFORE the LayerNorm (post-norm layers)
     kReluIn = 128,   // ReLU applied to X as it is staged (the producing FFN layer's activation)
+    kBf16x3 = 256,   // split-bf16 products (x = hi + lo; hi*hi + hi*lo + lo*hi on 32x32x16 bf16 MFMA)
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
@@ -146,7 +147,21 @@ __device__ __forceinline__ void stage_load(const Args& a, int m0, int n0, int K,
         st.w[i] = *reinterpret_cast<const floatx4*>(a.w + (size_t)(n0 + srow + 32 * i) * K + k0 + 4 * sq);
 }
 
-template <int BM>
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// bf16x3 staging: a 256-B row holds the chunk's 64 channels as [hi: 8 units of 8 bf16 | lo: 8 units],
+// 16-B unit u at slot u ^ (row & 15) (the fp32 image's swizzle); fp32 unit sq (channels 4 sq ..
+// 4 sq + 3) is the (sq & 1) half of bf16 unit sq >> 1
+__device__ __forceinline__ void store_split(char* base, int r, int sq, floatx4 v) {
+    const bf16x4 hi = __builtin_convertvector(v, bf16x4);
+    const bf16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, floatx4), bf16x4);
+    char* row = base + r * 256 + (sq & 1) * 8;
+    *reinterpret_cast<bf16x4*>(row + (((sq >> 1) ^ (r & 15)) << 4)) = hi;
+    *reinterpret_cast<bf16x4*>(row + (((8 + (sq >> 1)) ^ (r & 15)) << 4)) = lo;
+}
+
+template <int BM, bool X3>
 __device__ __forceinline__ void stage_store(float* sX, float* sW, int tid, const Stage<BM>& st, bool gelu_in,
                                             bool relu_in) {
     const int srow = tid >> 4, sq = tid & 15;
@@ -156,12 +171,38 @@ __device__ __forceinline__ void stage_store(float* sX, float* sW, int tid, const
         floatx4 x = st.x[i];
         if (gelu_in) x = (floatx4){gelu_erf(x.x), gelu_erf(x.y), gelu_erf(x.z), gelu_erf(x.w)};
         if (relu_in) x = (floatx4){fmaxf(x.x, 0.f), fmaxf(x.y, 0.f), fmaxf(x.z, 0.f), fmaxf(x.w, 0.f)};
-        *reinterpret_cast<floatx4*>(&sX[r * kBK + ((sq ^ (r & 15)) * 4)]) = x;
+        if (X3)
+            store_split(reinterpret_cast<char*>(sX), r, sq, x);
+        else
+            *reinterpret_cast<floatx4*>(&sX[r * kBK + ((sq ^ (r & 15)) * 4)]) = x;
     }
 #pragma unroll
     for (int i = 0; i < kBN / 32; ++i) {
         const int r = srow + 32 * i;
-        *reinterpret_cast<floatx4*>(&sW[r * kBK + ((sq ^ (r & 15)) * 4)]) = st.w[i];
+        if (X3)
+            store_split(reinterpret_cast<char*>(sW), r, sq, st.w[i]);
+        else
+            *reinterpret_cast<floatx4*>(&sW[r * kBK + ((sq ^ (r & 15)) * 4)]) = st.w[i];
+    }
+}
+
+// bf16x3 k-steps s0 .. s0 + NS - 1 of a chunk (16 channels each; lane half h supplies channels
+// 16 s + 8 h .. + 7): A = W row wrow, B = X row xr, each as (hi, lo) bf16x8 from the split image
+template <int NS>
+__device__ __forceinline__ void chunk_mfma_x3(const float* sX, const float* sW, int wrow, int xr, int h, int s0,
+                                              floatx16& acc) {
+    const char* bx = reinterpret_cast<const char*>(sX) + xr * 256;
+    const char* bw = reinterpret_cast<const char*>(sW) + wrow * 256;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const int u = 2 * (s0 + i) + h;
+        const bf16x8 wh = *reinterpret_cast<const bf16x8*>(bw + ((u ^ (wrow & 15)) << 4));
+        const bf16x8 wl = *reinterpret_cast<const bf16x8*>(bw + (((8 + u) ^ (wrow & 15)) << 4));
+        const bf16x8 xh = *reinterpret_cast<const bf16x8*>(bx + ((u ^ (xr & 15)) << 4));
+        const bf16x8 xl = *reinterpret_cast<const bf16x8*>(bx + (((8 + u) ^ (xr & 15)) << 4));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh, acc, 0, 0, 0);
     }
 }
 
@@ -197,7 +238,7 @@ __device__ __forceinline__ void chunk_mfma(const float* sX, const float* sW, int
 // before the epilogue. Pipeline: LDS ping-pong (one barrier per chunk) and two register stages,
 // so chunk t+2's global loads are issued before chunk t's MFMAs and stored to LDS only after
 // chunk t+1's; the loop is unrolled by two so every register stage index is static.
-template <int BM, bool ATTN>
+template <int BM, bool ATTN, bool X3>
 __global__ void __launch_bounds__(kThreads)
 linear_f32_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) float sX[2][BM * kBK];
@@ -220,6 +261,12 @@ linear_f32_kernel(Args a) {
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    auto mfma_chunk = [&](const float* bx, const float* bw) {
+        if constexpr (X3)  // 4 bf16 k-steps per chunk: all of them (BM 64) or this wave's K half
+            chunk_mfma_x3<BM == 64 ? 4 : 2>(bx, bw, wrow, xr, h, BM == 64 ? 0 : 2 * sel, acc);
+        else
+            chunk_mfma<NQ>(bx, bw, wrow, xr, h, q0, acc);
+    };
     Stage<BM> s0, s1;
     AttnRow ar[BM / 32];
     if (ATTN) {
@@ -231,20 +278,20 @@ linear_f32_kernel(Args a) {
     }
     stage_load<BM, ATTN>(a, m0, n0, K, 0, tid, s0, ar);
     if (nchunks > 1) stage_load<BM, ATTN>(a, m0, n0, K, 1, tid, s1, ar);
-    stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in, relu_in);
+    stage_store<BM, X3>(sX[0], sW[0], tid, s0, gelu_in, relu_in);
     __syncthreads();
     for (int ck = 0; ck < nchunks; ck += 2) {
         // even chunk ck (buffer 0); s1 holds chunk ck + 1, s0 is free
         if (ck + 2 < nchunks) stage_load<BM, ATTN>(a, m0, n0, K, ck + 2, tid, s0, ar);
-        chunk_mfma<NQ>(sX[0], sW[0], wrow, xr, h, q0, acc);
+        mfma_chunk(sX[0], sW[0]);
         if (ck + 1 >= nchunks) break;
-        stage_store<BM>(sX[1], sW[1], tid, s1, gelu_in, relu_in);
+        stage_store<BM, X3>(sX[1], sW[1], tid, s1, gelu_in, relu_in);
         __syncthreads();
         // odd chunk ck + 1 (buffer 1); s0 holds chunk ck + 2, s1 is free
         if (ck + 3 < nchunks) stage_load<BM, ATTN>(a, m0, n0, K, ck + 3, tid, s1, ar);
-        chunk_mfma<NQ>(sX[1], sW[1], wrow, xr, h, q0, acc);
+        mfma_chunk(sX[1], sW[1]);
         if (ck + 2 >= nchunks) break;
-        stage_store<BM>(sX[0], sW[0], tid, s0, gelu_in, relu_in);
+        stage_store<BM, X3>(sX[0], sW[0], tid, s0, gelu_in, relu_in);
         __syncthreads();
     }
     __syncthreads();  // every wave is done with the LDS tiles
@@ -366,10 +413,18 @@ extern "C" int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x
     // 64-row blocks when that still fills the 256 CUs, else 32-row blocks with the K halves split
     // over the wave pairs (a 128-column GEMM of 8,192 rows: 256 workgroups)
     const bool tall = (long long)((M + 63) / 64) * (N / kBN) >= 256;
-    if (tall)
-        hipLaunchKernelGGL((linear_f32_kernel<64, false>), dim3((M + 63) / 64, N / kBN), dim3(kThreads), 0, stream, a);
-    else
-        hipLaunchKernelGGL((linear_f32_kernel<32, false>), dim3((M + 31) / 32, N / kBN), dim3(kThreads), 0, stream, a);
+    const dim3 g64((M + 63) / 64, N / kBN), g32((M + 31) / 32, N / kBN);
+    if (flags & kBf16x3) {
+        if (tall)
+            hipLaunchKernelGGL((linear_f32_kernel<64, false, true>), g64, dim3(kThreads), 0, stream, a);
+        else
+            hipLaunchKernelGGL((linear_f32_kernel<32, false, true>), g32, dim3(kThreads), 0, stream, a);
+    } else {
+        if (tall)
+            hipLaunchKernelGGL((linear_f32_kernel<64, false, false>), g64, dim3(kThreads), 0, stream, a);
+        else
+            hipLaunchKernelGGL((linear_f32_kernel<32, false, false>), g32, dim3(kThreads), 0, stream, a);
+    }
     TSPLAT_PROF_END(prof::kLinear, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
@@ -408,7 +463,12 @@ extern "C" int tsplat_linear_f32_attn_merge_fwd(const float* partials, int32_t b
     a.pl = a.pm + n;
     hipStream_t stream = (hipStream_t)stream_;
     TSPLAT_PROF_BEGIN(prof::kLinear, stream);
-    hipLaunchKernelGGL((linear_f32_kernel<32, true>), dim3((M + 31) / 32, N / kBN), dim3(kThreads), 0, stream, a);
+    if (flags & kBf16x3)
+        hipLaunchKernelGGL((linear_f32_kernel<32, true, true>), dim3((M + 31) / 32, N / kBN), dim3(kThreads), 0, stream,
+                           a);
+    else
+        hipLaunchKernelGGL((linear_f32_kernel<32, true, false>), dim3((M + 31) / 32, N / kBN), dim3(kThreads), 0,
+                           stream, a);
     TSPLAT_PROF_END(prof::kLinear, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

@@ -318,12 +318,20 @@ def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", 
 
 
 _LIN_GELU, _LIN_LN, _LIN_RES, _LIN_SPLIT, _LIN_BIAS, _LIN_GELU_IN = 1, 2, 4, 8, 16, 32
-_LIN_RES_PRE_LN, _LIN_RELU_IN = 64, 128
+_LIN_RES_PRE_LN, _LIN_RELU_IN, _LIN_BF16X3 = 64, 128, 256
+# the fused transformer linears' products in bf16x3 inside dense_precision("bf16x3") (the kernel's
+# split-bf16 form, flag 256); TSPLAT_LINF3=0 keeps them exact fp32 in that mode
+_LINF3 = os.environ.get("TSPLAT_LINF3", "1") == "1"
+
+
+def _lin_precision_flag() -> int:
+    return _LIN_BF16X3 if _LINF3 and _DENSE == "bf16x3" else 0
 
 
 def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, residual=None, split: bool = False,
                  gelu_in: bool = False, relu_in: bool = False, res_pre_ln: bool = False):
-    """epilogue([x1 | x2] weight^T) in one exact-fp32 MFMA launch (tsplat_linear_f32_fwd):
+    """epilogue([x1 | x2] weight^T) in one exact-fp32 MFMA launch (tsplat_linear_f32_fwd; bf16x3
+    products inside dense_precision("bf16x3"), see _LINF3):
     (+ bias) -> (exact GELU) -> (LayerNorm with ln = (gamma, beta, eps), N = 128) -> (+ residual);
     gelu_in / relu_in apply exact GELU / ReLU to the input first (the producing layer's activation,
     N = 128); res_pre_ln adds the residual before the LayerNorm (post-norm: LN(y + residual)).
@@ -344,6 +352,7 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     flags = (_LIN_GELU if gelu else 0) | (_LIN_LN if ln is not None else 0) | (_LIN_BIAS if bias is not None else 0)
     flags |= (_LIN_GELU_IN if gelu_in else 0) | (_LIN_RELU_IN if relu_in else 0)
     flags |= _LIN_RES_PRE_LN if res_pre_ln and residual is not None else 0
+    flags |= _lin_precision_flag()
     res = None
     if residual is not None:
         res = _f32(residual).reshape(m, n)
@@ -399,7 +408,7 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     _lib.check(rc, "tsplat_win_attn_partials_fwd")
     n = merge_weight.shape[0]
     out = torch.empty((b, l, n), dtype=torch.float32, device=q.device)
-    flags = _LIN_LN if ln is not None else 0
+    flags = (_LIN_LN if ln is not None else 0) | _lin_precision_flag()
     res = None
     if residual is not None:
         res = _f32(residual)
