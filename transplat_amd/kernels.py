@@ -823,12 +823,16 @@ def linear_bf16x3(x, weight, bias=None, act: str = "none", out=None, cache: bool
     return y
 
 
-# nn.Linear in bf16x3 mode: OFF by default (TSPLAT_LIN3=1 turns it on). Measured on the step's linears
-# (tools/bench_split_gemm.py; profiles/r4/split_gemm.log, split_gemm2.log): neither hipBLASLt's bf16 GEMM
-# at K' = 3K (DINOv2 qkv 23.9 vs 29.0 us fp32, proj 23.9 vs 19.0, fc1 27.3 vs 30.4, fc2 29.3 vs 27.8)
-# nor the first tsplat_linear_bf16x3_fwd (37.3 / 24.8 / 51.9 / 83.6 us: at M = 650 a 64 x 64 tile per
-# workgroup gives 132-528 workgroups whose 32-wide K chunks serialise on load latency) beats the
-# library's fp32 SGEMM; the M = 650 shapes stay exact fp32 until the kernel is pipelined deeper.
+# tsplat_linear_bf16x3_fwd for nn.Linear in bf16x3 mode: OFF by default (TSPLAT_LIN3=1 turns it on;
+# linear_xf32 above takes the large linears first). Measured on the step's linears
+# (tools/bench_split_gemm.py; profiles/r4/split_gemm2.log, profiles/r4/g12/split_gemm.log): hipBLASLt's
+# bf16 GEMM at K' = 3K (DINOv2 qkv 23.9 vs 29.0 us fp32, proj 23.9 vs 19.0, fc1 27.3 vs 30.4, fc2 29.3 vs
+# 27.8); the first kernel form 37.3 / 24.8 / 51.9 / 83.6 us (one 32-deep chunk of register prefetch:
+# a full L2 round trip per chunk); the pipelined LDS-DMA form 22.4 / 20.1 / 38.6 / 60.7 us and C2 381
+# vs 394 views/s with it dispatched (profiles/r4/g12/): a 64 x 128 tile needs 48 KB of operands per
+# 64-deep stage against 24 bf16 MFMAs per wave, ~62 B per CU cycle, while a CU ingests ~25 GB/s
+# (~11 B/cycle) here -- bf16x3 cuts the MFMA cycles but not the fp32-sized operand bytes, so at
+# M = 650 these GEMMs stay bound by operand delivery, where the library is already tuned.
 _LIN3 = os.environ.get("TSPLAT_LIN3", "0") == "1"
 _LIN3_MIN_FLOP = float(os.environ.get("TSPLAT_LIN3_MIN_FLOP", "2e8"))
 
