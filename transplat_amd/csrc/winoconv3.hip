@@ -208,41 +208,6 @@ __device__ __forceinline__ void transform_pair(const float (&da)[16], const floa
     }
 }
 
-// The same transform into registers (vt[xi] = hi, vt[16 + xi] = lo of the pair), for a schedule that
-// computes a chunk's transform beside the previous chunk's MFMAs and stores it to sV afterwards
-__device__ __forceinline__ void transform_pair_regs(const float (&da)[16], const float (&db)[16], uint32_t (&vt)[32]) {
-    float ta[16], tb[16];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        ta[0 + j] = da[0 + j] - da[8 + j];
-        ta[4 + j] = da[4 + j] + da[8 + j];
-        ta[8 + j] = da[8 + j] - da[4 + j];
-        ta[12 + j] = da[4 + j] - da[12 + j];
-        tb[0 + j] = db[0 + j] - db[8 + j];
-        tb[4 + j] = db[4 + j] + db[8 + j];
-        tb[8 + j] = db[8 + j] - db[4 + j];
-        tb[12 + j] = db[4 + j] - db[12 + j];
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float va[4] = {ta[4 * r] - ta[4 * r + 2], ta[4 * r + 1] + ta[4 * r + 2], ta[4 * r + 2] - ta[4 * r + 1],
-                             ta[4 * r + 1] - ta[4 * r + 3]};
-        const float vb[4] = {tb[4 * r] - tb[4 * r + 2], tb[4 * r + 1] + tb[4 * r + 2], tb[4 * r + 2] - tb[4 * r + 1],
-                             tb[4 * r + 1] - tb[4 * r + 3]};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) split_pair(va[s], vb[s], vt[4 * r + s], vt[16 + 4 * r + s]);
-    }
-}
-
-template <int T>
-__device__ __forceinline__ void store_vt(const uint32_t (&vt)[32], uint32_t* sV) {
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        sV[i * 8 * T] = vt[i];
-        sV[(16 + i) * 8 * T] = vt[16 + i];
-    }
-}
-
 // Staged input (ST): per 16-channel chunk the tile block's input region -- rows 2 ty0 - 1 ..
 // 2 (ty0 + TBY), columns from the 16-B-aligned 2 tx0 - 4, TBX / 2 + 2 float4 per row -- is loaded
 // with coalesced float4 loads (a chunk ahead, in registers) into an LDS slot sIn[ch][row][col], and
@@ -352,11 +317,11 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     float* sIn = reinterpret_cast<float*>(sG + NSV * BUF);
     // DS: two register sets for the region loads (the 32-co forms have the registers): the loads of
     // chunk it + 3 are issued at iteration it and stored at it + 2, a whole iteration in flight
-    // PT: the 32 x 32 forms compute each chunk's transform beside the previous chunk's MFMAs (below);
-    // DS: two register sets for the region loads -- measured on the plain loop, it no longer fits
-    // the register budget beside PT's transform registers (spills), so PT runs with one set
-    constexpr bool PT = ST && CB == 1 && NB == 1;
-    constexpr bool DS = false;
+    // (tried and reverted: computing the next chunk's transform beside the MFMAs in registers,
+    // sched_barrier-fenced quarters, one register set -- census 1695 vs 1637 us, C2 397.4 / 397.8 vs
+    // 399.4 / 401.0 views/s, profiles/r4/g15/: the loop is bound by its VALU + LDS issue, not by the
+    // phase order)
+    constexpr bool DS = ST && CB == 1 && NB == 1;
     float4 gr[DS ? 2 : 1][ST ? NL : 1];
     // region loads: thread gtid stages channel gch = gtid / TPC of the chunk (one plane pointer per
     // chunk) and its elements j = sub + TPC k of that channel's R x C4 float4 ([row][c4] order). The
@@ -471,72 +436,10 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
             load_a(ch + KS, 0, 4);
             __syncthreads();  // every wave is done with sV(it) and with sIn slot it & 1
         };
-        if constexpr (PT) {
-            // the transform of chunk it + 1 runs beside chunk it's MFMAs (into registers vt) and is
-            // stored to sV at the top of the next iteration: the VALU work no longer sits between
-            // the MFMA phases of the SIMD's two waves
-            static_assert(!PT || PP == 1, "one channel pair per thread");
-            uint32_t vt[32];
-            read_patches(0);
-            transform_pair_regs(d[0][0], d[0][1], vt);
-            // MFMAs of xi 4 rr + s beside one quarter of the next chunk's transform each: groups fenced
-            // by sched_barrier so the scheduler cannot pull all MFMAs ahead of the VALU work (the
-            // MFMAs issue asynchronously, the VALU runs while the matrix pipe works)
-            auto mm = [&](int s) {
-                const uint32_t* ph = sG + ((lane >> 5) * T + (lane & 31)) * 4 + (4 * rr + s) * 8 * T;
-                const bf16x8 ah = __builtin_bit_cast(bf16x8, af[s][0]);
-                const bf16x8 al = __builtin_bit_cast(bf16x8, af[s][1]);
-                const bf16x8 bh = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ph));
-                const bf16x8 bl = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ph + 16 * 8 * T));
-                acc[s][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[s][0], 0, 0, 0);
-                acc[s][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[s][0], 0, 0, 0);
-                acc[s][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[s][0], 0, 0, 0);
-            };
-            auto pstep = [&](int it, auto S) {
-                const int ch = kg + it * KS;
-                const bool more = it + 1 < iters;
-                if (more) sstore((it + 1) & 1, S);
-                store_vt<T>(vt, sG + (ph0 * T + t) * 4 + pl);
-                gload(ch + (DS ? 3 : 2) * KS, S);
-                __syncthreads();  // sV(it) and sIn slot (it + 1) & 1 complete
-                if (more) read_patches((it + 1) & 1);
-                float ta[16], tb[16];  // B^T d of the next chunk's pair
-                mm(0);
-                if (more) {
-                    const float(&da)[16] = d[0][0];
-                    const float(&db)[16] = d[0][1];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        ta[0 + j] = da[0 + j] - da[8 + j];
-                        ta[4 + j] = da[4 + j] + da[8 + j];
-                        ta[8 + j] = da[8 + j] - da[4 + j];
-                        ta[12 + j] = da[4 + j] - da[12 + j];
-                        tb[0 + j] = db[0 + j] - db[8 + j];
-                        tb[4 + j] = db[4 + j] + db[8 + j];
-                        tb[8 + j] = db[8 + j] - db[4 + j];
-                        tb[12 + j] = db[4 + j] - db[12 + j];
-                    }
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    if (r < 3) mm(r + 1);
-                    if (more) {  // row r of (B^T d) B, split into vt
-                        const float va[4] = {ta[4 * r] - ta[4 * r + 2], ta[4 * r + 1] + ta[4 * r + 2],
-                                             ta[4 * r + 2] - ta[4 * r + 1], ta[4 * r + 1] - ta[4 * r + 3]};
-                        const float vb[4] = {tb[4 * r] - tb[4 * r + 2], tb[4 * r + 1] + tb[4 * r + 2],
-                                             tb[4 * r + 2] - tb[4 * r + 1], tb[4 * r + 1] - tb[4 * r + 3]};
-#pragma unroll
-                        for (int s2 = 0; s2 < 4; ++s2) split_pair(va[s2], vb[s2], vt[4 * r + s2], vt[16 + 4 * r + s2]);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                load_a(ch + KS, 0, 4);
-                __syncthreads();  // every wave is done with sV(it)
-            };
+        if constexpr (DS) {
             for (int it = 0; it < iters; it += 2) {
-                pstep(it, I1);
-                if (it + 1 < iters) pstep(it + 1, I0);
+                step(it, I1);
+                if (it + 1 < iters) step(it + 1, I0);
             }
         } else {
             for (int it = 0; it < iters; ++it) step(it, I0);
