@@ -243,6 +243,20 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     __shared__ const float* planes[kMaxCiPad];
 
     W3_STAMP(0);
+    // XCD-aware order: the dispatcher deals workgroup ids (x fastest) round-robin over the 8 XCDs.
+    // The bijective remap gives each XCD a contiguous range of (tile block, output block) pairs with
+    // the output blocks of one tile block adjacent, so a tile block's input regions are fetched into
+    // that XCD's L2 once for all its output blocks (x-fastest order re-read the whole input map from
+    // HBM / MALL once per output block: 673 MB fetched for the 85 MB input of 2 x 163 -> 168 at 256^2,
+    // profiles/r4/traffic_wino3_163x168_b1.json)
+    int tbk, cbk;
+    {
+        const int nwg = gridDim.x * gridDim.y, id = blockIdx.x + blockIdx.y * gridDim.x;
+        const int q = nwg / 8, r = nwg % 8, xcd = id % 8;
+        const int logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
+        tbk = logical / gridDim.y;
+        cbk = logical - tbk * gridDim.y;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int kg = wid / (4 * CB), wg = wid % (4 * CB);
     const int hh = wg >> 2, rr = wg & 3;
@@ -250,7 +264,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     // a wave's 64 lanes are 16 tiles x 4 pairs, so its sV dword stores are 64 consecutive dwords
     const int gtid = tid % GT;
     const int pl = gtid & 3, t = (gtid >> 2) % T, ph0 = (gtid >> 2) / T;
-    const Patch<T> pt(a, blockIdx.x, t);
+    const Patch<T> pt(a, tbk, t);
 
     for (int c = tid; c < a.ci_pad; c += 256 * CB * KS) {
         const float* src = nullptr;
@@ -265,7 +279,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     }
     __syncthreads();
 
-    const int cob = a.cob_base + blockIdx.y * CB + hh;
+    const int cob = a.cob_base + cbk * CB + hh;
     const bool co_ok = cob < a.cobs;
     // A fragments: [xi][cob][chunk][hl][lane] uint4
     const uint4* ub = a.u + ((size_t)(4 * rr) * a.cobs + (co_ok ? cob : 0)) * a.nchunk * 128 + lane;
@@ -311,7 +325,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
         for (int q = 0; q < PP; ++q) transform_pair<T>(d[q][0], d[q][1], sV + ((ph0 + q * PHR) * T + t) * 4 + pl);
     };
     // staged region of the chunk: R rows x C4 float4 per channel, origin (ry0, rx0)
-    const int blk = blockIdx.x % (a.bx * a.by);
+    const int blk = tbk % (a.bx * a.by);
     const int R = 2 * a.tby + 2, C4 = a.tbx / 2 + 2, RP = 4 * C4;
     const int ry0 = 2 * (blk / a.bx) * a.tby - 1, rx0 = 2 * (blk % a.bx) * a.tbx - 4;
     float* sIn = reinterpret_cast<float*>(sG + NSV * BUF);
@@ -494,7 +508,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     const size_t hw = (size_t)a.h * a.w;
     for (int pidx = tid; pidx < CO * T; pidx += 256 * CB * KS) {
         const int col = pidx / T, t2 = pidx % T;
-        const int o = (a.cob_base + blockIdx.y * CB) * 32 + col;
+        const int o = (a.cob_base + cbk * CB) * 32 + col;
         const int oty = (blk / a.bx) * a.tby + t2 / a.tbx, otx = (blk % a.bx) * a.tbx + t2 % a.tbx;
         if (o >= a.co || oty >= a.th || otx >= a.tw) continue;
         const float bv = a.bias ? a.bias[o] : 0.0f;
