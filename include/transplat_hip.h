@@ -358,6 +358,13 @@ int tsplat_small_inverse(const float* in, float* out, int32_t n, int32_t dim, vo
  * head_dim must be 64. */
 int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, int32_t tokens, int32_t heads,
                        int32_t head_dim, float scale, void* stream);
+/* The same with the qkv projection's bias folded in: qkv holds x W^T WITHOUT the bias and bias is
+ * its [3 * heads * 64] vector (16-B aligned): q + b_q is formed on load, b_k is dropped (it adds
+ * b_k . q to every score of a query, which the softmax cancels) and b_v is added to the normalised
+ * output -- the reference Attention.forward on qkv = Linear(x) with bias (dinov2_layers/attention.py),
+ * one elementwise pass fewer. bias = NULL is tsplat_mha_f32_fwd. */
+int tsplat_mha_bias_f32_fwd(const float* qkv, const float* bias, float* out, int32_t batch, int32_t tokens,
+                            int32_t heads, int32_t head_dim, float scale, void* stream);
 
 /* Legacy channels-first QKV attention of the depth predictor U-Nets (exact fp32 MFMA), replacing
  * QKVAttentionLegacy.forward (reference src/model/encoder/matching/ldm_unet/unet.py:510-552) with

@@ -564,6 +564,22 @@ def test_mha_kernel(device, b, n, heads, form, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("b,n", [(2, 325), (1, 5)])
+def test_mha_bias_folded(device, b, n):
+    """tsplat_mha_bias_f32_fwd (qkv without the projection bias + the bias vector: q bias on load,
+    k bias dropped -- the softmax cancels it -- v bias on the output) vs the CPU restatement on
+    qkv + bias, same tolerance as test_mha_kernel."""
+    from transplat_amd import kernels as K
+
+    heads = 12
+    qkv = seeded((b, n, 3 * heads * 64), 72) * 2.0
+    bias = seeded((3 * heads * 64,), 73) * 0.5
+    ref = E.mha(qkv + bias, heads, 64 ** -0.5)
+    out = K.mha(qkv.to(device), heads, 64 ** -0.5, bias=bias.to(device)).cpu()
+    assert (out - ref).abs().max().item() < 5e-5
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("rows,dim,with_y,with_ls", [(650, 768, True, True), (650, 768, False, False),
                                                      (7, 256, True, False), (33, 1024, True, True)])
 def test_residual_ln_kernel(device, rows, dim, with_y, with_ls):

@@ -362,7 +362,8 @@ mha_cf32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int B, i
 // Per-query softmax statistics reduce over the 4 registers and the 4 lane groups.
 template <int W>
 __global__ void __launch_bounds__(W * 64)
-mha16_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, int H, float scale) {
+mha16_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, int H, float scale,
+                 const float* __restrict__ bias) {
     __shared__ float sO[W][16][64];
     __shared__ float sML[W][2][16];
 
@@ -389,9 +390,13 @@ mha16_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, 
     {
         const float qs = scale * kLog2e;
         const floatx4* src = reinterpret_cast<const floatx4*>(base + (size_t)min(q, N - 1) * tok + 16 * g);
+        // the projection's bias (bias != null: qkv holds x W^T without it): q's part added here; k's part
+        // shifts every score of a query by the same b_k . q, which the softmax cancels, so it is
+        // dropped; v's part is added to the normalised output (the weights sum to 1)
+        const floatx4* bq = reinterpret_cast<const floatx4*>(bias + (size_t)head * kD + 16 * g);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const floatx4 t = src[i];
+            const floatx4 t = bias ? src[i] + bq[i] : src[i];
             qr[4 * i] = t.x * qs;
             qr[4 * i + 1] = t.y * qs;
             qr[4 * i + 2] = t.z * qs;
@@ -504,6 +509,7 @@ mha16_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, 
 #pragma unroll
         for (int w = 0; w < W; ++w) t += a[w] * sO[w][(j >> 2) * 4 + i][(j & 3) * 16 + qq];
         acc[i] = t * inv;
+        if (bias) acc[i] += bias[(size_t)(2 * H + head) * kD + 4 * j + i];
     }
     float* dst = out + (((size_t)b * N + qo) * H + head) * kD + 4 * j;
     *reinterpret_cast<floatx4*>(dst) = (floatx4){acc[0], acc[1], acc[2], acc[3]};
@@ -512,26 +518,34 @@ mha16_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, 
 }  // namespace mha
 }  // namespace tsplat
 
+extern "C" int tsplat_mha_bias_f32_fwd(const float* qkv, const float* bias, float* out, int32_t batch,
+                                       int32_t tokens, int32_t heads, int32_t head_dim, float scale, void* stream_);
+
 extern "C" int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, int32_t tokens, int32_t heads,
                                   int32_t head_dim, float scale, void* stream_) {
+    return tsplat_mha_bias_f32_fwd(qkv, nullptr, out, batch, tokens, heads, head_dim, scale, stream_);
+}
+
+extern "C" int tsplat_mha_bias_f32_fwd(const float* qkv, const float* bias, float* out, int32_t batch,
+                                       int32_t tokens, int32_t heads, int32_t head_dim, float scale, void* stream_) {
     using namespace tsplat::mha;
     if (!qkv || !out || batch <= 0 || tokens <= 0 || heads <= 0 || head_dim != kD) return TSPLAT_EINVAL;
-    if ((int64_t)batch * heads > 65535) return TSPLAT_EINVAL;
+    if ((int64_t)batch * heads > 65535 || (reinterpret_cast<uintptr_t>(bias) & 15)) return TSPLAT_EINVAL;
     hipStream_t stream = (hipStream_t)stream_;
     // TSPLAT_MHA: "16" (default, 4 waves per 16-query block), "16x8" (8 waves), "32" (the
-    // 32-query kernel); A/B knob
+    // 32-query kernel); A/B knob. The bias form is the default kernel's.
     const char* env = getenv("TSPLAT_MHA");
-    const int form = !env ? 0 : (!strcmp(env, "32") ? 2 : (!strcmp(env, "16x8") ? 1 : 0));
+    const int form = !env || bias ? 0 : (!strcmp(env, "32") ? 2 : (!strcmp(env, "16x8") ? 1 : 0));
     TSPLAT_PROF_BEGIN(tsplat::prof::kMha, stream);
     if (form == 2)
         hipLaunchKernelGGL(mha_f32_kernel, dim3((tokens + kQW - 1) / kQW, batch * heads), dim3(kThreads), 0, stream,
                            qkv, out, tokens, heads, scale);
     else if (form == 1)
         hipLaunchKernelGGL(mha16_f32_kernel<8>, dim3((tokens + 15) / 16, batch * heads), dim3(512), 0, stream, qkv,
-                           out, tokens, heads, scale);
+                           out, tokens, heads, scale, nullptr);
     else
         hipLaunchKernelGGL(mha16_f32_kernel<4>, dim3((tokens + 15) / 16, batch * heads), dim3(256), 0, stream, qkv,
-                           out, tokens, heads, scale);
+                           out, tokens, heads, scale, bias);
     TSPLAT_PROF_END(tsplat::prof::kMha, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

@@ -825,19 +825,18 @@ static int pick_form(int n, int th, int tw, int co) {
         const int f = atoi(e);
         if (f >= 1 && f <= 5) return f;
     }
-    // measured per census shape (tools/bench_wino3.py, profiles/r4/g9/bench_wino3.log): the 64 x 64
-    // form above 128 workgroups (2 x 128 -> 64 at 144^2, 162 of them: 34.9 vs 47.8 us for 32 x 32;
-    // at 128 -- 64 -> 64 at 128^2, 128 -> 256 at 64^2 -- half the CUs idle and 32 x 32 wins, 17.3
-    // vs 20.7 us), the persistent form for one 32-channel output block over more than 256 blocks
-    // (32 -> 32 at 256^2: 24.0 vs 26.9 us), two k-groups where 32 x 32 workgroups would leave CUs
-    // idle, the 32 x 64 form never
+    // measured per census shape (tools/bench_wino3.py, profiles/r4/g17/bench_wino3.log, XCD-ordered
+    // blocks): the 64 x 64 form above 128 workgroups (2 x 128 -> 64 at 144^2, 162 of them: 30.8 vs
+    // 38.1 us for 32 x 32; at 128 -- 64 -> 64 at 128^2, 128 -> 256 at 64^2 -- half the CUs idle and
+    // 32 x 32 wins), two k-groups where 32 x 32 workgroups would leave CUs idle, else 32 x 32 (the
+    // persistent form measured 24.3 vs 23.1 us at 32 -> 32 / 256^2 once blocks were XCD-ordered; the
+    // 32 x 64 form never)
     const long tiles = (long)n * th * tw;
     const int cob32 = (co + 31) / 32;
     const long wg64 = (tiles + 63) / 64 * ((co + 63) / 64);
     const long wg32 = (tiles + 31) / 32 * cob32;
     if (co > 32 && wg64 > 128) return 4;
-    if (wg32 <= 256) return 2;
-    return co <= 32 ? 5 : 1;
+    return wg32 <= 256 ? 2 : 1;
 }
 
 template <int CB, int NB, int KS>

@@ -484,14 +484,19 @@ def depth_softmax(logits, disp):
     return coarse, pmax
 
 
-def mha(qkv, heads: int, scale: float):
+def mha(qkv, heads: int, scale: float, bias=None):
     """Multi-head self-attention from the qkv projection output [B, N, 3 * heads * 64] ->
-    [B, N, heads * 64] (tsplat_mha_f32_fwd; no permute copies)."""
+    [B, N, heads * 64] (tsplat_mha_f32_fwd; no permute copies). bias: the projection's bias when
+    qkv was computed without it (tsplat_mha_bias_f32_fwd folds it in)."""
     lib = _lib.load()
     b, n, c3 = qkv.shape
     d = c3 // (3 * heads)
     x = _f32(qkv)
     out = torch.empty((b, n, heads * d), dtype=torch.float32, device=qkv.device)
+    if bias is not None:
+        _lib.check(lib.tsplat_mha_bias_f32_fwd(_lib.ptr(x), _lib.ptr(_f32(bias)), _lib.ptr(out), b, n, heads, d,
+                                               float(scale), _lib.stream_ptr(qkv.device)), "tsplat_mha_bias_f32_fwd")
+        return out
     _lib.check(lib.tsplat_mha_f32_fwd(_lib.ptr(x), _lib.ptr(out), b, n, heads, d, float(scale),
                                       _lib.stream_ptr(qkv.device)), "tsplat_mha_f32_fwd")
     return out

@@ -83,7 +83,12 @@ class Attention(nn.Module):
     def forward(self, x):
         b, n, c = x.shape
         if x.dtype == torch.float32 and c // self.num_heads == 64 and not torch.is_autocast_enabled(x.device.type):
-            # exact-fp32 MFMA attention straight from the qkv projection's layout
+            # exact-fp32 MFMA attention straight from the qkv projection's layout; in bf16x3 mode the
+            # projection runs without its bias (hipBLASLt's emulated-xf32 GEMM) and the attention
+            # kernel folds the bias in (no separate bias pass)
+            if self.qkv.bias is not None and kernels.linear_xf32_ok(x, self.qkv.weight):
+                qkv = kernels.linear_xf32(x, self.qkv.weight)
+                return self.proj(kernels.mha(qkv, self.num_heads, self.scale, bias=self.qkv.bias))
             return self.proj(kernels.mha(self.qkv(x), self.num_heads, self.scale))
         qkv = self.qkv(x).reshape(b, n, 3, self.num_heads, c // self.num_heads).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
