@@ -190,6 +190,7 @@ WINO_CASES = [
     (1, 38, 32, 17, 21, True, "none"),     # odd sizes: half tiles on the last row / column (tbx 8)
     (1, 128, 128, 18, 18, True, "gelu"),   # tw 9 -> tbx 8
     (3, 16, 16, 9, 70, False, "none"),     # tw 35 -> tbx 32, a partial second tile block per row
+    (1, 64, 2, 40, 36, True, "none"),      # a 2-channel head (co << 32: one mostly idle output block)
 ]
 
 

@@ -667,7 +667,10 @@ def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=
     co = weight.shape[0]
     groups_ = n * ((h + 1) // 2 * ((w + 1) // 2) + 31) // 32 * ((co + 31) // 32)  # ~ workgroups
     vs_miopen = vs_miopen and _WINO_MODE != "big"  # "big": the FLOP floor everywhere (A/B knob)
-    return (ci >= 16 and co >= 16 and (vs_miopen or 2.0 * n * h * w * co * ci * 9 > _CONV_MAX_FLOP)
+    # (a head with a handful of output channels on a large map -- 64 -> 2 at 256^2 -- still beats
+    # MIOpen's 53 us with one mostly idle 32-channel output block: the transform dominates there)
+    return (ci >= 16 and (co >= 16 or (vs_miopen and n * h * w >= 65536))
+            and (vs_miopen or 2.0 * n * h * w * co * ci * 9 > _CONV_MAX_FLOP)
             and (ci <= 192 or groups_ >= 256))
 
 
