@@ -7,7 +7,7 @@ R=$(pwd)
 OUT=$R/gpurun_out/${TAG:-r4_g19}
 mkdir -p $OUT
 export PYTHONPATH=$R
-timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv.py tests/test_modules.py tests/test_e2e.py tests/test_reference_golden.py -k "wino or depth_predictor or bf16x3 or encoder" -m gpu > $OUT/pytest.log 2>&1 || { grep -E "FAILED|Error" $OUT/pytest.log | head; tail -3 $OUT/pytest.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_conv.py tests/test_modules.py tests/test_e2e.py tests/test_reference_golden.py tests/test_encoder_ops.py -k "wino or depth_predictor or bf16x3 or encoder or fused_linear or attention_merge or mvt or backbone" -m gpu > $OUT/pytest.log 2>&1 || { grep -E "FAILED|Error" $OUT/pytest.log | head; tail -3 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 for v in x3_1 fp32 x3_2; do
   case $v in

@@ -248,7 +248,19 @@ linear_f32_kernel(Args a) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int c = lane & 31, h = lane >> 5;
     const int cb = wid & 3, sel = wid >> 2;  // column block, row half (BM 64) or K half (BM 32)
-    const int m0 = blockIdx.x * BM, n0 = blockIdx.y * kBN;
+    // XCD-aware order: ids are dealt (x fastest) round-robin over the 8 XCDs; remapped bijectively so
+    // each XCD runs a contiguous range of (row block, column block) pairs with the column blocks of a
+    // row block adjacent: the row block's X rows come from that XCD's L2 for all of them instead of
+    // being re-fetched once per column block (x-fastest order)
+    int mb, nb_;
+    {
+        const int nwg = gridDim.x * gridDim.y, id = blockIdx.x + blockIdx.y * gridDim.x;
+        const int q = nwg / 8, r = nwg % 8, xcd = id % 8;
+        const int logical = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
+        mb = logical / gridDim.y;
+        nb_ = logical - mb * gridDim.y;
+    }
+    const int m0 = mb * BM, n0 = nb_ * kBN;
     const int K = a.k1 + a.k2;
     const int nchunks = K / kBK;
     const int wrow = 32 * cb + c;                     // this lane's W row (output column)
