@@ -380,7 +380,9 @@ static void launch_tw(const Args& a, int src_mode, hipStream_t stream) {
     b.tiles_y = ceil_div(a.h, TH);
     // enough workgroups to fill every CU a few times over; each streams its share of the tiles
     const int ntiles = a.n * b.tiles_x * b.tiles_y, cob = ceil_div(a.co, 32 * CT);
-    const int want = std::max(1, a.wg_target / cob);
+    // a multiple of 8 workgroups per output block: workgroup (x, y) is dispatched to XCD (x + y gx) % 8, so
+    // the output blocks of one pixel tile then share an XCD and its L2 (the input tile is fetched once)
+    const int want = std::max(8, a.wg_target / cob / 8 * 8);
     dim3 grid(std::min(ntiles, want), cob);
     if (src_mode == 2)
         hipLaunchKernelGGL((conv_bf16_kernel<TW, CT, KS, 2, 2, WCT, NT>), grid, dim3(kThreads), 0, stream, b);
