@@ -510,12 +510,12 @@ _CONV_PACKED: dict = {}
 _CONV_MODE = os.environ.get("TSPLAT_CONV", "auto")
 _CONV_KSPLIT = int(os.environ.get("TSPLAT_CONV_KSPLIT", "0"))  # tuning override (tools/bench_conv.py)
 _CONV_MAX_FLOP = 1.5e9  # above this MIOpen's kernels are as fast or faster (tools/bench_conv.py)
-# 1x1 launch shape: grid cap in waves and minimum ci pairs per wave. Same-box A/B (tools/sessions/ab_conv1.sh):
+# 1x1 launch shape: grid cap in waves and minimum ci pairs per wave. Same-box A/B (tools/sessions/archive/ab_conv1.sh):
 # 16384 / 8 reads 338.98 / 338.99 views/s vs 337.91 / 337.58 for the 3x3 rule (4096 / 16); 8192 / 16
 # and 16384 / 4 sit in between
 _CONV1_WAVES = int(os.environ.get("TSPLAT_CONV1_WAVES", "16384"))
 _CONV1_PAIRS = int(os.environ.get("TSPLAT_CONV1_PAIRS", "8"))
-# the same for 3x3 (tools/sessions/ab_conv3.sh, same box: 8192 / 2 reads 340.3 / 339.7 views/s vs 339.3 /
+# the same for 3x3 (tools/sessions/archive/ab_conv3.sh, same box: 8192 / 2 reads 340.3 / 339.7 views/s vs 339.3 /
 # 339.2 at 4096 / 2; 16384 / 1 and 8192 / 1 in between)
 _CONV3_WAVES = int(os.environ.get("TSPLAT_CONV3_WAVES", "8192"))
 _CONV3_PAIRS = int(os.environ.get("TSPLAT_CONV3_PAIRS", "2"))
