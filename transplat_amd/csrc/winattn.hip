@@ -44,6 +44,14 @@ constexpr float kMaskLog2 = -100.0f * kLog2e;  // the reference's -100 mask, log
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// v_max3_f32 as written: fmaxf() on MFMA results makes the compiler insert canonicalising
+// v_max_f32 x, x first (scores are finite products, no signalling NaNs to quieten)
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // max / sum of lanes l and l ^ 32 (the two half-waves), in VALU via v_permlane32_swap instead of
 // an LDS-routed ds_bpermute: swap(x, x) returns (x[row 0], x[row 1]) in every lane
 __device__ __forceinline__ float halves_max(float x) {
@@ -543,11 +551,12 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
                     s[sub][4 * u + 3] += rg.w == qreg ? 0.0f : kMaskLog2;
                 }
         }
-        float bmax = -INFINITY;
+        // row max as a v_max3 tree (16 instructions for 32 scores)
+        float bmax = max3_raw(s[0][0], s[1][0], s[0][1]);
+        bmax = max3_raw(bmax, s[1][1], s[0][2]);
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) bmax = fmaxf(bmax, s[sub][r]);
+        for (int r = 2; r < 15; ++r) bmax = max3_raw(bmax, s[1][r], s[0][r + 1]);
+        bmax = fmaxf(bmax, s[1][15]);
         bmax = halves_max(bmax);
         const float m_new = fmaxf(m_run, bmax);
         if (__any(m_new > m_run)) {  // exact: corr == 1 for every lane otherwise
@@ -557,16 +566,21 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
             for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
             m_run = m_new;
         }
-        float bsum = 0.f;
+        // s - m and the row sum on packed pairs (v_pk_add_f32: half the issue slots)
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const f2v nm2 = {-m_run, -m_run};
+        f2v bsum2 = {0.f, 0.f};
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float e = fast_exp2(s[sub][r] - m_run);
-                s[sub][r] = e;
-                bsum += e;
+            for (int r = 0; r < 16; r += 2) {
+                const f2v arg = (f2v){s[sub][r], s[sub][r + 1]} + nm2;
+                const f2v e = {fast_exp2(arg.x), fast_exp2(arg.y)};
+                s[sub][r] = e.x;
+                s[sub][r + 1] = e.y;
+                bsum2 += e;
             }
-        l_run += halves_sum(bsum);
+        l_run += halves_sum(bsum2.x + bsum2.y);
 
         __syncthreads();  // every wave is done with K(t) / regions(t)
         if (has_next) {
@@ -662,13 +676,6 @@ __device__ __forceinline__ int vimg_off(int r, int ch) {
 
 typedef short shortx4 __attribute__((ext_vector_type(4)));
 
-// v_max3_f32 as written: fmaxf() on MFMA results makes the compiler insert canonicalising
-// v_max_f32 x, x first (scores are finite products, no signalling NaNs to quieten)
-__device__ __forceinline__ float max3_raw(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
 
 __global__ void __launch_bounds__(kThreads, 2)
 win_attn_bf16_v2_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __restrict__ k,
@@ -1083,16 +1090,23 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
             for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
             m_run = m_new;
         }
-        float bsum = 0.f;
+        // exponent arguments s * c - m and the row sum on packed pairs (v_pk_fma_f32 / v_pk_add_f32:
+        // half the issue slots of the scalar forms)
+        typedef float f2v __attribute__((ext_vector_type(2)));
+        const f2v c2 = {cl2, cl2}, nm2 = {-m_run, -m_run};
+        f2v bsum2 = {0.f, 0.f};
 #pragma unroll
         for (int ksx = 0; ksx < 4; ++ksx)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-                const float ex = fast_exp2(fmaf(sacc[ksx >> 1][8 * (ksx & 1) + e], cl2, -m_run));
-                bsum += ex;
-                pf[ksx][e] = (__bf16)ex;
+            for (int e = 0; e < 8; e += 2) {
+                const f2v sv = {sacc[ksx >> 1][8 * (ksx & 1) + e], sacc[ksx >> 1][8 * (ksx & 1) + e + 1]};
+                const f2v arg = __builtin_elementwise_fma(sv, c2, nm2);
+                const f2v ex = {fast_exp2(arg.x), fast_exp2(arg.y)};
+                bsum2 += ex;
+                pf[ksx][e] = (__bf16)ex.x;
+                pf[ksx][e + 1] = (__bf16)ex.y;
             }
-        l_run += halves_sum(bsum);
+        l_run += halves_sum(bsum2.x + bsum2.y);
         lds_barrier();
         return false;
     };
