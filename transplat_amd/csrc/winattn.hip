@@ -1090,23 +1090,18 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
             for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
             m_run = m_new;
         }
-        // exponent arguments s * c - m and the row sum on packed pairs (v_pk_fma_f32 / v_pk_add_f32:
-        // half the issue slots of the scalar forms)
-        typedef float f2v __attribute__((ext_vector_type(2)));
-        const f2v c2 = {cl2, cl2}, nm2 = {-m_run, -m_run};
-        f2v bsum2 = {0.f, 0.f};
+        // scalar fma per score: the packed v_pk_fma / v_pk_add form measured 1.5 us slower at B = 16
+        // (same box, profiles/r4/g22: 53.9 / 54.3 vs 52.2 / 52.9 us)
+        float bsum = 0.f;
 #pragma unroll
         for (int ksx = 0; ksx < 4; ++ksx)
 #pragma unroll
-            for (int e = 0; e < 8; e += 2) {
-                const f2v sv = {sacc[ksx >> 1][8 * (ksx & 1) + e], sacc[ksx >> 1][8 * (ksx & 1) + e + 1]};
-                const f2v arg = __builtin_elementwise_fma(sv, c2, nm2);
-                const f2v ex = {fast_exp2(arg.x), fast_exp2(arg.y)};
-                bsum2 += ex;
-                pf[ksx][e] = (__bf16)ex.x;
-                pf[ksx][e + 1] = (__bf16)ex.y;
+            for (int e = 0; e < 8; ++e) {
+                const float ex = fast_exp2(fmaf(sacc[ksx >> 1][8 * (ksx & 1) + e], cl2, -m_run));
+                bsum += ex;
+                pf[ksx][e] = (__bf16)ex;
             }
-        l_run += halves_sum(bsum2.x + bsum2.y);
+        l_run += halves_sum(bsum);
         lds_barrier();
         return false;
     };
