@@ -63,6 +63,28 @@ __device__ __forceinline__ float halves_sum(float x) {
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+#ifndef TSPLAT_WA_STAMP
+#define TSPLAT_WA_STAMP 0  // diagnostic builds only (tools/build_stamp_wa.sh): per-workgroup phase clocks
+#endif
+#if TSPLAT_WA_STAMP
+// [workgroup][16] uint64, written by thread 0 with vector stores: 0 wall clock at entry, 1 HW_ID |
+// XCC_ID << 32, 2 shader clock at entry, 3 after the prologue barrier, 4 + t after key tile t
+// (t < 8), 12 after the epilogue, 13 wall clock at the end
+__device__ unsigned long long* g_wa_stamps = nullptr;
+#define WA_STAMP(slot, val)                                                                          \
+    do {                                                                                             \
+        if (threadIdx.x == 0 && g_wa_stamps)                                                         \
+            g_wa_stamps[(size_t)(blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z)) * 16 \
+                        + (slot)] = (val);                                                           \
+    } while (0)
+#define WA_CLOCK() ((unsigned long long)__builtin_readcyclecounter())
+#define WA_HWID()                                                                                    \
+    ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |                      \
+     ((unsigned long long)(unsigned)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32))
+#else
+#define WA_STAMP(slot, val) do {} while (0)
+#endif
+
 constexpr int kC = 128;          // channels (d_model of the reference transformer)
 constexpr int kBQ = 64;          // queries per workgroup
 constexpr int kBK = 64;          // keys per LDS tile
@@ -418,7 +440,9 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // Staging is the T14 split of the key-pair kernel below: K(t+1) is loaded into registers during
 // QK(t) and stored after the barrier that retires K(t); the same registers then carry V(t+1)
-// during PV(t). Two barriers per tile, two workgroups per CU.
+// during PV(t). Two barriers per tile, two workgroups per CU. (Round 4, measured slower and
+// removed: Q and K by LDS-DMA in whole-row pieces with per-key offset tables, 60.4 vs 57.7 us at
+// b = 2 -- the per-lane row gathers are not what bounds the prologue; profiles/r4/g25.)
 __global__ void __launch_bounds__(kThreads, 2)
 win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __restrict__ k,
                        const float* __restrict__ v, float* __restrict__ out, Partials part) {
@@ -426,6 +450,9 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
     __shared__ __attribute__((aligned(16))) float sVt[kC * kVtStride];
     __shared__ __attribute__((aligned(16))) int sKeyRegion[kBK];
 
+    WA_STAMP(0, wall_clock64());
+    WA_STAMP(1, WA_HWID());
+    WA_STAMP(2, WA_CLOCK());
     int qblk, wi, bz;
     xcd_block_coords(qblk, wi, bz);
     const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
@@ -511,6 +538,7 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
         store_v();
     }
     __syncthreads();
+    WA_STAMP(3, WA_CLOCK());
     for (int k0 = kbeg; k0 < kend; k0 += kBK) {
         const bool has_next = k0 + kBK < kend;
         if (has_next) load_k(k0 + kBK);
@@ -608,6 +636,7 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
                 }
         __syncthreads();  // every wave is done with V(t); K(t+1) is visible
         if (has_next) store_v();  // read after the next tile's first barrier
+        if ((k0 - kbeg) / kBK < 8) WA_STAMP(4 + (k0 - kbeg) / kBK, WA_CLOCK());
     }
 
     // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
@@ -635,6 +664,8 @@ win_attn_f32x32_kernel(Params p, const float* __restrict__ q, const float* __res
             part.l[row] = l_run;
         }
     }
+    WA_STAMP(12, WA_CLOCK());
+    WA_STAMP(13, wall_clock64());
 }
 
 
@@ -1284,6 +1315,14 @@ extern "C" int tsplat_win_attn_partials_fwd(const float* q, const float* k, cons
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
+
+#if TSPLAT_WA_STAMP
+// diagnostic builds only: buffer of [workgroups][16] uint64 the next x32 launches stamp (null = off)
+extern "C" int tsplat_win_attn_stamps(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(tsplat::winattn::g_wa_stamps), &buf, sizeof(buf)) == hipSuccess
+               ? TSPLAT_OK : TSPLAT_EINVAL;
+}
+#endif
 
 extern "C" size_t tsplat_win_attn_bf16_workspace_bytes(int32_t batch, int32_t height, int32_t width,
                                                        int32_t key_views, int32_t splits) {
