@@ -233,7 +233,8 @@ def tf32_round(t: torch.Tensor) -> torch.Tensor:
 @pytest.mark.parametrize("form", ["auto", "1", "2", "3", "4", "5"])
 @pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES + [(1, 24, 48, 10, 96, True, "relu"),
                                                                (2, 40, 64, 22, 136, False, "none"),
-                                                               (3, 32, 40, 36, 64, True, "gelu")])
+                                                               (3, 32, 40, 36, 64, True, "gelu"),
+                                                               (2, 32, 32, 160, 160, True, "relu")])
 def test_conv3x3_wino_bf16x3_kernel(device, monkeypatch, stage, form, n, ci, co, h, w, bias, act):
     """Winograd F(2x2, 3x3) in split-bf16 precision (tsplat_conv3x3_wino_bf16x3_fwd: hi*hi + hi*lo +
     lo*hi on bf16 MFMA, fp32 accumulation) against torch's conv2d in float64, with the launch's own
@@ -294,16 +295,20 @@ def test_conv3x3_wino_bf16x3_relu_in_residual(device, monkeypatch, stage, n, c, 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("wgs", ["3", "7", "512"])
-def test_conv3x3_wino_bf16x3_persistent_walk(device, monkeypatch, wgs):
+@pytest.mark.parametrize("chans", [(24, 16), (16, 16), (12, 8)])
+def test_conv3x3_wino_bf16x3_persistent_walk(device, monkeypatch, wgs, chans):
     """The persistent form (TSPLAT_WINO3_FORM=5) with 3 / 7 / 512 workgroups per output block
     (TSPLAT_WINO3_PWG): each workgroup's flat (tile block, chunk) sequence crosses image and
-    concatenation-source boundaries; ReLU-on-load and both residuals in the epilogue; against float64."""
+    concatenation-source boundaries; ReLU-on-load and both residuals in the epilogue; against float64.
+    Inputs of 40 channels (three 16-channel chunks) and of 32 / 20 (two chunks: the A fragments held
+    in registers for the whole walk)."""
     from transplat_amd import kernels as K
 
     monkeypatch.setenv("TSPLAT_WINO3_FORM", "5")
     monkeypatch.setenv("TSPLAT_WINO3_PWG", wgs)
-    parts = [seeded((3, c, 40, 72), 120 + c) for c in (24, 16)]
-    wt = seeded((48, 40, 3, 3), 131) * (1.0 / (9 * 40) ** 0.5)
+    ci = sum(chans)
+    parts = [seeded((3, c, 40, 72), 120 + c + 7 * i) for i, c in enumerate(chans)]
+    wt = seeded((48, ci, 3, 3), 131) * (1.0 / (9 * ci) ** 0.5)
     b = seeded((48,), 132)
     r1, r2 = seeded((3, 48, 40, 72), 133), seeded((3, 48, 40, 72), 134)
     x = torch.cat(parts, 1)

@@ -829,8 +829,10 @@ static int pick_form(int n, int th, int tw, int co) {
     // blocks): the 64 x 64 form above 128 workgroups (2 x 128 -> 64 at 144^2, 162 of them: 30.8 vs
     // 38.1 us for 32 x 32; at 128 -- 64 -> 64 at 128^2, 128 -> 256 at 64^2 -- half the CUs idle and
     // 32 x 32 wins), two k-groups where 32 x 32 workgroups would leave CUs idle, else 32 x 32 (the
-    // persistent form measured 24.3 vs 23.1 us at 32 -> 32 / 256^2 once blocks were XCD-ordered; the
-    // 32 x 64 form never)
+    // persistent form measured 24.3 vs 23.1 us at 32 -> 32 / 256^2 once blocks were XCD-ordered, and
+    // 23.9 vs 23.2 us with both chunks' A fragments held in registers for the whole walk, i.e. the
+    // packed-U stream is not what bounds these few-channel maps, profiles/r4/g28; the 32 x 64 form
+    // never)
     const long tiles = (long)n * th * tw;
     const int cob32 = (co + 31) / 32;
     const long wg64 = (tiles + 63) / 64 * ((co + 63) / 64);
