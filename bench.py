@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--no-conv-search", action="store_true",
                     help="MIOpen's default convolution algorithm choice instead of its measured search "
                          "(torch.backends.cudnn.benchmark, on by default: +2.4%% e2e at b = 1)")
+    ap.add_argument("--conv-deterministic", action="store_true",
+                    help="only MIOpen's run-to-run deterministic solvers for the convolutions left on it "
+                         "(torch.backends.cudnn.deterministic; the DPT's MIOpen convolutions vary in the last "
+                         "bits otherwise, tools/determinism_probe.py): C2 386 vs 407 views/s, profiles/r4/g32")
     return ap.parse_args()
 
 
@@ -372,6 +376,7 @@ def main():
         dtype_label += f" + {attn_dtype} attention + fp32 raster"
     if not args.no_conv_search:
         torch.backends.cudnn.benchmark = True
+    torch.backends.cudnn.deterministic = args.conv_deterministic
     from transplat_amd import _lib
 
     _lib.load()

@@ -25,4 +25,8 @@ def device():
 
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
+    # deterministic MIOpen solvers for the convolutions left on the library (the DPT's 1x1s varied run
+    # to run otherwise: tools/determinism_probe.py), so the measured errors the parity bounds are
+    # derived from are reproducible
+    torch.backends.cudnn.deterministic = True
     return torch.device("cuda:0")

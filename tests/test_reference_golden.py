@@ -329,9 +329,12 @@ def test_encoder_gpu_vs_reference(device, dense):
     _check_encoder(_encoder(device, dense), ENCODER_GPU_TOL[dense], f" (GPU, dense {dense})")
 
 
-# measured on MI355X (profiles/r4/pytest_e2e_x3.log): fp32 means 6.5e-6, covariances 3.1e-6, harmonics
-# 2.9e-6, opacities 2.3e-6; bf16x3 5.6e-5 / 2.7e-5 / 3.4e-5 / 3.1e-5 -- bounds 2x the largest, rounded up
-ENCODER_GPU_TOL = {"fp32": 1.5e-5, "bf16x3": 1.2e-4}
+# measured on MI355X with MIOpen's deterministic solvers (tests/conftest.py; reproducible run to run,
+# profiles/r4/g32/enc_repeat_det.log): fp32 means 8.3e-6, covariances 3.9e-6, harmonics 3.2e-6, opacities
+# 2.5e-6; bf16x3 1.56e-4 / 7.5e-5 / 3.9e-5 / 3.4e-5 -- bounds 2x the largest of each precision, rounded
+# up. (With the library's default solvers the DPT's 1x1 / transposed convolutions vary in the last bits
+# and the bf16x3 errors spread over 0.8-1.7e-4 from run to run: profiles/r4/g30/enc_repeat.log.)
+ENCODER_GPU_TOL = {"fp32": 1.7e-5, "bf16x3": 3.2e-4}
 
 
 # --------------------------------------------------------------------------- .ply export
