@@ -510,6 +510,7 @@ _CONV_PACKED: dict = {}
 _CONV_MODE = os.environ.get("TSPLAT_CONV", "auto")
 _CONV_KSPLIT = int(os.environ.get("TSPLAT_CONV_KSPLIT", "0"))  # tuning override (tools/bench_conv.py)
 _CONV_MAX_FLOP = 1.5e9  # above this MIOpen's kernels are as fast or faster (tools/bench_conv.py)
+_SMALL_MAP_DIRECT = os.environ.get("TSPLAT_CONV_SMALLMAP", "1") == "1"
 # 1x1 launch shape: grid cap in waves and minimum ci pairs per wave. Same-box A/B (tools/sessions/archive/ab_conv1.sh):
 # 16384 / 8 reads 338.98 / 338.99 views/s vs 337.91 / 337.58 for the 3x3 rule (4096 / 16); 8192 / 16
 # and 16384 / 4 sit in between
@@ -569,6 +570,8 @@ def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsa
     flop = 2.0 * npx * co * ci * k * k
     # (since the batch loads are scheduled ahead of the MFMAs, the few-tile / long-reduction 3x3s
     # -- 2 x 256 -> 128 at 16^2 -- also beat MIOpen: 23.5 vs 25.7 us, bench_conv.py)
+    if _SMALL_MAP_DIRECT and npx <= 512:
+        return True  # tiny maps with long reductions (the DPT's 768 -> 768 stride-2 at 18^2, 1.7 GFLOP)
     return flop <= _CONV_MAX_FLOP
 
 
