@@ -62,11 +62,12 @@ def parse():
     ap.add_argument("--no-conv-search", action="store_true",
                     help="MIOpen's default convolution algorithm choice instead of its measured search "
                          "(torch.backends.cudnn.benchmark, on by default: +2.4%% e2e at b = 1)")
-    ap.add_argument("--conv-nondeterministic", action="store_true",
-                    help="let MIOpen use run-to-run nondeterministic solvers for the convolutions left on it "
-                         "(default: torch.backends.cudnn.deterministic, so the step's outputs are reproducible -- "
-                         "the DPT's MIOpen convolutions varied in the last bits otherwise, tools/determinism_probe.py; "
-                         "same speed since the DPT's stride-2 3x3 runs on the direct kernel, profiles/r4/g36)")
+    ap.add_argument("--conv-deterministic", action="store_true",
+                    help="only MIOpen's run-to-run deterministic solvers for the convolutions left on it "
+                         "(torch.backends.cudnn.deterministic; the DPT's MIOpen convolutions vary in the last bits "
+                         "otherwise, tools/determinism_probe.py). Free for C2 in bf16x3 mode (406.5 vs 407.0 "
+                         "views/s, profiles/r4/g36), but MIOpen's deterministic choices collapse exact-fp32 C2 "
+                         "(22.8 views/s) and the bf16-dense C3 variant (53.4): profiles/r4/final_det/")
     return ap.parse_args()
 
 
@@ -377,7 +378,7 @@ def main():
         dtype_label += f" + {attn_dtype} attention + fp32 raster"
     if not args.no_conv_search:
         torch.backends.cudnn.benchmark = True
-    torch.backends.cudnn.deterministic = not args.conv_nondeterministic
+    torch.backends.cudnn.deterministic = args.conv_deterministic
     from transplat_amd import _lib
 
     _lib.load()
