@@ -442,14 +442,6 @@ int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const int32_t* c
  * [x_hi | x_hi | x_lo] [W_hi | W_lo | W_hi]^T = x_hi W_hi^T + x_hi W_lo^T + x_lo W_hi^T. */
 int tsplat_split_bf16x3(const float* x, void* out, int64_t rows, int32_t k, int32_t weight_order, void* stream);
 
-/* y [M, N] = act(x W^T + bias) in bf16x3 precision for the fp32 path's small-M linears (DINOv2
- * qkv / proj / fc1 + GELU / fc2 at M = 650, src/depth_anything_v2/dinov2_layers/{attention,mlp}.py;
- * nn.Linear.forward, which the reference runs in TF32, src/main.py:15): x [M, K] fp32 (split into
- * hi / lo bf16 as it is staged), w_packed = tsplat_split_bf16x3(W, weight_order = 1) ([N][3K] bf16),
- * bias fp32 [N] or null, act 0 none / 2 GELU (erf); N % 64 == 0, K % 32 == 0. */
-int tsplat_linear_bf16x3_fwd(const float* x, const void* w_packed, const float* bias, float* y, int32_t M, int32_t N,
-                             int32_t K, int32_t act, void* stream);
-
 /* bf16 3x3 / 1x1 convolution (stride 1, padding ksize / 2) for config C3 (bf16 autocast of the same
  * reference nn.Conv2d layers: ldm_unet/unet.py ResBlock in/out convolutions and 1x1 skips
  * unet.py:212-266, Upsample unet.py:105-137, the output blocks' skip concatenation unet.py:1130,

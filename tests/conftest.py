@@ -27,6 +27,21 @@ def device():
         pytest.skip("no HIP device")
     # deterministic MIOpen solvers for the convolutions left on the library (the DPT's 1x1s varied run
     # to run otherwise: tools/determinism_probe.py), so the measured errors the parity bounds are
-    # derived from are reproducible
+    # derived from are reproducible; restored at the end of the session. The bench's own solver
+    # settings (benchmark on, deterministic off) are covered by the `bench_solvers` fixture.
+    prev = torch.backends.cudnn.deterministic
     torch.backends.cudnn.deterministic = True
-    return torch.device("cuda:0")
+    yield torch.device("cuda:0")
+    torch.backends.cudnn.deterministic = prev
+
+
+@pytest.fixture
+def bench_solvers(device):
+    """bench.py's default MIOpen settings for one test (cudnn.benchmark on, deterministic off: the
+    solvers the headline number runs), restored afterwards."""
+    import torch
+
+    prev = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = False, True
+    yield device
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = prev

@@ -37,3 +37,21 @@ def test_library_reports_version_and_workspace_without_gpu():
     assert lib.tsplat_version() >= 1
     nb = lib.tsplat_raster_workspace_bytes(131072, 3, 256, 256, 1 << 20)
     assert nb >= (1 << 20) * 8 + 3 * 131072 * 40
+
+
+def test_debug_mode_refuses_graph_capture():
+    """TSPLAT_DEBUG=1 / tsplat_set_debug syncs after every launch, which hipGraph capture forbids:
+    GraphedStep (bench.py's default) refuses up front instead of failing inside the capture."""
+    import pytest
+
+    from transplat_amd.e2e import GraphedStep
+
+    lib = _lib.load()
+    was = lib.tsplat_set_debug(1)
+    try:
+        assert _lib.debug_enabled()
+        with pytest.raises(RuntimeError, match="cannot be captured"):
+            GraphedStep(None, {})
+    finally:
+        lib.tsplat_set_debug(was)
+    assert _lib.debug_enabled() == bool(was)

@@ -348,10 +348,9 @@ def test_conv3x3_wino_bf16x3_concat_and_production_size(device):
                                            (8192, 256, 1024, False, "none"), (33, 64, 64, True, "gelu"),
                                            (20, 64, 128, True, "gelu")])
 def test_linear_bf16x3_kernel(device, m, k, n, bias, act):
-    """tsplat_linear_bf16x3_fwd (DINOv2's linears in the bf16x3 dense mode: x split while staged, W
-    packed [hi | lo | hi]) against float64 F.linear (+ exact GELU): within 2e-5 of max |y| and at
-    most 1/8 of the TF32-operand error (tolerances written here); 64- and 32-row workgroups, M not
-    a multiple of the block."""
+    """kernels.linear_bf16x3 (tsplat_split_bf16x3 + one hipBLASLt bf16 GEMM over K' = 3K, the
+    correlation table's form) against float64 F.linear (+ exact GELU): within 2e-5 of max |y| and
+    at most 1/8 of the TF32-operand error (tolerances written here); M not a multiple of a tile."""
     from transplat_amd import kernels as K
 
     x = seeded((m, k), 81)

@@ -92,7 +92,6 @@ SIGNATURES = {
     "tsplat_conv3x3_wino_bf16x3_cat_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P] + [_I32] * 5 + [_P]),
     "tsplat_conv3x3_wino_bf16x3_ex_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P] + [_I32] * 6 + [_P]),
     "tsplat_split_bf16x3": (ctypes.c_int, [_P, _P, ctypes.c_int64, _I32, _I32, _P]),
-    "tsplat_linear_bf16x3_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _P]),
     "tsplat_conv2d_bf16_weight_bytes": (ctypes.c_size_t, [_I32, _I32, _I32]),
     "tsplat_conv2d_bf16_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P] + [_I32] * 7 + [_P]),
 }
@@ -127,6 +126,15 @@ def load(build_if_missing: bool = False):
         lib.tsplat_set_debug(1)
     _lib = lib
     return lib
+
+
+def debug_enabled() -> bool:
+    """Whether tsplat_set_debug mode is on (it synchronises after every launch, which stream capture
+    forbids: callers that capture a hipGraph refuse to while it is on)."""
+    lib = load()
+    was = lib.tsplat_set_debug(1)
+    lib.tsplat_set_debug(was)
+    return bool(was)
 
 
 def check(status: int, what: str) -> None:

@@ -111,6 +111,12 @@ class GraphedStep:
     replays; outputs are the graph's static output tensors (valid until the next replay)."""
 
     def __init__(self, model: TransplatModel, example: dict, warmup: int = 2):
+        from . import _lib
+
+        if _lib.debug_enabled():  # its per-launch hipDeviceSynchronize is illegal inside a capture
+            raise RuntimeError("tsplat debug mode (TSPLAT_DEBUG=1 / tsplat_set_debug) synchronises after every "
+                               "launch and cannot be captured into a hipGraph: run the step eagerly "
+                               "(bench.py --no-graph, graph=False)")
         self.model = model
         self.static = _clone_batch(example)
         side = torch.cuda.Stream()
@@ -149,7 +155,9 @@ def precision_label(dense_dtype: str, attn_dtype: str = "auto") -> str:
     attn = attn_dtype if attn_dtype != "auto" else ("bf16" if dense_dtype == "bf16" else "fp32")
     dense = {"fp32": "exact fp32", "bf16x3": "bf16x3 (split-bf16 products, fp32 accumulation; >= TF32)",
              "bf16": "bf16 (autocast)"}[dense_dtype]
-    return (f"dense convs/GEMMs {dense}, window attention {attn}, correlation / norms / adapter / raster fp32"
+    corr = ("correlation table bf16x3 (split-bf16 GEMM), correlation gathers / norms / adapter / raster fp32"
+            if dense_dtype == "bf16x3" else "correlation / norms / adapter / raster fp32")
+    return (f"dense convs/GEMMs {dense}, window attention {attn}, {corr}"
             + ("; DPT-head / stem / transposed convs on MIOpen exact fp32" if dense_dtype == "bf16x3" else ""))
 
 

@@ -511,12 +511,12 @@ _CONV_MODE = os.environ.get("TSPLAT_CONV", "auto")
 _CONV_KSPLIT = int(os.environ.get("TSPLAT_CONV_KSPLIT", "0"))  # tuning override (tools/bench_conv.py)
 _CONV_MAX_FLOP = 1.5e9  # above this MIOpen's kernels are as fast or faster (tools/bench_conv.py)
 _SMALL_MAP_DIRECT = os.environ.get("TSPLAT_CONV_SMALLMAP", "1") == "1"
-# 1x1 launch shape: grid cap in waves and minimum ci pairs per wave. Same-box A/B (tools/sessions/archive/ab_conv1.sh):
+# 1x1 launch shape: grid cap in waves and minimum ci pairs per wave. Same-box A/B (round-2 session script ab_conv1.sh, pruned in round 5):
 # 16384 / 8 reads 338.98 / 338.99 views/s vs 337.91 / 337.58 for the 3x3 rule (4096 / 16); 8192 / 16
 # and 16384 / 4 sit in between
 _CONV1_WAVES = int(os.environ.get("TSPLAT_CONV1_WAVES", "16384"))
 _CONV1_PAIRS = int(os.environ.get("TSPLAT_CONV1_PAIRS", "8"))
-# the same for 3x3 (tools/sessions/archive/ab_conv3.sh, same box: 8192 / 2 reads 340.3 / 339.7 views/s vs 339.3 /
+# the same for 3x3 (round-2 session script ab_conv3.sh, pruned in round 5, same box: 8192 / 2 reads 340.3 / 339.7 views/s vs 339.3 /
 # 339.2 at 4096 / 2; 16384 / 1 and 8192 / 1 in between)
 _CONV3_WAVES = int(os.environ.get("TSPLAT_CONV3_WAVES", "8192"))
 _CONV3_PAIRS = int(os.environ.get("TSPLAT_CONV3_PAIRS", "2"))
@@ -718,9 +718,11 @@ _DENSE = "fp32"
 _DENSE_MODES = ("fp32", "bf16x3")
 
 
-# bf16x3 mode's library fp32 GEMMs (F.linear / matmul on hipBLASLt): with TSPLAT_XF32=1 they run
-# with torch's allow_tf32, which on gfx950 selects hipBLASLt's emulated-xf32 kernels (fp32 in / out,
-# bf16 MFMA; tools/bench_xf32.py measures their error next to the split kernels')
+# bf16x3 mode's OTHER library fp32 GEMMs (the ones linear_xf32 below does not admit): with
+# TSPLAT_XF32=1 the whole dense_precision("bf16x3") block runs with torch's allow_tf32, which on
+# gfx950 selects hipBLASLt's emulated-xf32 kernels (fp32 in / out, bf16 MFMA; tools/bench_xf32.py
+# measures their error next to the split kernels'). Off by default; independently of it, the linears
+# linear_xf32_ok admits (on by default, TSPLAT_LINX) always run under allow_tf32 -- see linear_xf32.
 _XF32 = os.environ.get("TSPLAT_XF32", "0") == "1"
 
 
@@ -804,24 +806,16 @@ def _split_weight(weight):
     return packed
 
 
-def linear_bf16x3(x, weight, bias=None, act: str = "none", out=None, cache: bool = True):
-    """act(F.linear(x, weight, bias)) in split-bf16 precision (act "none" or "gelu", exact erf):
-    tsplat_linear_bf16x3_fwd where the shape fits (N % 64 == 0, K % 32 == 0: x split while it is
-    staged, W packed once per version -- cache=False packs it for this call only, for a weight that
-    is an activation), else ONE hipBLASLt bf16 GEMM with K' = 3K on [x_hi | x_hi | x_lo] and
-    [W_hi | W_lo | W_hi] (fp32 accumulation and output). out: a contiguous [M, N] fp32 destination."""
-    lib = _lib.load()
+def linear_bf16x3(x, weight, bias=None, act: str = "none", cache: bool = True):
+    """act(F.linear(x, weight, bias)) in split-bf16 precision (act "none" or "gelu", exact erf) as ONE
+    hipBLASLt bf16 GEMM with K' = 3K on [x_hi | x_hi | x_lo] and [W_hi | W_lo | W_hi] (fp32
+    accumulation and output); W packed once per version (cache=False: for this call only, for a
+    weight that is an activation). Round 4's hand-written split GEMM for DINOv2's M = 650 linears
+    (csrc/gemm3.hip) measured slower than the library in the step (C2 381 vs 394 views/s,
+    profiles/r4/g12/: at M = 650 bf16x3 cuts the MFMA cycles but not the fp32-sized operand bytes)
+    and was removed from the library in round 5."""
     k, n = x.shape[-1], weight.shape[0]
     w3 = _split_weight(weight) if cache else split_bf16x3(weight, weight_order=True)
-    if n % 64 == 0 and k % 32 == 0:
-        xf = _f32(x).reshape(-1, k)
-        y = out if out is not None else torch.empty((xf.shape[0], n), dtype=torch.float32, device=x.device)
-        if y.dtype != torch.float32 or not y.is_contiguous() or y.numel() != xf.shape[0] * n:
-            raise ValueError("linear_bf16x3: out must be a contiguous fp32 [M, N] tensor")
-        bb = _f32(bias) if bias is not None else None
-        _lib.check(lib.tsplat_linear_bf16x3_fwd(_lib.ptr(xf), _lib.ptr(w3), _lib.ptr(bb), _lib.ptr(y), xf.shape[0], n, k,
-                                                _ACTS[act], _lib.stream_ptr(x.device)), "tsplat_linear_bf16x3_fwd")
-        return y.reshape(*x.shape[:-1], n)
     x3 = split_bf16x3(x).reshape(-1, 3 * k)
     with torch.autocast("cuda", enabled=False):
         if bias is not None:
@@ -832,27 +826,6 @@ def linear_bf16x3(x, weight, bias=None, act: str = "none", out=None, cache: bool
     if act == "gelu":
         y = torch.nn.functional.gelu(y)
     return y
-
-
-# tsplat_linear_bf16x3_fwd for nn.Linear in bf16x3 mode: OFF by default (TSPLAT_LIN3=1 turns it on;
-# linear_xf32 above takes the large linears first). Measured on the step's linears
-# (tools/bench_split_gemm.py; profiles/r4/split_gemm2.log, profiles/r4/g12/split_gemm.log): hipBLASLt's
-# bf16 GEMM at K' = 3K (DINOv2 qkv 23.9 vs 29.0 us fp32, proj 23.9 vs 19.0, fc1 27.3 vs 30.4, fc2 29.3 vs
-# 27.8); the first kernel form 37.3 / 24.8 / 51.9 / 83.6 us (one 32-deep chunk of register prefetch:
-# a full L2 round trip per chunk); the pipelined LDS-DMA form 22.4 / 20.1 / 38.6 / 60.7 us and C2 381
-# vs 394 views/s with it dispatched (profiles/r4/g12/): a 64 x 128 tile needs 48 KB of operands per
-# 64-deep stage against 24 bf16 MFMAs per wave, ~62 B per CU cycle, while a CU ingests ~25 GB/s
-# (~11 B/cycle) here -- bf16x3 cuts the MFMA cycles but not the fp32-sized operand bytes, so at
-# M = 650 these GEMMs stay bound by operand delivery, where the library is already tuned.
-_LIN3 = os.environ.get("TSPLAT_LIN3", "0") == "1"
-_LIN3_MIN_FLOP = float(os.environ.get("TSPLAT_LIN3_MIN_FLOP", "2e8"))
-
-
-def linear_ok(x, weight) -> bool:
-    """True when linear_forward takes the bf16x3 kernel for F.linear(x, weight) in the current mode."""
-    return (_LIN3 and _DENSE == "bf16x3" and x.is_cuda and x.dtype == torch.float32 and weight.dtype == torch.float32
-            and not torch.is_autocast_enabled("cuda") and weight.shape[0] % 128 == 0 and x.shape[-1] % 64 == 0
-            and 2.0 * x.numel() * weight.shape[0] >= _LIN3_MIN_FLOP)
 
 
 # Library fp32 GEMMs in bf16x3 mode: hipBLASLt's emulated-xf32 kernels (fp32 in / out on bf16 MFMA;
@@ -897,14 +870,11 @@ def linear_xf32(x, weight, bias=None, act: str = "none"):
 
 def linear_forward(mod, x):
     """nn.Linear.forward (installed by install_linear_dispatch): in dense_precision("bf16x3") the
-    fp32 linears that linear_xf32_ok admits run as linear_xf32, those linear_ok admits as
-    linear_bf16x3; everything else is F.linear."""
+    fp32 linears that linear_xf32_ok admits run as linear_xf32; everything else is F.linear."""
     import torch.nn.functional as F
 
     if linear_xf32_ok(x, mod.weight):
         return linear_xf32(x, mod.weight, mod.bias)
-    if linear_ok(x, mod.weight):
-        return linear_bf16x3(x, mod.weight, mod.bias)
     return F.linear(x, mod.weight, mod.bias)
 
 
@@ -989,7 +959,7 @@ def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=(), precision: s
     rc = lib.tsplat_conv3x3_wino_cat_f32_fwd(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p),
                                              len(srcs), _lib.ptr(wino_pack_weight(weight)), _lib.ptr(pb),
                                              _lib.ptr(y), n, h, w, co, _WINO_ACT[act], _lib.stream_ptr(x.device))
-    _lib.check(rc, "tsplat_conv3x3_wino_f32_cat_fwd")
+    _lib.check(rc, "tsplat_conv3x3_wino_cat_f32_fwd")
     return y
 
 

@@ -7,10 +7,12 @@ available (and its version is unpinned), so its published construction is restat
     with the (-i)^l phase, which cancels) -> real so(3) generators X_x, X_y, X_z;
   * wigner_D = exp(alpha X_y) exp(beta X_x) exp(gamma X_y)  (Y-X-Y Euler angles);
   * matrix_to_angles: beta/alpha from R e_y (xyz_to_angles), gamma from the residual rotation.
-The only in-repo pin (reference src/misc/fast_sh_rotation.py:56-60,217-228) is D^1 = R with rows
-and columns permuted to (y, z, x); tests/test_sh_rotation.py checks it plus the representation
-properties (orthogonality, D(R1 R2) = D(R1) D(R2)) for l <= 4. Higher degrees are "parity
-unpinned" against e3nn itself.
+The restated construction gives D^1 = R itself in e3nn's real basis, and that is what
+tests/test_sh_rotation.py asserts, together with the representation properties (orthogonality,
+D(R1 R2) = D(R1) D(R2)) for l <= 4. The reference's own, unasserted script
+(src/misc/fast_sh_rotation.py:56-60,217-228) claims D^1 = R with rows and columns permuted to
+(y, z, x) instead; the two disagree, and which convention the trained checkpoint saw cannot be settled
+without e3nn (absent, version unpinned): A4 is "parity unpinned" against e3nn itself.
 The D matrices are built per camera in float64 (a handful of 9x9 exponentials) and applied to the
 per-pixel coefficients as one batched contraction.
 """

@@ -55,11 +55,9 @@ class Mlp(nn.Module):
     def forward(self, x):
         if type(self.act) is nn.GELU and self.act.approximate == "none":
             # bf16x3 dense mode: fc1 on hipBLASLt's emulated-xf32 GEMM + bias + exact GELU in one pass
-            # (kernels.linear_xf32), or fc1 + bias + GELU in one tsplat_linear_bf16x3_fwd launch
+            # (kernels.linear_xf32)
             if kernels.linear_xf32_ok(x, self.fc1.weight):
                 return self.fc2(kernels.linear_xf32(x, self.fc1.weight, self.fc1.bias, act="gelu"))
-            if kernels.linear_ok(x, self.fc1.weight):
-                return self.fc2(kernels.linear_bf16x3(x, self.fc1.weight, self.fc1.bias, act="gelu"))
         return self.fc2(self.act(self.fc1(x)))
 
 

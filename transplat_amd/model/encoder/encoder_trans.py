@@ -70,8 +70,9 @@ class EncoderTransCfg:
     # Arithmetic of the conv / GEMM layers around the hand-written kernels (CNN, cam encoders,
     # DA-V2, U-Nets, heads): "fp32" (exact fp32, parity mode), "bf16x3" (split-bf16 products with
     # fp32 accumulation -- the stand-in for the reference's TF32, src/main.py:15, more precise than
-    # it; kernels.dense_precision) or "bf16" (autocast). Correlation and the rasterizer always run
-    # fp32.
+    # it; kernels.dense_precision) or "bf16" (autocast). The rasterizer and the correlation gathers
+    # always run fp32; the fine-cross correlation TABLE is a dense GEMM and follows dense_dtype
+    # (bf16x3: one split-bf16 hipBLASLt GEMM over K' = 3K, kernels.uv_cross).
     dense_dtype: str = "fp32"
     # Window attention (T2): "auto" (bf16 MFMA under bf16 dense layers, else exact fp32), "fp32" or
     # "bf16" (config C3 as BASELINE.json states it: bf16 attention beside fp32-class dense layers).
