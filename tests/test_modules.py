@@ -47,9 +47,50 @@ def _run(dev, fn):
         return fn(dev)
 
 
-# GPU module-golden bounds per (output, dense mode). Until a measured table lands, the round-4
-# bounds (1e-3 / 1e-4 / 2e-3) apply.
-GPU_TOL: dict = {}
+# GPU module-golden bounds per (output, dense mode): 2x the error measured on MI355X with the
+# deterministic solvers of tests/conftest.py (profiles/r5/pytest_module_errors.log), rounded up to two
+# digits, never above the round-4 bound. The round-4 bounds (1e-3 / 1e-4 / 2e-3, _GPU_TOL_DEFAULT)
+# were up to 1000x looser.
+GPU_TOL: dict = {
+    ("mvt_v2", "fp32"): 2.1e-05,
+    ("mvt_v3", "fp32"): 7.0e-05,
+    ("mvt_v2", "bf16x3"): 2.7e-04,
+    ("mvt_v3", "bf16x3"): 4.4e-04,
+    ("backbone.cnn", "fp32"): 4.4e-06,
+    ("backbone.trans", "fp32"): 2.3e-06,
+    ("backbone.cnn", "bf16x3"): 4.4e-06,
+    ("backbone.trans", "bf16x3"): 2.3e-05,
+    ("uv.coarse", "fp32"): 5.3e-06,
+    ("uv.fine", "fp32"): 4.9e-06,
+    ("uv.coarse", "bf16x3"): 5.3e-06,
+    ("uv.fine", "bf16x3"): 1.6e-05,
+    ("unet_cv", "fp32"): 2.7e-06,
+    ("unet_depth", "fp32"): 1.9e-06,
+    ("unet_cv", "bf16x3"): 2.7e-06,
+    ("unet_depth", "bf16x3"): 1.9e-06,
+    ("depth_predictor_v2.depths", "fp32"): 3.3e-04,
+    ("depth_predictor_v2.densities", "fp32"): 2.0e-06,
+    ("depth_predictor_v2.raw", "fp32"): 3.0e-06,
+    ("depth_predictor_v3.depths", "fp32"): 2.0e-04,
+    ("depth_predictor_v3.densities", "fp32"): 2.0e-06,
+    ("depth_predictor_v3.raw", "fp32"): 2.4e-06,
+    ("depth_predictor_v4.depths", "fp32"): 1.2e-04,
+    ("depth_predictor_v4.densities", "fp32"): 1.9e-06,
+    ("depth_predictor_v4.raw", "fp32"): 3.5e-06,
+    ("depth_predictor_v2.depths", "bf16x3"): 2.0e-03,  # 2x would loosen the round-4 bound
+    ("depth_predictor_v2.densities", "bf16x3"): 2.3e-05,
+    ("depth_predictor_v2.raw", "bf16x3"): 3.9e-05,
+    ("depth_predictor_v3.depths", "bf16x3"): 2.0e-03,  # 2x would loosen the round-4 bound
+    ("depth_predictor_v3.densities", "bf16x3"): 2.3e-05,
+    ("depth_predictor_v3.raw", "bf16x3"): 2.9e-05,
+    ("depth_predictor_v4.depths", "bf16x3"): 2.0e-03,
+    ("depth_predictor_v4.densities", "bf16x3"): 2.2e-05,
+    ("depth_predictor_v4.raw", "bf16x3"): 3.2e-05,
+    ("depth_anything.depth", "fp32"): 4.6e-06,
+    ("depth_anything.feat", "fp32"): 2.0e-06,
+    ("depth_anything.depth", "bf16x3"): 4.2e-05,
+    ("depth_anything.feat", "bf16x3"): 1.5e-05,
+}
 _GPU_TOL_DEFAULT = {"mvt_v2": 1e-3, "mvt_v3": 1e-3, "backbone.cnn": 1e-3, "backbone.trans": 1e-3, "uv.coarse": 1e-4,
                     "uv.fine": 1e-3, "unet_cv": 1e-4, "unet_depth": 1e-4, "depth_anything.depth": 1e-3,
                     "depth_anything.feat": 1e-3}
