@@ -389,6 +389,19 @@ int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x2, int32_t 
                           const float* bias, float* y, int32_t batch, int32_t height, int32_t width, int32_t c_out,
                           int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit, void* stream);
 
+/* tsplat_conv2d_f32_fwd with the input-channel pairs of each 32 x 32 output tile also split over
+ * zsplit (1..64) workgroups, for few-tile maps with long reductions (the same nn.Conv2d layers at
+ * 9^2-32^2, and the Depth-Anything DPT's tiny stride-2 768-channel level, reference
+ * src/depth_anything_v2/dpt.py:117-151). partials: device workspace of ceil(npx / 32) *
+ * ceil(c_out / 32) * zsplit * 1024 floats; counters: that many (tiles) int32 arrival counters, zero
+ * on entry and left zero on return (the last workgroup of a tile resets its counter), so one buffer
+ * serves every launch on one stream. The result does not depend on which workgroup finishes last
+ * (partials summed in z order). zsplit = 1 is tsplat_conv2d_f32_fwd. */
+int tsplat_conv2d_f32_zsplit_fwd(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* w_packed,
+                                 const float* bias, float* y, int32_t batch, int32_t height, int32_t width,
+                                 int32_t c_out, int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit,
+                                 int32_t zsplit, float* partials, int32_t* counters, void* stream);
+
 /* 3x3 / stride 1 / padding 1 convolution as Winograd F(2x2, 3x3) on exact-fp32 MFMA (replaces the
  * nn.Conv2d(c_in, c_out, 3, 1, 1) calls of the depth predictor's full-resolution heads and U-Net
  * levels, reference src/model/encoder/matching/depth_predictor_trans.py:110-125 and

@@ -78,6 +78,37 @@ def test_conv2d_direct_kernel(device, n, c1, c2, h, w, cout, k, stride, up, has_
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,ci,h,w,co,k,stride,zmax", [(2, 768, 9, 9, 128, 3, 1, 64), (2, 256, 16, 16, 128, 3, 1, 64),
+                                                      (2, 384, 18, 18, 128, 3, 1, 64), (1, 768, 9, 9, 96, 1, 1, 64),
+                                                      (2, 768, 18, 18, 64, 3, 2, 4), (2, 512, 5, 7, 40, 3, 1, 3)])
+def test_conv2d_direct_zsplit(device, monkeypatch, n, ci, h, w, co, k, stride, zmax):
+    """tsplat_conv2d_f32_zsplit_fwd (ci pairs of each tile over zsplit workgroups, the last arriving
+    one sums the partials in z order): against the oracle at the direct kernel's 2e-5; bit-identical
+    over repeated launches (the counters reset themselves, the sum order does not depend on arrival
+    order); ragged tiles and a non-power-of-2 cap (zmax 3 -> zsplit 2)."""
+    from transplat_amd import kernels as K
+
+    monkeypatch.setattr(K, "_ZSPLIT", zmax)
+    x = seeded((n, ci, h, w), 31)
+    wt = seeded((co, ci, k, k), 32) * (1.0 / ci**0.5)
+    b = seeded((co,), 33)
+    ho = (h + 2 * (k // 2) - k) // stride + 1
+    wo = (w + 2 * (k // 2) - k) // stride + 1
+    tiles = -(-(n * ho * wo) // 32) * -(-co // 32)
+    assert K.conv_zsplit(tiles, ci // 2, 16, k) > 1
+    ref = E.conv2d_direct(x, wt, b, stride)
+    xd, wd, bd = x.to(device), wt.to(device), b.to(device)
+    outs = [K.conv2d_direct(xd, wd, bd, stride).cpu() for _ in range(3)]
+    err = (outs[0] - ref).abs().max().item() / ref.abs().max().item()
+    print(f"zsplit {(n, ci, h, w, co, k, stride)}: z = {K.conv_zsplit(tiles, ci // 2, 16, k)}, rel err {err:.2e}")
+    assert err < 2e-5, err
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    monkeypatch.setattr(K, "_ZSPLIT", 0)
+    one = K.conv2d_direct(xd, wd, bd, stride).cpu()
+    assert (one - ref).abs().max().item() / ref.abs().max().item() < 2e-5
+
+
+@pytest.mark.gpu
 def test_conv2d_direct_weight_cache_tracks_updates(device):
     """The packed-weight cache is keyed on the tensor version: an in-place update repacks."""
     from transplat_amd import kernels as K

@@ -38,6 +38,9 @@ struct Args {
     const float* bias;  // [cout] or null
     const float* res;   // residual added to the output (y's layout) or null
     float* y;           // [n, cout, hout, wout] (NHWC: [n, hout, wout, cout])
+    float* part;        // zsplit > 1: [tiles][zsplit][1024] partial tiles
+    int* cnt;           // zsplit > 1: [tiles] arrival counters (zero between launches)
+    int zsplit;         // workgroups per output tile (grid z)
     int c1, c2, cout, n;
     int hin, win;       // stored input size
     int hv, wv;         // virtual input size (2x when upsampling)
@@ -88,8 +91,10 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
         return cp < cp1 ? p.x1 + ((size_t)nb * p.c1 + 2 * cp + h) * hwi
                         : p.x2 + ((size_t)nb * p.c2 + 2 * (cp - cp1) + h) * hwi;
     };
-    // this wave's ci pairs: w, w + ksplit, ... in batches of G
-    const int ncp = cp_all > w ? (cp_all - w + ksplit - 1) / ksplit : 0;
+    // this wave's ci pairs: gw, gw + ksplit * zsplit, ... in batches of G (gw = its index over the
+    // tile's zsplit workgroups)
+    const int gw = blockIdx.z * ksplit + w, gstride = ksplit * p.zsplit;
+    const int ncp = cp_all > gw ? (cp_all - gw + gstride - 1) / gstride : 0;
     const int nbatch = (ncp + G - 1) / G;
     // (called only when ncp > 0) every load is issued unconditionally from a clamped, valid
     // address and masked afterwards: a conditional load would become a branch with its own
@@ -99,7 +104,7 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
         for (int g = 0; g < G; ++g) {
             const int i = bi * G + g;
             const bool ok = i < ncp;
-            const int cp = w + min(i, ncp - 1) * ksplit;
+            const int cp = gw + min(i, ncp - 1) * gstride;
             const float* src = chan(cp);
             const float* wq = wbase + (size_t)cp * 64;
 #pragma unroll
@@ -162,6 +167,34 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) sred[(w * 16 + r) * 64 + lane] = acc[r];
     __syncthreads();
+    const int tile = blockIdx.x + gridDim.x * blockIdx.y;
+    if (p.zsplit > 1) {
+        // this workgroup's partial tile -> workspace; the last of the tile's zsplit workgroups to
+        // arrive finishes it (release: the partial stores are visible device-wide before the counter
+        // moves; acquire: the last one reads every partial after seeing the count)
+        float* mine = p.part + ((size_t)tile * p.zsplit + blockIdx.z) * 1024;
+        for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
+            float s = 0.f;
+            for (int k = 0; k < ksplit; ++k) s += sred[(k * 16 + (idx >> 6)) * 64 + (idx & 63)];
+            mine[idx] = s;
+        }
+        __threadfence();
+        __syncthreads();
+        __shared__ int s_last;
+        if (threadIdx.x == 0) s_last = atomicAdd(p.cnt + tile, 1) == p.zsplit - 1;
+        __syncthreads();
+        if (!s_last) return;
+        __threadfence();
+        const float* all = p.part + (size_t)tile * p.zsplit * 1024;
+        for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
+            float s = 0.f;
+            for (int z = 0; z < p.zsplit; ++z) s += all[(size_t)z * 1024 + idx];
+            sred[idx] = s;
+        }
+        if (threadIdx.x == 0) atomicExch(p.cnt + tile, 0);
+        __syncthreads();
+    }
+    const int nsum = p.zsplit > 1 ? 1 : ksplit;  // partial rows left in sred
     for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
         // NCHW: consecutive threads -> consecutive pixels; NHWC: -> consecutive output channels
         int r, l;
@@ -174,7 +207,7 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
             l = idx & 63;
         }
         float s = 0.f;
-        for (int k = 0; k < ksplit; ++k) s += sred[(k * 16 + r) * 64 + l];
+        for (int k = 0; k < nsum; ++k) s += sred[(k * 16 + r) * 64 + l];
         const int co = cot * 32 + 8 * (r >> 2) + 4 * (l >> 5) + (r & 3);
         const int q = blockIdx.x * 32 + (l & 31);
         if (co >= p.cout || q >= p.npx) continue;
@@ -194,17 +227,22 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
 }  // namespace conv
 }  // namespace tsplat
 
-extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* w_packed,
-                                     const float* bias, float* y, int32_t batch, int32_t height, int32_t width,
-                                     int32_t c_out, int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit,
-                                     void* stream_) {
+extern "C" int tsplat_conv2d_f32_zsplit_fwd(const float* x1, int32_t c1, const float* x2, int32_t c2,
+                                            const float* w_packed, const float* bias, float* y, int32_t batch,
+                                            int32_t height, int32_t width, int32_t c_out, int32_t ksize,
+                                            int32_t stride, int32_t upsample, int32_t ksplit, int32_t zsplit,
+                                            float* partials, int32_t* counters, void* stream_) {
     using namespace tsplat::conv;
     if (!x1 || !w_packed || !y || batch <= 0 || height <= 0 || width <= 0 || c_out <= 0) return TSPLAT_EINVAL;
+    if (zsplit < 1 || zsplit > 64 || (zsplit > 1 && (!partials || !counters))) return TSPLAT_EINVAL;
     if (c1 <= 0 || (c1 & 1) || c2 < 0 || (c2 & 1) || (c2 > 0 && !x2)) return TSPLAT_EINVAL;
     if (!(ksize == 1 || ksize == 3) || !(stride == 1 || stride == 2) || !(upsample == 0 || upsample == 1))
         return TSPLAT_EINVAL;
     if (ksplit < 1 || ksplit > kMaxWaves) return TSPLAT_EINVAL;
     Args p{};
+    p.zsplit = zsplit;
+    p.part = partials;
+    p.cnt = counters;
     p.x1 = x1;
     p.x2 = x2;
     p.wp = w_packed;
@@ -227,7 +265,7 @@ extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x
     if (npx >= (1ll << 31) || in_elems >= (1ll << 31)) return TSPLAT_EINVAL;
     p.npx = (int)npx;
     hipStream_t stream = (hipStream_t)stream_;
-    const dim3 grid((unsigned)((npx + 31) / 32), (unsigned)((c_out + 31) / 32));
+    const dim3 grid((unsigned)((npx + 31) / 32), (unsigned)((c_out + 31) / 32), (unsigned)zsplit);
     const dim3 block(64 * ksplit);
     const size_t lds = (size_t)ksplit * 16 * 64 * sizeof(float);
     TSPLAT_PROF_BEGIN(tsplat::prof::kConv, stream);
@@ -235,7 +273,7 @@ extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x
     hipLaunchKernelGGL((conv_f32_kernel<KS, S, UP, G, false, false>), grid, block, lds, stream, p)
     // ci pairs per batch: 3x3 -> all of a wave's 3-4 pairs in one batch, else 2 (1 if it has 1);
     // 1x1 -> 16 once a wave has that many, else 8
-    const int per_wave = ((c1 + c2) / 2 + ksplit - 1) / ksplit;
+    const int per_wave = ((c1 + c2) / 2 + ksplit * zsplit - 1) / (ksplit * zsplit);
     const bool wide = per_wave >= (ksize == 3 ? 2 : 16);
     const bool one = ksize == 3 && per_wave >= 3 && per_wave <= 4;
     if (ksize == 3 && stride == 1 && !upsample) {
@@ -253,6 +291,14 @@ extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x
     TSPLAT_PROF_END(tsplat::prof::kConv, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
+}
+
+extern "C" int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* w_packed,
+                                     const float* bias, float* y, int32_t batch, int32_t height, int32_t width,
+                                     int32_t c_out, int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit,
+                                     void* stream_) {
+    return tsplat_conv2d_f32_zsplit_fwd(x1, c1, x2, c2, w_packed, bias, y, batch, height, width, c_out, ksize, stride,
+                                        upsample, ksplit, 1, nullptr, nullptr, stream_);
 }
 
 extern "C" int tsplat_conv2d_f32_nhwc_fwd(const float* x, int32_t c_in, const float* w_packed, const float* bias,
@@ -277,6 +323,7 @@ extern "C" int tsplat_conv2d_f32_nhwc_fwd(const float* x, int32_t c_in, const fl
     p.hin = p.hv = p.hout = height;
     p.win = p.wv = p.wout = width;
     p.npx = batch * height * width;
+    p.zsplit = 1;
     hipStream_t stream = (hipStream_t)stream_;
     const dim3 grid((unsigned)((p.npx + 31) / 32), (unsigned)((c_out + 31) / 32));
     const dim3 block(64 * ksplit);

@@ -520,24 +520,41 @@ _CONV1_PAIRS = int(os.environ.get("TSPLAT_CONV1_PAIRS", "8"))
 # 339.2 at 4096 / 2; 16384 / 1 and 8192 / 1 in between)
 _CONV3_WAVES = int(os.environ.get("TSPLAT_CONV3_WAVES", "8192"))
 _CONV3_PAIRS = int(os.environ.get("TSPLAT_CONV3_PAIRS", "2"))
+# Split of each tile's ci pairs over workgroups (tsplat_conv2d_f32_zsplit_fwd) for few-tile maps:
+# doubled while a wave still has more than one load batch of pairs (4 for a 3x3, 16 for a 1x1) and
+# the grid stays within one round of 16-wave workgroups (one per CU). TSPLAT_CONV_ZSPLIT=0 turns it
+# off, =N caps it at N.
+_ZSPLIT = int(os.environ.get("TSPLAT_CONV_ZSPLIT", "-1"))
+_ZSPLIT_WGS = int(os.environ.get("TSPLAT_CONV_ZSPLIT_WGS", "256"))
+# arrival counters of the zsplit launches: one zeroed slab per device, handed out in rotating ranges
+# (each launch leaves its range at zero again), so launches in flight on concurrent streams never share
+# a counter while the slab holds more tiles than the launches of one step
+_ZSPLIT_CNT: dict = {}
+_ZSPLIT_SLAB = 1 << 20
 
 
-def conv_pack_weight(weight):
-    """[cout, cin, k, k] -> [ceil(cout / 32), k * k, cin / 2, 2, 32] (zero-padded couts), cached per
-    weight tensor version: the A-operand order of tsplat_conv2d_f32_fwd."""
-    hit = _CONV_PACKED.get(id(weight))
-    if hit is not None and hit[0]() is weight and hit[1] == weight._version:
-        return hit[2]
-    co, ci, k = weight.shape[:3]  # a Conv1d weight [cout, cin, 1] packs as the 1x1 it is
-    cot = (co + 31) // 32
-    w = torch.zeros((cot * 32, ci, k * k), dtype=torch.float32, device=weight.device)
-    w[:co] = weight.detach().float().reshape(co, ci, k * k)
-    packed = w.reshape(cot, 32, ci // 2, 2, k * k).permute(0, 4, 2, 3, 1).contiguous()
-    if len(_CONV_PACKED) > 512:
-        for k in [k for k, v in _CONV_PACKED.items() if v[0]() is None]:
-            del _CONV_PACKED[k]
-    _CONV_PACKED[id(weight)] = (weakref.ref(weight), weight._version, packed)
-    return packed
+def _zsplit_counters(device, tiles: int):
+    slab = _ZSPLIT_CNT.get(device)
+    if slab is None:
+        slab = [torch.zeros(_ZSPLIT_SLAB, dtype=torch.int32, device=device), 0]
+        _ZSPLIT_CNT[device] = slab
+    if slab[1] + tiles > _ZSPLIT_SLAB:
+        slab[1] = 0
+    view = slab[0][slab[1]:slab[1] + tiles]
+    slab[1] += tiles
+    return view
+
+
+def conv_zsplit(tiles: int, pairs: int, ksplit: int, k: int) -> int:
+    """Workgroups per output tile for tsplat_conv2d_f32_zsplit_fwd (1 = no split)."""
+    if _ZSPLIT == 0:
+        return 1
+    per_batch = 4 if k == 3 else 16
+    z = 1
+    while (z < 64 and tiles * 2 * z <= _ZSPLIT_WGS and -(-pairs // (ksplit * z)) > per_batch
+           and (_ZSPLIT < 0 or 2 * z <= _ZSPLIT)):
+        z *= 2
+    return z
 
 
 def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsample: bool = False) -> bool:
@@ -601,11 +618,16 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
     while ksplit > 1 and (tiles * ksplit > cap or pairs < min_pairs * ksplit):
         ksplit //= 2
     ksplit = _CONV_KSPLIT or ksplit
+    zsplit = conv_zsplit(tiles, pairs, ksplit, k) if ksplit == 16 else 1
     pb = _f32(bias) if bias is not None else None
-    rc = lib.tsplat_conv2d_f32_fwd(_lib.ptr(a), c1, _lib.ptr(b), c2, _lib.ptr(conv_pack_weight(weight)),
-                                   _lib.ptr(pb), _lib.ptr(y), n, h, w, co, k, stride, int(upsample), ksplit,
-                                   _lib.stream_ptr(x1.device))
-    _lib.check(rc, "tsplat_conv2d_f32_fwd")
+    part = cnt = None
+    if zsplit > 1:
+        part = torch.empty(tiles * zsplit * 1024, dtype=torch.float32, device=x1.device)
+        cnt = _zsplit_counters(x1.device, tiles)
+    rc = lib.tsplat_conv2d_f32_zsplit_fwd(_lib.ptr(a), c1, _lib.ptr(b), c2, _lib.ptr(conv_pack_weight(weight)),
+                                          _lib.ptr(pb), _lib.ptr(y), n, h, w, co, k, stride, int(upsample), ksplit,
+                                          zsplit, _lib.ptr(part), _lib.ptr(cnt), _lib.stream_ptr(x1.device))
+    _lib.check(rc, "tsplat_conv2d_f32_zsplit_fwd")
     return y
 
 
