@@ -55,3 +55,17 @@ def test_debug_mode_refuses_graph_capture():
     finally:
         lib.tsplat_set_debug(was)
     assert _lib.debug_enabled() == bool(was)
+
+
+def test_package_reads_no_undefined_names():
+    """Every name the package's modules read is defined or imported somewhere in them
+    (tools/namecheck.py): the GPU dispatch code cannot run in the CPU suite, so a helper an edit
+    removed would otherwise surface only on the GPU box."""
+    import subprocess
+    import sys
+
+    root = Path(__file__).resolve().parents[1]
+    files = [str(p) for p in (root / "transplat_amd").rglob("*.py")] + [str(root / "bench.py")]
+    out = subprocess.run([sys.executable, str(root / "tools" / "namecheck.py")] + files, capture_output=True,
+                         text=True)
+    assert out.returncode == 0, out.stdout

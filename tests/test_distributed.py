@@ -81,18 +81,27 @@ def test_index_batch_places_targets():
 @pytest.mark.gpu
 def test_evaluate_cli_small_index(device):
     """C1 plumbing on the GPU: the reference's re10k_small evaluation index through the full
-    model (synthetic frames and weights), one JSON summary."""
+    model (synthetic frames and weights), one JSON summary -- by default on the benched step (one
+    replayed hipGraph per scene, bf16x3 dense layers, one sync per shard); the eager step of the
+    same precision gives the same PSNR."""
     import json
     import subprocess
     import sys
 
     repo = Path(__file__).resolve().parents[1]
-    out = subprocess.run([sys.executable, "-m", "transplat_amd.evaluate", "--index", str(INDEX)], cwd=repo,
-                         capture_output=True, text=True, timeout=600)
-    assert out.returncode == 0, out.stderr[-2000:]
-    summary = json.loads(out.stdout.strip().splitlines()[-1])
-    assert summary["scenes"] == 2 and summary["views"] == 6
-    assert summary["psnr"] == summary["psnr"]  # finite
+    runs = {}
+    for extra in ([], ["--no-graph"]):
+        out = subprocess.run([sys.executable, "-m", "transplat_amd.evaluate", "--index", str(INDEX)] + extra,
+                             cwd=repo, capture_output=True, text=True, timeout=600)
+        assert out.returncode == 0, out.stderr[-2000:]
+        summary = json.loads(out.stdout.strip().splitlines()[-1])
+        assert summary["scenes"] == 2 and summary["views"] == 6
+        assert summary["psnr"] == summary["psnr"]  # finite
+        assert summary["dense_dtype"] == "bf16x3" and summary["graph"] == (not extra)
+        runs[bool(extra)] = summary
+    print(f"evaluate: graphed {runs[False]['psnr']:.4f} dB in {runs[False]['seconds']:.4f} s, "
+          f"eager {runs[True]['psnr']:.4f} dB")
+    assert abs(runs[False]["psnr"] - runs[True]["psnr"]) < 1e-2
 
 
 def _bench_worker(rank, world, port, out):

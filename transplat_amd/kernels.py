@@ -557,6 +557,24 @@ def conv_zsplit(tiles: int, pairs: int, ksplit: int, k: int) -> int:
     return z
 
 
+def conv_pack_weight(weight):
+    """[cout, cin, k, k] -> [ceil(cout / 32), k * k, cin / 2, 2, 32] (zero-padded couts), cached per
+    weight tensor version: the A-operand order of tsplat_conv2d_f32_fwd."""
+    hit = _CONV_PACKED.get(id(weight))
+    if hit is not None and hit[0]() is weight and hit[1] == weight._version:
+        return hit[2]
+    co, ci, k = weight.shape[:3]  # a Conv1d weight [cout, cin, 1] packs as the 1x1 it is
+    cot = (co + 31) // 32
+    w = torch.zeros((cot * 32, ci, k * k), dtype=torch.float32, device=weight.device)
+    w[:co] = weight.detach().float().reshape(co, ci, k * k)
+    packed = w.reshape(cot, 32, ci // 2, 2, k * k).permute(0, 4, 2, 3, 1).contiguous()
+    if len(_CONV_PACKED) > 512:
+        for k in [k for k, v in _CONV_PACKED.items() if v[0]() is None]:
+            del _CONV_PACKED[k]
+    _CONV_PACKED[id(weight)] = (weakref.ref(weight), weight._version, packed)
+    return packed
+
+
 def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsample: bool = False) -> bool:
     """True when tsplat_conv2d_f32_fwd takes this convolution and (mode "auto") it is a
     latency-bound one where the direct kernel beats MIOpen."""
