@@ -169,29 +169,39 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
     __syncthreads();
     const int tile = blockIdx.x + gridDim.x * blockIdx.y;
     if (p.zsplit > 1) {
-        // this workgroup's partial tile -> workspace; the last of the tile's zsplit workgroups to
-        // arrive finishes it (release: the partial stores are visible device-wide before the counter
-        // moves; acquire: the last one reads every partial after seeing the count)
-        float* mine = p.part + ((size_t)tile * p.zsplit + blockIdx.z) * 1024;
+        // this workgroup's partial tile -> workspace with write-through (sc1) stores, so no release
+        // fence; drained by every wave, then ONE lane takes an arrival ticket. The tile's last
+        // arriver: ONE agent-scope acquire (its L1 may hold stale lines of the other partials), then
+        // plain loads (cdna_hip_programming.md §5 "In-launch split-K reduction"; a __threadfence()
+        // in every thread instead made the C2 step 5 % slower)
+        typedef __attribute__((address_space(1))) unsigned gu32;
+        unsigned* mine = reinterpret_cast<unsigned*>(p.part + ((size_t)tile * p.zsplit + blockIdx.z) * 1024);
         for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
             float s = 0.f;
             for (int k = 0; k < ksplit; ++k) s += sred[(k * 16 + (idx >> 6)) * 64 + (idx & 63)];
-            mine[idx] = s;
+            __hip_atomic_store((gu32*)(mine + idx), __float_as_uint(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        __threadfence();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        __shared__ int s_last;
-        if (threadIdx.x == 0) s_last = atomicAdd(p.cnt + tile, 1) == p.zsplit - 1;
+        int* flag = reinterpret_cast<int*>(sred + ksplit * 1024);  // one LDS word past the partials
+        if (threadIdx.x == 0) {
+            const int t = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = t == p.zsplit - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            *flag = last;
+        }
         __syncthreads();
-        if (!s_last) return;
-        __threadfence();
+        if (!*flag) return;
         const float* all = p.part + (size_t)tile * p.zsplit * 1024;
         for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
             float s = 0.f;
             for (int z = 0; z < p.zsplit; ++z) s += all[(size_t)z * 1024 + idx];
             sred[idx] = s;
         }
-        if (threadIdx.x == 0) atomicExch(p.cnt + tile, 0);
         __syncthreads();
     }
     const int nsum = p.zsplit > 1 ? 1 : ksplit;  // partial rows left in sred
@@ -267,7 +277,7 @@ extern "C" int tsplat_conv2d_f32_zsplit_fwd(const float* x1, int32_t c1, const f
     hipStream_t stream = (hipStream_t)stream_;
     const dim3 grid((unsigned)((npx + 31) / 32), (unsigned)((c_out + 31) / 32), (unsigned)zsplit);
     const dim3 block(64 * ksplit);
-    const size_t lds = (size_t)ksplit * 16 * 64 * sizeof(float);
+    const size_t lds = (size_t)ksplit * 16 * 64 * sizeof(float) + 16;  // + the last-arriver flag
     TSPLAT_PROF_BEGIN(tsplat::prof::kConv, stream);
 #define TSPLAT_CONV_LAUNCH(KS, S, UP, G) \
     hipLaunchKernelGGL((conv_f32_kernel<KS, S, UP, G, false, false>), grid, block, lds, stream, p)

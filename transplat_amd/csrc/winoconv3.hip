@@ -284,24 +284,20 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     // A fragments: [xi][cob][chunk][hl][lane] uint4
     const uint4* ub = a.u + ((size_t)(4 * rr) * a.cobs + (co_ok ? cob : 0)) * a.nchunk * 128 + lane;
     const size_t xi_stride = (size_t)a.cobs * a.nchunk * 128;
-    // DA (the staged 32-co forms, which have the registers): two A-fragment sets, chunk it's in set
-    // it & 1, loaded two chunks ahead -- one chunk ahead left the L2 round trip of the packed U
-    // exposed between the transform and the MFMAs of every chunk
-    constexpr bool DA = ST && CB == 1 && NB == 1;
-    uint4 af[DA ? 2 : 1][4][2];
+    uint4 af[4][2];
     // unconditional loads (a chunk past the last reads the last one's weights again: its B operand is
     // all zeros): a branch around them would make every later wait a vmcnt(0), draining the region
-    // prefetch before the MFMAs (A: the register set, a compile-time constant)
-    auto load_a = [&](int chunk, int s0, int s1, auto A) {
+    // prefetch before the MFMAs
+    auto load_a = [&](int chunk, int s0, int s1) {
         const size_t cofs = (size_t)min(chunk, a.nchunk - 1) * 128;
 #pragma unroll
         for (int s = s0; s < s1; ++s)
 #pragma unroll
             for (int hl = 0; hl < 2; ++hl) {
 #if TSPLAT_W3_ABL == 3  // diagnostic build: no A loads
-                af[decltype(A)::value][s][hl] = make_uint4(chunk, s, hl, lane);
+                af[s][hl] = make_uint4(chunk, s, hl, lane);
 #else
-                af[decltype(A)::value][s][hl] = ub[s * xi_stride + cofs + hl * 64];
+                af[s][hl] = ub[s * xi_stride + cofs + hl * 64];
 #endif
             }
     };
@@ -398,7 +394,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     };
     // MFMAs of xi s0 .. s1 - 1 on buffer sV: B fragment of lane (n, h) = the 16 B of
     // [hl][xi][half h][tile 32 nb + n][4 pairs] (channels 8 h .. 8 h + 7), one ds_read_b128
-    auto mfma = [&](const uint32_t* sV, int s0, int s1, auto A) {
+    auto mfma = [&](const uint32_t* sV, int s0, int s1) {
 #if TSPLAT_W3_ABL == 2  // diagnostic build: no MFMAs (the B reads stay)
         const uint32_t* bq = sV + ((lane >> 5) * T + (lane & 31)) * 4;
         for (int s = s0; s < s1; ++s) acc[s][0][0] += __builtin_bit_cast(float, bq[(4 * rr + s) * 8 * T]);
@@ -408,8 +404,8 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
 #pragma unroll
         for (int s = s0; s < s1; ++s) {
             const int xi = 4 * rr + s;
-            const bf16x8 ah = __builtin_bit_cast(bf16x8, af[decltype(A)::value][s][0]);
-            const bf16x8 al = __builtin_bit_cast(bf16x8, af[decltype(A)::value][s][1]);
+            const bf16x8 ah = __builtin_bit_cast(bf16x8, af[s][0]);
+            const bf16x8 al = __builtin_bit_cast(bf16x8, af[s][1]);
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb) {
                 const uint32_t* ph = bb + xi * 8 * T + 32 * nb * 4;
@@ -434,17 +430,13 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
         sstore(0, I0);
         gload(kg + KS, I1);
         if (DS) gload(kg + 2 * KS, I0);
-        load_a(kg, 0, 4, I0);
-        if (DA) load_a(kg + KS, 0, 4, std::integral_constant<int, DA ? 1 : 0>{});
+        load_a(kg, 0, 4);
         __syncthreads();
         W3_STAMP(1);
-        // S = the register set of region it + 1; with DA chunk it's A fragments are in set 1 - S
-        // (it even: set 0, S = 1), refilled with chunk it + 2's right after its MFMAs
+        // S = the register set of region it + 1
         auto step = [&](int it, auto S) {
             const int ch = kg + it * KS;
             const bool more = it + 1 < iters;
-            constexpr int AS = DA ? 1 - decltype(S)::value : 0;
-            const std::integral_constant<int, AS> A;
             // the region of chunk it + 1 (its loads flew during the last iteration(s)) goes to LDS
             // first, so its registers are free again during the transform; slot (it + 1) & 1 was last
             // read by read_patches(it - 1), before the last barrier
@@ -454,8 +446,8 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
             // unconditional (past the last chunk: zero-page loads), see load_a
             gload(ch + (DS ? 3 : 2) * KS, S);
             __syncthreads();  // sV(it) complete
-            mfma(sG, 0, 4, A);
-            load_a(ch + (DA ? 2 : 1) * KS, 0, 4, A);
+            mfma(sG, 0, 4);
+            load_a(ch + KS, 0, 4);
             __syncthreads();  // every wave is done with sV(it) and with sIn slot it & 1
         };
         if constexpr (DS) {
@@ -468,7 +460,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
         }
     } else {
     load_patches(kg);
-    load_a(kg, 0, 4, I0);
+    load_a(kg, 0, 4);
     transform(sG);
     if (iters > 1) load_patches(kg + KS);
     __syncthreads();
@@ -476,15 +468,15 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
         const int ch = kg + it * KS;
         const uint32_t* sV = sG + (it & 1) * BUF;
         const bool more = it + 1 < iters;
-        mfma(sV, 0, 2, I0);
-        if (more) load_a(ch + KS, 0, 2, I0);  // the first two xi's registers are free again
+        mfma(sV, 0, 2);
+        if (more) load_a(ch + KS, 0, 2);  // the first two xi's registers are free again
         if (more) {
             transform(sG + ((it + 1) & 1) * BUF);
             if (it + 2 < iters) load_patches(ch + 2 * KS);
         }
-        mfma(sV, 2, 4, I0);
+        mfma(sV, 2, 4);
         if (more) {
-            load_a(ch + KS, 2, 4, I0);
+            load_a(ch + KS, 2, 4);
             __syncthreads();  // sV(it + 1) complete; every wave is done reading sV(it)
         }
     }
