@@ -304,6 +304,23 @@ int tsplat_win_attn_partials_fwd(const float* q, const float* k, const float* v,
                                  int32_t height, int32_t width, int32_t channels, int32_t key_views,
                                  int32_t splits, int32_t with_shift, int32_t key_batch_shift, void* stream);
 
+/* bf16x3 ("split-bf16") form of the same fp32 attention -- the C2 step's dense-precision mode: the
+ * reference runs QK^T and PV as TF32 matmuls (multiview_transformer.py:57-206 under
+ * set_float32_matmul_precision('high'), src/main.py:15). Every fp32 operand x = xh + xl (bf16
+ * hi / lo), each product xh yh + xh yl + xl yh on bf16 MFMA with fp32 accumulation and an fp32
+ * softmax: <= ~3 * 2^-18 relative per product (TF32: 2^-11 per operand). Window pixels must be a
+ * multiple of 128. kv_x3 = [kh | kl | vh | vl] bf16, each batch * key_views * H * W * 128 elements,
+ * from tsplat_split_kv_bf16x3(k, v, kv_x3, n = that count). q / out fp32 as tsplat_win_attn_fwd;
+ * workspace and key split as tsplat_win_attn_fwd / _partials_fwd (same partials layout, so
+ * tsplat_linear_f32_attn_merge_fwd consumes the _x3_partials_fwd output unchanged). */
+int tsplat_split_kv_bf16x3(const float* k, const float* v, void* kv_x3, int64_t n, void* stream);
+int tsplat_win_attn_x3_fwd(const float* q, const void* kv_x3, float* out, void* workspace, int32_t batch,
+                           int32_t height, int32_t width, int32_t channels, int32_t key_views, int32_t splits,
+                           int32_t with_shift, void* stream);
+int tsplat_win_attn_x3_partials_fwd(const float* q, const void* kv_x3, void* workspace, int32_t batch, int32_t height,
+                                    int32_t width, int32_t channels, int32_t key_views, int32_t splits,
+                                    int32_t with_shift, int32_t key_batch_shift, void* stream);
+
 /* bf16 variant (config C3): q, k, v, out are bf16 (raw 16-bit storage), same layouts and
  * semantics; bf16 MFMA with fp32 accumulation and an fp32 softmax (P rounded to bf16 for the
  * PV product). Window pixels must be a multiple of 128. */

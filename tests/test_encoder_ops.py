@@ -358,6 +358,31 @@ def test_sh_rotation_op_matches_oracle(device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("hw,m,shift,b,grow", [(64, 1, False, 2, False), (64, 1, True, 2, False), (64, 2, True, 2, False),
+                                               (32, 1, True, 2, False), (64, 1, True, 8, False), (64, 1, True, 1, False),
+                                               (64, 1, True, 2, True), (64, 1, False, 1, True)])
+def test_window_attention_x3_kernel(device, hw, m, shift, b, grow):
+    """bf16x3 window attention (tsplat_win_attn_x3_fwd: split-bf16 products, fp32 softmax; the C2
+    step's dense-precision mode) vs the oracle in float64: within 3e-5 of max(1, max |O|) -- the
+    exact-fp32 kernel's bound is 2e-4; TF32 operands (the reference's own GPU arithmetic) would be
+    ~1e-3. grow: scores that keep rising along the keys (the deferred-rescale path, P up to 2^8)."""
+    from transplat_amd import kernels as K
+
+    q = seeded((b, hw * hw, 128), 51) * (3.0 if grow else 1.0)
+    k = seeded((b, m, hw * hw, 128), 52) if m > 1 else seeded((b, hw * hw, 128), 52)
+    if grow:
+        ys, xs = torch.meshgrid(torch.arange(hw), torch.arange(hw), indexing="ij")
+        t = ((ys % (hw // 2)) * (hw // 2) + xs % (hw // 2)).reshape(-1).float() / (hw * hw / 4)
+        k = k * (0.25 + 3.75 * t)[None, :, None]
+    v = seeded(k.shape, 53)
+    ref = E.window_attention(q.double(), k.double(), v.double(), hw, hw, 2, shift)
+    out = K.window_attention_x3(q.to(device), k.to(device), v.to(device), hw, hw, 2, shift).cpu().double()
+    err = (out - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+    print(f"x3 attention hw={hw} m={m} shift={shift} b={b} grow={grow}: rel err {err:.2e}")
+    assert err < 3e-5, err
+
+
+@pytest.mark.gpu
 def test_window_attention_dtu_stress(device):
     """C5 stress: 3 context views at 512x384 -> a 128x96 feature map, 2 windows per side
     (L = 3072 queries, 6144 keys over two key views), shifted layer."""

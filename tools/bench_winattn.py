@@ -16,7 +16,7 @@ ap.add_argument("--batch", type=int, default=2)
 ap.add_argument("--hw", type=int, default=64)
 ap.add_argument("--iters", type=int, default=50)
 ap.add_argument("--shift", type=int, default=1)
-ap.add_argument("--dtype", choices=["fp32", "bf16"], default="fp32")
+ap.add_argument("--dtype", choices=["fp32", "bf16", "x3"], default="fp32")
 args = ap.parse_args()
 dev = torch.device("cuda:0")
 _lib.load()
@@ -24,12 +24,24 @@ b, hw = args.batch, args.hw
 g = torch.Generator(device=dev).manual_seed(0)
 dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
 q, k, v = (torch.randn((b, hw * hw, 128), device=dev, generator=g).to(dt) for _ in range(3))
+if args.dtype == "x3":  # bf16x3: K / V split once (as the merge path does per layer), main kernel timed
+    L0 = (hw // 2) ** 2
+    kv = kernels.split_kv_bf16x3(k, v)
+    ws = torch.empty(max(int(_lib.load().tsplat_win_attn_workspace_bytes(b, hw, hw, 1, 2)), 4), dtype=torch.uint8,
+                     device=dev)
+
+    def attn():
+        _lib.check(_lib.load().tsplat_win_attn_x3_partials_fwd(_lib.ptr(q), _lib.ptr(kv), _lib.ptr(ws), b, hw, hw, 128,
+                                                               1, 2, int(args.shift), 0, _lib.stream_ptr(dev)), "x3")
+else:
+    def attn():
+        kernels.window_attention(q, k, v, hw, hw, 2, bool(args.shift))
 for _ in range(3):
-    kernels.window_attention(q, k, v, hw, hw, 2, bool(args.shift))
+    attn()
 torch.cuda.synchronize()
 _lib.prof_enable("win_attn")  # HIP events around the kernel launches only (no Python overhead)
 for _ in range(args.iters):
-    kernels.window_attention(q, k, v, hw, hw, 2, bool(args.shift))
+    attn()
 ms, n = _lib.prof_read()
 _lib.prof_enable(None)
 us = ms / n * 1e3

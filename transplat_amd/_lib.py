@@ -79,6 +79,9 @@ SIGNATURES = {
     "tsplat_bias_act_fwd": (ctypes.c_int, [_P] * 4 + [_I32, _I32, ctypes.c_int64, _I32, _P]),
     "tsplat_bias_act_nhwc_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int64, _I32, _I32, _P]),
     "tsplat_win_attn_partials_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 8 + [_P]),
+    "tsplat_split_kv_bf16x3": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, _P]),
+    "tsplat_win_attn_x3_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 7 + [_P]),
+    "tsplat_win_attn_x3_partials_fwd": (ctypes.c_int, [_P] * 3 + [_I32] * 8 + [_P]),
     "tsplat_linear_f32_attn_merge_fwd": (ctypes.c_int, [_P] + [_I32] * 6 + [_P] * 3 + [ctypes.c_float, _P, _P, _I32,
                                                                                        _I32, _P]),
     "tsplat_linear_f32_fwd": (ctypes.c_int, [_P, _I32, _P, _I32] + [_P] * 4 + [ctypes.c_float, _P, _P, ctypes.c_int64]

@@ -1154,6 +1154,252 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
                                                       o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
 }
 
+// ============================================================================================
+// bf16x3 ("split-bf16") form of the exact-fp32 128-query kernel: the C2 step's dense-precision
+// mode (the reference runs both contractions as TF32 matmuls, src/main.py:15; gfx950 has no xf32
+// MFMA). Every fp32 operand is x = xh + xl (xh = bf16(x), xl = bf16(x - xh)), every product
+// xh yh + xh yl + xl yh on v_mfma_f32_32x32x16_bf16 with fp32 accumulation: <= ~3 * 2^-18 relative
+// per product (TF32: 2^-11 per operand), at 3 / 16 of the exact-fp32 MFMA cycles.
+//   * Q (fp32) is split in registers once per lane; K and V arrive pre-split (tsplat_split_kv_bf16x3:
+//     every K / V row is staged by L / 128 query blocks, so splitting at staging would repeat it)
+//     and are staged as hi / lo LDS images -- K row-major XOR-swizzled, V in the T10 image (b) read
+//     transposed by ds_read_b64_tr_b16 (win_attn_bf16_v2_kernel's operand maps);
+//   * softmax: raw fp32 scores, log2 domain, deferred rescale (P <= 2^kThr, split exactly as well);
+//   * the shifted-window mask as the v2 kernel's extra MFMA step on the hi part (+kMaskBonus to
+//     same-region scores: different-region weights e^-99.7 instead of e^-100, both 0 to fp32 output);
+//   * K / V / mask tiles double-buffered, one barrier per tile; one workgroup per CU (132 KB LDS).
+// Writes the same split-key partials (lane-contiguous O, natural-log m, l) as the exact kernel, so
+// tsplat_linear_f32_attn_merge_fwd combines them in its operand staging unchanged.
+// ============================================================================================
+__device__ __forceinline__ void split8(const float (&x)[8], bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        hi[j] = (__bf16)x[j];
+        lo[j] = (__bf16)(x[j] - (float)hi[j]);
+    }
+}
+
+__global__ void __launch_bounds__(kThreads, 1)
+win_attn_x3_kernel(Params p, const float* __restrict__ q, const __bf16* __restrict__ khg,
+                   const __bf16* __restrict__ klg, const __bf16* __restrict__ vhg, const __bf16* __restrict__ vlg,
+                   float* __restrict__ out, Partials part) {
+    __shared__ __attribute__((aligned(16))) __bf16 sKh[2][kBK * kC];
+    __shared__ __attribute__((aligned(16))) __bf16 sKl[2][kBK * kC];
+    __shared__ __attribute__((aligned(16))) unsigned char sVh[2][kBK * kC * 2];
+    __shared__ __attribute__((aligned(16))) unsigned char sVl[2][kBK * kC * 2];
+    __shared__ __attribute__((aligned(16))) bf16x8 sMaskAb[2][kBK][2];
+
+    int qblk, wi, bz;
+    xcd_block_coords(qblk, wi, bz);
+    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const size_t HW = (size_t)p.H * p.W;
+    const int kvb = (b + p.kv_shift) % p.nbatch;
+    const size_t kvoff = (size_t)kvb * p.m * HW * kC;
+    const float cl2 = p.scale * kLog2e;
+
+    const int tq = qblk * kBQ3 + wid * kQW + c;
+    const int qpix = win_pixel(p, wi, tq);
+    // Q[query c][16 i + 8 h .. + 7] split into hi / lo (the B operand of k-step i)
+    bf16x8 qh[8], ql[8];
+    {
+        const float4* src = reinterpret_cast<const float4*>(q + ((size_t)b * HW + qpix) * kC + 8 * h);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float4 a0 = src[4 * i], a1 = src[4 * i + 1];
+            const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            split8(x, qh[i], ql[i]);
+        }
+    }
+    bf16x8 qmask;
+    {
+        const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qmask[j] = (__bf16)(qreg == 8 * h + j ? 1.0f : 0.0f);
+    }
+    floatx16 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+
+    // gather: thread = (key row grow, 32-channel quarter gpart), hi and lo rows of K and V
+    const int grow = tid & 63, gpart = tid >> 6;
+    const int kbeg = ks * p.keys_per_split, kend = kbeg + p.keys_per_split;
+    bf16x8 kvh[4], kvl[4], vvh[4], vvl[4];
+    int kreg = 0;
+    auto gather = [&](int k0) {
+        const int j = k0 + grow;
+        const int tk = j / p.m, vi = j - tk * p.m;
+        const int kpix = win_pixel(p, wi, tk);
+        const size_t off = kvoff + ((size_t)vi * HW + kpix) * kC + 32 * gpart;
+        const bf16x8* a = reinterpret_cast<const bf16x8*>(khg + off);
+        const bf16x8* bl = reinterpret_cast<const bf16x8*>(klg + off);
+        const bf16x8* cv = reinterpret_cast<const bf16x8*>(vhg + off);
+        const bf16x8* dv = reinterpret_cast<const bf16x8*>(vlg + off);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            kvh[i] = a[i];
+            kvl[i] = bl[i];
+            vvh[i] = cv[i];
+            vvl[i] = dv[i];
+        }
+        kreg = p.shift ? win_region(p, wi, j % p.L) : 0;
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int chunk = 4 * gpart + i;
+            const int ko = grow * kC + ((chunk ^ (grow & 15)) * 8);
+            *reinterpret_cast<bf16x8*>(&sKh[buf][ko]) = kvh[i];
+            *reinterpret_cast<bf16x8*>(&sKl[buf][ko]) = kvl[i];
+            *reinterpret_cast<bf16x8*>(&sVh[buf][vimg_off(grow, chunk)]) = vvh[i];
+            *reinterpret_cast<bf16x8*>(&sVl[buf][vimg_off(grow, chunk)]) = vvl[i];
+        }
+        if (p.shift && gpart < 2) {
+            bf16x8 a;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) a[j] = (__bf16)(kreg == 8 * gpart + j ? kMaskBonus : 0.0f);
+            sMaskAb[buf][grow][gpart] = a;
+        }
+    };
+    gather(kbeg);
+    stage(0);
+    __syncthreads();
+    if (kbeg + kBK < kend) gather(kbeg + kBK);
+    for (int k0 = kbeg, buf = 0; k0 < kend; k0 += kBK, buf ^= 1) {
+        // ---- S^T = K Q^T (+ the mask step): per 16-channel k-step kl qh + kh ql + kh qh
+        floatx16 s[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[0][r] = s[1][r] = 0.f;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+            const int row = 32 * sub + c;
+            bf16x8 kh8[8], kl8[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int ko = row * kC + (((2 * i + h) ^ (row & 15)) * 8);
+                kh8[i] = *reinterpret_cast<const bf16x8*>(&sKh[buf][ko]);
+                kl8[i] = *reinterpret_cast<const bf16x8*>(&sKl[buf][ko]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl8[i], qh[i], s[sub], 0, 0, 0);
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh8[i], ql[i], s[sub], 0, 0, 0);
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh8[i], qh[i], s[sub], 0, 0, 0);
+            }
+            if (p.shift)
+                s[sub] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sMaskAb[buf][row][h], qmask, s[sub], 0, 0, 0);
+        }
+        // ---- online softmax (fp32, log2 domain), deferred rescale
+        float bmax = max3_raw(s[0][0], s[1][0], s[0][1]);
+        bmax = max3_raw(bmax, s[1][1], s[0][2]);
+#pragma unroll
+        for (int r = 2; r < 15; ++r) bmax = max3_raw(bmax, s[1][r], s[0][r + 1]);
+        bmax = fmaxf(bmax, s[1][15]);
+        const float bm2 = halves_max(bmax) * cl2;
+        if (__any(bm2 > m_run + kThr)) {
+            const float m_new = fmaxf(m_run, bm2);
+            const float corr = fast_exp2(m_run - m_new);
+            l_run *= corr;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+            m_run = m_new;
+        }
+        float bsum = 0.f;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float e = fast_exp2(fmaf(s[sub][r], cl2, -m_run));
+                s[sub][r] = e;
+                bsum += e;
+            }
+        l_run += halves_sum(bsum);
+
+        // ---- O^T += V^T P^T: 4 k-steps of 16 keys, per d tile vl ph + vh pl + vh ph
+        const int gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+#pragma unroll
+        for (int ksx = 0; ksx < 4; ++ksx) {
+            const int sub = ksx >> 1, st = ksx & 1;
+            float pv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) pv[e] = s[sub][8 * st + e];
+            bf16x8 ph, pl;
+            split8(pv, ph, pl);
+            const int r0 = 16 * ksx + 4 * h + qq;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const int c0 = 4 * dt + 2 * ((lane >> 4) & 1) + (pp >> 1);
+                const int a0 = vimg_off(r0, c0) + 8 * (pp & 1), a1 = vimg_off(r0 + 8, c0) + 8 * (pp & 1);
+                typedef __attribute__((address_space(3))) shortx4 lds4;
+                const shortx4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(sVh[buf] + a0));
+                const shortx4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(sVh[buf] + a1));
+                const shortx4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(sVl[buf] + a0));
+                const shortx4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(sVl[buf] + a1));
+                typedef short shortx8 __attribute__((ext_vector_type(8)));
+                const shortx8 vh8 = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+                const shortx8 vl8 = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vl8), ph, o[dt], 0, 0, 0);
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vh8), pl, o[dt], 0, 0, 0);
+                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vh8), ph, o[dt], 0, 0, 0);
+            }
+        }
+        // write-late: the next tile's rows go to the other buffer (its readers passed the previous
+        // barrier), then the tile after that is requested
+        if (k0 + kBK < kend) {
+            stage(buf ^ 1);
+            if (k0 + 2 * kBK < kend) gather(k0 + 2 * kBK);
+        }
+        __syncthreads();
+    }
+
+    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
+    if (p.ksplit == 1) {
+        const float inv = 1.0f / l_run;
+        float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                store4(dst + 32 * dt + 8 * u, make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv,
+                                                          o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
+    } else {
+        const size_t row = pidx(p, b, wi, ks, tq);
+        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, wid)) + lane;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
+        if (h == 0) {
+            part.m[row] = m_run * kLn2;  // natural-log maxima for the combine
+            part.l[row] = l_run;
+        }
+    }
+}
+
+// K and V (fp32, n elements each) -> [kh | kl | vh | vl] bf16, x = xh + xl (see win_attn_x3_kernel)
+__global__ void __launch_bounds__(256) split_kv_kernel(const float4* __restrict__ k, const float4* __restrict__ v,
+                                                       __bf16* __restrict__ out, size_t n4) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const float4 x = blockIdx.y ? v[i] : k[i];
+    typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+    bf16x4v hi, lo;
+    const float e[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        hi[j] = (__bf16)e[j];
+        lo[j] = (__bf16)(e[j] - (float)hi[j]);
+    }
+    bf16x4v* o = reinterpret_cast<bf16x4v*>(out + (size_t)blockIdx.y * 2 * (4 * n4));
+    o[i] = hi;
+    o[n4 + i] = lo;
+}
+
 }  // namespace winattn
 }  // namespace tsplat
 
@@ -1394,3 +1640,102 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     return TSPLAT_OK;
 }
 
+
+// bf16x3 key / value split for tsplat_win_attn_x3_*: out = [kh | kl | vh | vl], each n bf16
+extern "C" int tsplat_split_kv_bf16x3(const float* k, const float* v, void* out, int64_t n, void* stream_) {
+    if (!k || !v || !out || n <= 0 || n % 4 || ((uintptr_t)k & 15) || ((uintptr_t)v & 15) || ((uintptr_t)out & 7))
+        return TSPLAT_EINVAL;
+    const size_t n4 = (size_t)n / 4;
+    hipLaunchKernelGGL(tsplat::winattn::split_kv_kernel, dim3((unsigned)((n4 + 255) / 256), 2), dim3(256), 0,
+                       (hipStream_t)stream_, (const float4*)k, (const float4*)v, (__bf16*)out, n4);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+static int x3_params(tsplat::winattn::Params& p, int32_t batch, int32_t height, int32_t width, int32_t channels,
+                     int32_t key_views, int32_t splits, int32_t with_shift, int32_t key_batch_shift) {
+    using namespace tsplat::winattn;
+    if (channels != kC || batch <= 0 || key_views <= 0 || splits <= 0 || height % splits || width % splits)
+        return TSPLAT_EINVAL;
+    if (key_batch_shift < 0 || key_batch_shift >= batch) return TSPLAT_EINVAL;
+    p.H = height;
+    p.W = width;
+    p.splits = splits;
+    p.m = key_views;
+    p.L = (height / splits) * (width / splits);
+    p.shift_h = with_shift ? (height / splits) / 2 : 0;
+    p.shift_w = with_shift ? (width / splits) / 2 : 0;
+    p.shift = with_shift ? 1 : 0;
+    p.wh = height / splits;
+    p.ww = width / splits;
+    p.ww_log2 = (p.ww & (p.ww - 1)) == 0 ? __builtin_ctz(p.ww) : -1;
+    p.kv_shift = key_batch_shift;
+    p.nbatch = batch;
+    if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
+    if (p.L % kBQ3 || (p.L * p.m) % kBK) return TSPLAT_EINVAL;
+    p.scale = 1.0f / sqrtf((float)kC);
+    // the exact kernel's key split (so the workspace / partials layout is the same)
+    const int base = (p.L / kBQ3) * splits * splits * batch;
+    p.ksplit = pick_ksplit(base, p.L * p.m / kBK, kBQ3);
+    p.keys_per_split = p.L * p.m / p.ksplit;
+    return TSPLAT_OK;
+}
+
+// bf16x3 window attention, main kernel only (partials for the merge projection); kv_x3 =
+// tsplat_split_kv_bf16x3(k, v) ([kh | kl | vh | vl], k / v [batch, key_views, H*W, 128]). Same
+// shapes, key split and workspace as tsplat_win_attn_partials_fwd.
+extern "C" int tsplat_win_attn_x3_partials_fwd(const float* q, const void* kv_x3, void* workspace, int32_t batch,
+                                               int32_t height, int32_t width, int32_t channels, int32_t key_views,
+                                               int32_t splits, int32_t with_shift, int32_t key_batch_shift,
+                                               void* stream_) {
+    using namespace tsplat::winattn;
+    if (!q || !kv_x3 || !workspace) return TSPLAT_EINVAL;
+    Params p;
+    if (x3_params(p, batch, height, width, channels, key_views, splits, with_shift, key_batch_shift) != TSPLAT_OK)
+        return TSPLAT_EINVAL;
+    if (p.ksplit <= 1) return TSPLAT_EINVAL;
+    const size_t n = (size_t)batch * splits * splits * p.ksplit * p.L;
+    Partials part{(float*)workspace, nullptr, nullptr};
+    part.m = part.o + n * kC;
+    part.l = part.m + n;
+    const size_t nkv = (size_t)batch * key_views * height * width * kC;
+    const __bf16* kv = (const __bf16*)kv_x3;
+    hipStream_t stream = (hipStream_t)stream_;
+    const prof::ExtEvents ev = prof::ext_events(prof::kWinAttn);
+    hipExtLaunchKernelGGL(win_attn_x3_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit), dim3(kThreads), 0,
+                          stream, ev.start, ev.stop, 0, p, q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv,
+                          (float*)nullptr, part);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+// bf16x3 window attention, standalone (main + combine when the keys are split): out [batch, H*W,
+// 128] fp32, the same result class as tsplat_win_attn_fwd at >= TF32 precision (tests, benchmarks)
+extern "C" int tsplat_win_attn_x3_fwd(const float* q, const void* kv_x3, float* out, void* workspace, int32_t batch,
+                                      int32_t height, int32_t width, int32_t channels, int32_t key_views,
+                                      int32_t splits, int32_t with_shift, void* stream_) {
+    using namespace tsplat::winattn;
+    if (!q || !kv_x3 || !out) return TSPLAT_EINVAL;
+    Params p;
+    if (x3_params(p, batch, height, width, channels, key_views, splits, with_shift, 0) != TSPLAT_OK)
+        return TSPLAT_EINVAL;
+    Partials part{nullptr, nullptr, nullptr};
+    if (p.ksplit > 1) {
+        if (!workspace) return TSPLAT_EINVAL;
+        const size_t n = (size_t)batch * splits * splits * p.ksplit * p.L;
+        part.o = (float*)workspace;
+        part.m = part.o + n * kC;
+        part.l = part.m + n;
+    }
+    const size_t nkv = (size_t)batch * key_views * height * width * kC;
+    const __bf16* kv = (const __bf16*)kv_x3;
+    hipStream_t stream = (hipStream_t)stream_;
+    const prof::ExtEvents ev = prof::ext_events(prof::kWinAttn);
+    hipExtLaunchKernelGGL(win_attn_x3_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit), dim3(kThreads), 0,
+                          stream, ev.start, ev.stop, 0, p, q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
+    if (p.ksplit > 1)
+        hipLaunchKernelGGL(win_attn_combine_x32_kernel<float>, dim3(p.L / kBQ3 * 16, splits * splits, batch),
+                           dim3(kThreads), 0, stream, p, part, out);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

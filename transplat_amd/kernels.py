@@ -373,6 +373,40 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     return out.reshape(*lead, n)
 
 
+# bf16x3 window attention (tsplat_win_attn_x3_*) inside dense_precision("bf16x3") for the key-split
+# shapes (the C2 step's b = 1 transformer); TSPLAT_ATTN_X3=0 keeps the exact-fp32 kernel in that mode
+_ATTN_X3 = os.environ.get("TSPLAT_ATTN_X3", "1") == "1"
+
+
+def split_kv_bf16x3(k, v):
+    """[kh | kl | vh | vl] bf16 (x = xh + xl) of two same-shape fp32 tensors, one launch."""
+    lib = _lib.load()
+    k, v = _f32(k).contiguous(), _f32(v).contiguous()
+    if k.shape != v.shape:
+        raise ValueError(f"k {tuple(k.shape)} and v {tuple(v.shape)} differ")
+    out = torch.empty((4, k.numel()), dtype=torch.bfloat16, device=k.device)
+    _lib.check(lib.tsplat_split_kv_bf16x3(_lib.ptr(k), _lib.ptr(v), _lib.ptr(out), k.numel(),
+                                          _lib.stream_ptr(k.device)), "tsplat_split_kv_bf16x3")
+    return out
+
+
+def window_attention_x3(q, k, v, h: int, w: int, num_splits: int, with_shift: bool):
+    """window_attention(q, k, v) (fp32 [B, HW, 128], one key view) in bf16x3 precision
+    (tsplat_win_attn_x3_fwd: split-bf16 products on bf16 MFMA, fp32 softmax)."""
+    lib = _lib.load()
+    b, l, c = q.shape
+    m = 1 if k.dim() == 3 else k.shape[1]
+    kv = split_kv_bf16x3(k, v)
+    qf = _f32(q).contiguous()
+    out = torch.empty_like(qf)
+    ws = torch.empty(max(int(lib.tsplat_win_attn_workspace_bytes(b, h, w, m, num_splits)), 4), dtype=torch.uint8,
+                     device=q.device)
+    _lib.check(lib.tsplat_win_attn_x3_fwd(_lib.ptr(qf), _lib.ptr(kv), _lib.ptr(out), _lib.ptr(ws), b, h, w, c, m,
+                                          num_splits, int(with_shift), _lib.stream_ptr(q.device)),
+               "tsplat_win_attn_x3_fwd")
+    return out
+
+
 def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, merge_weight, ln, residual=None,
                     kv_shift: int = 0):
     """norm(window_attention(q, k, v) merge_weight^T) [+ residual] for the fp32 transformer layer.
@@ -403,9 +437,15 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
     ws = torch.empty(int(lib.tsplat_win_attn_workspace_bytes(b, h, w, m, num_splits)), dtype=torch.uint8,
                      device=q.device)
-    rc = lib.tsplat_win_attn_partials_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(ws), b, h, w, c, m,
-                                          num_splits, int(with_shift), int(kv_shift), _lib.stream_ptr(q.device))
-    _lib.check(rc, "tsplat_win_attn_partials_fwd")
+    if _ATTN_X3 and _DENSE == "bf16x3":
+        kv = split_kv_bf16x3(k, v)
+        rc = lib.tsplat_win_attn_x3_partials_fwd(_lib.ptr(q), _lib.ptr(kv), _lib.ptr(ws), b, h, w, c, m, num_splits,
+                                                 int(with_shift), int(kv_shift), _lib.stream_ptr(q.device))
+        _lib.check(rc, "tsplat_win_attn_x3_partials_fwd")
+    else:
+        rc = lib.tsplat_win_attn_partials_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(ws), b, h, w, c, m,
+                                              num_splits, int(with_shift), int(kv_shift), _lib.stream_ptr(q.device))
+        _lib.check(rc, "tsplat_win_attn_partials_fwd")
     n = merge_weight.shape[0]
     out = torch.empty((b, l, n), dtype=torch.float32, device=q.device)
     flags = (_LIN_LN if ln is not None else 0) | _lin_precision_flag()
