@@ -50,8 +50,9 @@ def parse():
                     help="dense convs / GEMMs: bf16x3 = split-bf16 products with fp32 accumulation (the "
                          "stand-in for the reference's TF32, src/main.py:15; more precise than it), fp32 = "
                          "exact fp32, bf16 = autocast (narrower than the reference)")
-    ap.add_argument("--attn-dtype", choices=["auto", "fp32", "bf16"], default="auto",
-                    help="window attention: auto = bf16 under bf16 dense layers, else exact fp32")
+    ap.add_argument("--attn-dtype", choices=["auto", "fp32", "bf16x3", "bf16"], default="auto",
+                    help="window attention: auto = bf16 under bf16 dense layers, bf16x3 (split-bf16 products, "
+                         "fp32 softmax) under bf16x3 ones, else exact fp32")
     ap.add_argument("--dominant", default=None, help="kernel timed for the roofline object")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one hipGraph per step")
     ap.add_argument("--batch", type=int, default=1, help="scenes per step per GPU")
@@ -197,9 +198,17 @@ def e2e_roofline_info(kernel: str, batch: int, attn_dtype: str = "fp32") -> dict
         per = n * hw * (c * 4 + d * 4) + n * hw * c * 4  # own + other features, output
         return {"dominant": kernel, "alg_bytes_per_launch": per, "bound": "hbm"}
     if kernel == "win_attn":
-        # 4 L S d FLOPs per window, 8 windows per scene-call (v = 2), fp32 MFMA
-        # bf16 attention runs the bf16-MFMA kernel (priced against the dense bf16 peak)
-        return {"dominant": kernel, "alg_flops_per_launch": 4 * 1024 * 1024 * 128 * 8 * batch, "bound": "mfma",
+        # 4 L S d FLOPs per window, 8 windows per scene-call (v = 2). fp32: exact fp32 MFMA, priced
+        # against the fp32 MFMA peak; bf16: the bf16-MFMA kernel, against the dense bf16 peak; bf16x3:
+        # three bf16 MFMA products per fp32 product (hi*hi + hi*lo + lo*hi), so the MFMA work is 3x
+        # the algorithmic FLOPs, priced against the dense bf16 peak (its fp32-equivalent rate is
+        # reported beside it)
+        flops = 4 * 1024 * 1024 * 128 * 8 * batch
+        if attn_dtype == "bf16x3":
+            return {"dominant": kernel, "alg_flops_per_launch": 3 * flops, "fp32_equivalent_flops_per_launch": flops,
+                    "bound": "mfma", "peak_tflops": BF16_MFMA_PEAK_TFS,
+                    "flops_note": "bf16 MFMA products: 3 x 4 L S d per window (split-bf16 hi*hi + hi*lo + lo*hi)"}
+        return {"dominant": kernel, "alg_flops_per_launch": flops, "bound": "mfma",
                 "peak_tflops": BF16_MFMA_PEAK_TFS if attn_dtype == "bf16" else FP32_MFMA_PEAK_TFS}
     if kernel == "raster":
         return {"dominant": kernel, "alg_bytes_per_launch": raster_bytes_per_view(131072, 25, 256, 256) * 3 * batch,
@@ -369,7 +378,9 @@ def main():
         return selftest_main(args, world, rank)
     device = torch.device(f"cuda:{local}")
     torch.cuda.set_device(device)
-    attn_dtype = args.attn_dtype if args.attn_dtype != "auto" else ("bf16" if args.dense_dtype == "bf16" else "fp32")
+    from transplat_amd.kernels import auto_attention
+
+    attn_dtype = args.attn_dtype if args.attn_dtype != "auto" else auto_attention(args.dense_dtype)
     if args.workload == "raster":
         dtype_label = "fp32"
     else:
@@ -502,6 +513,9 @@ def main():
             "launches": launches,
         },
     }
+    if "fp32_equivalent_flops_per_launch" in info:
+        result["roofline"]["flops_note"] = info["flops_note"]
+        result["roofline"]["fp32_equivalent_achieved"] = info["fp32_equivalent_flops_per_launch"] / (avg_ms * 1e-3) / 1e12
     if conv_roofline is not None:
         result["roofline_step_dominant"] = conv_roofline
     if rank == 0 and not args.no_cpu_baseline and cpu_inputs is not None:

@@ -152,7 +152,10 @@ def _copy_batch(dst, src):
 
 def precision_label(dense_dtype: str, attn_dtype: str = "auto") -> str:
     """What runs in which arithmetic, for the bench line's workload string."""
-    attn = attn_dtype if attn_dtype != "auto" else ("bf16" if dense_dtype == "bf16" else "fp32")
+    from .kernels import auto_attention
+
+    attn = attn_dtype if attn_dtype != "auto" else auto_attention(dense_dtype)
+    attn = {"bf16x3": "bf16x3 (split-bf16 products, fp32 softmax)"}.get(attn, attn)
     dense = {"fp32": "exact fp32", "bf16x3": "bf16x3 (split-bf16 products, fp32 accumulation; >= TF32)",
              "bf16": "bf16 (autocast)"}[dense_dtype]
     corr = ("correlation table bf16x3 (split-bf16 GEMM), correlation gathers / norms / adapter / raster fp32"

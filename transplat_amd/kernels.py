@@ -373,8 +373,8 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     return out.reshape(*lead, n)
 
 
-# bf16x3 window attention (tsplat_win_attn_x3_*) inside dense_precision("bf16x3") for the key-split
-# shapes (the C2 step's b = 1 transformer); TSPLAT_ATTN_X3=0 keeps the exact-fp32 kernel in that mode
+# bf16x3 window attention (tsplat_win_attn_x3_*) as the "auto" attention of the bf16x3 dense mode
+# (see auto_attention); TSPLAT_ATTN_X3=0 keeps the exact-fp32 kernel in that mode
 _ATTN_X3 = os.environ.get("TSPLAT_ATTN_X3", "1") == "1"
 
 
@@ -437,7 +437,7 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
     ws = torch.empty(int(lib.tsplat_win_attn_workspace_bytes(b, h, w, m, num_splits)), dtype=torch.uint8,
                      device=q.device)
-    if _ATTN_X3 and _DENSE == "bf16x3":
+    if _ATTN == "bf16x3":
         kv = split_kv_bf16x3(k, v)
         rc = lib.tsplat_win_attn_x3_partials_fwd(_lib.ptr(q), _lib.ptr(kv), _lib.ptr(ws), b, h, w, c, m, num_splits,
                                                  int(with_shift), int(kv_shift), _lib.stream_ptr(q.device))
@@ -833,17 +833,28 @@ def split_mode() -> bool:
     return _DENSE == "bf16x3"
 
 
-# Window-attention precision of the fp32 transformer path: "fp32" (exact fp32 MFMA) or "bf16"
-# (q / k / v rounded to bf16, bf16 MFMA with fp32 softmax and accumulation: config C3's "bf16
+# Window-attention precision of the fp32 transformer path: "fp32" (exact fp32 MFMA), "bf16x3"
+# (split-bf16 products on bf16 MFMA, fp32 softmax: the bf16x3 dense mode's attention, >= the
+# reference's TF32; tsplat_win_attn_x3_*, where the launch splits the keys -- else exact fp32) or
+# "bf16" (q / k / v rounded to bf16, bf16 MFMA with fp32 softmax and accumulation: config C3's "bf16
 # attention" beside fp32-class dense layers). Under bf16 autocast the attention is bf16 regardless.
 _ATTN = "fp32"
+ATTN_MODES = ("fp32", "bf16x3", "bf16")
+
+
+def auto_attention(dense_dtype: str) -> str:
+    """The attention precision "auto" means beside `dense_dtype` (TSPLAT_ATTN_X3=0: exact fp32
+    attention in the bf16x3 dense mode, the A/B knob)."""
+    if dense_dtype == "bf16":
+        return "bf16"
+    return "bf16x3" if dense_dtype == "bf16x3" and _ATTN_X3 else "fp32"
 
 
 class attention_precision:
     """Context manager: the window-attention precision inside the block (see _ATTN)."""
 
     def __init__(self, mode: str):
-        if mode not in ("fp32", "bf16"):
+        if mode not in ATTN_MODES:
             raise ValueError(f"attention precision {mode!r}")
         self.mode, self.prev = mode, None
 

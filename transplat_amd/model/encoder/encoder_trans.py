@@ -74,8 +74,9 @@ class EncoderTransCfg:
     # always run fp32; the fine-cross correlation TABLE is a dense GEMM and follows dense_dtype
     # (bf16x3: one split-bf16 hipBLASLt GEMM over K' = 3K, kernels.uv_cross).
     dense_dtype: str = "fp32"
-    # Window attention (T2): "auto" (bf16 MFMA under bf16 dense layers, else exact fp32), "fp32" or
-    # "bf16" (config C3 as BASELINE.json states it: bf16 attention beside fp32-class dense layers).
+    # Window attention (T2): "auto" (bf16 MFMA under bf16 dense layers, bf16x3 under bf16x3 ones,
+    # else exact fp32; kernels.auto_attention), "fp32", "bf16x3" or "bf16" (config C3 as
+    # BASELINE.json states it: bf16 attention beside fp32-class dense layers).
     attn_dtype: str = "auto"
 
 
@@ -164,7 +165,7 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
 
         attn = self.cfg.attn_dtype
         if attn == "auto":
-            attn = "bf16" if self.cfg.dense_dtype == "bf16" else "fp32"
+            attn = kernels.auto_attention(self.cfg.dense_dtype)
 
         def backbone(images, img2world):
             with bench("encoder_2_backbone"), self._dense(), kernels.attention_precision(attn):
