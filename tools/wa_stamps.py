@@ -3,7 +3,7 @@ tools/_bin/wastamp.so, tools/build_stamp_wa.sh; run with TSPLAT_LIB pointing at 
 For each shape: workgroups per CU (HW_ID / XCC_ID), the spread of start times, the shader clock
 rate, and the median / p90 of each phase in shader cycles: prologue (Q + first K/V tile, first
 barrier), each key tile, epilogue (partial or output store).
-usage: TSPLAT_LIB=tools/_bin/wastamp.so python tools/wa_stamps.py"""
+usage: TSPLAT_LIB=tools/_bin/wastamp.so python tools/wa_stamps.py [--x3]  (--x3: the bf16x3 kernel)"""
 import collections
 import ctypes
 import sys
@@ -27,17 +27,19 @@ def q(t, f):
     return t[min(len(t) - 1, int(f * len(t)))].item()
 
 
+X3 = "--x3" in sys.argv
+attn = kernels.window_attention_x3 if X3 else kernels.window_attention
 g = torch.Generator(device=dev).manual_seed(0)
 with torch.no_grad():
     for b, shift in ((2, 0), (2, 1), (16, 1)):
         hw = 64
         qq, k, v = (torch.randn((b, hw * hw, 128), device=dev, generator=g) for _ in range(3))
         for _ in range(3):
-            kernels.window_attention(qq, k, v, hw, hw, 2, bool(shift))
+            attn(qq, k, v, hw, hw, 2, bool(shift))
         torch.cuda.synchronize()
         buf.zero_()
         assert fn(buf.data_ptr()) == 0
-        kernels.window_attention(qq, k, v, hw, hw, 2, bool(shift))
+        attn(qq, k, v, hw, hw, 2, bool(shift))
         torch.cuda.synchronize()
         assert fn(None) == 0
         st = buf[buf[:, 0] != 0].cpu()

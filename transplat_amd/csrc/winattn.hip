@@ -1189,6 +1189,12 @@ win_attn_x3_kernel(Params p, const float* __restrict__ q, const __bf16* __restri
     __shared__ __attribute__((aligned(16))) unsigned char sVl[2][kBK * kC * 2];
     __shared__ __attribute__((aligned(16))) bf16x8 sMaskAb[2][kBK][2];
 
+    WA_STAMP(0, wall_clock64());
+    WA_STAMP(1, WA_HWID());
+    WA_STAMP(2, WA_CLOCK());
+    // (tried: all key splits of a (batch, window) on one XCD, so Q is fetched into one L2 once --
+    // prologue 10.2k vs 10.4k cycles, C2 unchanged, profiles/r5/x3/: the prologue is bound by the
+    // chip-wide L2 -> CU ingest rate of a 256-CU burst, not by HBM bytes)
     int qblk, wi, bz;
     xcd_block_coords(qblk, wi, bz);
     const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
@@ -1201,17 +1207,7 @@ win_attn_x3_kernel(Params p, const float* __restrict__ q, const __bf16* __restri
 
     const int tq = qblk * kBQ3 + wid * kQW + c;
     const int qpix = win_pixel(p, wi, tq);
-    // Q[query c][16 i + 8 h .. + 7] split into hi / lo (the B operand of k-step i)
     bf16x8 qh[8], ql[8];
-    {
-        const float4* src = reinterpret_cast<const float4*>(q + ((size_t)b * HW + qpix) * kC + 8 * h);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const float4 a0 = src[4 * i], a1 = src[4 * i + 1];
-            const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            split8(x, qh[i], ql[i]);
-        }
-    }
     bf16x8 qmask;
     {
         const int qreg = p.shift ? win_region(p, wi, tq) : 0;
@@ -1265,9 +1261,27 @@ win_attn_x3_kernel(Params p, const float* __restrict__ q, const __bf16* __restri
             sMaskAb[buf][grow][gpart] = a;
         }
     };
+    // prologue: the first tile's K / V loads go out before Q's, so stage(0) waits only for them;
+    // Q[query c][16 i + 8 h .. + 7] is split into hi / lo (the B operand of k-step i) after it
     gather(kbeg);
+    float4 qraw[16];
+    {
+        const float4* src = reinterpret_cast<const float4*>(q + ((size_t)b * HW + qpix) * kC + 8 * h);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            qraw[2 * i] = src[4 * i];
+            qraw[2 * i + 1] = src[4 * i + 1];
+        }
+    }
     stage(0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float4 a0 = qraw[2 * i], a1 = qraw[2 * i + 1];
+        const float x[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        split8(x, qh[i], ql[i]);
+    }
     __syncthreads();
+    WA_STAMP(3, WA_CLOCK());
     if (kbeg + kBK < kend) gather(kbeg + kBK);
     for (int k0 = kbeg, buf = 0; k0 < kend; k0 += kBK, buf ^= 1) {
         // ---- S^T = K Q^T (+ the mask step): per 16-channel k-step kl qh + kh ql + kh qh
@@ -1354,6 +1368,7 @@ win_attn_x3_kernel(Params p, const float* __restrict__ q, const __bf16* __restri
             if (k0 + 2 * kBK < kend) gather(k0 + 2 * kBK);
         }
         __syncthreads();
+        if ((k0 - kbeg) / kBK < 8) WA_STAMP(4 + (k0 - kbeg) / kBK, WA_CLOCK());
     }
 
     // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
@@ -1379,6 +1394,8 @@ win_attn_x3_kernel(Params p, const float* __restrict__ q, const __bf16* __restri
             part.l[row] = l_run;
         }
     }
+    WA_STAMP(12, WA_CLOCK());
+    WA_STAMP(13, wall_clock64());
 }
 
 // K and V (fp32, n elements each) -> [kh | kl | vh | vl] bf16, x = xh + xl (see win_attn_x3_kernel)
