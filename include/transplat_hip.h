@@ -314,6 +314,14 @@ int tsplat_win_attn_partials_fwd(const float* q, const float* k, const float* v,
  * workspace and key split as tsplat_win_attn_fwd / _partials_fwd (same partials layout, so
  * tsplat_linear_f32_attn_merge_fwd consumes the _x3_partials_fwd output unchanged). */
 int tsplat_split_kv_bf16x3(const float* k, const float* v, void* kv_x3, int64_t n, void* stream);
+/* The transformer's q | k | v (or k | v) projection writing its column blocks 128-wide as
+ * tsplat_linear_f32_fwd's split form does, except that blocks j >= x3_from land in kv_x3 as bf16
+ * hi / lo (block x3_from + i: hi at kv_x3 + 2 i M 128, lo at kv_x3 + (2 i + 1) M 128 elements) --
+ * the [kh | kl | vh | vl] operand of tsplat_win_attn_x3_* without a separate split pass. Blocks
+ * j < x3_from go to out + j M 128 (fp32). x1 [M, k1], w [N, k1], k1 % 64 == 0, N % 128 == 0;
+ * flags: 256 = bf16x3 products (else exact fp32). */
+int tsplat_linear_f32_split_x3_fwd(const float* x1, int32_t k1, const float* w, float* out, void* kv_x3, int32_t M,
+                                   int32_t N, int32_t x3_from, int32_t flags, void* stream);
 int tsplat_win_attn_x3_fwd(const float* q, const void* kv_x3, float* out, void* workspace, int32_t batch,
                            int32_t height, int32_t width, int32_t channels, int32_t key_views, int32_t splits,
                            int32_t with_shift, void* stream);
@@ -521,6 +529,10 @@ int tsplat_resize_bilinear_nhwc_fwd(const float* x, float* y, int32_t n, int32_t
  * torch's arithmetic (source = dst * (in - 1) / (out - 1) in float). */
 int tsplat_resize_bilinear_nchw_fwd(const float* x, float* y, int32_t planes, int32_t height, int32_t width,
                                     int32_t out_height, int32_t out_width, void* stream);
+
+/* Diagnostics: write the 100-MHz device wall clock into ((uint64_t*)buf)[slot] when this launch
+ * runs on `stream` (stage marks of a captured / replayed step, tools/graph_stages.py). */
+int tsplat_timestamp(void* buf, int32_t slot, void* stream);
 
 #ifdef __cplusplus
 }

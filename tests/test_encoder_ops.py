@@ -392,6 +392,38 @@ def test_window_attention_x3_kernel(device, hw, m, shift, b, grow):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dense", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("x3_from,n", [(1, 384), (0, 256)])
+def test_linear_kv_x3_matches_split(device, dense, x3_from, n):
+    """tsplat_linear_f32_split_x3_fwd (the q | k | v or k | v projection writing k / v as the bf16x3
+    attention's hi / lo operand) == the fp32 split projection followed by tsplat_split_kv_bf16x3,
+    bit for bit (same kernel arithmetic, the split applied to the same fp32 values); and the
+    attention merge fed the pre-split operand == the one fed fp32 k / v."""
+    from transplat_amd import kernels as K
+
+    m = 8192
+    x = seeded((2, m // 2, 128), 61).to(device)
+    w = (seeded((n, 128), 62) / math.sqrt(128)).to(device)
+    with K.dense_precision(dense):
+        ref_blocks = K.fused_linear(x, w, split=True)
+        blocks, kv = K.linear_kv_x3(x, w, x3_from)
+    assert len(blocks) == x3_from
+    for a, b in zip(blocks, ref_blocks[:x3_from]):
+        assert torch.equal(a, b)
+    k, v = ref_blocks[x3_from:]
+    assert torch.equal(kv, K.split_kv_bf16x3(k, v))
+    if x3_from == 1:
+        q = blocks[0]
+        wm = (seeded((128, 128), 63) / math.sqrt(128)).to(device)
+        ln = (torch.ones(128, device=device), torch.zeros(128, device=device), 1e-5)
+        with K.dense_precision(dense), K.attention_precision("bf16x3"):
+            assert K.attention_x3_ready(2, 64, 64, 1, 2)
+            a = K.attention_merge(q, k, v, 64, 64, 2, True, wm, ln, kv_shift=1)
+            b = K.attention_merge(q, None, None, 64, 64, 2, True, wm, ln, kv_shift=1, kv_x3=kv)
+        assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
 def test_window_attention_dtu_stress(device):
     """C5 stress: 3 context views at 512x384 -> a 128x96 feature map, 2 windows per side
     (L = 3072 queries, 6144 keys over two key views), shifted layer."""

@@ -37,6 +37,7 @@ _I32 = ctypes.c_int32
 SIGNATURES = {
     "tsplat_version": (ctypes.c_int, []),
     "tsplat_set_debug": (ctypes.c_int, [_I32]),
+    "tsplat_timestamp": (ctypes.c_int, [_P, _I32, _P]),
     "tsplat_prof_enable": (ctypes.c_int, [_I32]),
     "tsplat_prof_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I32)]),
     "tsplat_raster_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, _I32, _I32, _I32]),
@@ -80,6 +81,7 @@ SIGNATURES = {
     "tsplat_bias_act_nhwc_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int64, _I32, _I32, _P]),
     "tsplat_win_attn_partials_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 8 + [_P]),
     "tsplat_split_kv_bf16x3": (ctypes.c_int, [_P, _P, _P, ctypes.c_int64, _P]),
+    "tsplat_linear_f32_split_x3_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P] + [_I32] * 4 + [_P]),
     "tsplat_win_attn_x3_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 7 + [_P]),
     "tsplat_win_attn_x3_partials_fwd": (ctypes.c_int, [_P] * 3 + [_I32] * 8 + [_P]),
     "tsplat_linear_f32_attn_merge_fwd": (ctypes.c_int, [_P] + [_I32] * 6 + [_P] * 3 + [ctypes.c_float, _P, _P, _I32,

@@ -103,3 +103,19 @@ extern "C" int tsplat_prof_read(double* total_ms, int32_t* launches) {
     g_open = false;
     return TSPLAT_OK;
 }
+
+// Diagnostic stage marks (tools/graph_stages.py, TSPLAT_MARKS=1): one lane writes the 100-MHz
+// wall clock into buf[slot] when the launch runs on `stream` -- captured into a hipGraph like any
+// launch, so the stage boundaries of a replayed step can be read back per stream
+namespace tsplat {
+__global__ void stamp_kernel(unsigned long long* buf, int slot) {
+    if (threadIdx.x == 0) buf[slot] = wall_clock64();
+}
+}  // namespace tsplat
+
+extern "C" int tsplat_timestamp(void* buf, int32_t slot, void* stream) {
+    if (!buf || slot < 0) return TSPLAT_EINVAL;
+    hipLaunchKernelGGL(tsplat::stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, (unsigned long long*)buf, slot);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

@@ -58,6 +58,11 @@ struct Args {
     const float* pm;
     const float* pl;
     int aks, aH, aW, aS, aL, awh, aww, ash, asw;
+    // kSplit outputs from column block x3_from on go to kv_x3 as bf16 hi / lo pairs (x = hi + lo):
+    // block x3_from + i -> hi at kv_x3 + 2 i M 128, lo at kv_x3 + (2 i + 1) M 128 (the K / V operands
+    // of tsplat_win_attn_x3_*); x3_from < 0: none
+    __bf16* kv_x3;
+    int x3_from;
 };
 
 constexpr int kMaxSplit = 8;
@@ -382,6 +387,24 @@ linear_f32_kernel(Args a) {
         }
     }
     if (!active || m >= a.M) return;
+    if ((a.flags & kSplit) && a.x3_from >= 0 && nb / kBN >= a.x3_from) {
+        typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+        const size_t blk = (size_t)(nb / kBN - a.x3_from) * 2;
+        __bf16* hi = a.kv_x3 + blk * a.M * kBN + (size_t)m * kBN + nb % kBN;
+        __bf16* lo = hi + (size_t)a.M * kBN;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            bf16x4v vh, vl;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                vh[j] = (__bf16)y[4 * u + j];
+                vl[j] = (__bf16)(y[4 * u + j] - (float)vh[j]);
+            }
+            *reinterpret_cast<bf16x4v*>(hi + 8 * u) = vh;
+            *reinterpret_cast<bf16x4v*>(lo + 8 * u) = vl;
+        }
+        return;
+    }
     float* dst;
     int col0;
     if (a.flags & kSplit) {  // column block j of 128 -> its own [M, 128] matrix
@@ -405,6 +428,8 @@ linear_f32_kernel(Args a) {
 
 using namespace tsplat;
 
+static int launch_linear(tsplat::linear::Args a, void* stream_);
+
 extern "C" int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x2, int32_t k2, const float* w,
                                      const float* bias, const float* ln_gamma, const float* ln_beta,
                                      float ln_eps, const float* residual, float* out, int64_t split_stride,
@@ -420,6 +445,32 @@ extern "C" int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x
     if ((flags & kSplit) && split_stride < (int64_t)M * kBN) return TSPLAT_EINVAL;
     Args a{x1, x2, w, bias, ln_gamma, ln_beta, residual, out, split_stride, ln_eps, k1, k2, M, N, flags};
     a.po = a.pm = a.pl = nullptr;
+    a.kv_x3 = nullptr;
+    a.x3_from = -1;
+    return launch_linear(a, stream_);
+}
+
+// tsplat_linear_f32_fwd's split form with the column blocks from x3_from on written as bf16 hi / lo
+// (see Args::kv_x3): the transformer's k / v projections straight into the bf16x3 attention's
+// operand layout (no separate split pass). Blocks before x3_from go to out (fp32, split layout).
+extern "C" int tsplat_linear_f32_split_x3_fwd(const float* x1, int32_t k1, const float* w, float* out, void* kv_x3,
+                                             int32_t M, int32_t N, int32_t x3_from, int32_t flags, void* stream_) {
+    using namespace tsplat::linear;
+    if (!x1 || !w || !kv_x3 || M <= 0 || N <= 0 || k1 <= 0 || k1 % kBK || N % kBN) return TSPLAT_EINVAL;
+    if (x3_from < 0 || x3_from >= N / kBN || (x3_from > 0 && !out)) return TSPLAT_EINVAL;
+    if (flags & ~(kBf16x3 | kBias)) return TSPLAT_EINVAL;  // plain projections (the attention's q | k | v)
+    if (((uintptr_t)kv_x3) & 7) return TSPLAT_EINVAL;
+    Args a{x1, nullptr, w, nullptr, nullptr, nullptr, nullptr, out, (long long)M * kBN, 0.f, k1, 0, M, N,
+           flags | kSplit};
+    a.po = a.pm = a.pl = nullptr;
+    a.kv_x3 = (__bf16*)kv_x3;
+    a.x3_from = x3_from;
+    return launch_linear(a, stream_);
+}
+
+static int launch_linear(tsplat::linear::Args a, void* stream_) {
+    using namespace tsplat::linear;
+    const int M = a.M, N = a.N, flags = a.flags;
     hipStream_t stream = (hipStream_t)stream_;
     TSPLAT_PROF_BEGIN(prof::kLinear, stream);
     // 64-row blocks when that still fills the 256 CUs, else 32-row blocks with the K halves split
@@ -460,6 +511,8 @@ extern "C" int tsplat_linear_f32_attn_merge_fwd(const float* partials, int32_t b
     if (flags & kBias) return TSPLAT_EINVAL;
     const int M = batch * height * width;
     Args a{nullptr, nullptr, w, nullptr, ln_gamma, ln_beta, residual, out, 0, ln_eps, kBN, 0, M, N, flags};
+    a.kv_x3 = nullptr;
+    a.x3_from = -1;
     a.aks = ks;
     a.aH = height;
     a.aW = width;

@@ -407,16 +407,49 @@ def window_attention_x3(q, k, v, h: int, w: int, num_splits: int, with_shift: bo
     return out
 
 
+def attention_x3_ready(b: int, h: int, w: int, m: int, num_splits: int) -> bool:
+    """True when attention_merge runs the bf16x3 kernel for this shape (the x3 precision is active
+    and the launch splits the keys), i.e. when the k / v projection may hand it pre-split operands
+    (linear_kv_x3) instead of fp32 k / v."""
+    return _ATTN == "bf16x3" and int(_lib.load().tsplat_win_attn_split(b, h, w, m, num_splits)) > 1
+
+
+def linear_kv_x3(x, weight, x3_from: int):
+    """[x W^T] column blocks of 128 (the q | k | v or k | v projection): blocks before x3_from as fp32
+    [..., 128] tensors, the rest as ONE [kh | kl | vh | vl] bf16 buffer (tsplat_linear_f32_split_x3_fwd;
+    bf16x3 products inside dense_precision("bf16x3")). Returns (list of fp32 blocks, kv_x3)."""
+    lib = _lib.load()
+    lead = x.shape[:-1]
+    k1, n = x.shape[-1], weight.shape[0]
+    a = _f32(x).reshape(-1, k1)
+    m = a.shape[0]
+    nb = n // 128
+    out = torch.empty((x3_from, m, 128), dtype=torch.float32, device=x.device) if x3_from else None
+    kv = torch.empty((2 * (nb - x3_from), m * 128), dtype=torch.bfloat16, device=x.device)
+    _lib.check(lib.tsplat_linear_f32_split_x3_fwd(_lib.ptr(a), k1, _lib.ptr(_f32(weight)), _lib.ptr(out), _lib.ptr(kv), m,
+                                                  n, x3_from, _lin_precision_flag(), _lib.stream_ptr(x.device)),
+               "tsplat_linear_f32_split_x3_fwd")
+    blocks = [t.reshape(*lead, 128) for t in out.unbind(0)] if out is not None else []
+    return blocks, kv
+
+
 def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, merge_weight, ln, residual=None,
-                    kv_shift: int = 0):
+                    kv_shift: int = 0, kv_x3=None):
     """norm(window_attention(q, k, v) merge_weight^T) [+ residual] for the fp32 transformer layer.
     Where the attention kernel splits the keys (b = 1 at 64x64), the combine of its partials runs
     in the merge kernel's operand staging (tsplat_win_attn_partials_fwd +
     tsplat_linear_f32_attn_merge_fwd: no combine launch, no [B, L, 128] attention output);
     otherwise window_attention + fused_linear. kv_shift: query batch i attends to the keys /
-    values of batch (i + kv_shift) % B (the two-view cross pairing without a swapped copy)."""
+    values of batch (i + kv_shift) % B (the two-view cross pairing without a swapped copy). kv_x3:
+    the bf16x3 kernel's pre-split [kh | kl | vh | vl] operand (linear_kv_x3) in place of k / v
+    (None), for shapes where attention_x3_ready() holds."""
     lib = _lib.load()
     b, l, c = q.shape
+    if kv_x3 is not None:
+        if not attention_x3_ready(b, h, w, 1, num_splits):
+            raise ValueError("kv_x3 given for a shape / precision that does not run the bf16x3 kernel")
+        return _merge_partials(lib, q, None, None, h, w, num_splits, with_shift, merge_weight, ln, residual,
+                               kv_shift, 1, kv_x3)
     m = 1 if k.dim() == 3 else k.shape[1]
     fp32 = q.dtype == k.dtype == v.dtype == torch.float32
     wl = (h // num_splits) * (w // num_splits)
@@ -434,15 +467,22 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
             k, v = torch.roll(k, -kv_shift, dims=0), torch.roll(v, -kv_shift, dims=0)
         msg = window_attention(q, k, v, h, w, num_splits, with_shift)
         return fused_linear(msg, merge_weight, ln=ln, residual=residual)
-    q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+    return _merge_partials(lib, q, k, v, h, w, num_splits, with_shift, merge_weight, ln, residual, kv_shift, m, None)
+
+
+def _merge_partials(lib, q, k, v, h, w, num_splits, with_shift, merge_weight, ln, residual, kv_shift, m, kv_x3):
+    """attention_merge's key-split path: the attention kernel's partials + the merge projection."""
+    b, l, c = q.shape
+    q = q.contiguous()
     ws = torch.empty(int(lib.tsplat_win_attn_workspace_bytes(b, h, w, m, num_splits)), dtype=torch.uint8,
                      device=q.device)
     if _ATTN == "bf16x3":
-        kv = split_kv_bf16x3(k, v)
+        kv = kv_x3 if kv_x3 is not None else split_kv_bf16x3(k, v)
         rc = lib.tsplat_win_attn_x3_partials_fwd(_lib.ptr(q), _lib.ptr(kv), _lib.ptr(ws), b, h, w, c, m, num_splits,
                                                  int(with_shift), int(kv_shift), _lib.stream_ptr(q.device))
         _lib.check(rc, "tsplat_win_attn_x3_partials_fwd")
     else:
+        k, v = k.contiguous(), v.contiguous()
         rc = lib.tsplat_win_attn_partials_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(ws), b, h, w, c, m,
                                               num_splits, int(with_shift), int(kv_shift), _lib.stream_ptr(q.device))
         _lib.check(rc, "tsplat_win_attn_partials_fwd")

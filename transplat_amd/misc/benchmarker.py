@@ -90,7 +90,49 @@ class _RangesOnly:
                 self._nvtx.range_pop()
 
 
-_RANGES = _RangesOnly() if os.environ.get("TSPLAT_ROCTX", "0") == "1" else None
+class StageMarks:
+    """Device-clock stage marks (TSPLAT_MARKS=1, no Benchmarker passed): entering and leaving a stage
+    launches tsplat_timestamp on the current stream, so a captured step replays them in place;
+    `read()` returns (tag, "begin" / "end", stream id, seconds since the first mark) per slot, in
+    slot order (tools/graph_stages.py)."""
+
+    def __init__(self, capacity: int = 256):
+        self.capacity, self.slots, self.buf = capacity, [], None
+
+    def _mark(self, tag: str, kind: str) -> None:
+        from .. import _lib
+
+        if not torch.cuda.is_available():
+            return
+        if self.buf is None:
+            self.buf = torch.zeros(self.capacity, dtype=torch.int64, device="cuda")
+        if len(self.slots) >= self.capacity:
+            return
+        s = torch.cuda.current_stream()
+        self.slots.append((tag, kind, s.stream_id))
+        _lib.check(_lib.load().tsplat_timestamp(_lib.ptr(self.buf), len(self.slots) - 1, _lib.stream_ptr(s.device)),
+                   "tsplat_timestamp")
+
+    def reset(self) -> None:
+        """Forget the recorded slots (a new capture / eager step records them again)."""
+        self.slots = []
+
+    @contextmanager
+    def time(self, tag: str, num_calls: int = 1):
+        self._mark(tag, "begin")
+        try:
+            yield
+        finally:
+            self._mark(tag, "end")
+
+    def read(self) -> list:
+        t = self.buf[: len(self.slots)].cpu().tolist()
+        t0 = min(t)
+        return [(tag, kind, sid, (v - t0) / 1e8) for (tag, kind, sid), v in zip(self.slots, t)]
+
+
+MARKS = StageMarks() if os.environ.get("TSPLAT_MARKS", "0") == "1" else None
+_RANGES = MARKS if MARKS is not None else (_RangesOnly() if os.environ.get("TSPLAT_ROCTX", "0") == "1" else None)
 
 
 def stage(benchmarker, tag: str):

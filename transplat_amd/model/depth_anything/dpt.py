@@ -252,8 +252,12 @@ class DepthAnythingV2(nn.Module):
                 pending[k] = streams.fork(tokens.device, head.reassemble, k, tokens[:, 1:], patch_h, patch_w,
                                           slot=1)
 
-        features = self.pretrained.get_intermediate_layers(x, self.intermediate_layer_idx[self.encoder],
-                                                           return_class_token=True, on_output=on_output)
+        from ...misc.benchmarker import stage
+
+        with stage(None, "da_dinov2"):  # diagnostic sub-stage marks (TSPLAT_MARKS / TSPLAT_ROCTX)
+            features = self.pretrained.get_intermediate_layers(x, self.intermediate_layer_idx[self.encoder],
+                                                               return_class_token=True, on_output=on_output)
         rn = [streams.join(pending[k]) if k in pending else None for k in range(n_take)]
-        depth, out_features = head(features, patch_h, patch_w, rn=rn)
+        with stage(None, "da_dpt"):
+            depth, out_features = head(features, patch_h, patch_w, rn=rn)
         return F.relu(depth).squeeze(1), out_features

@@ -65,11 +65,15 @@ class BackboneMultiview(torch.nn.Module):
         return features_list
 
     def forward(self, images, attn_splits=2, return_cnn_features=False, img2world=None):
-        features_list = self.extract_feature(self.normalize_images(images))
+        from ....misc.benchmarker import stage
+
+        with stage(None, "backbone_cnn"):  # diagnostic sub-stage marks (TSPLAT_MARKS / TSPLAT_ROCTX)
+            features_list = self.extract_feature(self.normalize_images(images))
         cur_features_list = [x[0] for x in features_list]
         cnn_features = torch.stack(cur_features_list, dim=1) if return_cnn_features else None
         cur_features_list = [self.cam_param_encoder(f, img2world[:, v_id]) for v_id, f in enumerate(cur_features_list)]
         cur_features_list = feature_add_position_list(cur_features_list, attn_splits, self.feature_channels)
-        cur_features_list = self.transformer(cur_features_list, attn_num_splits=attn_splits)
+        with stage(None, "backbone_mvt"):
+            cur_features_list = self.transformer(cur_features_list, attn_num_splits=attn_splits)
         features = torch.stack(cur_features_list, dim=1)
         return [features, cnn_features]

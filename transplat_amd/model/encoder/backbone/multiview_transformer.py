@@ -58,7 +58,16 @@ class TransformerLayer(nn.Module):
         kv_shift > 0: `target` is NOT view-swapped; query batch i reads the keys / values of its
         batch (i + kv_shift) % B (the swap is index arithmetic in the attention kernel)."""
         K = kernels
-        if target is source:
+        kv_x3 = key = value = None
+        if source.dim() == 3 and K.attention_x3_ready(source.shape[0], height, width, 1, attn_num_splits):
+            # bf16x3 attention: the k / v column blocks leave the projection as the kernel's bf16 hi / lo
+            # operand (no fp32 k / v, no split pass)
+            if target is source:
+                (query,), kv_x3 = K.linear_kv_x3(source, self._cat_weights(("q_proj", "k_proj", "v_proj")), 1)
+            else:
+                query = K.fused_linear(source, self.q_proj.weight)
+                _, kv_x3 = K.linear_kv_x3(target, self._cat_weights(("k_proj", "v_proj")), 0)
+        elif target is source:
             query, key, value = K.fused_linear(source, self._cat_weights(("q_proj", "k_proj", "v_proj")), split=True)
         else:
             query = K.fused_linear(source, self.q_proj.weight)
@@ -66,9 +75,9 @@ class TransformerLayer(nn.Module):
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
         if self.no_ffn:
             return K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
-                                     self.merge.weight, ln1, residual=source, kv_shift=kv_shift)
+                                     self.merge.weight, ln1, residual=source, kv_shift=kv_shift, kv_x3=kv_x3)
         message = K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
-                                    self.merge.weight, ln1, kv_shift=kv_shift)
+                                    self.merge.weight, ln1, kv_shift=kv_shift, kv_x3=kv_x3)
         # mlp[0] is the one large plain GEMM of the layer (8192 x 256 x 1024 at b = 1): hipBLASLt
         # runs it at 103 TF, above this build's kernel (66 TF); its GELU moves into mlp[2]'s load
         hidden = self.mlp[0](torch.cat([source, message], dim=-1))
