@@ -3,6 +3,7 @@
 # (tools/build_prev_lib.sh <rev>) on the Winograd census and C2, alternating; extra env A/Bs via
 # AB_ENV ("NAME=VALUE" applied to the 'env' leg, run against the current library).
 # usage: TAG=<tag> TESTS="tests/test_conv.py" AB_ENV="TSPLAT_CONV_ZSPLIT=0" bash tools/sessions/r5_ab.sh
+# (LEGS="cur env env2 env3" with AB_ENV2 / AB_ENV3: more env legs against the current library)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd)
@@ -28,6 +29,8 @@ for i in 1 2; do
     envs=""
     [ $leg = prev ] && export TSPLAT_LIB=tools/_bin/prev.so
     [ $leg = env ] && envs="$AB_ENV"
+    [ $leg = env2 ] && envs="$AB_ENV2"
+    [ $leg = env3 ] && envs="$AB_ENV3"
     [ $leg = env ] && [ -z "$AB_ENV" ] && continue
     env $envs timeout -k 10 300 python -u bench.py --no-cpu-baseline ${BENCH_ARGS} > $OUT/bench_${leg}_$i.log 2>&1 || { tail -5 $OUT/bench_${leg}_$i.log; exit 4; }
     echo "$leg $i c2 $(tail -1 $OUT/bench_${leg}_$i.log | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["value"],1), round(d["roofline"]["frac"],4), d["roofline"]["avg_launch_ms"], round(d["roofline_step_dominant"]["ms_per_step"],3))')"

@@ -601,11 +601,14 @@ _CONV1_PAIRS = int(os.environ.get("TSPLAT_CONV1_PAIRS", "8"))
 _CONV3_WAVES = int(os.environ.get("TSPLAT_CONV3_WAVES", "8192"))
 _CONV3_PAIRS = int(os.environ.get("TSPLAT_CONV3_PAIRS", "2"))
 # Split of each tile's ci pairs over workgroups (tsplat_conv2d_f32_zsplit_fwd) for few-tile maps:
-# doubled while a wave still has more than one load batch of pairs (4 for a 3x3, 16 for a 1x1) and
-# the grid stays within one round of 16-wave workgroups (one per CU). TSPLAT_CONV_ZSPLIT=0 turns it
-# off, =N caps it at N.
+# doubled while the grid stays within one round of 16-wave workgroups (one per CU) and every wave
+# keeps more than _ZSPLIT_MIN pairs (3x3; 1x1: 4x that). A 32 x 32 tile's workgroup loads the
+# weights of its 32 output channels over the whole reduction, so on few-tile maps the per-CU ingest
+# of those weights, not the MFMAs, sets the time: splitting the reduction over more CUs divides it.
+# TSPLAT_CONV_ZSPLIT=0 turns it off, =N caps it at N.
 _ZSPLIT = int(os.environ.get("TSPLAT_CONV_ZSPLIT", "-1"))
 _ZSPLIT_WGS = int(os.environ.get("TSPLAT_CONV_ZSPLIT_WGS", "256"))
+_ZSPLIT_MIN = int(os.environ.get("TSPLAT_CONV_ZSPLIT_MIN", "4"))
 # arrival counters of the zsplit launches: one zeroed slab per device, handed out in rotating ranges
 # (each launch leaves its range at zero again), so launches in flight on concurrent streams never share
 # a counter while the slab holds more tiles than the launches of one step
@@ -629,7 +632,7 @@ def conv_zsplit(tiles: int, pairs: int, ksplit: int, k: int) -> int:
     """Workgroups per output tile for tsplat_conv2d_f32_zsplit_fwd (1 = no split)."""
     if _ZSPLIT == 0:
         return 1
-    per_batch = 4 if k == 3 else 16
+    per_batch = _ZSPLIT_MIN if k == 3 else 4 * _ZSPLIT_MIN
     z = 1
     while (z < 64 and tiles * 2 * z <= _ZSPLIT_WGS and -(-pairs // (ksplit * z)) > per_batch
            and (_ZSPLIT < 0 or 2 * z <= _ZSPLIT)):
