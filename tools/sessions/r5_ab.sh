@@ -11,7 +11,7 @@ OUT=$R/gpurun_out/${TAG:-r5_ab}
 mkdir -p $OUT
 export PYTHONPATH=$R
 if [ -n "$TESTS" ]; then
-  timeout -k 10 600 python -u -m pytest $TESTS -m gpu -q -x --timeout 200 --timeout-method thread -s > $OUT/pytest.log 2>&1 \
+  timeout -k 10 600 python -u -m pytest $TESTS -m gpu -q -x --timeout 200 --timeout-method thread -s ${TESTK:+-k "$TESTK"} > $OUT/pytest.log 2>&1 \
     || { tail -30 $OUT/pytest.log; exit 1; }
   tail -1 $OUT/pytest.log
 fi

@@ -608,7 +608,7 @@ _CONV3_PAIRS = int(os.environ.get("TSPLAT_CONV3_PAIRS", "2"))
 # TSPLAT_CONV_ZSPLIT=0 turns it off, =N caps it at N.
 _ZSPLIT = int(os.environ.get("TSPLAT_CONV_ZSPLIT", "-1"))
 _ZSPLIT_WGS = int(os.environ.get("TSPLAT_CONV_ZSPLIT_WGS", "256"))
-_ZSPLIT_MIN = int(os.environ.get("TSPLAT_CONV_ZSPLIT_MIN", "4"))
+_ZSPLIT_MIN = int(os.environ.get("TSPLAT_CONV_ZSPLIT_MIN", "1"))  # 4 / 2 / 1: C2 413.4 / 415.8 / 417.3 (profiles/r5/ab_zsplit.txt)
 # arrival counters of the zsplit launches: one zeroed slab per device, handed out in rotating ranges
 # (each launch leaves its range at zero again), so launches in flight on concurrent streams never share
 # a counter while the slab holds more tiles than the launches of one step
