@@ -418,16 +418,6 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
         }
     };
 
-    // epilogue outputs of this thread: pidx = tid + NT i, i < NIT (see the store loop below)
-    constexpr int NT = 256 * CB * KS, NIT = (CO * T + NT - 1) / NT;
-    float bias_r[ST ? NIT : 1];
-    auto prefetch_bias = [&]() {  // staged forms only (the unstaged 64 x 64 form has no registers to spare)
-#pragma unroll
-        for (int i = 0; i < (ST ? NIT : 0); ++i) {
-            const int o = (a.cob_base + cbk * CB) * 32 + (tid + NT * i) / T;
-            bias_r[i] = a.bias && o < a.co ? a.bias[o] : 0.0f;
-        }
-    };
     // k-group kg takes chunks kg, kg + KS, ...; every group runs the same iteration count (a chunk
     // past the last one is all zeros) so the groups meet at every barrier
     const int iters = (a.nchunk + KS - 1) / KS;
@@ -437,21 +427,10 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
         // single sV: store region(it + 1) | transform(it) | loads of region(it + 3) (DS) or it + 2 |
         // barrier | MFMAs(it) | barrier. Region r lives in register set r & 1 (DS) or set 0.
         gload(kg, I0);
-        if constexpr (DS) {
-            // the second region's and the first A fragments' loads go out before region 0 is stored,
-            // so the prologue waits for one round trip, not three
-            gload(kg + KS, I1);
-            load_a(kg, 0, 4);
-            sstore(0, I0);
-            gload(kg + 2 * KS, I0);
-        } else {
-            sstore(0, I0);
-            gload(kg + KS, I1);
-            load_a(kg, 0, 4);
-        }
-        // the epilogue's bias values, loaded now (in the epilogue the load would be a dependent
-        // round trip between the Z fold and the stores)
-        prefetch_bias();
+        sstore(0, I0);
+        gload(kg + KS, I1);
+        if (DS) gload(kg + 2 * KS, I0);
+        load_a(kg, 0, 4);
         __syncthreads();
         W3_STAMP(1);
         // S = the register set of region it + 1
@@ -527,15 +506,12 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
         __syncthreads();
     }
     const size_t hw = (size_t)a.h * a.w;
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-        const int pidx = tid + NT * i;
-        if (pidx >= CO * T) break;
+    for (int pidx = tid; pidx < CO * T; pidx += 256 * CB * KS) {
         const int col = pidx / T, t2 = pidx % T;
         const int o = (a.cob_base + cbk * CB) * 32 + col;
         const int oty = (blk / a.bx) * a.tby + t2 / a.tbx, otx = (blk % a.bx) * a.tbx + t2 % a.tbx;
         if (o >= a.co || oty >= a.th || otx >= a.tw) continue;
-        const float bv = ST ? bias_r[ST ? i : 0] : (a.bias ? a.bias[o] : 0.0f);
+        const float bv = a.bias ? a.bias[o] : 0.0f;
         float z[4][2];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
