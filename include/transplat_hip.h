@@ -407,7 +407,7 @@ int tsplat_qkv_attention_cf_fwd(const float* qkv, float* out, int32_t batch, int
  * unet.py:105-137): y [batch, c_out, hout, wout] = conv(x, w, bias, stride, padding = ksize / 2)
  * with x = cat([x1 (c1 channels), x2 (c2 channels, may be 0)], dim 1) [batch, c1 + c2, height, width]
  * read in place, nearest-upsampled 2x first when upsample = 1. ksize 1 or 3, stride 1 or 2 (not
- * with upsample), c1 and c2 even. w_packed is the weight [c_out, cin, k, k] laid out as
+ * with upsample; the strided 1x1 is the UniMatch CNN's shortcut), c1 and c2 even. w_packed is the weight [c_out, cin, k, k] laid out as
  * [ceil(c_out / 32)][k * k][cin / 2][2][32] (zero rows past c_out); bias may be null. ksplit
  * (1..16) waves share one 32 x 32 output tile. */
 int tsplat_conv2d_f32_fwd(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* w_packed,

@@ -28,6 +28,8 @@ CASES = [
     (1, 6, 0, 9, 13, 40, 3, 2, False, True),
     (3, 2, 0, 5, 7, 1, 3, 1, True, True),
     (2, 128, 0, 32, 32, 128, 3, 2, False, True),      # single-shot (4 ci pairs per wave) stride 2
+    (2, 64, 0, 128, 128, 96, 1, 2, False, True),      # the UniMatch CNN's strided 1x1 shortcut
+    (1, 6, 0, 9, 13, 40, 1, 2, False, False),         # strided 1x1, ragged
     (1, 96, 0, 12, 12, 64, 3, 1, False, True),        # single-shot with 3 pairs per wave
 ]
 
@@ -106,6 +108,82 @@ def test_conv2d_direct_zsplit(device, monkeypatch, n, ci, h, w, co, k, stride, z
     monkeypatch.setattr(K, "_ZSPLIT", 0)
     one = K.conv2d_direct(xd, wd, bd, stride).cpu()
     assert (one - ref).abs().max().item() / ref.abs().max().item() < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,ci,co,h,w,s", [(2, 96, 96, 18, 18, 4), (2, 192, 192, 18, 18, 2), (1, 6, 10, 5, 7, 3)])
+def test_conv_transpose_direct(device, n, ci, co, h, w, s):
+    """ConvTranspose2d with kernel = stride (the DPT's resize_layers, reference dpt.py:105-118) as a
+    1x1 convolution to co s^2 channels on the direct exact-fp32 kernel + pixel_shuffle, vs float64."""
+    from transplat_amd import kernels as K
+
+    x = seeded((n, ci, h, w), 71)
+    wt = seeded((ci, co, s, s), 72) / ci ** 0.5
+    b = seeded((co,), 73)
+    ref = torch.nn.functional.conv_transpose2d(x.double(), wt.double(), b.double(), stride=s)
+    out = K.conv_transpose_direct(x.to(device), wt.to(device), b.to(device), s).cpu().double()
+    err = (out - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-6, err
+    m = torch.nn.ConvTranspose2d(ci, co, s, stride=s).to(device)
+    K.install_conv2d_dispatch(m)
+    with torch.no_grad():
+        m.weight.copy_(wt.to(device))
+        m.bias.copy_(b.to(device))
+        assert torch.equal(m(x.to(device)), K.conv_transpose_direct(x.to(device), m.weight, m.bias, s))
+
+
+@pytest.mark.gpu
+def test_conv_unfold_gemm_stem(device):
+    """The UniMatch CNN's 7x7 stride-2 stem on 3 channels as im2col + one exact-fp32 GEMM, vs
+    float64, and through the installed Conv2d dispatch."""
+    from transplat_amd import kernels as K
+
+    x = seeded((2, 3, 256, 256), 74)
+    wt = seeded((64, 3, 7, 7), 75) / 147 ** 0.5
+    ref = torch.nn.functional.conv2d(x.double(), wt.double(), None, stride=2, padding=3)
+    out = K.conv_unfold_gemm(x.to(device), wt.to(device), None, 2, 3).cpu().double()
+    assert (out - ref).abs().max().item() / ref.abs().max().item() < 2e-6
+    m = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(device)
+    K.install_conv2d_dispatch(m)
+    with torch.no_grad():
+        m.weight.copy_(wt.to(device))
+        assert torch.equal(m(x.to(device)), K.conv_unfold_gemm(x.to(device), m.weight, None, 2, 3))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dense", ["fp32", "bf16x3"])
+def test_encoder_runs_no_library_convolution(device, dense):
+    """Every convolution of the encoder's step (UniMatch CNN, camera encoder, DA-V2's DPT head,
+    U-Nets, heads) runs on the hand-written kernels: no aten convolution reaches MIOpen, so no
+    algorithm choice by timing (cudnn.benchmark) can change the step's bits from one process to
+    the next."""
+    import sys
+    from pathlib import Path
+
+    from torch.utils._python_dispatch import TorchDispatchMode
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent / "golden"))
+    from canonical import canonical_init
+
+    from transplat_amd import synthetic as S
+    from transplat_amd.model.encoder import EncoderTrans, EncoderTransCfg
+
+    class Convs(TorchDispatchMode):
+        def __init__(self):
+            super().__init__()
+            self.seen = []
+
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            if "convolution" in func.__name__:
+                self.seen.append((func.__name__, tuple(args[0].shape), tuple(args[1].shape)))
+            return func(*args, **(kwargs or {}))
+
+    enc = canonical_init(EncoderTrans(EncoderTransCfg(dense_dtype=dense)), seed=61).eval().to(device)
+    ctx = {k: t.to(device) for k, t in S.make_batch(1, image_shape=(256, 256))["context"].items()}
+    mode = Convs()
+    with torch.no_grad(), mode:
+        enc(ctx, global_step=0, deterministic=True)
+    assert not mode.seen, mode.seen
 
 
 @pytest.mark.gpu

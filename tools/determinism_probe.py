@@ -2,7 +2,8 @@
 squares, and a strided sample) of every module output in call order, twice; the first modules whose
 outputs differ are printed with the size of the difference (a module whose children all match but
 whose own output differs did the nondeterministic work itself).
-usage: determinism_probe.py [fp32|bf16x3] [cudnn-deterministic 0|1]"""
+usage: determinism_probe.py [fp32|bf16x3] [cudnn-deterministic 0|1]  (0: bench.py's default MIOpen settings,
+cudnn.benchmark on and deterministic off)"""
 import sys
 from pathlib import Path
 
@@ -18,6 +19,8 @@ dense = sys.argv[1] if len(sys.argv) > 1 else "fp32"
 if len(sys.argv) > 2 and sys.argv[2] == "1":
     torch.backends.cudnn.deterministic = True
     torch.backends.cudnn.benchmark = False
+else:
+    torch.backends.cudnn.benchmark = True
 dev = torch.device("cuda:0")
 enc = T.canonical_init(EncoderTrans(EncoderTransCfg(dense_dtype=dense)), seed=61).eval().to(dev)
 ctx = {k: t.to(dev) for k, t in S.make_batch(1, image_shape=(256, 256))["context"].items()}

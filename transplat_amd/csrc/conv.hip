@@ -294,6 +294,8 @@ extern "C" int tsplat_conv2d_f32_zsplit_fwd(const float* x1, int32_t c1, const f
         if (one) TSPLAT_CONV_LAUNCH(3, 1, 1, 4); else if (wide) TSPLAT_CONV_LAUNCH(3, 1, 1, 2); else TSPLAT_CONV_LAUNCH(3, 1, 1, 1);
     } else if (ksize == 1 && stride == 1 && !upsample) {
         if (wide) TSPLAT_CONV_LAUNCH(1, 1, 0, 16); else TSPLAT_CONV_LAUNCH(1, 1, 0, 8);
+    } else if (ksize == 1 && stride == 2 && !upsample) {  // the CNN's strided 1x1 shortcut
+        TSPLAT_CONV_LAUNCH(1, 2, 0, 8);
     } else {
         return TSPLAT_EINVAL;
     }

@@ -670,8 +670,7 @@ def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsa
             return False
         weight = weight.unsqueeze(-1)
     co, ci, k, k2 = weight.shape
-    # (the kernel has no strided 1x1 variant: tsplat_conv2d_f32_fwd rejects it)
-    if k != k2 or k not in (1, 3) or stride not in (1, 2) or (upsample and stride != 1) or (k == 1 and stride != 1):
+    if k != k2 or k not in (1, 3) or stride not in (1, 2) or (upsample and stride != 1):
         return False
     pad = padding if padding is not None else k // 2
     if isinstance(pad, (tuple, list)):
@@ -817,7 +816,71 @@ def conv2d_forward(mod, x):
         if (_ENC_DIRECT and st and x.is_contiguous() and x.dtype == torch.float32
                 and conv2d_direct_ok(x, mod.weight, st, mod.padding)):
             return conv2d_direct(x, mod.weight, mod.bias, st)
+        k = mod.kernel_size
+        if (_LIBFREE and st and k[0] == k[1] and k[0] > 3 and mod.padding[0] == mod.padding[1] and x.is_cuda
+                and x.dtype == torch.float32 and mod.weight.dtype == torch.float32
+                and not torch.is_autocast_enabled("cuda")):
+            return conv_unfold_gemm(x, mod.weight, mod.bias, st, mod.padding[0])
     return mod._conv_forward(x, mod.weight, mod.bias)
+
+
+# Convolutions the encoder used to leave on MIOpen (round 5): the UniMatch CNN's 7x7 stride-2 stem
+# and the DPT's transposed convolutions (kernel = stride). MIOpen picks their algorithms by timing
+# (cudnn.benchmark), so their bits could differ from process to process; these forms are exact fp32
+# and fixed. TSPLAT_CONV_LIBFREE=0 keeps them on MIOpen (A/B knob).
+_LIBFREE = os.environ.get("TSPLAT_CONV_LIBFREE", "1") == "1"
+_DERIVED: dict = {}
+
+
+def _derived(weight, tag, make):
+    """A tensor derived from `weight` (cached per weight tensor and version, like _CONV_PACKED)."""
+    key = (id(weight), tag)
+    hit = _DERIVED.get(key)
+    if hit is not None and hit[0]() is weight and hit[1] == weight._version:
+        return hit[2]
+    val = make(weight.detach())
+    if len(_DERIVED) > 256:
+        for k in [k for k, v in _DERIVED.items() if v[0]() is None]:
+            del _DERIVED[k]
+    _DERIVED[key] = (weakref.ref(weight), weight._version, val)
+    return val
+
+
+def conv_unfold_gemm(x, weight, bias, stride: int, padding: int):
+    """conv2d(x, weight, bias, stride, padding) as im2col (F.unfold) + one exact-fp32 GEMM: the
+    7x7 stride-2 stem on 3 channels (reference backbone/unimatch CNN conv1), which the direct and
+    Winograd kernels do not take."""
+    n, ci, h, w = x.shape
+    co, _, kh, kw = weight.shape
+    ho, wo = (h + 2 * padding - kh) // stride + 1, (w + 2 * padding - kw) // stride + 1
+    cols = torch.nn.functional.unfold(x, (kh, kw), padding=padding, stride=stride)  # [n, ci kh kw, L]
+    with torch.autocast("cuda", enabled=False):
+        y = torch.matmul(weight.reshape(co, -1), cols)  # [n, co, L]
+    if bias is not None:
+        y = y + bias.view(1, co, 1)
+    return y.view(n, co, ho, wo)
+
+
+def conv_transpose_direct(x, weight, bias, s: int):
+    """conv_transpose2d(x, weight [ci, co, s, s], bias, stride s) -- the DPT's resize_layers
+    (kernel = stride, no overlap, reference dpt.py:105-118): a 1x1 convolution to co * s^2 channels
+    on the direct exact-fp32 kernel (bias in its epilogue) + pixel_shuffle (a copy)."""
+    ci, co = weight.shape[:2]
+    w1 = _derived(weight, "convT", lambda t: t.permute(1, 2, 3, 0).reshape(co * s * s, ci, 1, 1).contiguous())
+    b1 = _derived(bias, "convT_b", lambda t: t.repeat_interleave(s * s).contiguous()) if bias is not None else None
+    return torch.nn.functional.pixel_shuffle(conv2d_direct(x, w1, b1, 1), s)
+
+
+def conv_transpose_forward(mod, x):
+    """nn.ConvTranspose2d.forward (installed by install_conv2d_dispatch): kernel = stride, no padding
+    -> conv_transpose_direct; anything else through MIOpen."""
+    k, st = mod.kernel_size, mod.stride
+    if (_LIBFREE and k[0] == k[1] == st[0] == st[1] and tuple(mod.padding) == (0, 0) and mod.groups == 1
+            and tuple(mod.output_padding) == (0, 0) and tuple(mod.dilation) == (1, 1) and x.is_cuda
+            and x.dtype == torch.float32 and mod.weight.dtype == torch.float32 and x.shape[1] % 2 == 0
+            and not torch.is_autocast_enabled("cuda")):
+        return conv_transpose_direct(x.contiguous(), mod.weight, mod.bias, st[0])
+    return torch.nn.ConvTranspose2d.forward(mod, x)
 
 
 def install_conv2d_dispatch(module) -> int:
@@ -829,6 +892,9 @@ def install_conv2d_dispatch(module) -> int:
     for m in module.modules():
         if type(m) is torch.nn.Conv2d:
             m.forward = functools.partial(conv2d_forward, m)
+            n += 1
+        elif type(m) is torch.nn.ConvTranspose2d:
+            m.forward = functools.partial(conv_transpose_forward, m)
             n += 1
     return n
 
