@@ -236,10 +236,13 @@ def ms_deform_attn(value, spatial_shapes, level_start_index, sampling_locations,
 
 # --------------------------------------------------------------------- Gaussian adapter (A1-A4)
 def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape, scale_min: float,
-                     scale_max: float, opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1):
+                     scale_max: float, opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1,
+                     camera_consts=None):
     """Encoder stage 5 (reference encoder_trans.py:294-353) + GaussianAdapter.forward
     (reference gaussian_adapter.py:48-96), restated with the reference's torch expressions.
-    The SH rotation uses the e3nn construction restated in transplat_amd.misc.sh_rotation."""
+    The SH rotation uses the e3nn construction restated in transplat_amd.misc.sh_rotation.
+    camera_consts (the kernel path's precomputed per-camera inputs) is ignored: the restatement
+    derives everything from the cameras itself."""
     from transplat_amd.misc.sh_rotation import rotate_sh
 
     b, v, hw, r = raw.shape

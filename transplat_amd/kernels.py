@@ -1389,11 +1389,21 @@ def sh_rotation(rotations, d_sh: int):
     return out
 
 
+def adapter_camera_consts(extrinsics, intrinsics, image_shape, d_sh: int):
+    """The adapter's per-camera inputs, which depend on the cameras alone: (adapter_cameras, the
+    per-camera Wigner-D blocks of sh_rotation) -- computed at the start of the step on a side stream
+    by the encoder and handed to gaussian_adapter(camera_consts=...)."""
+    return (adapter_cameras(extrinsics, intrinsics, image_shape),
+            sh_rotation(extrinsics.reshape(-1, 4, 4)[:, :3, :3], d_sh))
+
+
 def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape, scale_min: float,
-                     scale_max: float, opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1):
+                     scale_max: float, opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1,
+                     camera_consts=None):
     """Raw head output -> Gaussians (see oracle.gaussian_adapter). raw [B, V, HW, 9 + 3 d_sh];
     depths, densities [B, V, HW]; extrinsics [B, V, 4, 4]; intrinsics [B, V, 3, 3]
-    -> means [B, V*HW, 3], covariances [B, V*HW, 3, 3], harmonics [B, V*HW, 3, d_sh], opacities [B, V*HW]."""
+    -> means [B, V*HW, 3], covariances [B, V*HW, 3, 3], harmonics [B, V*HW, 3, d_sh], opacities [B, V*HW].
+    camera_consts: adapter_camera_consts(...) if already computed."""
     lib = _lib.load()
     b, v, hw, r = raw.shape
     d_sh = (r - 9) // 3
@@ -1405,8 +1415,8 @@ def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape
     if not nchw:
         raw = _f32(raw)
     depths, densities = _f32(depths), _f32(densities)
-    cams = adapter_cameras(extrinsics, intrinsics, image_shape)
-    shrot = sh_rotation(extrinsics.reshape(-1, 4, 4)[:, :3, :3], d_sh)
+    cams, shrot = camera_consts if camera_consts is not None else adapter_camera_consts(extrinsics, intrinsics,
+                                                                                       image_shape, d_sh)
     dev = raw.device
     g = v * hw
     means = torch.empty((b, g, 3), device=dev)

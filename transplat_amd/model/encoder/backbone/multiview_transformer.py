@@ -73,11 +73,12 @@ class TransformerLayer(nn.Module):
             query = K.fused_linear(source, self.q_proj.weight)
             key, value = K.fused_linear(target, self._cat_weights(("k_proj", "v_proj")), split=True)
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
+        x3 = {"kv_x3": kv_x3} if kv_x3 is not None else {}
         if self.no_ffn:
             return K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
-                                     self.merge.weight, ln1, residual=source, kv_shift=kv_shift, kv_x3=kv_x3)
+                                     self.merge.weight, ln1, residual=source, kv_shift=kv_shift, **x3)
         message = K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
-                                    self.merge.weight, ln1, kv_shift=kv_shift, kv_x3=kv_x3)
+                                    self.merge.weight, ln1, kv_shift=kv_shift, **x3)
         # mlp[0] is the one large plain GEMM of the layer (8192 x 256 x 1024 at b = 1): hipBLASLt
         # runs it at 103 TF, above this build's kernel (66 TF); its GELU moves into mlp[2]'s load
         hidden = self.mlp[0](torch.cat([source, message], dim=-1))

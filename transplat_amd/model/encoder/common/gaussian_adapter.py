@@ -38,13 +38,14 @@ class GaussianAdapter(nn.Module):
             self.sh_mask[degree**2:(degree + 1) ** 2] = 0.1 * 0.25**degree
 
     def forward(self, extrinsics, intrinsics, raw_gaussians, depths, densities, image_shape,
-                opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1):
+                opacity_exponent: float = 1.0, gaussians_per_pixel: int = 1, camera_consts=None):
         """Fused stage 5 + adapter on the GPU (kernels.gaussian_adapter):
         raw [b, v, HW, 2 + d_in] head output, depths / densities [b, v, HW], cameras [b, v, ...]
         -> (means, covariances, harmonics, opacities) flattened to [b, v*HW, ...]."""
+        extra = {"camera_consts": camera_consts} if camera_consts is not None else {}
         return kernels.gaussian_adapter(raw_gaussians, depths, densities, extrinsics, intrinsics, image_shape,
                                         self.cfg.gaussian_scale_min, self.cfg.gaussian_scale_max,
-                                        opacity_exponent, gaussians_per_pixel)
+                                        opacity_exponent, gaussians_per_pixel, **extra)
 
     def get_scale_multiplier(self, intrinsics, pixel_size, multiplier: float = 0.1):
         xy_multipliers = multiplier * einsum(kernels.small_inverse(intrinsics[..., :2, :2].contiguous()), pixel_size, "... i j, j -> ... i")

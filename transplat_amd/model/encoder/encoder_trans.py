@@ -9,6 +9,8 @@ kernels), Gaussian adapter (e3nn-free SH rotation). No host synchronisation betw
 """
 from __future__ import annotations
 
+import os
+
 from contextlib import nullcontext
 from dataclasses import dataclass, field
 from typing import List, Literal, Optional
@@ -80,6 +82,11 @@ class EncoderTransCfg:
     attn_dtype: str = "auto"
 
 
+# camera-only prep of the depth predictor and the adapter on a side stream at the start of the step
+# (TSPLAT_CAM_HOIST=0: computed where it is used, the A/B knob)
+_CAM_HOIST = os.environ.get("TSPLAT_CAM_HOIST", "1") == "1"
+
+
 class EncoderTrans(Encoder[EncoderTransCfg]):
     def __init__(self, cfg: EncoderTransCfg) -> None:
         super().__init__(cfg)
@@ -136,13 +143,24 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         def bench(tag):  # the reference's stage tags (encoder_trans.py:188-294) as roctx ranges
             return stage(benchmarker, tag)
 
-        with bench("encoder_1_prep_intrinsics"):
-            intr_curr = context["intrinsics"][:, :, :3, :3].clone().detach()
-            intr_curr[:, :, 0, :] *= float(w)
-            intr_curr[:, :, 1, :] *= float(h)
-            camk = torch.eye(4, device=device).view(1, 1, 4, 4).repeat(b, v, 1, 1).float()
-            camk[:, :, :3, :3] = intr_curr
-            img2world = torch.matmul(context["extrinsics"].clone().detach(), kernels.small_inverse(camk))
+        def prep_intrinsics(intrinsics, extrinsics):  # the backbone's camera input (runs on its stream)
+            with bench("encoder_1_prep_intrinsics"):
+                intr_curr = intrinsics[:, :, :3, :3].clone().detach()
+                intr_curr[:, :, 0, :] *= float(w)
+                intr_curr[:, :, 1, :] *= float(h)
+                camk = torch.eye(4, device=device).view(1, 1, 4, 4).repeat(b, v, 1, 1).float()
+                camk[:, :, :3, :3] = intr_curr
+                return torch.matmul(extrinsics.clone().detach(), kernels.small_inverse(camk))
+
+        def camera_consts(intrinsics, extrinsics, near, far):
+            # everything the depth predictor and the adapter derive from the cameras alone: computed
+            # on a side stream at the start of the step, beside Depth-Anything and the backbone,
+            # instead of as ~40 tiny launches on the critical path before those stages
+            with bench("encoder_cameras"):
+                f = self.cfg.downscale_factor  # the depth predictor works on the feature maps
+                dp = self.depth_predictor.camera_prep(intrinsics, extrinsics, near, far, h // f, w // f)
+                ad = kernels.adapter_camera_consts(extrinsics, intrinsics, (h, w), self.gaussian_adapter.d_sh)
+            return dp, ad
 
         def depth_anything():
             with bench("encoder_3_depth_anything"), torch.no_grad(), self._dense():
@@ -167,7 +185,8 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         if attn == "auto":
             attn = kernels.auto_attention(self.cfg.dense_dtype)
 
-        def backbone(images, img2world):
+        def backbone(images, intrinsics, extrinsics):
+            img2world = prep_intrinsics(intrinsics, extrinsics)
             with bench("encoder_2_backbone"), self._dense(), kernels.attention_precision(attn):
                 tf, cf = self.backbone(images, attn_splits=self.cfg.multiview_trans_attn_split,
                                        return_cnn_features=True, img2world=img2world)
@@ -179,18 +198,22 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         # the MVT's 256-workgroup kernels) that leave CUs idle on their own. Depth-Anything stays on
         # the current stream because it forks again (its DPT reassemble branches, dpt.py): a fork
         # from a side stream inside hipGraph capture crashed HIP's capture_end.
-        bb = streams.fork(device, backbone, context["image"], img2world)  # inputs marked for the side stream
+        bb = streams.fork(device, backbone, context["image"], context["intrinsics"], context["extrinsics"])
+        cams = (streams.fork(device, camera_consts, context["intrinsics"], context["extrinsics"], context["near"],
+                             context["far"], slot=2) if _CAM_HOIST else None)
         da_depth, out_feature = depth_anything()
         trans_features, cnn_features = streams.join(bb)
         dino_feature = out_feature.view(b, v, *out_feature.shape[1:])
 
         extra_info = {"images": rearrange(context["image"], "b v c h w -> (v b) c h w"), "scene_names": scene_names}
         gpp = self.cfg.gaussians_per_pixel
+        dp_cams, adapter_cams = streams.join(cams) if cams is not None else (None, None)
         with bench("encoder_4_depth_predictor"), self._dense():
             depths, densities, raw_gaussians = self.depth_predictor(
                 trans_features, context["intrinsics"], context["extrinsics"], context["near"], context["far"],
                 gaussians_per_pixel=gpp, deterministic=deterministic, extra_info=extra_info,
-                cnn_features=cnn_features, da_depth=da_depth, dino_feature=dino_feature, benchmarker=benchmarker)
+                cnn_features=cnn_features, da_depth=da_depth, dino_feature=dino_feature, benchmarker=benchmarker,
+                cams=dp_cams)
         depths, densities, raw_gaussians = depths.float(), densities.float(), raw_gaussians.float()
 
         with bench("encoder_5_gaussian_adapter"):
@@ -202,7 +225,8 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
             exponent = 2 ** (x.initial + min(global_step / x.warm_up, 1) * (x.final - x.initial))
             means, covariances, harmonics, opacities = self.gaussian_adapter(
                 context["extrinsics"], context["intrinsics"], raw_gaussians, depths.reshape(b, v, h * w),
-                densities.reshape(b, v, h * w), (h, w), opacity_exponent=exponent, gaussians_per_pixel=gpp)
+                densities.reshape(b, v, h * w), (h, w), opacity_exponent=exponent, gaussians_per_pixel=gpp,
+                camera_consts=adapter_cams)
         if visualization_dump is not None:
             visualization_dump["depth"] = rearrange(depths, "b v (h w) srf s -> b v h w srf s", h=h, w=w)
         return Gaussians(means, covariances, harmonics, opacities)

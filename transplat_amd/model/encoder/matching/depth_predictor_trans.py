@@ -47,23 +47,21 @@ def _conv_gelu_conv(seq: nn.Sequential, x, extra=()):
 
 
 @torch.autocast("cuda", enabled=False)
-def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, num_samples):
-    """(reference :59-109) per-view features, pixel intrinsics, relative poses and disparity
-    candidates 1/far + linspace(0, 1, D) (1/near - 1/far), all in (v b) order. Camera math stays
-    fp32 when the dense layers run under bf16 autocast."""
-    b, v, _, h, w = features.shape
-    feat_lists = [rearrange(features, "b v ... -> (v b) ...")]
+def camera_lists(intrinsics, extrinsics, near, far, num_samples: int, h: int, w: int):
+    """The camera half of prepare_feat_proj_data_lists (reference :59-109): pixel intrinsics, relative
+    poses and disparity candidates 1/far + linspace(0, 1, D) (1/near - 1/far), all in (v b) order,
+    fp32. Depends on the cameras only, so the encoder computes it at the start of the step on a
+    side stream (EncoderTrans.forward), off the depth predictor's critical path."""
+    b, v = intrinsics.shape[:2]
     pose_curr_lists = []
     init_view_order = list(range(v))
-    for idx in range(1, v):
-        cur_view_order = init_view_order[idx:] + init_view_order[:idx]
-        # features[:, cur_view_order] as a roll (list indexing is a host copy: not graph-capturable)
-        feat_lists.append(rearrange(torch.roll(features, -idx, dims=1), "b v ... -> (v b) ..."))
-        if v > 2:
+    if v > 2:
+        for idx in range(1, v):
+            cur_view_order = init_view_order[idx:] + init_view_order[:idx]
             cur = [kernels.small_inverse(extrinsics[:, v1].clone().detach()) @ extrinsics[:, v0].clone().detach()
                    for v0, v1 in zip(init_view_order, cur_view_order)]
             pose_curr_lists.append(torch.cat(cur, dim=0))
-    if v == 2:
+    else:
         pose_ref = extrinsics[:, 0].clone().detach()
         pose_tgt = extrinsics[:, 1].clone().detach()
         pose = kernels.small_inverse(pose_tgt) @ pose_ref
@@ -75,9 +73,36 @@ def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, nu
     min_depth = rearrange(1.0 / far.clone().detach(), "b v -> (v b) 1")
     max_depth = rearrange(1.0 / near.clone().detach(), "b v -> (v b) 1")
     depth_candi_curr = (min_depth + torch.linspace(0.0, 1.0, num_samples, device=min_depth.device).unsqueeze(0)
-                        * (max_depth - min_depth)).type_as(features)
+                        * (max_depth - min_depth)).float()
     depth_candi_curr = repeat(depth_candi_curr, "vb d -> vb d () ()")
-    return feat_lists, intr_curr, pose_curr_lists, depth_candi_curr
+    return intr_curr, pose_curr_lists, depth_candi_curr
+
+
+def match_img2world(intr_curr, extrinsics):
+    """[(v b), 16] c2w @ inv(K_pixel) of every view (reference :241-248), the camera-parameter
+    encoder's input in match_two."""
+    b, v = extrinsics.shape[:2]
+    with torch.autocast("cuda", enabled=False):
+        camk = torch.eye(4, device=intr_curr.device).view(1, 4, 4).repeat(intr_curr.shape[0], 1, 1).float()
+        camk[:, :3, :3] = intr_curr
+        c2w = rearrange(extrinsics.clone().detach(), "b v ... -> (v b) ...", b=b, v=v)
+        return torch.matmul(c2w, kernels.small_inverse(camk)).reshape(-1, 16)
+
+
+def prepare_feat_proj_data_lists(features, intrinsics, extrinsics, near, far, num_samples, cams=None):
+    """(reference :59-109) per-view features, pixel intrinsics, relative poses and disparity
+    candidates 1/far + linspace(0, 1, D) (1/near - 1/far), all in (v b) order. Camera math stays
+    fp32 when the dense layers run under bf16 autocast. cams: camera_lists' result, if already
+    computed."""
+    b, v, _, h, w = features.shape
+    feat_lists = [rearrange(features, "b v ... -> (v b) ...")]
+    for idx in range(1, v):
+        # features[:, cur_view_order] as a roll (list indexing is a host copy: not graph-capturable)
+        feat_lists.append(rearrange(torch.roll(features, -idx, dims=1), "b v ... -> (v b) ..."))
+    if cams is None:
+        cams = camera_lists(intrinsics, extrinsics, near, far, num_samples, h, w)
+    intr_curr, pose_curr_lists, depth_candi_curr = cams
+    return feat_lists, intr_curr, pose_curr_lists, depth_candi_curr.type_as(features)
 
 
 # view pairs matched for V > 2 in the reference's order (depth_predictor_trans.py:351-414): the ring
@@ -134,15 +159,21 @@ class DepthPredictorTrans(nn.Module):
         self.fine_transformer = UVTransformer(embed_dims=self.embed_dims, mode="fine", num_layers=2)
         self.cam_param_encoder = cam_param_encoder(in_channels=DA_size, mid_channels=128, embed_dims=128)
 
-    def match_two(self, intr_curr, pose_curr, extrinsics, disp_candi_curr, dino_feature, features):
+    def camera_prep(self, intrinsics, extrinsics, near, far, h: int, w: int) -> dict:
+        """Everything the depth predictor derives from the cameras alone (camera_lists, and
+        match_two's img2world for two views), for forward(cams=...)."""
+        intr, poses, disp = camera_lists(intrinsics, extrinsics, near, far, self.num_depth_candidates, h, w)
+        out = {"lists": (intr, poses, disp)}
+        if intrinsics.shape[1] == 2:
+            out["img2world"] = match_img2world(intr, extrinsics)
+        return out
+
+    def match_two(self, intr_curr, pose_curr, extrinsics, disp_candi_curr, dino_feature, features, img2world=None):
         """(reference :236-290) coarse then fine correlation for a pair of views -> [(v b), D, h, w]."""
         b, v, c, h, w = features.shape
         cameras = (intr_curr, pose_curr, disp_candi_curr.flatten(1).float())
-        with torch.autocast("cuda", enabled=False):
-            camk = torch.eye(4, device=intr_curr.device).view(1, 4, 4).repeat(intr_curr.shape[0], 1, 1).float()
-            camk[:, :3, :3] = intr_curr
-            c2w = rearrange(extrinsics.clone().detach(), "b v ... -> (v b) ...", b=b, v=v)
-            img2world = torch.matmul(c2w, kernels.small_inverse(camk)).reshape(-1, 16)
+        if img2world is None:
+            img2world = match_img2world(intr_curr, extrinsics)
         pos_feature = self.cam_param_encoder(dino_feature, img2world)  # [(v b), C, h, w]
         # (b v)-ordered channel-last query positions: the reference's bev_pos after its permutes
         bev_pos = rearrange(pos_feature, "(v b) c h w -> (b v) (h w) c", v=v, b=b)
@@ -177,7 +208,7 @@ class DepthPredictorTrans(nn.Module):
         return torch.cat(per_view, dim=0)  # (v b)
 
     def forward(self, features, intrinsics, extrinsics, near, far, gaussians_per_pixel=1, deterministic=True,
-                extra_info=None, cnn_features=None, da_depth=None, dino_feature=None, benchmarker=None):
+                extra_info=None, cnn_features=None, da_depth=None, dino_feature=None, benchmarker=None, cams=None):
         b, v, c, h, w = features.shape
         # the reference's stage tags (depth_predictor_trans.py:320-456) as roctx ranges
 
@@ -194,14 +225,16 @@ class DepthPredictorTrans(nn.Module):
                 dino_feature = rearrange(dino_feature, "b v ... -> (v b) ...")
                 dino_feature = kernels.interpolate_bilinear_ac(dino_feature, (h, w))
             feat_comb_lists, intr_curr, pose_curr_lists, disp_candi_curr = prepare_feat_proj_data_lists(
-                features, intrinsics, extrinsics, near, far, num_samples=self.num_depth_candidates)
+                features, intrinsics, extrinsics, near, far, num_samples=self.num_depth_candidates,
+                cams=cams["lists"] if cams is not None else None)
             feat01 = feat_comb_lists[0]
             # the full-resolution feature projection runs on a side stream beside the cost volume
             # (matching, refine U-Net, depth head: a chain of 64^2 launches), transplat_amd/streams.py
             proj = streams.fork(features.device, projection, feat01, cnn_features)
         with stage(benchmarker, "encoder_4b_cost_volume_matching"):
             raw_correlation_in = self._match(v, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr,
-                                             dino_feature, features, feat01)
+                                             dino_feature, features, feat01,
+                                             cams.get("img2world") if cams is not None else None)
         with stage(benchmarker, "encoder_4c_cost_volume_unet"):
             raw_correlation = (run_sequential(self.corr_refine_net, raw_correlation_in)
                                + self.regressor_residual(raw_correlation_in))
@@ -222,10 +255,11 @@ class DepthPredictorTrans(nn.Module):
             depths = repeat(1.0 / fine_disps, "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
         return depths, densities, raw_gaussians
 
-    def _match(self, v, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr, dino_feature, features, feat01):
+    def _match(self, v, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr, dino_feature, features, feat01,
+               img2world=None):
         if v == 2:
             raw_correlation_in = self.match_two(intr_curr, pose_curr_lists[0], extrinsics, disp_candi_curr,
-                                                dino_feature, features)
+                                                dino_feature, features, img2world)
         elif v in _VIEW_PAIRS:
             raw_correlation_in = self.match_pairs(intr_curr, pose_curr_lists, extrinsics, disp_candi_curr,
                                                   dino_feature, features)
