@@ -168,6 +168,47 @@ def build_raster_workload(batch: int, device, scene_offset: int):
     return step, info, cpu_inputs
 
 
+# blend VALU per (entry, 8x8 block) of the render kernel: one wave64 instruction per (entry, pixel)
+# step -- dx, dy, the power's Horner form (3 mul + 2 fma), exp2, o * e, min 0.99, the three decisions
+# (2 compares + the test_T fma and compare), w = alpha T and its select, 3 colour fmas, the T select:
+# 20, counted in the gfx950 ISA of the quad loop (81 VALU per 4 entries, csrc/raster.hip render_kernel)
+RENDER_VALU_PER_ENTRY = 20
+# wave64 VALU issue: 32 lanes per clock per SIMD (157.3 TFLOP/s fp32 FMA = 1024 SIMDs x 64 FLOP/clk x 2.4 GHz)
+VALU_PEAK_TLANE_OPS = 1024 * 32 * 2.4e9 / 1e12
+
+
+def render_valu_roofline(step, n_prof: int) -> dict:
+    """The render kernel against its VALU roofline (what bounds it; HBM is far off): entry-pixel
+    evaluations per launch (the diag-5 counters: entries each 8x8-block wave blended) x the blend's
+    VALU per evaluation / the render kernel's average duration (HIP events), against the gfx950
+    VALU issue peak. Measured outside the timed region."""
+    from transplat_amd import _lib
+
+    _lib.prof_enable("raster_render")
+    for _ in range(n_prof):
+        step()
+    ms, launches = _lib.prof_read()
+    _lib.prof_enable(None)
+    os.environ["TSPLAT_RASTER_DIAG"] = "5"
+    try:
+        color = step()[0]
+        torch.cuda.synchronize()
+    finally:
+        os.environ["TSPLAT_RASTER_DIAG"] = "0"
+    # diag 5 writes (cycles, entries, chunks) of the wave into each pixel of its 8x8 block
+    c = color.reshape(-1, 3, color.shape[-2] // 8, 8, color.shape[-1] // 8, 8)[:, :, :, 0, :, 0].double()
+    entries, chunks = float(c[:, 1].sum()), float(c[:, 2].sum())
+    avg_ms = ms / launches
+    evals = entries * 64
+    achieved = evals * RENDER_VALU_PER_ENTRY / (avg_ms * 1e-3) / 1e12
+    cyc = c[:, 0].flatten()
+    return {"kernel": "raster_render", "bound": "valu", "achieved": achieved, "peak": VALU_PEAK_TLANE_OPS,
+            "unit": "T lane-ops/s", "frac": achieved / VALU_PEAK_TLANE_OPS, "avg_launch_ms": avg_ms,
+            "entry_pixel_evals_per_launch": evals, "valu_per_eval": RENDER_VALU_PER_ENTRY,
+            "chunks_per_launch": chunks,
+            "wave_cycles_p50_max": [float(cyc.median()), float(cyc.max())]}
+
+
 def committed_traffic(kernel: str, dense_dtype: str, batch: int):
     """HBM traffic per launch of `kernel` from the newest committed PMC digest
     (profiles/<round>/traffic_<kernel>_<dtype>_b<batch>.json, written by tools/pmc_traffic.py from
@@ -477,6 +518,7 @@ def main():
                 "ms_per_step": cms / n_prof, "share_of_step": cms / n_prof / (elapsed / args.steps * 1e3),
             }
 
+    render_valu = render_valu_roofline(step, n_prof) if args.workload == "raster" else None
     serial.__exit__(None, None, None)
     views = world * info["views_per_step"] * args.steps
     result = {
@@ -518,6 +560,8 @@ def main():
         result["roofline"]["fp32_equivalent_achieved"] = info["fp32_equivalent_flops_per_launch"] / (avg_ms * 1e-3) / 1e12
     if conv_roofline is not None:
         result["roofline_step_dominant"] = conv_roofline
+    if render_valu is not None:
+        result["roofline_render_valu"] = render_valu
     if rank == 0 and not args.no_cpu_baseline and cpu_inputs is not None:
         if isinstance(cpu_inputs, tuple) and cpu_inputs[0] == "e2e":
             result["cpu_baseline"] = cpu_baseline_e2e(cpu_inputs[1], args.cpu_baseline_seconds,

@@ -82,7 +82,7 @@ class EncoderTransCfg:
     attn_dtype: str = "auto"
 
 
-# camera-only prep of the depth predictor and the adapter on a side stream at the start of the step
+# camera-only prep of the depth predictor and the adapter on the backbone's branch
 # (TSPLAT_CAM_HOIST=0: computed where it is used, the A/B knob)
 _CAM_HOIST = os.environ.get("TSPLAT_CAM_HOIST", "1") == "1"
 
@@ -154,8 +154,8 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
 
         def camera_consts(intrinsics, extrinsics, near, far):
             # everything the depth predictor and the adapter derive from the cameras alone: computed
-            # on a side stream at the start of the step, beside Depth-Anything and the backbone,
-            # instead of as ~40 tiny launches on the critical path before those stages
+            # on the backbone's branch, beside Depth-Anything, instead of as ~40 tiny launches on the
+            # critical path before those stages (a stream of its own measured 2.7 % slower)
             with bench("encoder_cameras"):
                 f = self.cfg.downscale_factor  # the depth predictor works on the feature maps
                 dp = self.depth_predictor.camera_prep(intrinsics, extrinsics, near, far, h // f, w // f)
@@ -185,12 +185,14 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         if attn == "auto":
             attn = kernels.auto_attention(self.cfg.dense_dtype)
 
-        def backbone(images, intrinsics, extrinsics):
+        def backbone(images, intrinsics, extrinsics, near, far):
             img2world = prep_intrinsics(intrinsics, extrinsics)
             with bench("encoder_2_backbone"), self._dense(), kernels.attention_precision(attn):
                 tf, cf = self.backbone(images, attn_splits=self.cfg.multiview_trans_attn_split,
                                        return_cnn_features=True, img2world=img2world)
-            return tf.float(), cf.float()
+            # the backbone branch finishes well before Depth-Anything: its slack takes the camera prep
+            cams = camera_consts(intrinsics, extrinsics, near, far) if _CAM_HOIST else (None, None)
+            return tf.float(), cf.float(), cams
 
         # Stages 2 and 3 read only the context images: on a GPU, the backbone runs on a side stream
         # concurrently with Depth-Anything (transplat_amd/streams.py; captured into the step's
@@ -198,16 +200,14 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
         # the MVT's 256-workgroup kernels) that leave CUs idle on their own. Depth-Anything stays on
         # the current stream because it forks again (its DPT reassemble branches, dpt.py): a fork
         # from a side stream inside hipGraph capture crashed HIP's capture_end.
-        bb = streams.fork(device, backbone, context["image"], context["intrinsics"], context["extrinsics"])
-        cams = (streams.fork(device, camera_consts, context["intrinsics"], context["extrinsics"], context["near"],
-                             context["far"], slot=2) if _CAM_HOIST else None)
+        bb = streams.fork(device, backbone, context["image"], context["intrinsics"], context["extrinsics"],
+                          context["near"], context["far"])
         da_depth, out_feature = depth_anything()
-        trans_features, cnn_features = streams.join(bb)
+        trans_features, cnn_features, (dp_cams, adapter_cams) = streams.join(bb)
         dino_feature = out_feature.view(b, v, *out_feature.shape[1:])
 
         extra_info = {"images": rearrange(context["image"], "b v c h w -> (v b) c h w"), "scene_names": scene_names}
         gpp = self.cfg.gaussians_per_pixel
-        dp_cams, adapter_cams = streams.join(cams) if cams is not None else (None, None)
         with bench("encoder_4_depth_predictor"), self._dense():
             depths, densities, raw_gaussians = self.depth_predictor(
                 trans_features, context["intrinsics"], context["extrinsics"], context["near"], context["far"],
