@@ -35,7 +35,8 @@ for d in args.diag.split(","):
             step()
         ms, n = _lib.prof_read()
         _lib.prof_enable(None)
-        row.append(f"{k}={ms / n * 1e3:.1f}us")
+        if n:  # (raster_scan: folded into the scatter kernel in round 5)
+            row.append(f"{k}={ms / n * 1e3:.1f}us")
     print(f"diag={d}: " + " ".join(row), flush=True)
 os.environ["TSPLAT_RASTER_DIAG"] = "0"
 if args.waves:

@@ -99,6 +99,7 @@ struct Params {
     int diag;  // timing diagnostics only (TSPLAT_RASTER_DIAG; output is wrong when != 0)
     int count_sort;  // 1: counting sort for long tile lists (default); 0: bitonic only (A/B)
     int view_rot;    // render: view v's workgroups take tiles rotated by v * view_rot (load balance)
+    int sh_vec4;     // preprocess: every wave's SH block is 16-byte aligned (16-byte staging loads)
 };
 
 __device__ __forceinline__ void get_rect(float px, float py, int r, int tx, int ty, int& x0,
@@ -160,6 +161,13 @@ __global__ void __launch_bounds__(256) zero_kernel(uint4* __restrict__ p, size_t
 }
 
 // --- K1: preprocess + per-tile instance counts ----------------------------------------------
+// One thread per Gaussian for ALL views of its scene (blockIdx.y = scene): the scene-level inputs
+// (mean, covariance, opacity, SH) are read once, not once per view. The SH block of a wave's 64
+// Gaussians ([64][3][M] floats, contiguous) is staged into LDS by coalesced 16-byte loads: read
+// per thread in place, every load instruction of the wave touches 64 cache lines (a 3M-float
+// stride), which made the SH reads half of this kernel's time (TSPLAT_RASTER_DIAG=7 skips them).
+constexpr int kMaxShFloats = 75;  // 3 (deg 4 + 1)^2
+constexpr int kShStageIt = (kWave * kMaxShFloats / 4 + kWave - 1) / kWave;  // float4s per lane
 __global__ void __launch_bounds__(kPreThreads)
 preprocess_kernel(Params p, const float* __restrict__ means, const float* __restrict__ cov,
                   const float* __restrict__ shs, const float* __restrict__ opacity,
@@ -168,177 +176,250 @@ preprocess_kernel(Params p, const float* __restrict__ means, const float* __rest
                   const float* __restrict__ scene_scale, int32_t* __restrict__ out_radii,
                   Workspace ws) {
     extern __shared__ uint32_t hist[];  // [T]
-    const int v = blockIdx.y;
+    __shared__ __attribute__((aligned(16))) float s_sh[kPreThreads * kMaxShFloats];
+    const int scene = blockIdx.y;
+    const int lane = threadIdx.x % kWave, wid = threadIdx.x / kWave;
     const int g = blockIdx.x * kPreThreads + threadIdx.x;
-    for (int i = threadIdx.x; i < p.T; i += kPreThreads) hist[i] = 0;
-    __syncthreads();
-
+    const int nf = 3 * p.M;
+    const size_t sg = (size_t)scene * p.G + g;
+    float* my_sh = s_sh + (size_t)threadIdx.x * nf;
+    // the SH block's 16-byte loads are issued first and stay in flight through the geometry pass
+    // below (pass 1: projection, EWA covariance, records without colour, tile counts, per view);
+    // pass 2 stores them to LDS and evaluates the colours of every view
+    const int gw0 = blockIdx.x * kPreThreads + wid * kWave;
+    const int sh_total = max(0, min(kWave, p.G - gw0)) * nf;
+    const float* sh_src = shs + (size_t)nf * ((size_t)scene * p.G + gw0);
+    float* sh_dst = s_sh + (size_t)wid * kWave * nf;
+    const bool stage4 = p.sh_vec4 && p.diag != 7;
+    const int t4 = stage4 ? sh_total / 4 : 0;
+    // 19 named registers, loaded unconditionally at a clamped index (held in an array across the
+    // geometry pass, the staging lived in scratch memory)
+    const float4* sh_src4 = reinterpret_cast<const float4*>(sh_src);
+    const int t4c = max(t4 - 1, 0);
+    const bool any4 = t4 > 0;
+#define TSPLAT_SH_LD(e) \
+    float4 shr##e = any4 ? sh_src4[min(lane + (e) * kWave, t4c)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    TSPLAT_SH_LD(0) TSPLAT_SH_LD(1) TSPLAT_SH_LD(2) TSPLAT_SH_LD(3) TSPLAT_SH_LD(4) TSPLAT_SH_LD(5)
+    TSPLAT_SH_LD(6) TSPLAT_SH_LD(7) TSPLAT_SH_LD(8) TSPLAT_SH_LD(9) TSPLAT_SH_LD(10) TSPLAT_SH_LD(11)
+    TSPLAT_SH_LD(12) TSPLAT_SH_LD(13) TSPLAT_SH_LD(14) TSPLAT_SH_LD(15) TSPLAT_SH_LD(16) TSPLAT_SH_LD(17)
+    TSPLAT_SH_LD(18)
+#undef TSPLAT_SH_LD
+    static_assert(kShStageIt == 19, "staging registers are spelled out for 19 float4s per lane");
+    // scene-level inputs, once for all views
+    float m0 = 0.f, m1 = 0.f, m2 = 0.f, k00 = 0.f, k01 = 0.f, k02 = 0.f, k11 = 0.f, k12 = 0.f, k22 = 0.f,
+          o = 0.f;
     if (g < p.G) {
-        const size_t vg = (size_t)v * p.G + g;
-        const int scene = v / p.vps;
-        const size_t sg = (size_t)scene * p.G + g;
-        const float* vm = viewmat + 16 * v;
-        const float* pm = projmat + 16 * v;
-        const float s = scene_scale[2 * v], s2 = scene_scale[2 * v + 1];
-        int radius = 0;
-        // scale-invariant rendering: means * s, cov * s^2 (cuda_splatting.py:73-80)
-        const float mx = means[3 * sg] * s, my = means[3 * sg + 1] * s, mz = means[3 * sg + 2] * s;
-        // in_frustum: view-space depth test (auxiliary.h in_frustum)
-        const float vx = vm[0] * mx + vm[4] * my + vm[8] * mz + vm[12];
-        const float vy = vm[1] * mx + vm[5] * my + vm[9] * mz + vm[13];
-        const float vz = vm[2] * mx + vm[6] * my + vm[10] * mz + vm[14];
-        bool ok = vz > 0.2f;
-        float px = 0.f, py = 0.f, conic_a = 0.f, conic_b = 0.f, conic_c = 0.f;
-        float cov_a = 0.f, cov_c = 0.f;
-        int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-        if (ok) {
-            const float hx = pm[0] * mx + pm[4] * my + pm[8] * mz + pm[12];
-            const float hy = pm[1] * mx + pm[5] * my + pm[9] * mz + pm[13];
-            const float hw = pm[3] * mx + pm[7] * my + pm[11] * mz + pm[15];
-            const float pw = 1.0f / (hw + 0.0000001f);
-            const float ndc_x = hx * pw, ndc_y = hy * pw;
-            const float* C = cov + 9 * sg;
-            const float c00 = C[0] * s2, c01 = C[1] * s2, c02 = C[2] * s2;
-            const float c11 = C[4] * s2, c12 = C[5] * s2, c22 = C[8] * s2;
-            // EWA splatting (computeCov2D)
-            const float tfx = tanfov[2 * v], tfy = tanfov[2 * v + 1];
-            const float fx = (float)p.W / (2.0f * tfx), fy = (float)p.H / (2.0f * tfy);
-            const float limx = 1.3f * tfx, limy = 1.3f * tfy;
-            const float tz = vz;
-            const float tx = fminf(limx, fmaxf(-limx, vx / tz)) * tz;
-            const float ty = fminf(limy, fmaxf(-limy, vy / tz)) * tz;
-            const float j00 = fx / tz, j02 = -(fx * tx) / (tz * tz);
-            const float j11 = fy / tz, j12 = -(fy * ty) / (tz * tz);
-            // M = J * R_w2c, R[r][c] = vm[c*4 + r]
-            const float m00 = j00 * vm[0] + j02 * vm[2];
-            const float m01 = j00 * vm[4] + j02 * vm[6];
-            const float m02 = j00 * vm[8] + j02 * vm[10];
-            const float m10 = j11 * vm[1] + j12 * vm[2];
-            const float m11 = j11 * vm[5] + j12 * vm[6];
-            const float m12 = j11 * vm[9] + j12 * vm[10];
-            const float u00 = m00 * c00 + m01 * c01 + m02 * c02;
-            const float u01 = m00 * c01 + m01 * c11 + m02 * c12;
-            const float u02 = m00 * c02 + m01 * c12 + m02 * c22;
-            const float u10 = m10 * c00 + m11 * c01 + m12 * c02;
-            const float u11 = m10 * c01 + m11 * c11 + m12 * c12;
-            const float u12 = m10 * c02 + m11 * c12 + m12 * c22;
-            const float a = u00 * m00 + u01 * m01 + u02 * m02 + 0.3f;
-            const float b = u00 * m10 + u01 * m11 + u02 * m12;
-            const float c = u10 * m10 + u11 * m11 + u12 * m12 + 0.3f;
-            const float det = a * c - b * b;
-            cov_a = a;
-            cov_c = c;
-            ok = det != 0.0f;
+        m0 = means[3 * sg];
+        m1 = means[3 * sg + 1];
+        m2 = means[3 * sg + 2];
+        const float* C = cov + 9 * sg;
+        k00 = C[0];
+        k01 = C[1];
+        k02 = C[2];
+        k11 = C[4];
+        k12 = C[5];
+        k22 = C[8];
+        o = opacity[sg];
+    }
+
+    uint32_t okmask = 0;  // bit vv: the Gaussian is rendered in view vv (vps <= 32, host-checked)
+    for (int vv = 0; vv < p.vps; ++vv) {
+        const int v = scene * p.vps + vv;
+        for (int i = threadIdx.x; i < p.T; i += kPreThreads) hist[i] = 0;
+        __syncthreads();  // hist cleared
+        if (g < p.G) {
+            const size_t vg = (size_t)v * p.G + g;
+            const float* vm = viewmat + 16 * v;
+            const float* pm = projmat + 16 * v;
+            const float s = scene_scale[2 * v], s2 = scene_scale[2 * v + 1];
+            int radius = 0;
+            // scale-invariant rendering: means * s, cov * s^2 (cuda_splatting.py:73-80)
+            const float mx = m0 * s, my = m1 * s, mz = m2 * s;
+            // in_frustum: view-space depth test (auxiliary.h in_frustum)
+            const float vx = vm[0] * mx + vm[4] * my + vm[8] * mz + vm[12];
+            const float vy = vm[1] * mx + vm[5] * my + vm[9] * mz + vm[13];
+            const float vz = vm[2] * mx + vm[6] * my + vm[10] * mz + vm[14];
+            bool ok = vz > 0.2f;
+            float px = 0.f, py = 0.f, conic_a = 0.f, conic_b = 0.f, conic_c = 0.f;
+            float cov_a = 0.f, cov_c = 0.f;
+            int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
             if (ok) {
-                const float det_inv = 1.0f / det;
-                conic_a = c * det_inv;
-                conic_b = -b * det_inv;
-                conic_c = a * det_inv;
-                const float mid = 0.5f * (a + c);
-                const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
-                const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
-                radius = (int)ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
-                px = ((ndc_x + 1.0f) * (float)p.W - 1.0f) * 0.5f;
-                py = ((ndc_y + 1.0f) * (float)p.H - 1.0f) * 0.5f;
-                get_rect(px, py, radius, p.tiles_x, p.tiles_y, x0, y0, x1, y1);
-                ok = (x1 - x0) * (y1 - y0) != 0;
-            }
-        }
-        if (ok) {
-            float rgb[3];
-            const float* cp = campos + 3 * v;
-            sh_to_rgb(shs + (size_t)3 * p.M * sg, p.M, p.deg, mx - cp[0], my - cp[1], mz - cp[2],
-                      rgb);
-            // Conservative half-extents of the region where o * exp(power) >= 1/255 (power =
-            // -Q/2, Q <= 2 ln(255 o)); lets a wave skip Gaussians that miss its 8x8 pixels.
-            // Pure culling: pixels inside keep the exact reference arithmetic.
-            const float o = opacity[sg];
-            float ex = INFINITY, ey = INFINITY;
-            if (o == o) {
-                const float q = 2.0f * logf(255.0f * o);
-                if (q < 0.0f) {
-                    ex = ey = -1.0f;  // alpha < 1/255 everywhere
-                } else if (cov_a > 0.0f && cov_c > 0.0f && q < INFINITY) {
-                    ex = sqrtf(q * cov_a) * 1.001f + 0.01f;
-                    ey = sqrtf(q * cov_c) * 1.001f + 0.01f;
+                const float hx = pm[0] * mx + pm[4] * my + pm[8] * mz + pm[12];
+                const float hy = pm[1] * mx + pm[5] * my + pm[9] * mz + pm[13];
+                const float hw = pm[3] * mx + pm[7] * my + pm[11] * mz + pm[15];
+                const float pw = 1.0f / (hw + 0.0000001f);
+                const float ndc_x = hx * pw, ndc_y = hy * pw;
+                const float c00 = k00 * s2, c01 = k01 * s2, c02 = k02 * s2;
+                const float c11 = k11 * s2, c12 = k12 * s2, c22 = k22 * s2;
+                // EWA splatting (computeCov2D)
+                const float tfx = tanfov[2 * v], tfy = tanfov[2 * v + 1];
+                const float fx = (float)p.W / (2.0f * tfx), fy = (float)p.H / (2.0f * tfy);
+                const float limx = 1.3f * tfx, limy = 1.3f * tfy;
+                const float tz = vz;
+                const float tx = fminf(limx, fmaxf(-limx, vx / tz)) * tz;
+                const float ty = fminf(limy, fmaxf(-limy, vy / tz)) * tz;
+                const float j00 = fx / tz, j02 = -(fx * tx) / (tz * tz);
+                const float j11 = fy / tz, j12 = -(fy * ty) / (tz * tz);
+                // M = J * R_w2c, R[r][c] = vm[c*4 + r]
+                const float n00 = j00 * vm[0] + j02 * vm[2];
+                const float n01 = j00 * vm[4] + j02 * vm[6];
+                const float n02 = j00 * vm[8] + j02 * vm[10];
+                const float n10 = j11 * vm[1] + j12 * vm[2];
+                const float n11 = j11 * vm[5] + j12 * vm[6];
+                const float n12 = j11 * vm[9] + j12 * vm[10];
+                const float u00 = n00 * c00 + n01 * c01 + n02 * c02;
+                const float u01 = n00 * c01 + n01 * c11 + n02 * c12;
+                const float u02 = n00 * c02 + n01 * c12 + n02 * c22;
+                const float u10 = n10 * c00 + n11 * c01 + n12 * c02;
+                const float u11 = n10 * c01 + n11 * c11 + n12 * c12;
+                const float u12 = n10 * c02 + n11 * c12 + n12 * c22;
+                const float a = u00 * n00 + u01 * n01 + u02 * n02 + 0.3f;
+                const float b = u00 * n10 + u01 * n11 + u02 * n12;
+                const float c = u10 * n10 + u11 * n11 + u12 * n12 + 0.3f;
+                const float det = a * c - b * b;
+                cov_a = a;
+                cov_c = c;
+                ok = det != 0.0f;
+                if (ok) {
+                    const float det_inv = 1.0f / det;
+                    conic_a = c * det_inv;
+                    conic_b = -b * det_inv;
+                    conic_c = a * det_inv;
+                    const float mid = 0.5f * (a + c);
+                    const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+                    const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+                    radius = (int)ceilf(3.0f * sqrtf(fmaxf(l1, l2)));
+                    px = ((ndc_x + 1.0f) * (float)p.W - 1.0f) * 0.5f;
+                    py = ((ndc_y + 1.0f) * (float)p.H - 1.0f) * 0.5f;
+                    get_rect(px, py, radius, p.tiles_x, p.tiles_y, x0, y0, x1, y1);
+                    ok = (x1 - x0) * (y1 - y0) != 0;
                 }
             }
-            float4* rec = ws.rec + 4 * vg;
-            rec[0] = make_float4(px, py, ex, ey);
-            // power * log2(e): alpha = o * 2^(power2) is one v_exp_f32 in the blend
-            constexpr float kLog2e = 1.44269504088896341f;
-            rec[1] = make_float4(-0.5f * kLog2e * conic_a, -kLog2e * conic_b, -0.5f * kLog2e * conic_c, o);
-            rec[2] = make_float4(rgb[0], rgb[1], rgb[2], vz);
-            // cull threshold in the same log2 units as the stored conic: 2 log2(255 o), + margins
-            rec[3] = make_float4(2.0f * __log2f(255.0f * o) * 1.001f + 1.5e-3f,
-                                 -conic_b * __builtin_amdgcn_rcpf(conic_a), -conic_b * __builtin_amdgcn_rcpf(conic_c),
-                                 0.0f);
-            for (int ty = y0; ty < y1; ++ty)
-                for (int tx = x0; tx < x1; ++tx) atomicAdd(&hist[ty * p.tiles_x + tx], 1u);
-        } else {
-            radius = 0;
-        }
-        out_radii[vg] = radius;
-    }
-    __syncthreads();
-    uint32_t* gcount = ws.counts + (size_t)v * p.T;
-    for (int i = threadIdx.x; i < p.T; i += kPreThreads)
-        if (hist[i]) atomicAdd(&gcount[i], hist[i]);
-}
-
-// --- K2: exclusive scan of the V*T tile counts (single workgroup) ----------------------------
-constexpr int kScanThreads = 1024;
-__global__ void __launch_bounds__(kScanThreads)
-scan_kernel(int n, int capacity, const uint32_t* __restrict__ counts,
-            uint32_t* __restrict__ offsets, int32_t* __restrict__ status) {
-    __shared__ uint32_t wsum[kScanThreads / kWave];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
-    for (int base = 0; base < n; base += kScanThreads) {
-        const int i = base + threadIdx.x;
-        uint32_t x = i < n ? counts[i] : 0u;
-        uint32_t incl = x;
-#pragma unroll
-        for (int d = 1; d < kWave; d <<= 1) {
-            uint32_t y = __shfl_up(incl, d, kWave);
-            if (lane >= d) incl += y;
-        }
-        if (lane == kWave - 1) wsum[wid] = incl;
-        __syncthreads();
-        if (wid == 0) {
-            uint32_t w = lane < kScanThreads / kWave ? wsum[lane] : 0u;
-            uint32_t wi = w;
-#pragma unroll
-            for (int d = 1; d < kScanThreads / kWave; d <<= 1) {
-                uint32_t y = __shfl_up(wi, d, kWave);
-                if (lane >= d) wi += y;
+            if (ok) {
+                okmask |= 1u << vv;
+                // Conservative half-extents of the region where o * exp(power) >= 1/255 (power =
+                // -Q/2, Q <= 2 ln(255 o)); lets a wave skip Gaussians that miss its 8x8 pixels.
+                // Pure culling: pixels inside keep the exact reference arithmetic.
+                float ex = INFINITY, ey = INFINITY;
+                if (o == o) {
+                    const float q = 2.0f * logf(255.0f * o);
+                    if (q < 0.0f) {
+                        ex = ey = -1.0f;  // alpha < 1/255 everywhere
+                    } else if (cov_a > 0.0f && cov_c > 0.0f && q < INFINITY) {
+                        ex = sqrtf(q * cov_a) * 1.001f + 0.01f;
+                        ey = sqrtf(q * cov_c) * 1.001f + 0.01f;
+                    }
+                }
+                float4* rec = ws.rec + 4 * vg;
+                rec[0] = make_float4(px, py, ex, ey);
+                // power * log2(e): alpha = o * 2^(power2) is one v_exp_f32 in the blend
+                constexpr float kLog2e = 1.44269504088896341f;
+                rec[1] = make_float4(-0.5f * kLog2e * conic_a, -kLog2e * conic_b, -0.5f * kLog2e * conic_c, o);
+                // cull threshold in the same log2 units as the stored conic: 2 log2(255 o), + margins
+                rec[3] = make_float4(2.0f * __log2f(255.0f * o) * 1.001f + 1.5e-3f,
+                                     -conic_b * __builtin_amdgcn_rcpf(conic_a),
+                                     -conic_b * __builtin_amdgcn_rcpf(conic_c), 0.0f);
+                for (int ty = y0; ty < y1; ++ty)
+                    for (int tx = x0; tx < x1; ++tx) atomicAdd(&hist[ty * p.tiles_x + tx], 1u);
+            } else {
+                radius = 0;
             }
-            if (lane < kScanThreads / kWave) wsum[lane] = wi - w;  // exclusive wave prefix
+            out_radii[vg] = radius;
         }
         __syncthreads();
-        const uint32_t c0 = carry;
-        if (i < n) offsets[i] = c0 + wsum[wid] + incl - x;
-        __syncthreads();
-        if (threadIdx.x == kScanThreads - 1) carry = c0 + wsum[wid] + incl;
-        __syncthreads();
+        uint32_t* gcount = ws.counts + (size_t)v * p.T;
+        for (int i = threadIdx.x; i < p.T; i += kPreThreads)
+            if (hist[i]) atomicAdd(&gcount[i], hist[i]);
+        // the next view's clear of hist[i] is by this same thread, after its read above
     }
-    if (threadIdx.x == 0) {
-        offsets[n] = carry;
-        if (carry > (uint32_t)capacity) atomicOr(status, 1);
+
+    // pass 2: the staged SH to LDS (this wave's own block: a wave barrier orders it), then colours
+    float4* sh_dst4 = reinterpret_cast<float4*>(sh_dst);
+#define TSPLAT_SH_ST(e) \
+    if (lane + (e) * kWave < t4) sh_dst4[lane + (e) * kWave] = shr##e;
+    TSPLAT_SH_ST(0) TSPLAT_SH_ST(1) TSPLAT_SH_ST(2) TSPLAT_SH_ST(3) TSPLAT_SH_ST(4) TSPLAT_SH_ST(5)
+    TSPLAT_SH_ST(6) TSPLAT_SH_ST(7) TSPLAT_SH_ST(8) TSPLAT_SH_ST(9) TSPLAT_SH_ST(10) TSPLAT_SH_ST(11)
+    TSPLAT_SH_ST(12) TSPLAT_SH_ST(13) TSPLAT_SH_ST(14) TSPLAT_SH_ST(15) TSPLAT_SH_ST(16) TSPLAT_SH_ST(17)
+    TSPLAT_SH_ST(18)
+#undef TSPLAT_SH_ST
+    if (p.diag != 7)
+        for (int i = 4 * t4 + lane; i < sh_total; i += kWave) sh_dst[i] = sh_src[i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int vv = 0; vv < p.vps; ++vv) {
+        if (!((okmask >> vv) & 1u)) continue;
+        const int v = scene * p.vps + vv;
+        const float* vm = viewmat + 16 * v;
+        const float s = scene_scale[2 * v];
+        const float mx = m0 * s, my = m1 * s, mz = m2 * s;
+        const float vz = vm[2] * mx + vm[6] * my + vm[10] * mz + vm[14];  // as in pass 1, bit for bit
+        float rgb[3] = {0.5f, 0.5f, 0.5f};
+        const float* cp = campos + 3 * v;
+        if (p.diag != 7) sh_to_rgb(my_sh, p.M, p.deg, mx - cp[0], my - cp[1], mz - cp[2], rgb);
+        ws.rec[4 * ((size_t)v * p.G + g) + 2] = make_float4(rgb[0], rgb[1], rgb[2], vz);
     }
 }
 
 // --- K3: scatter (gaussian, tile) instances into per-tile ranges ------------------------------
+// The exclusive scan of the V*T tile counts is folded in (it was a single-workgroup launch of its
+// own): each workgroup sums the counts of the views before its own and scans its view's T counts
+// in LDS; the x = 0 workgroup of each view publishes that view's offsets for the render kernel,
+// and the last view's also the total (offsets[V T]) and the capacity-overflow status.
+__device__ __forceinline__ uint32_t block_sum_u32(uint32_t x, uint32_t* red) {
+    const int lane = threadIdx.x % kWave, wid = threadIdx.x / kWave;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o);
+    if (lane == 0) red[wid] = x;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kPreThreads / kWave; ++w) t += red[w];
+    return t;
+}
+
 __global__ void __launch_bounds__(kPreThreads)
-scatter_kernel(Params p, const int32_t* __restrict__ radii, Workspace ws) {
-    extern __shared__ uint32_t lds[];  // hist[T] then base[T]
+scatter_kernel(Params p, const int32_t* __restrict__ radii, Workspace ws, int32_t* __restrict__ status) {
+    extern __shared__ uint32_t lds[];  // hist[T], base[T], pre[T]
     uint32_t* hist = lds;
     uint32_t* base = lds + p.T;
+    uint32_t* pre = lds + 2 * p.T;
+    __shared__ uint32_t red[2][kPreThreads / kWave];
     const int v = blockIdx.y;
     const int g = blockIdx.x * kPreThreads + threadIdx.x;
+    const int lane = threadIdx.x % kWave, wid = threadIdx.x / kWave;
     for (int i = threadIdx.x; i < p.T; i += kPreThreads) hist[i] = 0;
+    // this view's tile counts: thread t owns the contiguous segment [t k, t k + k), k = ceil(T / 256)
+    const uint32_t* vcount = ws.counts + (size_t)v * p.T;
+    const int seg = (p.T + kPreThreads - 1) / kPreThreads;
+    const int s0 = min(p.T, (int)threadIdx.x * seg), s1 = min(p.T, s0 + seg);
+    uint32_t own = 0;
+    for (int i = s0; i < s1; ++i) own += vcount[i];
+    uint32_t prior = 0;  // counts of the views before this one
+    for (size_t i = threadIdx.x; i < (size_t)v * p.T; i += kPreThreads) prior += ws.counts[i];
+    prior = block_sum_u32(prior, red[0]);  // (its barrier also orders the hist clear)
+    uint32_t incl = own;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, d, kWave);
+        if (lane >= d) incl += y;
+    }
+    if (lane == kWave - 1) red[1][wid] = incl;
+    __syncthreads();
+    uint32_t run = prior + incl - own;
+    for (int w = 0; w < wid; ++w) run += red[1][w];
+    for (int i = s0; i < s1; ++i) {
+        pre[i] = run;
+        run += vcount[i];
+    }
+    if (blockIdx.x == 0) {
+        uint32_t* off = ws.offsets + (size_t)v * p.T;
+        for (int i = s0; i < s1; ++i) off[i] = pre[i];
+        if (v == p.V - 1 && threadIdx.x == kPreThreads - 1) {  // holds the view's last segment
+            ws.offsets[(size_t)p.V * p.T] = run;
+            if (run > (uint32_t)p.capacity) atomicOr(status, 1);
+        }
+    }
     __syncthreads();
     int r = 0, x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     uint64_t key_lo = 0, depth_bits = 0;
@@ -356,10 +437,9 @@ scatter_kernel(Params p, const int32_t* __restrict__ radii, Workspace ws) {
     }
     __syncthreads();
     uint32_t* gcur = ws.cursor + (size_t)v * p.T;
-    const uint32_t* goff = ws.offsets + (size_t)v * p.T;
     for (int i = threadIdx.x; i < p.T; i += kPreThreads) {
         uint32_t h = hist[i];
-        base[i] = h ? goff[i] + atomicAdd(&gcur[i], h) : 0u;
+        base[i] = h ? pre[i] + atomicAdd(&gcur[i], h) : 0u;
         hist[i] = 0;
     }
     __syncthreads();
@@ -896,7 +976,7 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
         const int rows = (p.tiles_y + 1) / 3;
         p.view_rot = (r && !strcmp(r, "0")) ? 0 : rows * p.tiles_x;
     }
-    if ((size_t)p.T * 2 * sizeof(uint32_t) > 64 * 1024) return TSPLAT_EINVAL;  // LDS histogram
+    if ((size_t)p.T * 3 * sizeof(uint32_t) > 64 * 1024) return TSPLAT_EINVAL;  // scatter's LDS
     Workspace ws = carve(workspace, p.G, p.V, p.T, p.capacity, nullptr);
 
     TSPLAT_PROF_BEGIN(prof::kRasterAll, stream);
@@ -907,21 +987,22 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
         hipLaunchKernelGGL(zero_kernel, dim3(blocks), dim3(256), 0, stream, (uint4*)ws.counts, n4);
         TSPLAT_CHECK_LAUNCH();
     }
+    if (3 * p.M > kMaxShFloats || p.vps > 32) return TSPLAT_EINVAL;
+    const int scenes = p.V / p.vps;
+    // a wave's SH block starts at 3 M (scene G + 64 k) floats: 16-byte aligned when the base is
+    // and 3 M G is a multiple of 4 (or there is one scene)
+    p.sh_vec4 = ((uintptr_t)shs % 16 == 0) && (scenes == 1 || ((size_t)3 * p.M * p.G) % 4 == 0);
     dim3 pre_grid(ceil_div(p.G, kPreThreads), p.V);
     TSPLAT_PROF_BEGIN(prof::kRasterPreprocess, stream);
-    hipLaunchKernelGGL(preprocess_kernel, pre_grid, dim3(kPreThreads), p.T * sizeof(uint32_t),
+    hipLaunchKernelGGL(preprocess_kernel, dim3(ceil_div(p.G, kPreThreads), scenes), dim3(kPreThreads),
+                       p.T * sizeof(uint32_t),
                        stream, p, means, cov, shs, opacity, viewmat, projmat, campos, tanfov,
                        scene_scale, out_radii, ws);
     TSPLAT_PROF_END(prof::kRasterPreprocess, stream);
     TSPLAT_CHECK_LAUNCH();
-    TSPLAT_PROF_BEGIN(prof::kRasterScan, stream);
-    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, p.V * p.T,
-                       p.capacity, (const uint32_t*)ws.counts, ws.offsets, status);
-    TSPLAT_PROF_END(prof::kRasterScan, stream);
-    TSPLAT_CHECK_LAUNCH();
     TSPLAT_PROF_BEGIN(prof::kRasterScatter, stream);
-    hipLaunchKernelGGL(scatter_kernel, pre_grid, dim3(kPreThreads), 2 * p.T * sizeof(uint32_t),
-                       stream, p, (const int32_t*)out_radii, ws);
+    hipLaunchKernelGGL(scatter_kernel, pre_grid, dim3(kPreThreads), 3 * p.T * sizeof(uint32_t),
+                       stream, p, (const int32_t*)out_radii, ws, status);
     TSPLAT_PROF_END(prof::kRasterScatter, stream);
     TSPLAT_CHECK_LAUNCH();
     TSPLAT_PROF_BEGIN(prof::kRasterRender, stream);
