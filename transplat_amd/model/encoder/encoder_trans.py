@@ -85,6 +85,8 @@ class EncoderTransCfg:
 # camera-only prep of the depth predictor and the adapter on the backbone's branch
 # (TSPLAT_CAM_HOIST=0: computed where it is used, the A/B knob)
 _CAM_HOIST = os.environ.get("TSPLAT_CAM_HOIST", "1") == "1"
+# the depth predictor's backbone-only first part on the backbone's branch ("0": after the join; A/B)
+_DP_BEGIN_SIDE = os.environ.get("TSPLAT_DP_BEGIN_SIDE", "1") == "1"
 
 
 class EncoderTrans(Encoder[EncoderTransCfg]):
@@ -162,11 +164,11 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
                 ad = kernels.adapter_camera_consts(extrinsics, intrinsics, (h, w), self.gaussian_adapter.d_sh)
             return dp, ad
 
-        def depth_anything():
+        def depth_anything(images):
             with bench("encoder_3_depth_anything"), torch.no_grad(), self._dense():
                 # channel order (2, 0, 1) as the reference, by slicing: a list index would be a
                 # pageable host-to-device copy, which is not allowed inside hipGraph capture
-                da_images = self.normalize_images(context["image"])
+                da_images = self.normalize_images(images)
                 da_images = torch.cat((da_images[:, :, 2:3], da_images[:, :, 0:2]), dim=2)
                 da_images = da_images.reshape(b * v, 3, h, w)
                 da_images = kernels.interpolate_bilinear_ac(da_images, (252, 252))
@@ -190,20 +192,38 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
             with bench("encoder_2_backbone"), self._dense(), kernels.attention_precision(attn):
                 tf, cf = self.backbone(images, attn_splits=self.cfg.multiview_trans_attn_split,
                                        return_cnn_features=True, img2world=img2world)
-            # the backbone branch finishes well before Depth-Anything: its slack takes the camera prep
+            # the backbone's branch finishes well before Depth-Anything: its slack takes the camera prep
             cams = camera_consts(intrinsics, extrinsics, near, far) if _CAM_HOIST else (None, None)
             return tf.float(), cf.float(), cams
 
-        # Stages 2 and 3 read only the context images: on a GPU, the backbone runs on a side stream
-        # concurrently with Depth-Anything (transplat_amd/streams.py; captured into the step's
-        # hipGraph as parallel branches). Both are chains of small launches (DINOv2's M = 650 GEMMs,
-        # the MVT's 256-workgroup kernels) that leave CUs idle on their own. Depth-Anything stays on
-        # the current stream because it forks again (its DPT reassemble branches, dpt.py): a fork
-        # from a side stream inside hipGraph capture crashed HIP's capture_end.
-        bb = streams.fork(device, backbone, context["image"], context["intrinsics"], context["extrinsics"],
-                          context["near"], context["far"])
-        da_depth, out_feature = depth_anything()
-        trans_features, cnn_features, (dp_cams, adapter_cams) = streams.join(bb)
+        # Stages 2 and 3 read only the context images, and the depth predictor's first part (its
+        # feature lists and the coarse correlation layer) reads only the backbone's outputs and the
+        # cameras: on a GPU, the backbone, the camera prep and that first part run on a side stream
+        # (transplat_amd/streams.py; captured into the step's hipGraph as a parallel branch) beside
+        # Depth-Anything -- together shorter than it. Both are chains of small launches (DINOv2's
+        # M = 650 GEMMs, the MVT's 256-workgroup kernels) that leave CUs idle on their own.
+        # Depth-Anything stays on the current stream: the other arrangement (it on the side stream,
+        # the backbone here) measured 1 % slower, its DPT then losing CUs to the MVT (C2 426 vs 430
+        # views/s same box, profiles/r5/ab_da_side.txt); and a fork from a side stream inside hipGraph
+        # capture crashes HIP's capture_end, so the depth predictor's projection fork waits for the
+        # current stream.
+        def dp_begin(tf, cf, dp_cams, fork_projection):
+            with bench("encoder_4_depth_predictor"), self._dense():
+                return self.depth_predictor.begin(tf, context["intrinsics"], context["extrinsics"], context["near"],
+                                                  context["far"], cnn_features=cf, benchmarker=benchmarker,
+                                                  cams=dp_cams, fork_projection=fork_projection)
+
+        def backbone_branch(*ctx):
+            tf, cf, cams = backbone(*ctx)
+            begun = dp_begin(tf, cf, cams[0], not streams.enabled(device)) if _DP_BEGIN_SIDE else None
+            return tf, cf, cams, begun
+
+        ctx = (context["image"], context["intrinsics"], context["extrinsics"], context["near"], context["far"])
+        bb = streams.fork(device, backbone_branch, *ctx)
+        da_depth, out_feature = depth_anything(context["image"])
+        trans_features, cnn_features, (dp_cams, adapter_cams), begun = streams.join(bb)
+        if begun is None:
+            begun = dp_begin(trans_features, cnn_features, dp_cams, True)
         dino_feature = out_feature.view(b, v, *out_feature.shape[1:])
 
         extra_info = {"images": rearrange(context["image"], "b v c h w -> (v b) c h w"), "scene_names": scene_names}
@@ -213,7 +233,7 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
                 trans_features, context["intrinsics"], context["extrinsics"], context["near"], context["far"],
                 gaussians_per_pixel=gpp, deterministic=deterministic, extra_info=extra_info,
                 cnn_features=cnn_features, da_depth=da_depth, dino_feature=dino_feature, benchmarker=benchmarker,
-                cams=dp_cams)
+                cams=dp_cams, begun=begun)
         depths, densities, raw_gaussians = depths.float(), densities.float(), raw_gaussians.float()
 
         with bench("encoder_5_gaussian_adapter"):

@@ -168,20 +168,35 @@ class DepthPredictorTrans(nn.Module):
             out["img2world"] = match_img2world(intr, extrinsics)
         return out
 
-    def match_two(self, intr_curr, pose_curr, extrinsics, disp_candi_curr, dino_feature, features, img2world=None):
-        """(reference :236-290) coarse then fine correlation for a pair of views -> [(v b), D, h, w]."""
+    def coarse_two(self, intr_curr, pose_curr, disp_candi_curr, features):
+        """(reference :236-290, first half) the coarse correlation layer of a pair of views: reads
+        only the backbone features and the cameras, so the encoder runs it before Depth-Anything's
+        features exist (the reference computes the camera-parameter embedding first; the two are
+        independent)."""
         b, v, c, h, w = features.shape
         cameras = (intr_curr, pose_curr, disp_candi_curr.flatten(1).float())
+        feat_cl = features.flatten(3).transpose(2, 3).contiguous()  # [b, v, HW, C]
+        query = torch.zeros((b * v, h * w, self.embed_dims), device=features.device, dtype=features.dtype)
+        corr = self.coarse_transformer([features], query, w, h, cameras=cameras, channel_last=feat_cl)
+        return corr, cameras, feat_cl
+
+    def fine_two(self, coarse, intr_curr, extrinsics, dino_feature, features, img2world=None):
+        """(reference :236-290, second half) the fine layers on the coarse correlation, with the
+        Depth-Anything-feature position embedding -> [(v b), D, h, w]."""
+        b, v, c, h, w = features.shape
+        corr, cameras, feat_cl = coarse
         if img2world is None:
             img2world = match_img2world(intr_curr, extrinsics)
         pos_feature = self.cam_param_encoder(dino_feature, img2world)  # [(v b), C, h, w]
         # (b v)-ordered channel-last query positions: the reference's bev_pos after its permutes
         bev_pos = rearrange(pos_feature, "(v b) c h w -> (b v) (h w) c", v=v, b=b)
-        feat_cl = features.flatten(3).transpose(2, 3).contiguous()  # [b, v, HW, C]
-        query = torch.zeros((b * v, h * w, self.embed_dims), device=features.device, dtype=features.dtype)
-        corr = self.coarse_transformer([features], query, w, h, cameras=cameras, channel_last=feat_cl)
         corr = self.fine_transformer([features], corr, w, h, bev_pos=bev_pos, cameras=cameras, channel_last=feat_cl)
         return rearrange(corr, "(b v) (h w) c -> (v b) c h w", b=b, v=v, h=h, w=w)
+
+    def match_two(self, intr_curr, pose_curr, extrinsics, disp_candi_curr, dino_feature, features, img2world=None):
+        """(reference :236-290) coarse then fine correlation for a pair of views -> [(v b), D, h, w]."""
+        coarse = self.coarse_two(intr_curr, pose_curr, disp_candi_curr, features)
+        return self.fine_two(coarse, intr_curr, extrinsics, dino_feature, features, img2world)
 
     def match_pairs(self, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr, dino_feature, features):
         """(reference :351-414) V = 3 / 4: match_two on every pair of _VIEW_PAIRS[V], then each view's
@@ -207,34 +222,61 @@ class DepthPredictorTrans(nn.Module):
             per_view.append(torch.stack(halves, dim=0).mean(dim=0))
         return torch.cat(per_view, dim=0)  # (v b)
 
-    def forward(self, features, intrinsics, extrinsics, near, far, gaussians_per_pixel=1, deterministic=True,
-                extra_info=None, cnn_features=None, da_depth=None, dino_feature=None, benchmarker=None, cams=None):
+    def _projection(self, feat01, cnn_features):  # (reference :448-452) reads backbone features only
+        proj_feat_in_fullres = _conv_upsample_gelu(self.upsampler, torch.cat((feat01, cnn_features), dim=1))
+        return proj_feat_in_fullres, self.proj_feature(proj_feat_in_fullres)
+
+    def begin(self, features, intrinsics, extrinsics, near, far, cnn_features=None, benchmarker=None, cams=None,
+              fork_projection=True):
+        """The part of forward that reads only the backbone's outputs and the cameras -- 4a's feature
+        lists, the full-resolution projection (forked beside the cost volume) and, for two views,
+        the coarse correlation layer -- so that the encoder can run it on the backbone's branch while
+        Depth-Anything is still computing; forward(begun=...) continues from it. fork_projection=False
+        (inside a forked branch, which must not fork again under capture): forward forks it."""
         b, v, c, h, w = features.shape
+
         # the reference's stage tags (depth_predictor_trans.py:320-456) as roctx ranges
-
-        def projection(feat01, cnn_features):  # (reference :448-452) reads backbone features only
-            proj_feat_in_fullres = _conv_upsample_gelu(self.upsampler, torch.cat((feat01, cnn_features), dim=1))
-            return proj_feat_in_fullres, self.proj_feature(proj_feat_in_fullres)
-
         with stage(benchmarker, "encoder_4a_prep_features"):
-            if da_depth is not None:
-                da_depth = rearrange(da_depth, "b v ... -> (v b) ...")
             if cnn_features is not None:
                 cnn_features = rearrange(cnn_features, "b v ... -> (v b) ...")
-            if dino_feature is not None:
-                dino_feature = rearrange(dino_feature, "b v ... -> (v b) ...")
-                dino_feature = kernels.interpolate_bilinear_ac(dino_feature, (h, w))
             feat_comb_lists, intr_curr, pose_curr_lists, disp_candi_curr = prepare_feat_proj_data_lists(
                 features, intrinsics, extrinsics, near, far, num_samples=self.num_depth_candidates,
                 cams=cams["lists"] if cams is not None else None)
             feat01 = feat_comb_lists[0]
             # the full-resolution feature projection runs on a side stream beside the cost volume
             # (matching, refine U-Net, depth head: a chain of 64^2 launches), transplat_amd/streams.py
-            proj = streams.fork(features.device, projection, feat01, cnn_features)
+            proj = (streams.fork(features.device, self._projection, feat01, cnn_features) if fork_projection
+                    else (feat01, cnn_features))
+        coarse = None
+        if v == 2:
+            with stage(None, "dp_coarse"):  # diagnostic sub-stage mark
+                coarse = self.coarse_two(intr_curr, pose_curr_lists[0], disp_candi_curr, features)
+        return {"lists": (intr_curr, pose_curr_lists, disp_candi_curr), "feat01": feat01, "proj": proj,
+                "proj_forked": fork_projection, "coarse": coarse}
+
+    def forward(self, features, intrinsics, extrinsics, near, far, gaussians_per_pixel=1, deterministic=True,
+                extra_info=None, cnn_features=None, da_depth=None, dino_feature=None, benchmarker=None, cams=None,
+                begun=None):
+        b, v, c, h, w = features.shape
+        if begun is None:
+            begun = self.begin(features, intrinsics, extrinsics, near, far, cnn_features, benchmarker, cams)
+        intr_curr, pose_curr_lists, disp_candi_curr = begun["lists"]
+        feat01, proj = begun["feat01"], begun["proj"]
+        if not begun["proj_forked"]:
+            proj = streams.fork(features.device, self._projection, *proj)
+        if da_depth is not None:
+            da_depth = rearrange(da_depth, "b v ... -> (v b) ...")
+        if dino_feature is not None:
+            dino_feature = rearrange(dino_feature, "b v ... -> (v b) ...")
+            dino_feature = kernels.interpolate_bilinear_ac(dino_feature, (h, w))
         with stage(benchmarker, "encoder_4b_cost_volume_matching"):
-            raw_correlation_in = self._match(v, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr,
-                                             dino_feature, features, feat01,
-                                             cams.get("img2world") if cams is not None else None)
+            img2world = cams.get("img2world") if cams is not None else None
+            if begun["coarse"] is not None:
+                raw_correlation_in = torch.cat((self.fine_two(begun["coarse"], intr_curr, extrinsics, dino_feature,
+                                                              features, img2world), feat01), dim=1)
+            else:
+                raw_correlation_in = self._match(v, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr,
+                                                 dino_feature, features, feat01, img2world)
         with stage(benchmarker, "encoder_4c_cost_volume_unet"):
             raw_correlation = (run_sequential(self.corr_refine_net, raw_correlation_in)
                                + self.regressor_residual(raw_correlation_in))
