@@ -427,6 +427,18 @@ int tsplat_conv2d_f32_zsplit_fwd(const float* x1, int32_t c1, const float* x2, i
                                  int32_t c_out, int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit,
                                  int32_t zsplit, float* partials, int32_t* counters, void* stream);
 
+/* tsplat_conv2d_f32_zsplit_fwd in split-bf16 ("bf16x3", the bf16x3 dense mode's precision: each
+ * product as hi*hi + hi*lo + lo*hi of x = hi + lo bf16 on bf16 MFMA, fp32 accumulation, <= ~3 * 2^-18
+ * relative per product -- finer than the reference's TF32, src/main.py:15). Same layers, arguments
+ * and workspaces, except: c1 and c2 any positive / non-negative counts (not only even), and
+ * w_packed is the weight as bf16 hi / lo fragments [ceil(c_out / 32)][k * k][ceil(cin / 16)][2 (hi,
+ * lo)][64][8] (element (l, j) of fragment (cot, tap, g): c_out 32 cot + (l & 31), cin 16 g + 8 (l >> 5)
+ * + j; zero past c_out / cin). */
+int tsplat_conv2d_bf16x3_fwd(const float* x1, int32_t c1, const float* x2, int32_t c2, const void* w_packed,
+                             const float* bias, float* y, int32_t batch, int32_t height, int32_t width,
+                             int32_t c_out, int32_t ksize, int32_t stride, int32_t upsample, int32_t ksplit,
+                             int32_t zsplit, float* partials, int32_t* counters, void* stream);
+
 /* 3x3 / stride 1 / padding 1 convolution as Winograd F(2x2, 3x3) on exact-fp32 MFMA (replaces the
  * nn.Conv2d(c_in, c_out, 3, 1, 1) calls of the depth predictor's full-resolution heads and U-Net
  * levels, reference src/model/encoder/matching/depth_predictor_trans.py:110-125 and

@@ -707,3 +707,48 @@ def test_conv_bf16_rejects_unsupported(device):
         assert not K.conv_bf16_ok(torch.zeros(1, 36, 16, 16, device=device), torch.zeros(32, 35, 3, 3, device=device))
         assert not K.conv_bf16_ok(x.contiguous(memory_format=torch.channels_last), w)
         assert not K.conv_bf16_ok(torch.zeros(1, 32, 16, 6, device=device), w, upsample=True)  # 12 % 8
+
+
+X3_CASES = CASES + [
+    (1, 3, 5, 9, 13, 40, 3, 1, False, True),          # odd channel counts (the split kernel's 16-groups)
+    (2, 768, 0, 9, 9, 128, 3, 1, False, True),        # long reduction -> zsplit
+    (2, 256, 0, 64, 64, 128, 1, 1, False, True),
+    (2, 768, 0, 18, 18, 768, 3, 2, False, True),      # the DPT's stride-2 768-channel level
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,c1,c2,h,w,cout,k,stride,up,has_bias", X3_CASES)
+def test_conv2d_direct_bf16x3_kernel(device, monkeypatch, n, c1, c2, h, w, cout, k, stride, up, has_bias):
+    """tsplat_conv2d_bf16x3_fwd (the direct convolution in the bf16x3 dense mode) against float64:
+    within 2e-5 of max |y| AND at most 1/8 of the error of TF32-rounded operands (the reference's
+    own arithmetic, src/main.py:15) on the same inputs; bit-identical over repeated launches. Every
+    case forced onto the split kernel (the dispatch keeps the small 3x3s exact fp32)."""
+    from transplat_amd import kernels as K
+
+    monkeypatch.setattr(K, "conv_x3_wins", lambda *a: True)
+
+    F = torch.nn.functional
+    x1 = seeded((n, c1, h, w), 11)
+    x2 = seeded((n, c2, h, w), 12) if c2 else None
+    wt = seeded((cout, c1 + c2, k, k), 13) * (1.0 / (c1 + c2) ** 0.5)
+    b = seeded((cout,), 14) if has_bias else None
+
+    def ref_of(a1, a2, ww):
+        x = torch.cat([a1, a2], 1) if a2 is not None else a1
+        if up:
+            x = F.interpolate(x, scale_factor=2, mode="nearest")
+        return F.conv2d(x.double(), ww.double(), b.double() if b is not None else None, stride, padding=k // 2)
+
+    ref = ref_of(x1, x2, wt)
+    ref_tf = ref_of(tf32_round(x1), tf32_round(x2) if x2 is not None else None, tf32_round(wt))
+    args = (x1.to(device), wt.to(device), b.to(device) if b is not None else None, stride)
+    with K.dense_precision("bf16x3"):
+        outs = [K.conv2d_direct(*args, x2=x2.to(device) if x2 is not None else None, upsample=up).cpu()
+                for _ in range(2)]
+    scale = ref.abs().max().item()
+    err = (outs[0].double() - ref).abs().max().item() / scale
+    etf = (ref_tf - ref).abs().max().item() / scale
+    print(f"direct bf16x3 {(n, c1, c2, h, w, cout, k, stride, up)}: rel err {err:.2e} (TF32 operands {etf:.2e})")
+    assert err < 2e-5 and err <= etf / 8, (err, etf)
+    assert torch.equal(outs[0], outs[1])

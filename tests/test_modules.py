@@ -66,8 +66,10 @@ GPU_TOL: dict = {
     ("uv.fine", "bf16x3"): 1.6e-05,
     ("unet_cv", "fp32"): 2.7e-06,
     ("unet_depth", "fp32"): 1.9e-06,
-    ("unet_cv", "bf16x3"): 2.7e-06,
-    ("unet_depth", "bf16x3"): 1.9e-06,
+    # the U-Nets' direct convolutions went split-bf16 in the bf16x3 mode (kernels.conv_x3_wins):
+    # measured 1.14e-05 / 8.9e-06 (profiles/r5/conv_x3/pytest_tol.log; exact-fp32 direct: 1.3e-06 / 9e-07)
+    ("unet_cv", "bf16x3"): 2.3e-05,
+    ("unet_depth", "bf16x3"): 1.8e-05,
     ("depth_predictor_v2.depths", "fp32"): 3.3e-04,
     ("depth_predictor_v2.densities", "fp32"): 2.0e-06,
     ("depth_predictor_v2.raw", "fp32"): 3.0e-06,

@@ -71,6 +71,7 @@ SIGNATURES = {
     "tsplat_qkv_attention_cf_fwd": (ctypes.c_int, [_P, _P] + [_I32] * 5 + [ctypes.c_float, _P]),
     "tsplat_conv2d_f32_fwd": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _P, _P] + [_I32] * 8 + [_P]),
     "tsplat_conv2d_f32_zsplit_fwd": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _P, _P] + [_I32] * 9 + [_P, _P, _P]),
+    "tsplat_conv2d_bf16x3_fwd": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _P, _P] + [_I32] * 9 + [_P, _P, _P]),
     "tsplat_resize_bilinear_nhwc_fwd": (ctypes.c_int, [_P, _P] + [_I32] * 6 + [_P]),
     "tsplat_resize_bilinear_nchw_fwd": (ctypes.c_int, [_P, _P] + [_I32] * 5 + [_P]),
     "tsplat_upsample_bilinear_act_fwd": (ctypes.c_int, [_P, _P, _P] + [_I32] * 6 + [_P]),

@@ -48,6 +48,85 @@ struct Args {
     int npx;            // n * hout * wout
 };
 
+// The tile's ksplit (and zsplit) partial sums -> bias (+ residual) -> y. Every kernel here holds one
+// 32 (cout) x 32 (pixel) tile per wave in the 32x32 MFMA accumulator layout (lane = pixel l & 31,
+// register r = cout 8 (r >> 2) + 4 (l >> 5) + (r & 3)).
+template <bool NHWC>
+__device__ __forceinline__ void tile_epilogue(const Args& p, const floatx16& acc, float* sred) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, ksplit = blockDim.x >> 6;
+    const int cot = blockIdx.y;
+    const int hwo = p.hout * p.wout;
+    // sum the ksplit partial tiles
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sred[(w * 16 + r) * 64 + lane] = acc[r];
+    __syncthreads();
+    const int tile = blockIdx.x + gridDim.x * blockIdx.y;
+    if (p.zsplit > 1) {
+        // this workgroup's partial tile -> workspace with write-through (sc1) stores, so no release
+        // fence; drained by every wave, then ONE lane takes an arrival ticket. The tile's last
+        // arriver: ONE agent-scope acquire (its L1 may hold stale lines of the other partials), then
+        // plain loads (cdna_hip_programming.md §5 "In-launch split-K reduction"; a __threadfence()
+        // in every thread instead made the C2 step 5 % slower)
+        typedef __attribute__((address_space(1))) unsigned gu32;
+        unsigned* mine = reinterpret_cast<unsigned*>(p.part + ((size_t)tile * p.zsplit + blockIdx.z) * 1024);
+        for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
+            float s = 0.f;
+            for (int k = 0; k < ksplit; ++k) s += sred[(k * 16 + (idx >> 6)) * 64 + (idx & 63)];
+            __hip_atomic_store((gu32*)(mine + idx), __float_as_uint(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int* flag = reinterpret_cast<int*>(sred + ksplit * 1024);  // one LDS word past the partials
+        if (threadIdx.x == 0) {
+            const int t = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const bool last = t == p.zsplit - 1;
+            if (last) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            *flag = last;
+        }
+        __syncthreads();
+        if (!*flag) return;
+        const float* all = p.part + (size_t)tile * p.zsplit * 1024;
+        for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
+            float s = 0.f;
+            for (int z = 0; z < p.zsplit; ++z) s += all[(size_t)z * 1024 + idx];
+            sred[idx] = s;
+        }
+        __syncthreads();
+    }
+    const int nsum = p.zsplit > 1 ? 1 : ksplit;  // partial rows left in sred
+    for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
+        // NCHW: consecutive threads -> consecutive pixels; NHWC: -> consecutive output channels
+        int r, l;
+        if (NHWC) {
+            const int col = idx & 31, pl = idx >> 5;
+            r = ((col >> 3) << 2) | (col & 3);
+            l = ((col >> 2) & 1) * 32 + pl;
+        } else {
+            r = idx >> 6;
+            l = idx & 63;
+        }
+        float s = 0.f;
+        for (int k = 0; k < nsum; ++k) s += sred[(k * 16 + r) * 64 + l];
+        const int co = cot * 32 + 8 * (r >> 2) + 4 * (l >> 5) + (r & 3);
+        const int q = blockIdx.x * 32 + (l & 31);
+        if (co >= p.cout || q >= p.npx) continue;
+        if (p.bias) s += p.bias[co];
+        size_t o;
+        if (NHWC) {
+            o = (size_t)q * p.cout + co;
+        } else {
+            const int qn = q / hwo, qp = q - qn * hwo;
+            o = ((size_t)qn * p.cout + co) * hwo + qp;
+        }
+        if (p.res) s += p.res[o];
+        p.y[o] = s;
+    }
+}
+
 // G = ci pairs per batch (all their taps): the loads of one batch are in flight while the previous
 // batch's G * T MFMAs run, so a wave's time is ~ (its batches) x (memory latency) for these small
 // layers -- larger G, fewer round trips.
@@ -163,75 +242,114 @@ __global__ void __launch_bounds__(1024) conv_f32_kernel(Args p) {
         }
     }
 
-    // sum the ksplit partial tiles
+    tile_epilogue<NHWC>(p, acc, sred);
+}
+
+// ---- split-bf16 ("bf16x3") form of the same convolution (the bf16x3 dense mode's precision: every
+// product as hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_bf16 with fp32 accumulation, x = hi + lo,
+// <= ~3 * 2^-18 relative per product; the exact-fp32 32x32x2 MFMA above runs at 1/5.3 of its rate).
+// The reduction is cut into units (tap t, 16-channel group g) -- one K = 16 MFMA triple each -- dealt
+// to the tile's waves (and zsplit workgroups) round-robin; a wave loads NB units at once (per unit
+// and lane: 8 channels of its pixel at the tap's shifted position, and the packed hi / lo weight
+// fragments, two 16-B loads), splits the 8 values into hi / lo bf16 and issues the 3 MFMAs. Weights
+// packed on the host as [co tile][tap][group][hi, lo][64 lanes][8] bf16 (lane l: cout 32 cot + (l & 31),
+// channels 16 g + 8 (l >> 5) + j; zero past cin / cout). Epilogue as the fp32 kernel's.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((floatx2){a, b}, bf16x2));
+}
+
+template <int KS, int S, int UP, int NB>
+__global__ void __launch_bounds__(1024) conv_x3_kernel(Args p) {
+    extern __shared__ float sred[];  // [ksplit][16][64]
+    constexpr int T = KS * KS, PAD = KS / 2;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, ksplit = blockDim.x >> 6;
+    const int h = lane >> 5;
+    const int cot = blockIdx.y;
+    const int hwo = p.hout * p.wout, hwi = p.hin * p.win;
+    const int px = blockIdx.x * 32 + (lane & 31);
+    const int pxc = min(px, p.npx - 1);
+    const int nb = pxc / hwo, pix = pxc - nb * hwo;
+    const int oy = pix / p.wout, ox = pix - oy * p.wout;
+    const int ci = p.c1 + p.c2, ng = (ci + 15) >> 4;
+    int off[T];
+    unsigned vmask = 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) sred[(w * 16 + r) * 64 + lane] = acc[r];
-    __syncthreads();
-    const int tile = blockIdx.x + gridDim.x * blockIdx.y;
-    if (p.zsplit > 1) {
-        // this workgroup's partial tile -> workspace with write-through (sc1) stores, so no release
-        // fence; drained by every wave, then ONE lane takes an arrival ticket. The tile's last
-        // arriver: ONE agent-scope acquire (its L1 may hold stale lines of the other partials), then
-        // plain loads (cdna_hip_programming.md §5 "In-launch split-K reduction"; a __threadfence()
-        // in every thread instead made the C2 step 5 % slower)
-        typedef __attribute__((address_space(1))) unsigned gu32;
-        unsigned* mine = reinterpret_cast<unsigned*>(p.part + ((size_t)tile * p.zsplit + blockIdx.z) * 1024);
-        for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
-            float s = 0.f;
-            for (int k = 0; k < ksplit; ++k) s += sred[(k * 16 + (idx >> 6)) * 64 + (idx & 63)];
-            __hip_atomic_store((gu32*)(mine + idx), __float_as_uint(s), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int* flag = reinterpret_cast<int*>(sred + ksplit * 1024);  // one LDS word past the partials
-        if (threadIdx.x == 0) {
-            const int t = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const bool last = t == p.zsplit - 1;
-            if (last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int t = 0; t < T; ++t) {
+        const int ky = t / KS, kx = t - ky * KS;
+        const int iy = oy * S + ky - PAD, ix = ox * S + kx - PAD;
+        const bool v = px < p.npx && iy >= 0 && iy < p.hv && ix >= 0 && ix < p.wv;
+        off[t] = v ? (UP ? (iy >> 1) * p.win + (ix >> 1) : iy * p.win + ix) : 0;
+        vmask |= (unsigned)v << t;
+    }
+    const uint4* wbase = reinterpret_cast<const uint4*>(p.wp) + (size_t)cot * T * ng * 128 + lane;
+    const int units = ng * T;
+    const int gw = blockIdx.z * ksplit + w, gstride = ksplit * p.zsplit;
+    const int nu = units > gw ? (units - gw + gstride - 1) / gstride : 0;
+    const float* x1 = p.x1 + (size_t)nb * p.c1 * hwi;
+    const float* x2 = p.x2 ? p.x2 + (size_t)nb * p.c2 * hwi : p.x1;
+
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll 1
+    for (int b0 = 0; b0 < nu; b0 += NB) {
+        float xv[NB][8];
+        uint4 ah[NB], al[NB];
+        // every load unconditional from a clamped, valid address, masked afterwards (a conditional
+        // load becomes a branch with its own wait, serialising the batch's round trips)
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            const int i = b0 + k;
+            const bool ok = i < nu;
+            const int u = gw + min(i, nu - 1) * gstride;
+            const int g = u / T, t = u - g * T;
+            const uint4* wq = wbase + (size_t)(t * ng + g) * 128;
+            const unsigned ma = ok ? ~0u : 0u;
+            const uint4 a0 = wq[0], a1 = wq[64];
+            ah[k] = make_uint4(a0.x & ma, a0.y & ma, a0.z & ma, a0.w & ma);
+            al[k] = make_uint4(a1.x & ma, a1.y & ma, a1.z & ma, a1.w & ma);
+            int o = 0;
+            bool tv = false;
+#pragma unroll
+            for (int tt = 0; tt < T; ++tt)
+                if (tt == t) {
+                    o = off[tt];
+                    tv = (vmask >> tt) & 1;
+                }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int ch = 16 * g + 8 * h + j;
+                const int cc = min(ch, ci - 1);
+                const float* src = cc < p.c1 ? x1 + (size_t)cc * hwi : x2 + (size_t)(cc - p.c1) * hwi;
+                const float v = src[o];
+                const unsigned mb = (ok && tv && ch < ci) ? ~0u : 0u;
+                xv[k][j] = __uint_as_float(__float_as_uint(v) & mb);
             }
-            *flag = last;
         }
-        __syncthreads();
-        if (!*flag) return;
-        const float* all = p.part + (size_t)tile * p.zsplit * 1024;
-        for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
-            float s = 0.f;
-            for (int z = 0; z < p.zsplit; ++z) s += all[(size_t)z * 1024 + idx];
-            sred[idx] = s;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < NB; ++k) {
+            uint32_t hi[4], lo[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float a = xv[k][2 * q], b = xv[k][2 * q + 1];
+                hi[q] = pack_bf16(a, b);
+                const float ah_ = __uint_as_float(hi[q] << 16), bh_ = __uint_as_float(hi[q] & 0xffff0000u);
+                lo[q] = pack_bf16(a - ah_, b - bh_);
+            }
+            const bf16x8 bh = __builtin_bit_cast(bf16x8, make_uint4(hi[0], hi[1], hi[2], hi[3]));
+            const bf16x8 bl = __builtin_bit_cast(bf16x8, make_uint4(lo[0], lo[1], lo[2], lo[3]));
+            const bf16x8 wh = __builtin_bit_cast(bf16x8, ah[k]), wl = __builtin_bit_cast(bf16x8, al[k]);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, bh, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, bl, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, bh, acc, 0, 0, 0);
         }
-        __syncthreads();
     }
-    const int nsum = p.zsplit > 1 ? 1 : ksplit;  // partial rows left in sred
-    for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
-        // NCHW: consecutive threads -> consecutive pixels; NHWC: -> consecutive output channels
-        int r, l;
-        if (NHWC) {
-            const int col = idx & 31, pl = idx >> 5;
-            r = ((col >> 3) << 2) | (col & 3);
-            l = ((col >> 2) & 1) * 32 + pl;
-        } else {
-            r = idx >> 6;
-            l = idx & 63;
-        }
-        float s = 0.f;
-        for (int k = 0; k < nsum; ++k) s += sred[(k * 16 + r) * 64 + l];
-        const int co = cot * 32 + 8 * (r >> 2) + 4 * (l >> 5) + (r & 3);
-        const int q = blockIdx.x * 32 + (l & 31);
-        if (co >= p.cout || q >= p.npx) continue;
-        if (p.bias) s += p.bias[co];
-        size_t o;
-        if (NHWC) {
-            o = (size_t)q * p.cout + co;
-        } else {
-            const int qn = q / hwo, qp = q - qn * hwo;
-            o = ((size_t)qn * p.cout + co) * hwo + qp;
-        }
-        if (p.res) s += p.res[o];
-        p.y[o] = s;
-    }
+    tile_epilogue<false>(p, acc, sred);
 }
 
 }  // namespace conv
@@ -359,6 +477,72 @@ extern "C" int tsplat_conv2d_f32_nhwc_fwd(const float* x, int32_t c_in, const fl
         }
     }
 #undef TSPLAT_CONV_LAUNCH
+    TSPLAT_PROF_END(tsplat::prof::kConv, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_conv2d_bf16x3_fwd(const float* x1, int32_t c1, const float* x2, int32_t c2,
+                                        const void* w_packed, const float* bias, float* y, int32_t batch,
+                                        int32_t height, int32_t width, int32_t c_out, int32_t ksize, int32_t stride,
+                                        int32_t upsample, int32_t ksplit, int32_t zsplit, float* partials,
+                                        int32_t* counters, void* stream_) {
+    using namespace tsplat::conv;
+    if (!x1 || !w_packed || !y || batch <= 0 || height <= 0 || width <= 0 || c_out <= 0) return TSPLAT_EINVAL;
+    if (zsplit < 1 || zsplit > 64 || (zsplit > 1 && (!partials || !counters))) return TSPLAT_EINVAL;
+    if (c1 <= 0 || c2 < 0 || (c2 > 0 && !x2)) return TSPLAT_EINVAL;
+    if (!(ksize == 1 || ksize == 3) || !(stride == 1 || stride == 2) || !(upsample == 0 || upsample == 1) ||
+        (upsample && stride != 1))
+        return TSPLAT_EINVAL;
+    if (ksplit < 1 || ksplit > kMaxWaves) return TSPLAT_EINVAL;
+    Args p{};
+    p.zsplit = zsplit;
+    p.part = partials;
+    p.cnt = counters;
+    p.x1 = x1;
+    p.x2 = c2 > 0 ? x2 : nullptr;
+    p.wp = (const float*)w_packed;
+    p.bias = bias;
+    p.y = y;
+    p.c1 = c1;
+    p.c2 = c2;
+    p.cout = c_out;
+    p.n = batch;
+    p.hin = height;
+    p.win = width;
+    p.hv = upsample ? 2 * height : height;
+    p.wv = upsample ? 2 * width : width;
+    const int pad = ksize / 2;
+    p.hout = (p.hv + 2 * pad - ksize) / stride + 1;
+    p.wout = (p.wv + 2 * pad - ksize) / stride + 1;
+    if (p.hout <= 0 || p.wout <= 0) return TSPLAT_EINVAL;
+    const int64_t npx = (int64_t)batch * p.hout * p.wout;
+    const int64_t in_elems = (int64_t)batch * (c1 > c2 ? c1 : c2) * height * width;
+    if (npx >= (1ll << 31) || in_elems >= (1ll << 31)) return TSPLAT_EINVAL;
+    p.npx = (int)npx;
+    hipStream_t stream = (hipStream_t)stream_;
+    const dim3 grid((unsigned)((npx + 31) / 32), (unsigned)((c_out + 31) / 32), (unsigned)zsplit);
+    const dim3 block(64 * ksplit);
+    const size_t lds = (size_t)ksplit * 16 * 64 * sizeof(float) + 16;
+    // units per wave: one batch when a wave has up to 4, else batches of 2 (batches of 4 measured up
+    // to 2x slower there: 120 VGPRs, profiles/r5/conv_x3/census_x3b.log)
+    const int units = (c1 + c2 + 15) / 16 * ksize * ksize;
+    const int per_wave = (units + ksplit * zsplit - 1) / (ksplit * zsplit);
+    const int nb = per_wave <= 4 ? per_wave : 2;
+    TSPLAT_PROF_BEGIN(tsplat::prof::kConv, stream);
+#define TSPLAT_X3_LAUNCH(KS, S, UP)                                                                       \
+    do {                                                                                                  \
+        if (nb == 1) hipLaunchKernelGGL((conv_x3_kernel<KS, S, UP, 1>), grid, block, lds, stream, p);     \
+        else if (nb == 3) hipLaunchKernelGGL((conv_x3_kernel<KS, S, UP, 3>), grid, block, lds, stream, p); \
+        else if (nb == 4) hipLaunchKernelGGL((conv_x3_kernel<KS, S, UP, 4>), grid, block, lds, stream, p); \
+        else hipLaunchKernelGGL((conv_x3_kernel<KS, S, UP, 2>), grid, block, lds, stream, p);             \
+    } while (0)
+    if (ksize == 3 && stride == 1 && !upsample) TSPLAT_X3_LAUNCH(3, 1, 0);
+    else if (ksize == 3 && stride == 2) TSPLAT_X3_LAUNCH(3, 2, 0);
+    else if (ksize == 3) TSPLAT_X3_LAUNCH(3, 1, 1);
+    else if (stride == 1) TSPLAT_X3_LAUNCH(1, 1, 0);
+    else TSPLAT_X3_LAUNCH(1, 2, 0);
+#undef TSPLAT_X3_LAUNCH
     TSPLAT_PROF_END(tsplat::prof::kConv, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

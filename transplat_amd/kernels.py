@@ -692,9 +692,78 @@ def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsa
     return flop <= _CONV_MAX_FLOP
 
 
+# the direct convolutions in the bf16x3 dense mode on split-bf16 MFMA (tsplat_conv2d_bf16x3_fwd) instead of
+# exact fp32; TSPLAT_CONV_X3=0 keeps them exact (A/B knob)
+_CONV_X3 = os.environ.get("TSPLAT_CONV_X3", "1") == "1"
+_CONV_X3_PACKED: dict = {}
+
+
+def conv_pack_weight_x3(weight):
+    """[cout, cin, k, k] -> hi / lo bf16 fragments [ceil(cout / 32)][k * k][ceil(cin / 16)][hi, lo][64 lanes]
+    [8] (lane l: cout 32 cot + (l & 31), cin 16 g + 8 (l >> 5) + j; zero-padded), cached per weight
+    tensor version: the A operand of tsplat_conv2d_bf16x3_fwd."""
+    hit = _CONV_X3_PACKED.get(id(weight))
+    if hit is not None and hit[0]() is weight and hit[1] == weight._version:
+        return hit[2]
+    co, ci = weight.shape[:2]
+    k = weight.shape[2] if weight.dim() == 4 else 1
+    cot, ng = (co + 31) // 32, (ci + 15) // 16
+    w = torch.zeros((cot * 32, ng * 16, k * k), dtype=torch.float32, device=weight.device)
+    w[:co, :ci] = weight.detach().float().reshape(co, ci, k * k)
+    a = w.reshape(cot, 32, ng, 2, 8, k * k).permute(0, 5, 2, 3, 1, 4)  # [cot, tap, g, h, m, j]
+    hi = a.to(torch.bfloat16)
+    lo = (a - hi.float()).to(torch.bfloat16)
+    packed = torch.stack((hi, lo), dim=3).contiguous()  # [cot, tap, g, hl, h, m, j]
+    if len(_CONV_X3_PACKED) > 512:
+        for key in [key for key, v in _CONV_X3_PACKED.items() if v[0]() is None]:
+            del _CONV_X3_PACKED[key]
+    _CONV_X3_PACKED[id(weight)] = (weakref.ref(weight), weight._version, packed)
+    return packed
+
+
+def conv_x3_wins(npx: int, ci: int, co: int, k: int) -> bool:
+    """Where the split-bf16 direct kernel beats the exact-fp32 one (graph-timed census of the C2 step,
+    profiles/r5/conv_x3/): every 1x1 (one 16-channel unit carries 16 channels' products: 0.8-12 us
+    faster per shape), and the 3x3s with >= 0.5 GFLOP over >= 64 input channels (the 768 -> 768
+    stride-2 level 53.6 vs 73.6 us). The few-channel / small-map 3x3s stay exact fp32: 32-channel
+    3x3s lost 1-2 us each (18 units of 8 gathered channels over 16 waves)."""
+    if k == 1:
+        return True
+    return ci >= 64 and 2.0 * npx * co * ci * k * k >= 0.5e9
+
+
+def _conv2d_direct_x3(lib, a, b, c1, c2, weight, bias, n, h, w, co, k, stride, upsample, y):
+    hout, wout = y.shape[2], y.shape[3]
+    tiles = ((n * hout * wout + 31) // 32) * ((co + 31) // 32)
+    units = (c1 + c2 + 15) // 16 * k * k
+    # waves per tile: up to 16 while the grid stays <= 8192 waves and every wave has a unit; then
+    # workgroups per tile (zsplit) doubled while the grid stays within 256 workgroups and every
+    # wave keeps >= 2 units (the alternative, >= 1 unit with 4-unit batches, measured slower:
+    # profiles/r5/conv_x3/census_x3b.log)
+    ksplit = 16
+    while ksplit > 1 and (tiles * ksplit > _CONV3_WAVES or units < ksplit):
+        ksplit //= 2
+    z = 1
+    if _ZSPLIT != 0:
+        while (z < 64 and tiles * 2 * z <= _ZSPLIT_WGS and units >= 2 * ksplit * 2 * z
+               and (_ZSPLIT < 0 or 2 * z <= _ZSPLIT)):
+            z *= 2
+    part = cnt = None
+    if z > 1:
+        part = torch.empty(tiles * z * 1024, dtype=torch.float32, device=y.device)
+        cnt = _zsplit_counters(y.device, tiles)
+    pb = _f32(bias) if bias is not None else None
+    rc = lib.tsplat_conv2d_bf16x3_fwd(_lib.ptr(a), c1, _lib.ptr(b), c2, _lib.ptr(conv_pack_weight_x3(weight)),
+                                      _lib.ptr(pb), _lib.ptr(y), n, h, w, co, k, stride, int(upsample), ksplit, z,
+                                      _lib.ptr(part), _lib.ptr(cnt), _lib.stream_ptr(y.device))
+    _lib.check(rc, "tsplat_conv2d_bf16x3_fwd")
+    return y
+
+
 def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: bool = False):
     """conv2d(cat([x1, x2], 1) (nearest-upsampled 2x if upsample), weight, bias, stride,
-    padding = k // 2) in one exact-fp32 MFMA launch (tsplat_conv2d_f32_fwd), NCHW fp32."""
+    padding = k // 2) in one MFMA launch, NCHW fp32: exact fp32 (tsplat_conv2d_f32_zsplit_fwd), or
+    split-bf16 in the bf16x3 dense mode (tsplat_conv2d_bf16x3_fwd)."""
     lib = _lib.load()
     n, c1, h, w = x1.shape
     a = _f32(x1)
@@ -708,6 +777,8 @@ def conv2d_direct(x1, weight, bias=None, stride: int = 1, x2=None, upsample: boo
     hv, wv = (2 * h, 2 * w) if upsample else (h, w)
     hout, wout = (hv + 2 * (k // 2) - k) // stride + 1, (wv + 2 * (k // 2) - k) // stride + 1
     y = torch.empty((n, co, hout, wout), dtype=torch.float32, device=x1.device)
+    if _CONV_X3 and split_mode() and conv_x3_wins(n * hout * wout, c1 + c2, co, k):
+        return _conv2d_direct_x3(lib, a, b, c1, c2, weight, bias, n, h, w, co, k, stride, upsample, y)
     # waves per 32 x 32 tile: the ci pairs split over up to 16 waves (>= 2 pairs of a 3x3 each while
     # the grid stays <= 8192 waves; >= 8 pairs of a 1x1 each up to 16384 waves: its waves are short,
     # one or two batches of loads, so more of them in flight hide more of the latency)
