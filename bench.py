@@ -64,11 +64,12 @@ def parse():
                     help="MIOpen's default convolution algorithm choice instead of its measured search "
                          "(torch.backends.cudnn.benchmark, on by default: +2.4%% e2e at b = 1)")
     ap.add_argument("--conv-deterministic", action="store_true",
-                    help="only MIOpen's run-to-run deterministic solvers for the convolutions left on it "
-                         "(torch.backends.cudnn.deterministic; the DPT's MIOpen convolutions vary in the last bits "
-                         "otherwise, tools/determinism_probe.py). Free for C2 in bf16x3 mode (406.5 vs 407.0 "
-                         "views/s, profiles/r4/g36), but MIOpen's deterministic choices collapse exact-fp32 C2 "
-                         "(22.8 views/s) and the bf16-dense C3 variant (53.4): profiles/r4/final_det/")
+                    help="only MIOpen's run-to-run deterministic solvers (torch.backends.cudnn.deterministic). "
+                         "A no-op for the bf16x3 default since round 5: no convolution of that step reaches "
+                         "MIOpen (tests/test_conv.py::test_encoder_runs_no_library_convolution) and its outputs "
+                         "are bit-identical run to run (tools/determinism_probe.py). Other modes still route "
+                         "convolutions to MIOpen, whose deterministic choices collapse exact-fp32 C2 (22.8 "
+                         "views/s) and the bf16-dense C3 variant (53.4): profiles/r4/final_det/")
     return ap.parse_args()
 
 
