@@ -171,6 +171,14 @@ int tsplat_msda_fwd(const float* value, const float* loc, const float* weights, 
                     int32_t n, int32_t height, int32_t width, int32_t channels, int32_t queries,
                     int32_t points, void* stream);
 
+/* tsplat_msda_fwd from the raw projections of the UV self-attention (reference
+ * src/model/utils/attention.py:232-262 UVSelfAttention.forward after its two linears): ow [n][h w]
+ * rows of ow_stride floats holding the points' (dx, dy) sampling offsets then their attention
+ * logits; the query grid's reference points ((x + 0.5) / w, (y + 0.5) / h), loc = ref + off / (w,
+ * h) and the softmax over the points are computed in the kernel. out [n, h w, 128]. */
+int tsplat_msda_raw_fwd(const float* value, const float* ow, float* out, int32_t n, int32_t height, int32_t width,
+                        int32_t channels, int32_t points, int32_t ow_stride, void* stream);
+
 /* Multi-scale deformable attention with mmcv's ms_deform_attn_forward contract (replaces
  * ext_module.ms_deform_attn_forward called from the reference's
  * MultiScaleDeformableAttnFunction_fp32.forward, src/model/utils/multi_scale_deformable_attn_function.py:111-117,

@@ -204,6 +204,19 @@ def msda(value, loc, weights, h: int, w: int):
     return torch.stack(out)
 
 
+def msda_raw(value, ow, points: int, h: int, w: int):
+    """kernels.msda_raw restated with the reference's operations (attention.py:232-262: offsets /
+    (W, H) + the pixel-centre reference points, softmax over the points) and msda above."""
+    n, hw, _ = value.shape
+    off = ow[..., :2 * points].reshape(n, hw, points, 2)
+    logits = ow[..., 2 * points:3 * points]
+    ref_y, ref_x = torch.meshgrid(torch.linspace(0.5, h - 0.5, h, dtype=value.dtype),
+                                  torch.linspace(0.5, w - 0.5, w, dtype=value.dtype), indexing="ij")
+    ref = torch.stack((ref_x.reshape(-1) / w, ref_y.reshape(-1) / h), -1)[None].to(value.device)
+    loc = ref[:, :, None, :] + off / torch.tensor([w, h], dtype=value.dtype, device=value.device)
+    return msda(value, loc, logits.softmax(-1), h, w)
+
+
 def resize_bilinear_nchw(x, size):
     """F.interpolate(x, size, mode="bilinear", align_corners=True) on NCHW maps (the PyTorch calls
     at the reference's encoder_trans.py / depth_predictor_trans.py resizes), on the CPU."""
@@ -474,7 +487,7 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     return fused_linear(msg, merge_weight, ln=ln, residual=residual)
 
 
-KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "ms_deform_attn", "gaussian_adapter", "group_norm",
+KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "msda_raw", "ms_deform_attn", "gaussian_adapter", "group_norm",
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
                        "conv_bias_act", "mha", "residual_ln", "depth_softmax", "conv2d_direct_ok",
                        "conv2d_direct", "conv2d_nhwc_ok", "conv2d_nhwc",

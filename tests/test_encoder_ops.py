@@ -160,6 +160,37 @@ def test_msda_kernel(device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("hw", [(16, 16), (12, 20)])
+def test_msda_raw_kernel(device, hw):
+    """tsplat_msda_raw_fwd (reference points, offset scaling and the softmax over the points in the
+    kernel) against the reference's operations restated (oracle.msda_raw), incl. samples pushed off
+    the map and a non-square grid; and UVSelfAttention.core_raw against core() on the same module."""
+    from transplat_amd import kernels as K
+    from transplat_amd.model.utils.uv_transformer import UVSelfAttention
+
+    h, w = hw
+    value = seeded((2, h * w, 128), 54)
+    ow = torch.zeros((2, h * w, 128))
+    ow[..., :8] = seeded((2, h * w, 8), 55) * 3.0
+    ow[..., 8:12] = seeded((2, h * w, 4), 56)
+    ref = E.msda_raw(value, ow, 4, h, w)
+    out = K.msda_raw(value.to(device), ow.to(device), 4, h, w).cpu()
+    assert (out - ref).abs().max().item() < 1e-5
+    torch.manual_seed(0)
+    sa = UVSelfAttention(embed_dims=128).to(device).eval()
+    q, pos = seeded((2, h * w, 128), 57).to(device), seeded((2, h * w, 128), 58).to(device)
+    from transplat_amd.model.utils.uv_transformer import UVTransformerEncoder
+
+    ref2d = UVTransformerEncoder.reference_points_2d(h, w, 2, torch.float32, device)
+    with torch.no_grad():
+        a = sa.core(q, q, pos, ref2d, h, w)
+        b = sa.core_raw(q, q, pos, h, w)
+    err = (a - b).abs().max().item() / a.abs().max().item()
+    print(f"msda raw vs module chain: {err:.2e}")
+    assert err < 1e-5
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("shape,size", [((6, 3, 256, 256), (252, 252)), ((2, 64, 18, 18), (64, 64)),
                                         ((16, 1, 252, 252), (256, 256)), ((3, 5, 7, 9), (13, 4)),
                                         ((2, 2, 1, 1), (3, 5)), ((2, 4, 64, 64), (256, 256))])

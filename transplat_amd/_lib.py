@@ -50,6 +50,7 @@ SIGNATURES = {
     "tsplat_uv_cross_fwd": (ctypes.c_int, [_P] * 7 + [_I32] * 6 + [_P]),
     "tsplat_uv_cross_table_fwd": (ctypes.c_int, [_P] * 6 + [_I32] * 6 + [_P]),
     "tsplat_msda_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 6 + [_P]),
+    "tsplat_msda_raw_fwd": (ctypes.c_int, [_P, _P, _P] + [_I32] * 6 + [_P]),
     "tsplat_ms_deform_attn_fwd": (ctypes.c_int, [_P] * 6 + [_I32] * 8 + [_P]),
     "tsplat_win_attn_workspace_bytes": (ctypes.c_size_t, [_I32] * 5),
     "tsplat_win_attn_fwd": (ctypes.c_int, [_P] * 5 + [_I32] * 7 + [_P]),

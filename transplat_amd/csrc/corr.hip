@@ -487,6 +487,42 @@ msda_kernel(Geo g, int Q, int P, const float* __restrict__ value, const float* _
     o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
 }
 
+// ---- the same sampling from the raw projections (the UV self-attention's glue folded in,
+// reference attention.py:232-262): per query q = y W + x, ow[n][q] holds the P (dx, dy) sampling
+// offsets then the P attention logits (one linear's output, row stride `ows`); loc_pt = ref + off /
+// (W, H) with ref = ((x + 0.5) / W, (y + 0.5) / H) (the reference points, encoder.py:61-71, same fp32
+// operations), weights = softmax(logits) -- instead of the softmax, division and addition launches
+// around msda_kernel.
+__global__ void __launch_bounds__(kThreads)
+msda_raw_kernel(Geo g, int Q, int P, const float* __restrict__ value, const float* __restrict__ ow, int ows,
+                float* __restrict__ out) {
+    const int n = blockIdx.y;
+    const int q = blockIdx.x * kGroups + (threadIdx.x >> 4);
+    const int gl = threadIdx.x & 15, c0 = gl * 8;
+    if (q >= Q) return;
+    const size_t HW = (size_t)g.H * g.W;
+    const float* img = value + (size_t)n * HW * kC;
+    const float* r = ow + ((size_t)n * Q + q) * ows;
+    const float fw = (float)g.W, fh = (float)g.H;
+    const int qy = q / g.W, qx = q - qy * g.W;
+    const float rx = ((float)qx + 0.5f) / fw, ry = ((float)qy + 0.5f) / fh;
+    float m = -INFINITY;
+    for (int pt = 0; pt < P; ++pt) m = fmaxf(m, r[2 * P + pt]);
+    float sum = 0.f;
+    for (int pt = 0; pt < P; ++pt) sum += expf(r[2 * P + pt] - m);
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    for (int pt = 0; pt < P; ++pt) {
+        const float wt = expf(r[2 * P + pt] - m) / sum;
+        const float lx = rx + r[2 * pt] / fw, ly = ry + r[2 * pt + 1] / fh;
+        bilinear_acc8(img, g, lx * fw - 0.5f, ly * fh - 0.5f, wt, c0, acc);
+    }
+    float4* o = reinterpret_cast<float4*>(out + ((size_t)n * Q + q) * kC + c0);
+    o[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    o[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+}
+
 // ---- mmcv ms_deform_attn_forward, general form: value [bs][num_keys][heads][hd] (level l's
 // H_l x W_l map starts at key level_start[l]), sampling_loc [bs][nq][heads][L][P][2] (x, y in
 // [0, 1]), attn_weight [bs][nq][heads][L][P] -> out [bs][nq][heads * hd]. One thread per (query,
@@ -680,6 +716,23 @@ extern "C" int tsplat_msda_fwd(const float* value, const float* loc, const float
     TSPLAT_PROF_BEGIN(prof::kMsda, stream);
     hipLaunchKernelGGL(msda_kernel, dim3(ceil_div(queries, kGroups), n), dim3(kThreads), 0, stream, g,
                        queries, points, value, loc, weights, out);
+    TSPLAT_PROF_END(prof::kMsda, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_msda_raw_fwd(const float* value, const float* ow, float* out, int32_t n, int32_t height,
+                                   int32_t width, int32_t channels, int32_t points, int32_t ow_stride, void* stream_) {
+    using namespace tsplat::corr;
+    if (!value || !ow || !out || channels != kC || n <= 0 || height <= 0 || width <= 0 || points <= 0 ||
+        ow_stride < 3 * points)
+        return TSPLAT_EINVAL;
+    Geo g{1, height, width, 1};
+    const int queries = height * width;
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(prof::kMsda, stream);
+    hipLaunchKernelGGL(msda_raw_kernel, dim3(ceil_div(queries, kGroups), n), dim3(kThreads), 0, stream, g, queries,
+                       points, value, ow, ow_stride, out);
     TSPLAT_PROF_END(prof::kMsda, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

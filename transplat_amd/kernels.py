@@ -188,6 +188,22 @@ def msda(value, loc, weights, h: int, w: int):
     return out
 
 
+def msda_raw(value, ow, points: int, h: int, w: int):
+    """msda(value, ref_2d + off / (w, h), softmax(logits), h, w) from the raw [N, h w, >= 3 points]
+    rows ow = [offsets (dx, dy) x points | logits x points | ...] (tsplat_msda_raw_fwd; see
+    oracle.msda_raw). value [N, h w, 128] -> [N, h w, 128]."""
+    lib = _lib.load()
+    n, hw, c = value.shape
+    value, ow = _f32(value), _f32(ow)
+    if ow.shape[:2] != (n, hw) or ow.shape[-1] < 3 * points or not ow.is_contiguous():
+        raise ValueError(f"ow {tuple(ow.shape)} does not match value {tuple(value.shape)} / {points} points")
+    out = torch.empty((n, hw, c), dtype=torch.float32, device=value.device)
+    rc = lib.tsplat_msda_raw_fwd(_lib.ptr(value), _lib.ptr(ow), _lib.ptr(out), n, h, w, c, points, ow.shape[-1],
+                                 _lib.stream_ptr(value.device))
+    _lib.check(rc, "tsplat_msda_raw_fwd")
+    return out
+
+
 def adapter_cameras(extrinsics: torch.Tensor, intrinsics: torch.Tensor, image_shape) -> torch.Tensor:
     """[N, 22] per-camera constants of tsplat_gaussian_adapter_fwd: c2w R, c2w t, K^-1 of the
     normalised intrinsics, and the scale multiplier of GaussianAdapter.get_scale_multiplier

@@ -15,6 +15,8 @@ Differences by design (MI355X):
 """
 from __future__ import annotations
 
+import os
+
 import math
 
 import torch
@@ -25,6 +27,11 @@ from ... import kernels
 
 _REF2D: dict = {}  # (h, w, dtype, device) -> [1, h*w, 2] reference points
 _WH: dict = {}     # (w, h, dtype, device) -> tensor([w, h])
+
+
+# the self-attention's projections + sampling glue as two launches (UVSelfAttention.core_raw);
+# TSPLAT_MSDA_RAW=0: the module chain (A/B knob)
+_MSDA_RAW = os.environ.get("TSPLAT_MSDA_RAW", "1") == "1"
 
 
 class UVSelfAttention(nn.Module):
@@ -63,6 +70,39 @@ class UVSelfAttention(nn.Module):
             wh = _WH[key] = torch.tensor([bev_w, bev_h], dtype=offsets.dtype, device=offsets.device)
         loc = ref_2d[:, :, None, :] + offsets / wh
         return kernels.msda(value, loc, weights, bev_h, bev_w)
+
+    def _proj_weights(self):
+        """sampling_offsets and attention_weights as ONE [128, 2 C] linear on [query | query_pos]
+        ((q + p) W^T = [q | p] [W | W]^T; rows 0-7 offsets, 8-11 logits, zero past them: the fused
+        linear kernel's 128-wide output block), cached per parameter version."""
+        so, aw = self.sampling_offsets, self.attention_weights
+        key = tuple((t.data_ptr(), t._version) for t in (so.weight, so.bias, aw.weight, aw.bias))
+        hit = self.__dict__.get("_pw")
+        if hit is None or hit[0] != key:
+            with torch.no_grad():
+                w = torch.cat((so.weight, aw.weight), 0)
+                b = torch.cat((so.bias, aw.bias), 0)
+                wp = torch.zeros((128, 2 * w.shape[1]), dtype=torch.float32, device=w.device)
+                wp[:w.shape[0], :w.shape[1]] = w
+                wp[:w.shape[0], w.shape[1]:] = w
+                bp = torch.zeros(128, dtype=torch.float32, device=w.device)
+                bp[:b.shape[0]] = b
+            hit = (key, wp, bp)
+            self.__dict__["_pw"] = hit
+        return hit[1], hit[2]
+
+    def core_raw(self, query, value, query_pos, bev_h: int, bev_w: int):
+        """core() with the position add and both projections as one fused linear launch and the
+        softmax / offset scaling / reference points inside the sampling kernel (kernels.msda_raw):
+        two launches instead of six. Needs the fp32 kernel path and query_pos."""
+        wp, bp = self._proj_weights()
+        ow = kernels.fused_linear(query, wp, x2=query_pos, bias=bp)
+        value = self.value_proj(value)
+        return kernels.msda_raw(value, ow.view(query.shape[0], query.shape[1], 128), self.num_points, bev_h, bev_w)
+
+    def raw_ok(self, query, query_pos) -> bool:
+        return (_MSDA_RAW and query_pos is not None and query.is_cuda and self.embed_dims <= 128
+                and 3 * self.num_points <= 128 and query.dtype == torch.float32)
 
     def forward(self, query, value, query_pos, ref_2d, bev_h: int, bev_w: int):
         out = self.core(query, value, query_pos, ref_2d, bev_h, bev_w)
@@ -193,7 +233,10 @@ class UVTransformerEncoderLayer(nn.Module):
         K = kernels
         sa, ca, ffn = self.attentions[0], self.attentions[1], self.ffns[0]
         ln = lambda m: (m.weight, m.bias, m.eps)
-        out = sa.core(query, query, bev_pos, ref_2d, bev_h, bev_w)
+        if sa.raw_ok(query, bev_pos):
+            out = sa.core_raw(query, query, bev_pos, bev_h, bev_w)
+        else:
+            out = sa.core(query, query, bev_pos, ref_2d, bev_h, bev_w)
         query = K.fused_linear(out, sa.output_proj.weight, bias=sa.output_proj.bias, ln=ln(self.norms[0]),
                                residual=query, res_pre_ln=True)
         out = ca.core(query, key_cl, key_cl, cameras, bev_h, bev_w)
