@@ -119,6 +119,13 @@ int tsplat_raster_fwd(const tsplat_raster_desc* desc,
 int tsplat_depth_softmax_fwd(const float* logits, const float* disp, float* coarse, float* pdf_max, int32_t n,
                              int32_t depths, int32_t hw, void* stream);
 
+/* Depth head tail (reference src/model/encoder/matching/depth_predictor_trans.py:480-491): fullres
+ * [v b][h w] refined disparity, head [v b][2][h w] (the to_disparity output: delta, raw density), near
+ * / far [b][v] -> depth [b][v][h w] = 1 / clamp(fullres + delta, 1 / far, 1 / near), density
+ * [b][v][h w] = sigmoid(raw). */
+int tsplat_depth_tail_fwd(const float* fullres, const float* head, const float* near, const float* far, float* depth,
+                          float* density, int32_t batch, int32_t views, int32_t hw, void* stream);
+
 /* Per-view camera constants of render_cuda (reference cuda_splatting.py:56-96 with get_fov and
  * get_projection_matrix) from extrinsics [V, 4, 4] (c2w), normalised intrinsics [V, 3, 3], near
  * and far [V], bg [V, 3] (bg_per_view) or [3]: writes the viewmat / projmat / campos / tanfov / bg

@@ -217,6 +217,19 @@ def msda_raw(value, ow, points: int, h: int, w: int):
     return msda(value, loc, logits.softmax(-1), h, w)
 
 
+def depth_tail(fullres, head, near, far):
+    """kernels.depth_tail restated with the reference's operations (depth_predictor_trans.py:480-491)."""
+    from einops import rearrange
+
+    b, v = near.shape
+    delta, raw = head.split(1, dim=1)
+    fine = (fullres + delta).clamp(1.0 / rearrange(far, "b v -> (v b) () () ()"),
+                                   1.0 / rearrange(near, "b v -> (v b) () () ()"))
+    depth = rearrange(1.0 / fine, "(v b) () h w -> b v (h w)", b=b, v=v)
+    dens = rearrange(torch.sigmoid(raw), "(v b) () h w -> b v (h w)", b=b, v=v)
+    return depth.contiguous(), dens.contiguous()
+
+
 def resize_bilinear_nchw(x, size):
     """F.interpolate(x, size, mode="bilinear", align_corners=True) on NCHW maps (the PyTorch calls
     at the reference's encoder_trans.py / depth_predictor_trans.py resizes), on the CPU."""
@@ -489,7 +502,7 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
 
 KERNEL_RESTATEMENTS = ("window_attention", "uv_coarse", "uv_cross", "msda", "msda_raw", "ms_deform_attn", "gaussian_adapter", "group_norm",
                        "sh_rotation", "fused_linear", "attention_merge", "instance_norm",
-                       "conv_bias_act", "mha", "residual_ln", "depth_softmax", "conv2d_direct_ok",
+                       "conv_bias_act", "mha", "residual_ln", "depth_softmax", "depth_tail", "conv2d_direct_ok",
                        "conv2d_direct", "conv2d_nhwc_ok", "conv2d_nhwc",
                        "upsample_bilinear_act", "qkv_attention_cf",
                        "conv_nhwc_epilogue", "resize_bilinear_nhwc")

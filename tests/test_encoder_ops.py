@@ -160,6 +160,25 @@ def test_msda_kernel(device):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("b,v", [(1, 2), (2, 3)])
+def test_depth_tail_kernel(device, b, v):
+    """tsplat_depth_tail_fwd (1 / clamp(fullres + delta, 1 / far, 1 / near) and sigmoid, written in
+    the (b v) layout) against the reference's operations (oracle.depth_tail), incl. values clamped
+    at both ends and the (v b) -> (b v) reorder at b > 1."""
+    from transplat_amd import kernels as K
+
+    h, w = 12, 20
+    fullres = seeded((v * b, 1, h, w), 61, kind="rand") * 0.5 + 0.02
+    head = seeded((v * b, 2, h, w), 62) * 0.3
+    near = seeded((b, v), 63, kind="rand") + 0.5
+    far = near + seeded((b, v), 64, kind="rand") * 50 + 5
+    rd, rn = E.depth_tail(fullres, head, near, far)
+    od, on = (t.cpu() for t in K.depth_tail(fullres.to(device), head.to(device), near.to(device), far.to(device)))
+    assert ((rd - od).abs() / rd.abs()).max().item() < 1e-6
+    assert (rn - on).abs().max().item() < 1e-6
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("hw", [(16, 16), (12, 20)])
 def test_msda_raw_kernel(device, hw):
     """tsplat_msda_raw_fwd (reference points, offset scaling and the softmax over the points in the

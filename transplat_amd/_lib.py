@@ -65,6 +65,7 @@ SIGNATURES = {
     "tsplat_gaussian_adapter_fwd": (ctypes.c_int, [_P] * 9 + [_I32] * 6 + [ctypes.c_float] * 3 + [_I32, _I32, _P]),
     "tsplat_win_attn_split": (_I32, [_I32] * 5),
     "tsplat_depth_softmax_fwd": (ctypes.c_int, [_P] * 4 + [_I32] * 3 + [_P]),
+    "tsplat_depth_tail_fwd": (ctypes.c_int, [_P] * 6 + [_I32] * 3 + [_P]),
     "tsplat_raster_cameras": (ctypes.c_int, [_P] * 5 + [_I32] * 3 + [_P] * 7),
     "tsplat_small_inverse": (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
     "tsplat_mha_f32_fwd": (ctypes.c_int, [_P, _P, _I32, _I32, _I32, _I32, ctypes.c_float, _P]),

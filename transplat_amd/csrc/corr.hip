@@ -813,3 +813,43 @@ extern "C" int tsplat_depth_softmax_fwd(const float* logits, const float* disp, 
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Depth head tail (reference depth_predictor_trans.py:480-491): from the refined full-resolution
+// disparity and the to_disparity head's two channels (delta, raw density) of map (v b) index m,
+//   depth   = 1 / clamp(fullres + delta, 1 / far, 1 / near)      (the reference's fp32 operations)
+//   density = sigmoid(raw)
+// written straight into the [b, v, h w] layouts the Gaussian adapter reads -- one launch for what
+// was nine elementwise ones (sigmoid, add, reciprocals, clamp, the (v b) -> (b v) repeats).
+namespace tsplat {
+namespace corr {
+__global__ void __launch_bounds__(256) depth_tail_kernel(const float* __restrict__ fullres, const float* __restrict__ head,
+                                                         const float* __restrict__ near, const float* __restrict__ far,
+                                                         float* __restrict__ depth, float* __restrict__ density, int b,
+                                                         int v, int hw) {
+    const int m = blockIdx.y;  // (v b) map index
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= hw) return;
+    const int vi = m / b, bi = m - vi * b;
+    const int bv = bi * v + vi;  // near / far are [b, v]
+    const float lo = 1.0f / far[bv], hi = 1.0f / near[bv];
+    const float d = fullres[(size_t)m * hw + p] + head[((size_t)m * 2) * hw + p];
+    const float c = fminf(fmaxf(d, lo), hi);
+    const float raw = head[((size_t)m * 2 + 1) * hw + p];
+    depth[(size_t)bv * hw + p] = 1.0f / c;
+    density[(size_t)bv * hw + p] = 1.0f / (1.0f + expf(-raw));
+}
+}  // namespace corr
+}  // namespace tsplat
+
+extern "C" int tsplat_depth_tail_fwd(const float* fullres, const float* head, const float* near, const float* far,
+                                     float* depth, float* density, int32_t batch, int32_t views, int32_t hw,
+                                     void* stream_) {
+    using namespace tsplat::corr;
+    if (!fullres || !head || !near || !far || !depth || !density || batch <= 0 || views <= 0 || hw <= 0)
+        return TSPLAT_EINVAL;
+    hipLaunchKernelGGL(depth_tail_kernel, dim3((hw + 255) / 256, batch * views), dim3(256), 0, (hipStream_t)stream_,
+                       fullres, head, near, far, depth, density, batch, views, hw);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

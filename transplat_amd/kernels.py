@@ -580,6 +580,22 @@ def depth_softmax(logits, disp):
     return coarse, pmax
 
 
+def depth_tail(fullres, head, near, far):
+    """(depths, densities) of the depth head tail: fullres [(v b), 1, h, w], head [(v b), 2, h, w]
+    (delta, raw density), near / far [b, v] -> two [b, v, h w] maps (tsplat_depth_tail_fwd; see
+    oracle.depth_tail)."""
+    lib = _lib.load()
+    b, v = near.shape
+    hw = fullres.shape[-2] * fullres.shape[-1]
+    fr, hd, nr, fa = _f32(fullres), _f32(head), _f32(near), _f32(far)
+    depth = torch.empty((b, v, hw), dtype=torch.float32, device=fullres.device)
+    dens = torch.empty_like(depth)
+    _lib.check(lib.tsplat_depth_tail_fwd(_lib.ptr(fr), _lib.ptr(hd), _lib.ptr(nr), _lib.ptr(fa), _lib.ptr(depth),
+                                         _lib.ptr(dens), b, v, hw, _lib.stream_ptr(fullres.device)),
+               "tsplat_depth_tail_fwd")
+    return depth, dens
+
+
 def mha(qkv, heads: int, scale: float, bias=None):
     """Multi-head self-attention from the qkv projection output [B, N, 3 * heads * 64] ->
     [B, N, heads * 64] (tsplat_mha_f32_fwd; no permute copies). bias: the projection's bias when

@@ -290,11 +290,17 @@ class DepthPredictorTrans(nn.Module):
             raw_gaussians = _conv_gelu_conv(self.to_gaussians, refine_out,
                                             extra=(extra_info["images"], proj_feat_in_fullres))
             raw_gaussians = rearrange(raw_gaussians, "(v b) c h w -> b v (h w) c", v=v, b=b)
-            delta_disps, raw_densities = _conv_gelu_conv(self.to_disparity, refine_out).split(gaussians_per_pixel, dim=1)
-            densities = repeat(F.sigmoid(raw_densities), "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
-            fine_disps = (fullres_disps + delta_disps).clamp(1.0 / rearrange(far, "b v -> (v b) () () ()"),
-                                                             1.0 / rearrange(near, "b v -> (v b) () () ()"))
-            depths = repeat(1.0 / fine_disps, "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
+            head = _conv_gelu_conv(self.to_disparity, refine_out)
+            if gaussians_per_pixel == 1:  # the tail below as one kernel, written in the (b v) layouts
+                depths, densities = kernels.depth_tail(fullres_disps, head, near, far)
+                depths = depths.view(b, v, -1, 1, 1)
+                densities = densities.view(b, v, -1, 1, 1)
+            else:
+                delta_disps, raw_densities = head.split(gaussians_per_pixel, dim=1)
+                densities = repeat(F.sigmoid(raw_densities), "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
+                fine_disps = (fullres_disps + delta_disps).clamp(1.0 / rearrange(far, "b v -> (v b) () () ()"),
+                                                                 1.0 / rearrange(near, "b v -> (v b) () () ()"))
+                depths = repeat(1.0 / fine_disps, "(v b) dpt h w -> b v (h w) srf dpt", b=b, v=v, srf=1)
         return depths, densities, raw_gaussians
 
     def _match(self, v, intr_curr, pose_curr_lists, extrinsics, disp_candi_curr, dino_feature, features, feat01,
