@@ -227,6 +227,14 @@ int tsplat_group_norm_fwd(const float* x, const float* pre_bias, const float* ga
                           const float* residual,
                           float* y, void* workspace, int32_t n, int32_t c, int64_t hw, int32_t groups,
                           float eps, int32_t act, void* stream);
+/* The same with the residual given as the channel concatenation [residual | residual2] read in
+ * place (the U-Net output blocks' identity skip over cat([h, skip]), reference unet.py:177-300):
+ * channels [0, c1) from residual [n, c1, hw], channels [c1, c) from residual2 [n, c - c1, hw];
+ * 0 < c1 < c. */
+int tsplat_group_norm_cat_res_fwd(const float* x, const float* pre_bias, const float* gamma, const float* beta,
+                                  const float* residual, const float* residual2, int32_t c1, float* y,
+                                  void* workspace, int32_t n, int32_t c, int64_t hw, int32_t groups, float eps,
+                                  int32_t act, void* stream);
 /* The same with bf16 x / residual / y (fp32 statistics, gamma, beta, pre_bias): the bf16
  * dense-layer mode (config C3), where the surrounding convolutions read and write bf16 -- the
  * reference's GroupNorm32 likewise normalises x.float() and casts back to x's dtype
@@ -352,6 +360,13 @@ size_t tsplat_win_attn_bf16_workspace_bytes(int32_t batch, int32_t height, int32
 int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void* v, void* out, void* workspace,
                              int32_t batch, int32_t height, int32_t width, int32_t channels,
                              int32_t key_views, int32_t splits, int32_t with_shift, void* stream);
+/* The same with query batch b reading the keys / values of batch (b + key_batch_shift) % batch, the
+ * two-view cross pairing (reference batch_features, multiview_transformer.py:495-515) as index
+ * arithmetic instead of a rolled copy; 0 <= key_batch_shift < batch. */
+int tsplat_win_attn_bf16_shift_fwd(const void* q, const void* k, const void* v, void* out, void* workspace,
+                                   int32_t batch, int32_t height, int32_t width, int32_t channels,
+                                   int32_t key_views, int32_t splits, int32_t with_shift,
+                                   int32_t key_batch_shift, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Fused linear of the multi-view transformer (exact fp32 MFMA), replacing the nn.Linear +
@@ -367,7 +382,9 @@ int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void* v, void* 
  *   64 with 4: the residual is added BEFORE the LayerNorm (post-norm layers: LN(x W^T + b + r));
  *   256 bf16x3 products: x and w split as hi + lo bf16 while staged, hi*hi + hi*lo + lo*hi on
  *   v_mfma_f32_32x32x16_bf16 with fp32 accumulation (<= 3 * 2^-18 relative per product, the
- *   stand-in for the reference's TF32, src/main.py:15); default exact fp32.
+ *   stand-in for the reference's TF32, src/main.py:15); default exact fp32;
+ *   512 x1 is bf16 [M, k1] (pass it as x1; k2 must be 0), widened exactly while staged;
+ *   1024 out is bf16 (rounded to nearest even; split_stride then counts bf16 elements; not with 4).
  *   Epilogues applied in that order.
  * ---------------------------------------------------------------------------------------- */
 int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x2, int32_t k2, const float* w,

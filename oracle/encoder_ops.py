@@ -49,14 +49,17 @@ def _region_ids(h: int, w: int, splits: int) -> torch.Tensor:
     return torch.stack(ids)
 
 
-def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool):
+def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, kv_shift: int = 0):
     """softmax(Q K^T / sqrt(C) + mask) V over split windows (reference
-    single_head_split_window_attention, multiview_transformer.py:57-206).
+    single_head_split_window_attention, multiview_transformer.py:57-206); kv_shift pairs query batch
+    i with key batch (i + kv_shift) % B (batch_features' view swap, :495-515).
 
     q [B, L, C]; k, v [B, L, C] (two views) or [B, m, L, C] (m = V - 1 key views).
     Multi-view keys are ordered pixel-major / view-minor within a window and the shift mask is
     tiled view-major (`attn_mask.repeat(b, 1, m)`, :130), so key j takes mask column j mod L.
     """
+    if kv_shift:
+        k, v = torch.roll(k, -kv_shift, dims=0), torch.roll(v, -kv_shift, dims=0)
     q = q.float()
     b, _, c = q.shape
     if k.dim() == 3:
@@ -314,7 +317,10 @@ def gaussian_adapter(raw, depths, densities, extrinsics, intrinsics, image_shape
 def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None, pre_bias=None):
     """torch.nn.GroupNorm followed by the module chain's activation and residual add (reference
     ldm_unet/unet.py:177-300 ResBlock: skip + SiLU(GN(conv)); :306-370 AttentionBlock:
-    x + GN(proj); depth_predictor_trans.py:142-206: GN -> GELU)."""
+    x + GN(proj); depth_predictor_trans.py:142-206: GN -> GELU). A residual pair (r1, r2) is the
+    channel concatenation torch.cat([r1, r2], 1) (the output blocks' identity skip)."""
+    if isinstance(residual, (tuple, list)):
+        residual = torch.cat([residual[0], residual[1]], dim=1)
     x = x.float()
     if pre_bias is not None:  # the producing convolution's bias (reference: conv2d with bias)
         x = x + pre_bias.float().view(1, -1, *([1] * (x.dim() - 2)))
@@ -466,10 +472,12 @@ def sh_rotation(rotations, d_sh: int):
 
 # kernels.<name> -> oracle.<name>: what a CPU run of the module glue swaps in (tests, bench cpu leg)
 def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, residual=None, split: bool = False,
-                 gelu_in: bool = False, relu_in: bool = False, res_pre_ln: bool = False):
+                 gelu_in: bool = False, relu_in: bool = False, res_pre_ln: bool = False, out_dtype=torch.float32):
     """CPU restatement of kernels.fused_linear: the reference TransformerLayer's chain
     (multiview_transformer.py:327-407) torch.cat -> nn.Linear -> nn.GELU -> nn.LayerNorm -> + x, and
-    the UV encoder layers' post-norm form LN(Linear(x) + identity) (utils/encoder.py:131-209)."""
+    the UV encoder layers' post-norm form LN(Linear(x) + identity) (utils/encoder.py:131-209); a bf16
+    x1 is widened, out_dtype rounds the result (the bf16 attention's operands under autocast)."""
+    x1 = x1.float()
     x = torch.cat([x1, x2], dim=-1) if x2 is not None else x1
     if gelu_in:
         x = torch.nn.functional.gelu(x)
@@ -484,6 +492,7 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
         y = torch.nn.functional.layer_norm(y, (y.shape[-1],), ln[0], ln[1], ln[2])
     if residual is not None and not res_pre_ln:
         y = residual + y
+    y = y.to(out_dtype)
     if split:
         return [t.contiguous() for t in y.split(128, dim=-1)]
     return y

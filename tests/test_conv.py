@@ -133,15 +133,17 @@ def test_conv_transpose_direct(device, n, ci, co, h, w, s):
 
 
 @pytest.mark.gpu
-def test_conv_unfold_gemm_stem(device):
-    """The UniMatch CNN's 7x7 stride-2 stem on 3 channels as im2col + one exact-fp32 GEMM, vs
-    float64, and through the installed Conv2d dispatch."""
+@pytest.mark.parametrize("bias", [False, True])
+def test_conv_unfold_gemm_stem(device, bias):
+    """The UniMatch CNN's 7x7 stride-2 stem on 3 channels as im2col + one exact-fp32 GEMM per image
+    (bias in the GEMM), vs float64, and through the installed Conv2d dispatch."""
     from transplat_amd import kernels as K
 
     x = seeded((2, 3, 256, 256), 74)
     wt = seeded((64, 3, 7, 7), 75) / 147 ** 0.5
-    ref = torch.nn.functional.conv2d(x.double(), wt.double(), None, stride=2, padding=3)
-    out = K.conv_unfold_gemm(x.to(device), wt.to(device), None, 2, 3).cpu().double()
+    b = seeded((64,), 76) if bias else None
+    ref = torch.nn.functional.conv2d(x.double(), wt.double(), b.double() if bias else None, stride=2, padding=3)
+    out = K.conv_unfold_gemm(x.to(device), wt.to(device), b.to(device) if bias else None, 2, 3).cpu().double()
     assert (out - ref).abs().max().item() / ref.abs().max().item() < 2e-6
     m = torch.nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(device)
     K.install_conv2d_dispatch(m)
@@ -340,7 +342,7 @@ def tf32_round(t: torch.Tensor) -> torch.Tensor:
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("stage", ["auto", "0"])
-@pytest.mark.parametrize("form", ["auto", "1", "2", "3", "4", "5"])
+@pytest.mark.parametrize("form", ["auto", "1", "2", "3", "4", "5", "6"])
 @pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES + [(1, 24, 48, 10, 96, True, "relu"),
                                                                (2, 40, 64, 22, 136, False, "none"),
                                                                (3, 32, 40, 36, 64, True, "gelu"),
@@ -350,7 +352,8 @@ def test_conv3x3_wino_bf16x3_kernel(device, monkeypatch, stage, form, n, ci, co,
     lo*hi on bf16 MFMA, fp32 accumulation) against torch's conv2d in float64, with the launch's own
     workgroup form and each form forced (TSPLAT_WINO3_FORM: 32 co x 32 tiles, the same with two
     k-groups, 32 x 64, 64 x 64, the persistent 32 x 32 form walking several tile blocks per workgroup
-    across images -- staged maps only, else form 1), with the staged input (coalesced region loads through LDS, maps
+    across images -- staged maps only, else form 1 --, 64 x 32 with half the waves transforming), with
+    the staged input (coalesced region loads through LDS, maps
     whose width is a multiple of 4: tile blocks 32 / 16 / 8 wide) and without it
     (TSPLAT_WINO3_STAGE=0). Bounds (written here): the same 2e-5 of max |y| as the exact-fp32
     kernel, and at most 1/8 of the error of the reference's own precision -- TF32 operands

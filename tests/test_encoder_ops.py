@@ -537,6 +537,80 @@ def test_window_attention_bf16_growing_scores(device, monkeypatch, kern, shift, 
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape,groups,c1", [((16, 256, 32, 32), 8, 128), ((2, 64, 64, 64), 8, 24),
+                                             ((2, 96, 16, 16), 4, 64), ((3, 40, 9, 7), 4, 30),
+                                             ((2, 128, 128, 128), 8, 64)])
+@pytest.mark.parametrize("act", ["silu", "none"])
+def test_group_norm_cat_residual(device, shape, groups, c1, act):
+    """tsplat_group_norm_cat_res_fwd: the residual as a channel concatenation [r1 | r2] read in place
+    (the U-Net output blocks' identity skip), bit-identical to the residual materialised by torch.cat;
+    both the single-launch (small groups) and the stats + apply forms, vector and scalar (odd HW)."""
+    from transplat_amd import kernels as K
+
+    n, c = shape[:2]
+    x = (seeded(shape, 76) * 2 + 0.5).to(device)
+    w = (seeded((c,), 77) * 0.5 + 1).to(device)
+    b = (seeded((c,), 78) * 0.2).to(device)
+    pb = (seeded((c,), 79) * 0.1).to(device)
+    r1 = seeded((n, c1) + shape[2:], 80).to(device)
+    r2 = seeded((n, c - c1) + shape[2:], 81).to(device)
+    ref = K.group_norm(x, groups, w, b, 1e-5, act, torch.cat([r1, r2], 1), pb)
+    out = K.group_norm(x, groups, w, b, 1e-5, act, (r1, r2), pb)
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kern", ["auto", "v2", "v3"])
+@pytest.mark.parametrize("b,kvs,m", [(2, 1, 1), (8, 4, 1), (4, 3, 1), (3, 2, 2)])
+def test_window_attention_bf16_kv_shift(device, monkeypatch, kern, b, kvs, m):
+    """tsplat_win_attn_bf16_shift_fwd (query batch i reads the keys / values of batch (i + s) % B,
+    forward_pair's cross pairing in C3) == the bf16 kernel on rolled copies of k / v: bit for bit
+    on the 8-wave v3 kernel (C3's b = 8 launch); the 4-wave v2 kernel is not repeatable run to run
+    by itself (its running-max handoff between waves is timing-dependent: up to 2e-3 on ~1.5 % of
+    the O(1) outputs between two identical calls, measured on MI355X), so it is held to 4e-3 there."""
+    from transplat_amd import kernels as K
+
+    if kern != "auto":
+        monkeypatch.setenv("TSPLAT_WINATTN_BF16", kern)
+    hw = 64
+    q = seeded((b, hw * hw, 128), 97).bfloat16().to(device)
+    k = (seeded((b, m, hw * hw, 128), 98) if m > 1 else seeded((b, hw * hw, 128), 98)).bfloat16().to(device)
+    v = seeded(k.shape, 99).bfloat16().to(device)
+    a = K.window_attention(q, k, v, hw, hw, 2, True, kv_shift=kvs)
+    ref = K.window_attention(q, torch.roll(k, -kvs, dims=0), torch.roll(v, -kvs, dims=0), hw, hw, 2, True)
+    v3 = kern == "v3" or (kern == "auto" and b * 4 * (hw * hw // 4 // 256) >= 256)
+    if v3:
+        assert torch.equal(a, ref)
+    else:
+        assert (a.float() - ref.float()).abs().max().item() <= 4e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dense", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("m,n,split,ln", [(8192, 384, True, False), (1000, 128, False, True), (65536, 256, True, False)])
+def test_fused_linear_bf16_io(device, dense, m, n, split, ln):
+    """fused_linear's bf16 operand / output flags (512, 1024): a bf16 x1 gives exactly the result of
+    its fp32 widening, and a bf16 output is exactly the fp32 output rounded to bf16 (the C3 layer's
+    q / k / v projections and bf16 message without cast launches)."""
+    from transplat_amd import kernels as K
+
+    xb = seeded((m, 128), 38).bfloat16().to(device)
+    w = (seeded((n, 128), 39) / math.sqrt(128)).to(device)
+    lnp = (seeded((n,), 35).to(device) * 0.1 + 1.0, seeded((n,), 36).to(device) * 0.1, 1e-5) if ln else None
+    with K.dense_precision(dense):
+        ref = K.fused_linear(xb.float(), w, ln=lnp, split=split)
+        a = K.fused_linear(xb, w, ln=lnp, split=split)
+        c = K.fused_linear(xb, w, ln=lnp, split=split, out_dtype=torch.bfloat16)
+    refs, outs, outc = (ref, a, c) if split else ([ref], [a], [c])
+    for r, x, y in zip(refs, outs, outc):
+        assert x.dtype == torch.float32 and y.dtype == torch.bfloat16 and y.shape == r.shape
+        assert torch.equal(x, r)
+        assert torch.equal(y, r.to(torch.bfloat16))
+    with pytest.raises(ValueError):
+        K.fused_linear(xb, w, out_dtype=torch.bfloat16, residual=torch.zeros((m, n), device=device))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("m,k1,k2,n,gelu,ln,res,split,bias,gin", [
     (8192, 128, 0, 384, False, False, False, True, False, False),    # self-attention q | k | v
     (8192, 128, 0, 128, False, True, True, False, False, False),     # merge + norm1 + residual

@@ -1,4 +1,4 @@
-"""usage: op_stacks.py [batch] [fp32|bf16]
+"""usage: op_stacks.py [batch] [fp32|bf16|bf16x3] [attn dtype: auto|bf16|...]
 Which Python call sites launch the small PyTorch kernels (copies, elementwise, cat, GELU, clamp ...)
 of one e2e step: a TorchDispatchMode records every launching aten op with the innermost repo frame
 that called it (torch.profiler's with_stack comes back empty on this build)."""
@@ -41,8 +41,9 @@ import sys
 
 batch = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 dense = sys.argv[2] if len(sys.argv) > 2 else "fp32"
+attn = sys.argv[3] if len(sys.argv) > 3 else "auto"
 dev = torch.device("cuda:0")
-model = build_model(dev, dense)
+model = build_model(dev, dense, attn_dtype=attn)
 data = S.make_batch(batch, image_shape=(256, 256), device=dev)
 for _ in range(2):
     model.test_step(data)

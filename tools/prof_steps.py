@@ -6,7 +6,7 @@ of the run are averaged (the first `--skip` spans hold warmup, MIOpen's algorith
 graph capture; the last span holds the eager pass bench.py times the roofline kernel with), so
 one-time work never lands in the per-step numbers.
 usage: prof_steps.py run_kernel_trace.csv|run_results.db [--marker render_kernel] [--skip 4] [--top 40]
-       [--timeline out.txt]  (one steady-state step, every dispatch in start order with its queue and the
+       [--timeline out.txt] [--grids substring]  (one steady-state step, every dispatch in start order with its queue and the
        idle time since the previous dispatch ended; rocprofv3's default SQLite output is read directly)"""
 import argparse
 import csv
@@ -18,6 +18,7 @@ ap.add_argument("--marker", default="render_kernel")
 ap.add_argument("--skip", type=int, default=4)
 ap.add_argument("--top", type=int, default=40)
 ap.add_argument("--timeline", default=None)
+ap.add_argument("--grids", default=None, help="kernels whose name contains this: per-step time by launch grid")
 a = ap.parse_args()
 if a.trace.endswith(".db"):
     import sqlite3
@@ -58,3 +59,21 @@ if a.timeline:
             f.write(f"{(s0 - lo) / 1e3:9.1f} {(e0 - s0) / 1e3:7.1f} gap={(s0 - last_end) / 1e3:6.1f} "
                     f"q={r.get('Queue_Id', '?')} {r.get('Grid', '')} {r['Kernel_Name'][:110]}\n")
             last_end = max(last_end, e0)
+
+if a.grids:
+    def grid_of(r):
+        if "Grid" in r:
+            return r["Grid"]
+        gx = r.get("Grid_Size_X", r.get("Grid_Size", "?"))
+        return f"{gx}x{r.get('Grid_Size_Y', '?')}/{r.get('Workgroup_Size_X', r.get('Workgroup_Size', '?'))}"
+    gt, gc = defaultdict(float), defaultdict(int)
+    for lo, hi in spans:
+        for r in rows:
+            s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            if lo < e <= hi and a.grids in r["Kernel_Name"]:
+                key = (r["Kernel_Name"][:70], grid_of(r))
+                gt[key] += e - s
+                gc[key] += 1
+    print(f"\nby grid ({a.grids}):")
+    for key, t in sorted(gt.items(), key=lambda kv: -kv[1]):
+        print(f"{t / n / 1e3:8.1f}us/step calls/step={gc[key] / n:5.1f} avg={t / gc[key] / 1e3:7.1f}us  grid={key[1]}  {key[0]}")

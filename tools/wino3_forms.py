@@ -1,5 +1,5 @@
 """Graph-timed bf16x3 Winograd launch per workgroup form for given shapes:
-python tools/wino3_forms.py "n,ci,co,h,w" ... (forms 1-5 via TSPLAT_WINO3_FORM, read per launch)."""
+python tools/wino3_forms.py "n,ci,co,h,w" ... (forms 1-6 via TSPLAT_WINO3_FORM, FORMS=0,1,..., read per launch)."""
 import os
 import sys
 
@@ -13,7 +13,7 @@ for spec in sys.argv[1:]:
     x = torch.randn(n, ci, h, w, device=dev)
     wt = torch.randn(co, ci, 3, 3, device=dev) * 0.05
     row = []
-    for form in ("0", "1", "2", "3", "4", "5"):
+    for form in os.environ.get("FORMS", "0,1,2,3,4,5,6").split(","):
         os.environ["TSPLAT_WINO3_FORM"] = form
         s = torch.cuda.Stream()
         try:

@@ -1,5 +1,5 @@
 """Census of the 3x3 Winograd launches of one eager e2e step (shape, precision, the bf16x3 launch
-form), with per-call HIP-event times: python tools/wino_census.py [dense_dtype]."""
+form), with per-call HIP-event times: python tools/wino_census.py [dense_dtype] [batch]."""
 import sys
 from collections import Counter
 
@@ -10,9 +10,10 @@ from transplat_amd import synthetic as S
 from transplat_amd.e2e import build_model
 
 dense = sys.argv[1] if len(sys.argv) > 1 else "bf16x3"
+batch = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 dev = torch.device("cuda:0")
 model = build_model(dev, dense)
-data = S.make_batch(1, image_shape=(256, 256), device=dev)
+data = S.make_batch(batch, image_shape=(256, 256), device=dev)
 orig = K.conv3x3_wino
 calls = Counter()
 times = Counter()
@@ -41,5 +42,8 @@ with torch.no_grad():
 tot = 0.0
 for key, c in sorted(calls.items(), key=lambda kv: -times[kv[0]]):
     tot += times[key]
-    print(f"{c:3d} x {times[key] / c:7.1f} us  (n, ci, co, h, w, contiguous, relu_in, residual) = {key}")
-print(f"total {tot:.1f} us over {sum(calls.values())} calls ({dense})")
+    n, ci, co, h, w = key[:5]
+    gf = 2.0 * n * ci * co * h * w * 9 / 1e9  # direct-equivalent FLOPs
+    print(f"{c:3d} x {times[key] / c:7.1f} us {gf / (times[key] / c) * 1e3:6.1f} TF/s  "
+          f"(n, ci, co, h, w, contiguous, relu_in, residual) = {key}")
+print(f"total {tot:.1f} us over {sum(calls.values())} calls ({dense}, b = {batch})")

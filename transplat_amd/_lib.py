@@ -56,8 +56,11 @@ SIGNATURES = {
     "tsplat_win_attn_fwd": (ctypes.c_int, [_P] * 5 + [_I32] * 7 + [_P]),
     "tsplat_win_attn_bf16_workspace_bytes": (ctypes.c_size_t, [_I32] * 5),
     "tsplat_win_attn_bf16_fwd": (ctypes.c_int, [_P] * 5 + [_I32] * 7 + [_P]),
+    "tsplat_win_attn_bf16_shift_fwd": (ctypes.c_int, [_P] * 5 + [_I32] * 8 + [_P]),
     "tsplat_group_norm_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, ctypes.c_int64, _I32]),
     "tsplat_group_norm_fwd": (ctypes.c_int, [_P] * 7 + [_I32, _I32, ctypes.c_int64, _I32, ctypes.c_float, _I32, _P]),
+    "tsplat_group_norm_cat_res_fwd": (ctypes.c_int, [_P] * 6 + [_I32, _P, _P, _I32, _I32, ctypes.c_int64, _I32,
+                                                                ctypes.c_float, _I32, _P]),
     "tsplat_layer_norm128_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, ctypes.c_float, _P, _I32, _I32, _P]),
     "tsplat_group_norm_bf16_fwd": (ctypes.c_int, [_P] * 7 + [_I32, _I32, ctypes.c_int64, _I32, ctypes.c_float, _I32,
                                                             _P]),

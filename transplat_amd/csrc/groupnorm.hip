@@ -120,12 +120,23 @@ __device__ __forceinline__ float activate(float v) {
 template <int ACT>
 __device__ __forceinline__ float post_residual(float v) { return ACT == 3 ? fmaxf(v, 0.0f) : v; }
 
+// The residual of element (sample n, channel ch, position p) at flat index e = (n C + ch) HW + p:
+// res + e, or -- a residual given as the channel concatenation [res (c1 channels) | res2 (C - c1)]
+// (a U-Net skip input, read in place) -- the element of whichever part holds channel ch
+template <typename T>
+__device__ __forceinline__ const T* res_at(const T* res, const T* res2, int c1, int C, int64_t e, int n, int ch,
+                                           int HW) {
+    if (c1 >= C) return res + e;
+    const int64_t p = e - ((int64_t)n * C + ch) * HW;
+    return ch < c1 ? res + ((int64_t)n * c1 + ch) * HW + p : res2 + ((int64_t)n * (C - c1) + (ch - c1)) * HW + p;
+}
+
 template <bool VEC, int ACT, bool RES, typename T>
 __global__ void __launch_bounds__(kThreads)
 apply_kernel(const T* __restrict__ x, const float* __restrict__ pb, const float2* __restrict__ partials,
              const float* __restrict__ gamma, const float* __restrict__ beta,
-             const T* __restrict__ res, T* __restrict__ y, int64_t L, int S, int HW, int C,
-             int cpg, int G, float eps) {
+             const T* __restrict__ res, const T* __restrict__ res2, int c1, T* __restrict__ y, int64_t L, int S,
+             int HW, int C, int cpg, int G, float eps) {
     const int chunk = blockIdx.x, seg = blockIdx.y, tid = threadIdx.x;
     __shared__ float s_scale_shift[2];
     if (tid < kWave) {
@@ -167,7 +178,7 @@ apply_kernel(const T* __restrict__ x, const float* __restrict__ pb, const float2
                 v.z = activate<ACT>(v.z * sc + sh);
                 v.w = activate<ACT>(v.w * sc + sh);
                 if (RES) {
-                    const float4 r = ld4(res + base + i);
+                    const float4 r = ld4(res_at(res, res2, c1, C, base + i, seg / G, c, HW));
                     v.x = post_residual<ACT>(v.x + r.x);
                     v.y = post_residual<ACT>(v.y + r.y);
                     v.z = post_residual<ACT>(v.z + r.z);
@@ -181,7 +192,7 @@ apply_kernel(const T* __restrict__ x, const float* __restrict__ pb, const float2
             const int c = g * cpg + (int)((start + i) / HW);
             const float sc = rstd * gamma[c];
             float v = activate<ACT>((ld1(x + base + i) + (pb ? pb[c] : 0.f)) * sc + (beta[c] - sc * mean));
-            if (RES) v = post_residual<ACT>(v + ld1(res + base + i));
+            if (RES) v = post_residual<ACT>(v + ld1(res_at(res, res2, c1, C, base + i, seg / G, c, HW)));
             st1(y + base + i, v);
         }
     }
@@ -209,8 +220,8 @@ __device__ __forceinline__ float block_sum512(float v, float* red) {
 template <int NPT, int ACT, bool RES, typename T>
 __global__ void __launch_bounds__(kFusedThreads)
 fused_kernel(const T* __restrict__ x, const float* __restrict__ pb, const float* __restrict__ gamma,
-             const float* __restrict__ beta, const T* __restrict__ res, T* __restrict__ y, int L, int HW,
-             int cpg, int G, float eps) {
+             const float* __restrict__ beta, const T* __restrict__ res, const T* __restrict__ res2, int c1,
+             T* __restrict__ y, int L, int HW, int cpg, int G, float eps) {
     __shared__ float red[kFusedThreads / kWave];
     const int seg = blockIdx.x, tid = threadIdx.x;
     const int g = seg % G;
@@ -255,7 +266,7 @@ fused_kernel(const T* __restrict__ x, const float* __restrict__ pb, const float*
             o.z = activate<ACT>(v[k].z * sc + sh);
             o.w = activate<ACT>(v[k].w * sc + sh);
             if (RES) {
-                const float4 r = ld4(res + base + i);
+                const float4 r = ld4(res_at(res, res2, c1, cpg * G, base + i, seg / G, c, HW));
                 o.x = post_residual<ACT>(o.x + r.x);
                 o.y = post_residual<ACT>(o.y + r.y);
                 o.z = post_residual<ACT>(o.z + r.z);
@@ -281,9 +292,12 @@ extern "C" size_t tsplat_group_norm_workspace_bytes(int32_t n, int32_t c, int64_
 template <typename T>
 static int group_norm_launch(const T* x, const float* pre_bias, const float* gamma, const float* beta,
                              const T* residual, T* y, void* workspace, int32_t n, int32_t c, int64_t hw,
-                             int32_t groups, float eps, int32_t act, void* stream_) {
+                             int32_t groups, float eps, int32_t act, void* stream_, const T* residual2 = nullptr,
+                             int32_t c1 = -1) {
     using namespace tsplat::gn;
     if (!x || !gamma || !beta || !y || !workspace) return TSPLAT_EINVAL;
+    if (c1 < 0) c1 = c;  // one residual tensor
+    if (c1 > c || (c1 < c && (!residual || !residual2 || c1 == 0))) return TSPLAT_EINVAL;
     if (n <= 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups || act < 0 || act > 3 ||
         hw > INT32_MAX)
         return TSPLAT_EINVAL;
@@ -295,14 +309,14 @@ static int group_norm_launch(const T* x, const float* pre_bias, const float* gam
     const dim3 grid((unsigned)S, (unsigned)(n * groups));
     const uintptr_t al = 4 * sizeof(T);  // one vector of 4 elements
     const bool vec = (hw % 4 == 0) && ((uintptr_t)x % al == 0) && ((uintptr_t)y % al == 0) &&
-                     (!residual || (uintptr_t)residual % al == 0);
+                     (!residual || (uintptr_t)residual % al == 0) && (!residual2 || (uintptr_t)residual2 % al == 0);
     if (vec && L <= (int64_t)kFusedThreads * 32 && x != y) {
         // the whole group fits one workgroup's registers: single launch
         const int npt = L <= kFusedThreads * 4 ? 4 : L <= kFusedThreads * 8 ? 8 : L <= kFusedThreads * 16 ? 16 : 32;
         TSPLAT_PROF_BEGIN(prof::kGroupNorm, stream);
 #define TSPLAT_GN_F(N, A, R)                                                                                  \
     hipLaunchKernelGGL((fused_kernel<N, A, R, T>), dim3((unsigned)(n * groups)), dim3(kFusedThreads), 0, stream, x, \
-                       pre_bias, gamma, beta, residual, y, (int)L, (int)hw, cpg, groups, eps)
+                       pre_bias, gamma, beta, residual, residual2, c1, y, (int)L, (int)hw, cpg, groups, eps)
 #define TSPLAT_GN_FA(N, R)                   \
     switch (act) {                           \
         case 0: TSPLAT_GN_F(N, 0, R); break; \
@@ -336,7 +350,7 @@ static int group_norm_launch(const T* x, const float* pre_bias, const float* gam
     TSPLAT_CHECK_LAUNCH();
 #define TSPLAT_GN_APPLY(V, A, R)                                                                   \
     hipLaunchKernelGGL((apply_kernel<V, A, R, T>), grid, dim3(kThreads), 0, stream, x, pre_bias, part, gamma,  \
-                       beta, residual, y, L, (int)S, (int)hw, c, cpg, groups, eps)
+                       beta, residual, residual2, c1, y, L, (int)S, (int)hw, c, cpg, groups, eps)
 #define TSPLAT_GN_ACT(V, R)              \
     switch (act) {                       \
         case 0: TSPLAT_GN_APPLY(V, 0, R); break; \
@@ -362,6 +376,17 @@ extern "C" int tsplat_group_norm_fwd(const float* x, const float* pre_bias, cons
                                      void* stream_) {
     return group_norm_launch<float>(x, pre_bias, gamma, beta, residual, y, workspace, n, c, hw, groups, eps, act,
                                     stream_);
+}
+
+// tsplat_group_norm_fwd with the residual given as a channel concatenation read in place:
+// channels [0, c1) from residual [n, c1, hw], [c1, c) from residual2 [n, c - c1, hw]
+extern "C" int tsplat_group_norm_cat_res_fwd(const float* x, const float* pre_bias, const float* gamma,
+                                             const float* beta, const float* residual, const float* residual2,
+                                             int32_t c1, float* y, void* workspace, int32_t n, int32_t c, int64_t hw,
+                                             int32_t groups, float eps, int32_t act, void* stream_) {
+    if (c1 <= 0 || c1 >= c || !residual || !residual2) return TSPLAT_EINVAL;
+    return group_norm_launch<float>(x, pre_bias, gamma, beta, residual, y, workspace, n, c, hw, groups, eps, act,
+                                    stream_, residual2, c1);
 }
 
 extern "C" int tsplat_group_norm_bf16_fwd(const void* x, const float* pre_bias, const float* gamma,

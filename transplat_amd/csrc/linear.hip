@@ -33,6 +33,8 @@ enum Flags : int {
     kResPreLN = 64,  // with kResidual: the residual is added BEFORE the LayerNorm (post-norm layers)
     kReluIn = 128,   // ReLU applied to X as it is staged (the producing FFN layer's activation)
     kBf16x3 = 256,   // split-bf16 products (x = hi + lo; hi*hi + hi*lo + lo*hi on 32x32x16 bf16 MFMA)
+    kXBf16 = 512,    // x1 is bf16 (widened exactly as it is staged; no x2)
+    kOutBf16 = 1024, // the output is written as bf16 (round to nearest even; no residual)
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
@@ -141,10 +143,22 @@ __device__ __forceinline__ void stage_load(const Args& a, int m0, int n0, int K,
         const bool first = k0 < a.k1;
         const float* xs = first ? a.x1 : a.x2;
         const int ld = first ? a.k1 : a.k2, kk = first ? k0 : k0 - a.k1;
+        if (a.flags & kXBf16) {  // x1 bf16: 4 channels = 8 B, widened exactly
+            typedef __bf16 bf16x4l __attribute__((ext_vector_type(4)));
+            const __bf16* xb = reinterpret_cast<const __bf16*>(a.x1);
 #pragma unroll
-        for (int i = 0; i < BM / 32; ++i) {
-            const int m = m0 + srow + 32 * i;
-            st.x[i] = m < a.M ? *reinterpret_cast<const floatx4*>(xs + (size_t)m * ld + kk + 4 * sq) : (floatx4)(0.f);
+            for (int i = 0; i < BM / 32; ++i) {
+                const int m = m0 + srow + 32 * i;
+                st.x[i] = m < a.M ? __builtin_convertvector(
+                                        *reinterpret_cast<const bf16x4l*>(xb + (size_t)m * a.k1 + k0 + 4 * sq), floatx4)
+                                  : (floatx4)(0.f);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < BM / 32; ++i) {
+                const int m = m0 + srow + 32 * i;
+                st.x[i] = m < a.M ? *reinterpret_cast<const floatx4*>(xs + (size_t)m * ld + kk + 4 * sq) : (floatx4)(0.f);
+            }
         }
     }
 #pragma unroll
@@ -405,6 +419,20 @@ linear_f32_kernel(Args a) {
         }
         return;
     }
+    if (a.flags & kOutBf16) {  // bf16 output (same layouts; split_stride in elements)
+        typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+        __bf16* ob = reinterpret_cast<__bf16*>(a.out) +
+                     ((a.flags & kSplit) ? (size_t)(nb / kBN) * a.split_stride + (size_t)m * kBN + nb % kBN
+                                         : (size_t)m * a.N + nb);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            bf16x4v vh;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vh[j] = (__bf16)y[4 * u + j];
+            *reinterpret_cast<bf16x4v*>(ob + 8 * u) = vh;
+        }
+        return;
+    }
     float* dst;
     int col0;
     if (a.flags & kSplit) {  // column block j of 128 -> its own [M, 128] matrix
@@ -443,6 +471,8 @@ extern "C" int tsplat_linear_f32_fwd(const float* x1, int32_t k1, const float* x
     if ((flags & kLayerNorm) && (N != kBN || !ln_gamma || !ln_beta)) return TSPLAT_EINVAL;
     if ((flags & kResidual) && (!residual || (flags & kSplit))) return TSPLAT_EINVAL;
     if ((flags & kSplit) && split_stride < (int64_t)M * kBN) return TSPLAT_EINVAL;
+    if ((flags & kXBf16) && (k2 > 0 || ((uintptr_t)x1 & 7))) return TSPLAT_EINVAL;
+    if ((flags & kOutBf16) && ((flags & kResidual) || ((uintptr_t)out & 7))) return TSPLAT_EINVAL;
     Args a{x1, x2, w, bias, ln_gamma, ln_beta, residual, out, split_stride, ln_eps, k1, k2, M, N, flags};
     a.po = a.pm = a.pl = nullptr;
     a.kv_x3 = nullptr;
@@ -505,7 +535,7 @@ extern "C" int tsplat_linear_f32_attn_merge_fwd(const float* partials, int32_t b
     if (!partials || !w || !out || N <= 0 || N % kBN) return TSPLAT_EINVAL;
     const int ks = tsplat_win_attn_split(batch, height, width, key_views, splits);
     if (ks <= 1 || ks > kMaxSplit) return TSPLAT_EINVAL;
-    if (flags & (kSplit | kGeluIn)) return TSPLAT_EINVAL;
+    if (flags & (kSplit | kGeluIn | kXBf16 | kOutBf16)) return TSPLAT_EINVAL;
     if ((flags & kLayerNorm) && (N != kBN || !ln_gamma || !ln_beta)) return TSPLAT_EINVAL;
     if ((flags & kResidual) && !residual) return TSPLAT_EINVAL;
     if (flags & kBias) return TSPLAT_EINVAL;

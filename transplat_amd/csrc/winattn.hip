@@ -1599,12 +1599,28 @@ extern "C" size_t tsplat_win_attn_bf16_workspace_bytes(int32_t batch, int32_t he
     return (size_t)batch * splits * splits * ks * L * (kC + 2) * sizeof(float);
 }
 
+extern "C" int tsplat_win_attn_bf16_shift_fwd(const void* q, const void* k, const void* v, void* out,
+                                              void* workspace, int32_t batch, int32_t height, int32_t width,
+                                              int32_t channels, int32_t key_views, int32_t splits,
+                                              int32_t with_shift, int32_t key_batch_shift, void* stream_);
+
 extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void* v, void* out,
                                         void* workspace, int32_t batch, int32_t height, int32_t width,
                                         int32_t channels, int32_t key_views, int32_t splits,
                                         int32_t with_shift, void* stream_) {
+    return tsplat_win_attn_bf16_shift_fwd(q, k, v, out, workspace, batch, height, width, channels, key_views, splits,
+                                          with_shift, 0, stream_);
+}
+
+// tsplat_win_attn_bf16_fwd where query batch b attends to the keys / values of batch
+// (b + key_batch_shift) % batch (the two-view cross pairing of forward_pair without a rolled copy)
+extern "C" int tsplat_win_attn_bf16_shift_fwd(const void* q, const void* k, const void* v, void* out,
+                                              void* workspace, int32_t batch, int32_t height, int32_t width,
+                                              int32_t channels, int32_t key_views, int32_t splits,
+                                              int32_t with_shift, int32_t key_batch_shift, void* stream_) {
     using namespace tsplat::winattn;
     if (!q || !k || !v || !out) return TSPLAT_EINVAL;
+    if (key_batch_shift < 0 || key_batch_shift >= batch) return TSPLAT_EINVAL;
     if (channels != kC || batch <= 0 || key_views <= 0 || splits <= 0) return TSPLAT_EINVAL;
     if (height % splits || width % splits) return TSPLAT_EINVAL;
     Params p;
@@ -1619,7 +1635,7 @@ extern "C" int tsplat_win_attn_bf16_fwd(const void* q, const void* k, const void
     p.wh = height / splits;
     p.ww = width / splits;
     p.ww_log2 = (p.ww & (p.ww - 1)) == 0 ? __builtin_ctz(p.ww) : -1;
-    p.kv_shift = 0;
+    p.kv_shift = key_batch_shift;
     p.nbatch = batch;
     if (with_shift && (p.shift_h == 0 || p.shift_w == 0)) return TSPLAT_EINVAL;
     if (p.L % kBQ3 || (p.L * p.m) % kBK) return TSPLAT_EINVAL;

@@ -228,8 +228,11 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     constexpr int T = 32 * NB;                 // tiles per workgroup
     constexpr int GT = 256 * CB;               // threads per k-group
     constexpr int PHR = GT / (4 * T);          // pair halves (4 pairs each) covered per pass
-    constexpr int PP = 2 / PHR;                // channel pairs per thread per chunk
-    static_assert(PHR * PP == 2, "pairs per chunk");
+    constexpr int PP = PHR > 2 ? 1 : 2 / PHR;  // channel pairs per thread per chunk
+    // more threads than channel pairs x tiles (64 co x 32 tiles): the waves of pair halves >= 2
+    // skip the transform and only load, stage and multiply (their SIMDs' VALU goes to the others)
+    constexpr bool XT = PHR > 2;
+    static_assert(XT || PHR * PP == 2, "pairs per chunk");
     constexpr int BUF = 2 * 16 * 8 * T;        // dwords per sV buffer (hi + lo)
     constexpr int CO = 32 * CB;
     constexpr int NSV = ST ? 1 : 2;            // sV buffers per k-group
@@ -264,6 +267,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     // a wave's 64 lanes are 16 tiles x 4 pairs, so its sV dword stores are 64 consecutive dwords
     const int gtid = tid % GT;
     const int pl = gtid & 3, t = (gtid >> 2) % T, ph0 = (gtid >> 2) / T;
+    const bool xf = !XT || ph0 < 2;  // this thread transforms (wave-uniform: a wave is 16 tiles of one ph0)
     const Patch<T> pt(a, tbk, t);
 
     for (int c = tid; c < a.ci_pad; c += 256 * CB * KS) {
@@ -312,6 +316,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
 
     float d[PP][2][16];
     auto load_patches = [&](int chunk) {
+        if (!xf) return;
 #pragma unroll
         for (int q = 0; q < PP; ++q) {
             const int c0 = chunk * 16 + 2 * (4 * (ph0 + q * PHR) + pl);
@@ -321,6 +326,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     };
     uint32_t* sG = smem + kg * (NSV * BUF + (ST ? 2 * RGN : 0));
     auto transform = [&](uint32_t* sV) {
+        if (!xf) return;
 #pragma unroll
         for (int q = 0; q < PP; ++q) transform_pair<T>(d[q][0], d[q][1], sV + ((ph0 + q * PHR) * T + t) * 4 + pl);
     };
@@ -379,6 +385,7 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
         }
     };
     auto read_patches = [&](int slot) {  // this thread's PP channel pairs of tile t from sIn
+        if (!xf) return;
         const int tyl = t / a.tbx, txl = t - tyl * a.tbx;
         const float* base = sIn + slot * RGN + 2 * tyl * RP + 2 * txl + 3;
 #pragma unroll
@@ -818,12 +825,13 @@ extern "C" int tsplat_wino_weight_bf16x3(const float* weight, void* packed, int3
 }
 
 // workgroup forms: 0 = auto, 1 = 32 co x 32 tiles (KS 1), 2 = 32 x 32 with two k-groups,
-// 3 = 32 co x 64 tiles, 4 = 64 co x 64 tiles, 5 = persistent 32 x 32 (staged maps only); staged
-// input (Region) on top where the map allows it
+// 3 = 32 co x 64 tiles, 4 = 64 co x 64 tiles, 5 = persistent 32 x 32 (staged maps only),
+// 6 = 64 co x 32 tiles (half the threads transform); staged input (Region) on top where the map
+// allows it
 static int pick_form(int n, int th, int tw, int co) {
     if (const char* e = getenv("TSPLAT_WINO3_FORM")) {
         const int f = atoi(e);
-        if (f >= 1 && f <= 5) return f;
+        if (f >= 1 && f <= 6) return f;
     }
     // measured per census shape (tools/bench_wino3.py, profiles/r4/g17/bench_wino3.log, XCD-ordered
     // blocks): the 64 x 64 form above 128 workgroups (2 x 128 -> 64 at 144^2, 162 of them: 30.8 vs
@@ -837,6 +845,13 @@ static int pick_form(int n, int th, int tw, int co) {
     const int cob32 = (co + 31) / 32;
     const long wg64 = (tiles + 63) / 64 * ((co + 63) / 64);
     const long wg32 = (tiles + 31) / 32 * cob32;
+    // 64 x 32 where it makes one or two workgroups per CU of a 64-channel-multiple output
+    // (tools/wino3_forms.py, profiles/r5/forms/: 64 -> 64 at 128^2 16.2 vs 17.8 us, 128 -> 128 at 72^2
+    // 21.7 vs 24.6, 96 -> 128 at 72^2 18.4 vs 20.6, 128 -> 256 at 64^2 24.3 vs 27.5; at 128 or
+    // fewer workgroups and at 324 or more it loses, and at b = 8 everywhere)
+    const long wg6 = (tiles + 31) / 32 * ((co + 63) / 64);
+    static const bool f6 = !getenv("TSPLAT_WINO3_F6") || atoi(getenv("TSPLAT_WINO3_F6")) != 0;  // A/B knob
+    if (f6 && co % 64 == 0 && wg6 >= 150 && wg6 <= 320) return 6;
     if (co > 32 && wg64 > 128) return 4;
     return wg32 <= 256 ? 2 : 1;
 }
@@ -925,6 +940,7 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const
     }
     switch (form) {
         case 4: launch<2, 2, 1>(a, blocks, staged, stream, ev.start, ev.stop); break;
+        case 6: launch<2, 1, 1>(a, blocks, staged, stream, ev.start, ev.stop); break;
         case 3: launch<1, 2, 1>(a, blocks, staged, stream, ev.start, ev.stop); break;
         case 2: launch<1, 1, 2>(a, blocks, staged, stream, ev.start, ev.stop); break;
         default: launch<1, 1, 1>(a, blocks, staged, stream, ev.start, ev.stop); break;

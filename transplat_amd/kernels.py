@@ -44,10 +44,11 @@ def pack_cameras(intr: torch.Tensor, pose: torch.Tensor) -> torch.Tensor:
          pose[:, :3, 3].float()], dim=1).contiguous()
 
 
-def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool):
+def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, kv_shift: int = 0):
     """Shifted-window attention (reference single_head_split_window_attention).
     q [B, L, C]; k, v [B, L, C] or [B, m, L, C] -> [B, L, C]. bf16 inputs (the dense layers under
-    bf16 autocast) run the bf16-MFMA kernel and return bf16; everything else runs exact fp32."""
+    bf16 autocast) run the bf16-MFMA kernel and return bf16; everything else runs exact fp32.
+    kv_shift: query batch i attends to the keys / values of batch (i + kv_shift) % B."""
     lib = _lib.load()
     b, l, c = q.shape
     m = 1 if k.dim() == 3 else k.shape[1]
@@ -57,10 +58,13 @@ def window_attention(q, k, v, h: int, w: int, num_splits: int, with_shift: bool)
         out = torch.empty((b, l, c), dtype=torch.bfloat16, device=q.device)
         nbytes = int(lib.tsplat_win_attn_bf16_workspace_bytes(b, h, w, m, num_splits))
         ws = torch.empty(nbytes, dtype=torch.uint8, device=q.device) if nbytes else None
-        rc = lib.tsplat_win_attn_bf16_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(out), _lib.ptr(ws), b, h,
-                                          w, c, m, num_splits, int(with_shift), _lib.stream_ptr(q.device))
-        _lib.check(rc, "tsplat_win_attn_bf16_fwd")
+        rc = lib.tsplat_win_attn_bf16_shift_fwd(_lib.ptr(q), _lib.ptr(k), _lib.ptr(v), _lib.ptr(out), _lib.ptr(ws),
+                                                b, h, w, c, m, num_splits, int(with_shift), int(kv_shift) % b,
+                                                _lib.stream_ptr(q.device))
+        _lib.check(rc, "tsplat_win_attn_bf16_shift_fwd")
         return out
+    if kv_shift:
+        k, v = torch.roll(k, -kv_shift, dims=0), torch.roll(v, -kv_shift, dims=0)
     q, k, v = _f32(q), _f32(k), _f32(v)
     out = torch.empty((b, l, c), dtype=torch.float32, device=q.device)
     nbytes = int(lib.tsplat_win_attn_workspace_bytes(b, h, w, m, num_splits))
@@ -289,6 +293,7 @@ def instance_norm(x, eps: float, act: str = "none", residual=None):
 
 
 _BF16_NORMS = os.environ.get("TSPLAT_BF16_NORMS", "1") != "0"  # A/B knob: bf16-I/O norm kernels (C3)
+_CAT_RES = os.environ.get("TSPLAT_GN_CAT_RES", "1") != "0"  # A/B knob: concatenated residuals read in place
 BF16_NORMS = _BF16_NORMS
 _UV_TABLE_BF16 = os.environ.get("TSPLAT_UV_TABLE_BF16", "1") != "0"  # A/B knob: split-bf16 table GEMM (C3)
 
@@ -296,10 +301,31 @@ _UV_TABLE_BF16 = os.environ.get("TSPLAT_UV_TABLE_BF16", "1") != "0"  # A/B knob:
 def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", residual=None, pre_bias=None):
     """act(GroupNorm(x + pre_bias)) [+ residual] over [N, C, *spatial] (see tsplat_group_norm_fwd);
     pre_bias is the bias of a convolution that ran without it. A bf16 x (bf16 dense mode) is read
-    and the result written in bf16 (tsplat_group_norm_bf16_fwd, fp32 statistics), else fp32."""
+    and the result written in bf16 (tsplat_group_norm_bf16_fwd, fp32 statistics), else fp32.
+    residual may be a pair (r1, r2): the channel concatenation cat([r1, r2], 1), read in place by
+    the fp32 kernel (tsplat_group_norm_cat_res_fwd)."""
     lib = _lib.load()
     n, c = x.shape[:2]
     hw = x[0, 0].numel()
+    if isinstance(residual, (tuple, list)):
+        r1, r2 = residual
+        if not (_CAT_RES and x.dtype == torch.float32 and r1.dtype == r2.dtype == torch.float32 and x.is_cuda):
+            return group_norm(x, num_groups, weight, bias, eps, act, torch.cat([r1, r2], dim=1), pre_bias)
+        r1, r2 = r1.contiguous(), r2.contiguous()
+        if (r1.shape[0] != n or r2.shape[0] != n or r1.shape[1] + r2.shape[1] != c or r1.shape[2:] != x.shape[2:]
+                or r2.shape[2:] != x.shape[2:]):
+            raise ValueError(f"residual parts {tuple(r1.shape)} + {tuple(r2.shape)} != input {tuple(x.shape)}")
+        xf = _f32(x)
+        y = torch.empty_like(xf)
+        ws = torch.empty(int(lib.tsplat_group_norm_workspace_bytes(n, c, hw, num_groups)), dtype=torch.uint8,
+                         device=x.device)
+        pb = _f32(pre_bias) if pre_bias is not None else None
+        rc = lib.tsplat_group_norm_cat_res_fwd(_lib.ptr(xf), _lib.ptr(pb), _lib.ptr(_f32(weight)),
+                                               _lib.ptr(_f32(bias)), _lib.ptr(r1), _lib.ptr(r2), r1.shape[1],
+                                               _lib.ptr(y), _lib.ptr(ws), n, c, hw, num_groups, float(eps),
+                                               _ACTS[act], _lib.stream_ptr(x.device))
+        _lib.check(rc, "tsplat_group_norm_cat_res_fwd")
+        return y
     if x.dtype == torch.bfloat16 and x.is_cuda and _BF16_NORMS:
         if residual is not None and residual.dtype != torch.bfloat16:
             # the module path rounds the norm's output to bf16 (GroupNorm32 casts back to x's dtype)
@@ -334,7 +360,7 @@ def group_norm(x, num_groups: int, weight, bias, eps: float, act: str = "none", 
 
 
 _LIN_GELU, _LIN_LN, _LIN_RES, _LIN_SPLIT, _LIN_BIAS, _LIN_GELU_IN = 1, 2, 4, 8, 16, 32
-_LIN_RES_PRE_LN, _LIN_RELU_IN, _LIN_BF16X3 = 64, 128, 256
+_LIN_RES_PRE_LN, _LIN_RELU_IN, _LIN_BF16X3, _LIN_X_BF16, _LIN_OUT_BF16 = 64, 128, 256, 512, 1024
 # the fused transformer linears' products in bf16x3 inside dense_precision("bf16x3") (the kernel's
 # split-bf16 form, flag 256); TSPLAT_LINF3=0 keeps them exact fp32 in that mode
 _LINF3 = os.environ.get("TSPLAT_LINF3", "1") == "1"
@@ -345,14 +371,16 @@ def _lin_precision_flag() -> int:
 
 
 def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, residual=None, split: bool = False,
-                 gelu_in: bool = False, relu_in: bool = False, res_pre_ln: bool = False):
+                 gelu_in: bool = False, relu_in: bool = False, res_pre_ln: bool = False, out_dtype=torch.float32):
     """epilogue([x1 | x2] weight^T) in one exact-fp32 MFMA launch (tsplat_linear_f32_fwd; bf16x3
     products inside dense_precision("bf16x3"), see _LINF3):
     (+ bias) -> (exact GELU) -> (LayerNorm with ln = (gamma, beta, eps), N = 128) -> (+ residual);
     gelu_in / relu_in apply exact GELU / ReLU to the input first (the producing layer's activation,
     N = 128); res_pre_ln adds the residual before the LayerNorm (post-norm: LN(y + residual)).
     x1 [..., k1], x2 [..., k2] (concatenated along the last axis without materialising it);
-    split=True returns the N / 128 column blocks as separate contiguous [..., 128] tensors."""
+    split=True returns the N / 128 column blocks as separate contiguous [..., 128] tensors. A bf16 x1
+    (no x2) is read as bf16 and widened exactly in the kernel; out_dtype=torch.bfloat16 writes the
+    output in bf16 (no residual) -- the bf16 window attention's operands / message without casts."""
     lib = _lib.load()
     lead = x1.shape[:-1]
     k1 = x1.shape[-1]
@@ -360,7 +388,10 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     n = weight.shape[0]
     if weight.shape[1] != k1 + k2:
         raise ValueError(f"weight {tuple(weight.shape)} does not match k1 + k2 = {k1 + k2}")
-    a = _f32(x1).reshape(-1, k1)
+    xbf = x1.dtype == torch.bfloat16 and x2 is None and x1.is_cuda
+    if out_dtype not in (torch.float32, torch.bfloat16) or (out_dtype == torch.bfloat16 and residual is not None):
+        raise ValueError(f"out_dtype {out_dtype} (with residual={residual is not None}) not supported")
+    a = (x1.contiguous() if xbf else _f32(x1)).reshape(-1, k1)
     m = a.shape[0]
     b = _f32(x2).reshape(-1, k2) if x2 is not None else None
     if b is not None and b.shape[0] != m:
@@ -369,15 +400,16 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     flags |= (_LIN_GELU_IN if gelu_in else 0) | (_LIN_RELU_IN if relu_in else 0)
     flags |= _LIN_RES_PRE_LN if res_pre_ln and residual is not None else 0
     flags |= _lin_precision_flag()
+    flags |= (_LIN_X_BF16 if xbf else 0) | (_LIN_OUT_BF16 if out_dtype == torch.bfloat16 else 0)
     res = None
     if residual is not None:
         res = _f32(residual).reshape(m, n)
         flags |= _LIN_RES
     if split:
         flags |= _LIN_SPLIT
-        out = torch.empty((n // 128, m, 128), dtype=torch.float32, device=x1.device)
+        out = torch.empty((n // 128, m, 128), dtype=out_dtype, device=x1.device)
     else:
-        out = torch.empty((m, n), dtype=torch.float32, device=x1.device)
+        out = torch.empty((m, n), dtype=out_dtype, device=x1.device)
     g, bt, eps = (_f32(ln[0]), _f32(ln[1]), float(ln[2])) if ln is not None else (None, None, 0.0)
     bb = _f32(bias) if bias is not None else None
     rc = lib.tsplat_linear_f32_fwd(_lib.ptr(a), k1, _lib.ptr(b), k2, _lib.ptr(_f32(weight)), _lib.ptr(bb),
@@ -469,14 +501,16 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     m = 1 if k.dim() == 3 else k.shape[1]
     fp32 = q.dtype == k.dtype == v.dtype == torch.float32
     wl = (h // num_splits) * (w // num_splits)
-    if _ATTN == "bf16" and wl % 128 == 0:
-        # bf16 attention (config C3): the projections' fp32 outputs rounded to bf16 once, the bf16
-        # MFMA kernel, the bf16 message widened by the merge projection's operand load
+    if attention_bf16_ready(h, w, num_splits):
+        # bf16 attention (config C3): the projections' outputs in bf16 (attention_bf16_ready lets the
+        # layer ask fused_linear for them; fp32 ones are rounded here), the bf16 MFMA kernel with the
+        # cross pairing as a key-batch shift, the bf16 message widened by the merge projection's load
         qb, kb, vb = q.to(torch.bfloat16), k.to(torch.bfloat16), v.to(torch.bfloat16)
-        if kv_shift:
+        if not _BF16IO and kv_shift:
             kb, vb = torch.roll(kb, -kv_shift, dims=0), torch.roll(vb, -kv_shift, dims=0)
-        msg = window_attention(qb, kb, vb, h, w, num_splits, with_shift)
-        return fused_linear(msg, merge_weight, ln=ln, residual=residual)
+            kv_shift = 0
+        msg = window_attention(qb, kb, vb, h, w, num_splits, with_shift, kv_shift=kv_shift)
+        return fused_linear(msg if _BF16IO else msg.float(), merge_weight, ln=ln, residual=residual)
     ks = int(lib.tsplat_win_attn_split(b, h, w, m, num_splits)) if fp32 and c == 128 else 0
     if ks <= 1:
         if kv_shift:
@@ -484,6 +518,23 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
         msg = window_attention(q, k, v, h, w, num_splits, with_shift)
         return fused_linear(msg, merge_weight, ln=ln, residual=residual)
     return _merge_partials(lib, q, k, v, h, w, num_splits, with_shift, merge_weight, ln, residual, kv_shift, m, None)
+
+
+# bf16 operands / outputs of the fused linear and the key-batch shift of the bf16 attention instead of
+# cast / roll launches around them (C3 as stated); TSPLAT_LIN_BF16IO=0 restores the casts (A/B knob)
+_BF16IO = os.environ.get("TSPLAT_LIN_BF16IO", "1") == "1"
+
+
+def attention_bf16_ready(h: int, w: int, num_splits: int) -> bool:
+    """True when attention_merge runs the bf16 window attention for this window shape (attention
+    precision "bf16", window pixels a multiple of 128): the layer's q / k / v projections may then
+    be written in bf16 directly (fused_linear out_dtype)."""
+    return _ATTN == "bf16" and ((h // num_splits) * (w // num_splits)) % 128 == 0
+
+
+def projections_bf16(h: int, w: int, num_splits: int) -> bool:
+    """True when a transformer layer should ask fused_linear for bf16 q / k / v (see _BF16IO)."""
+    return _BF16IO and attention_bf16_ready(h, w, num_splits)
 
 
 def _merge_partials(lib, q, k, v, h, w, num_splits, with_shift, merge_weight, ln, residual, kv_shift, m, kv_x3):
@@ -957,10 +1008,17 @@ def conv_unfold_gemm(x, weight, bias, stride: int, padding: int):
     co, _, kh, kw = weight.shape
     ho, wo = (h + 2 * padding - kh) // stride + 1, (w + 2 * padding - kw) // stride + 1
     cols = torch.nn.functional.unfold(x, (kh, kw), padding=padding, stride=stride)  # [n, ci kh kw, L]
+    # one GEMM per image straight into its [co, L] slab, bias in the GEMM's C term (a broadcast
+    # matmul over the batch transposed cols into a [n L, ci kh kw] copy first, and the bias add
+    # was another pass)
+    wm = weight.reshape(co, -1)
+    y = torch.empty((n, co, ho * wo), dtype=torch.float32, device=x.device)
     with torch.autocast("cuda", enabled=False):
-        y = torch.matmul(weight.reshape(co, -1), cols)  # [n, co, L]
-    if bias is not None:
-        y = y + bias.view(1, co, 1)
+        for i in range(n):
+            if bias is not None:
+                torch.addmm(bias.view(co, 1), wm, cols[i], out=y[i])
+            else:
+                torch.mm(wm, cols[i], out=y[i])
     return y.view(n, co, ho, wo)
 
 

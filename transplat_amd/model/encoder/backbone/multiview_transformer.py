@@ -67,11 +67,15 @@ class TransformerLayer(nn.Module):
             else:
                 query = K.fused_linear(source, self.q_proj.weight)
                 _, kv_x3 = K.linear_kv_x3(target, self._cat_weights(("k_proj", "v_proj")), 0)
-        elif target is source:
-            query, key, value = K.fused_linear(source, self._cat_weights(("q_proj", "k_proj", "v_proj")), split=True)
         else:
-            query = K.fused_linear(source, self.q_proj.weight)
-            key, value = K.fused_linear(target, self._cat_weights(("k_proj", "v_proj")), split=True)
+            # bf16 window attention (C3 as stated): the projections written in bf16 directly
+            od = torch.bfloat16 if K.projections_bf16(height, width, attn_num_splits) else torch.float32
+            if target is source:
+                query, key, value = K.fused_linear(source, self._cat_weights(("q_proj", "k_proj", "v_proj")),
+                                                   split=True, out_dtype=od)
+            else:
+                query = K.fused_linear(source, self.q_proj.weight, out_dtype=od)
+                key, value = K.fused_linear(target, self._cat_weights(("k_proj", "v_proj")), split=True, out_dtype=od)
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
         x3 = {"kv_x3": kv_x3} if kv_x3 is not None else {}
         if self.no_ffn:

@@ -168,7 +168,7 @@ class ResBlock(nn.Module):
             x, x2 = torch.cat([x, x2], dim=1), None  # materialised once for both convolutions
         h = conv_gn_act(self.in_layers[0], self.in_layers[1], x, "silu", x2=x2)
         if isinstance(self.skip_connection, nn.Identity):
-            skip = x if x2 is None else torch.cat([x, x2], dim=1)
+            skip = x if x2 is None else (x, x2)  # the concat read in place by the norm's residual add
         else:
             skip = conv(self.skip_connection, x, x2)
         return conv_gn_act(self.out_layers[0], self.out_layers[1], h, "silu", residual=skip)
