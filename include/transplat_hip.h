@@ -422,6 +422,14 @@ int tsplat_mha_f32_fwd(const float* qkv, float* out, int32_t batch, int32_t toke
  * one elementwise pass fewer. bias = NULL is tsplat_mha_f32_fwd. */
 int tsplat_mha_bias_f32_fwd(const float* qkv, const float* bias, float* out, int32_t batch, int32_t tokens,
                             int32_t heads, int32_t head_dim, float scale, void* stream);
+/* The same attention in split-bf16 ("bf16x3") precision, the dense-layer mode of the C2 step (the
+ * reference's SDPA matmuls run under TF32, src/main.py:15): qkv (+ bias, may be NULL) is split once
+ * into hi / lo bf16 images in workspace (tsplat_mha_x3_workspace_bytes), and QK^T / PV run as
+ * hi*hi + hi*lo + lo*hi on v_mfma_f32_16x16x32_bf16 / 16x16x16_bf16 with fp32 accumulation and the
+ * fp32 online softmax of tsplat_mha_f32_fwd. qkv, bias and workspace 16-B aligned. */
+size_t tsplat_mha_x3_workspace_bytes(int32_t batch, int32_t tokens, int32_t heads, int32_t head_dim);
+int tsplat_mha_x3_fwd(const float* qkv, const float* bias, float* out, void* workspace, int32_t batch,
+                      int32_t tokens, int32_t heads, int32_t head_dim, float scale, void* stream);
 
 /* Legacy channels-first QKV attention of the depth predictor U-Nets (exact fp32 MFMA), replacing
  * QKVAttentionLegacy.forward (reference src/model/encoder/matching/ldm_unet/unet.py:510-552) with

@@ -443,15 +443,14 @@ def test_window_attention_x3_kernel(device, hw, m, shift, b, grow):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dense", ["fp32", "bf16x3"])
-@pytest.mark.parametrize("x3_from,n", [(1, 384), (0, 256)])
-def test_linear_kv_x3_matches_split(device, dense, x3_from, n):
+@pytest.mark.parametrize("x3_from,n,m", [(1, 384, 8192), (0, 256, 8192), (1, 384, 65536)])
+def test_linear_kv_x3_matches_split(device, dense, x3_from, n, m):
     """tsplat_linear_f32_split_x3_fwd (the q | k | v or k | v projection writing k / v as the bf16x3
     attention's hi / lo operand) == the fp32 split projection followed by tsplat_split_kv_bf16x3,
     bit for bit (same kernel arithmetic, the split applied to the same fp32 values); and the
     attention merge fed the pre-split operand == the one fed fp32 k / v."""
     from transplat_amd import kernels as K
 
-    m = 8192
     x = seeded((2, m // 2, 128), 61).to(device)
     w = (seeded((n, 128), 62) / math.sqrt(128)).to(device)
     with K.dense_precision(dense):
@@ -462,7 +461,7 @@ def test_linear_kv_x3_matches_split(device, dense, x3_from, n):
         assert torch.equal(a, b)
     k, v = ref_blocks[x3_from:]
     assert torch.equal(kv, K.split_kv_bf16x3(k, v))
-    if x3_from == 1:
+    if x3_from == 1 and m == 8192:
         q = blocks[0]
         wm = (seeded((128, 128), 63) / math.sqrt(128)).to(device)
         ln = (torch.ones(128, device=device), torch.zeros(128, device=device), 1e-5)
@@ -617,6 +616,9 @@ def test_fused_linear_bf16_io(device, dense, m, n, split, ln):
     (1000, 128, 128, 1024, True, False, False, False, False, False),  # [x | msg] + GELU, ragged M
     (8192, 1024, 0, 128, False, True, True, False, False, True),     # GELU(h) mlp[2] + norm2 + res
     (96, 64, 0, 256, True, False, False, False, True, False),        # bias path, tiny M
+    (65536, 1024, 0, 128, False, True, True, False, False, True),    # C3 b = 8: 128-row blocks (bf16x3)
+    (65536, 128, 0, 384, False, False, False, True, False, False),   # C3 q | k | v, 128-row blocks
+    (65500, 128, 128, 128, False, True, False, False, True, False),  # ragged M, [x | pos], LN
 ])
 @pytest.mark.parametrize("dense", ["fp32", "bf16x3"])
 def test_fused_linear_kernel(device, m, k1, k2, n, gelu, ln, res, split, bias, gin, dense):
@@ -767,6 +769,27 @@ def test_mha_bias_folded(device, b, n):
     ref = E.mha(qkv + bias, heads, 64 ** -0.5)
     out = K.mha(qkv.to(device), heads, 64 ** -0.5, bias=bias.to(device)).cpu()
     assert (out - ref).abs().max().item() < 5e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bias", [False, True])
+@pytest.mark.parametrize("b,n,heads", [(2, 325, 12), (16, 325, 12), (1, 37, 12), (3, 5, 2), (1, 1025, 4)])
+def test_mha_x3_kernel(device, b, n, heads, bias):
+    """DINOv2 attention in split-bf16 precision (tsplat_mha_x3_fwd: qkv + bias split once into hi / lo
+    bf16, QK^T and PV as hi*hi + hi*lo + lo*hi on bf16 MFMA, fp32 softmax) vs the float64 SDPA
+    restatement on qkv + bias. Bound (written here): 1e-4 of max |O| -- the three-term split's
+    ~1e-5 per product accumulated over the keys; TF32 operands would give ~1e-3."""
+    from transplat_amd import kernels as K
+
+    qkv = seeded((b, n, 3 * heads * 64), 74) * 2.0
+    bv = seeded((3 * heads * 64,), 75) * 0.5 if bias else None
+    full = qkv + bv if bias else qkv
+    ref = E.mha(full.double(), heads, 64 ** -0.5)
+    out = K.mha(qkv.to(device), heads, 64 ** -0.5, bias=bv.to(device) if bias else None, precision="bf16x3")
+    assert out.shape == (b, n, heads * 64) and out.dtype == torch.float32
+    err = (out.cpu().double() - ref).abs().max().item() / ref.abs().max().item()
+    print(f"mha x3 b={b} n={n} heads={heads} bias={bias}: rel err {err:.2e}")
+    assert err < 1e-4, err
 
 
 @pytest.mark.gpu

@@ -225,6 +225,31 @@ __device__ __forceinline__ void chunk_mfma_x3(const float* sX, const float* sW, 
     }
 }
 
+// chunk_mfma_x3 for two 32-row X groups (BM = 128): each W fragment pair feeds both accumulators
+template <int NS>
+__device__ __forceinline__ void chunk_mfma_x3_2(const float* sX, const float* sW, int wrow, int xr0, int xr1, int h,
+                                                floatx16& acc0, floatx16& acc1) {
+    const char* bx0 = reinterpret_cast<const char*>(sX) + xr0 * 256;
+    const char* bx1 = reinterpret_cast<const char*>(sX) + xr1 * 256;
+    const char* bw = reinterpret_cast<const char*>(sW) + wrow * 256;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const int u = 2 * i + h;
+        const bf16x8 wh = *reinterpret_cast<const bf16x8*>(bw + ((u ^ (wrow & 15)) << 4));
+        const bf16x8 wl = *reinterpret_cast<const bf16x8*>(bw + (((8 + u) ^ (wrow & 15)) << 4));
+        const bf16x8 xh0 = *reinterpret_cast<const bf16x8*>(bx0 + ((u ^ (xr0 & 15)) << 4));
+        const bf16x8 xl0 = *reinterpret_cast<const bf16x8*>(bx0 + (((8 + u) ^ (xr0 & 15)) << 4));
+        const bf16x8 xh1 = *reinterpret_cast<const bf16x8*>(bx1 + ((u ^ (xr1 & 15)) << 4));
+        const bf16x8 xl1 = *reinterpret_cast<const bf16x8*>(bx1 + (((8 + u) ^ (xr1 & 15)) << 4));
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh1, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl1, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh1, acc1, 0, 0, 0);
+    }
+}
+
 // The k-steps of one chunk this wave owns: k-step t contracts chunk channels {t, 32 + t} (lane
 // half h supplies channel 32 h + t), t in [8 q0, 8 q0 + 8 NQ) in 16-B units; rows xr0 .. xr0 + 31
 template <int NQ>
@@ -283,17 +308,21 @@ linear_f32_kernel(Args a) {
     const int K = a.k1 + a.k2;
     const int nchunks = K / kBK;
     const int wrow = 32 * cb + c;                     // this lane's W row (output column)
-    const int xr = BM == 64 ? 32 * sel + c : c;       // this lane's X row
-    const int q0 = BM == 64 ? 0 : 4 * sel;            // first 16-B unit of the wave's k-steps
-    constexpr int NQ = BM == 64 ? 8 : 4;
+    // this lane's X row (BM 128: and xr + 32, the second accumulator's)
+    const int xr = BM == 128 ? 64 * sel + c : BM == 64 ? 32 * sel + c : c;
+    const int q0 = BM == 32 ? 4 * sel : 0;            // first 16-B unit of the wave's k-steps
+    constexpr int NQ = BM == 32 ? 4 : 8;
+    static_assert(BM != 128 || (X3 && !ATTN), "128-row blocks: split-bf16 plain linears only");
     const bool gelu_in = a.flags & kGeluIn;  // GELU of the producing layer applied to X on its way to LDS
     const bool relu_in = a.flags & kReluIn;
 
-    floatx16 acc;
+    floatx16 acc, acc2;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
     auto mfma_chunk = [&](const float* bx, const float* bw) {
-        if constexpr (X3)  // 4 bf16 k-steps per chunk: all of them (BM 64) or this wave's K half
+        if constexpr (BM == 128)
+            chunk_mfma_x3_2<4>(bx, bw, wrow, xr, xr + 32, h, acc, acc2);
+        else if constexpr (X3)  // 4 bf16 k-steps per chunk: all of them (BM 64) or this wave's K half
             chunk_mfma_x3<BM == 64 ? 4 : 2>(bx, bw, wrow, xr, h, BM == 64 ? 0 : 2 * sel, acc);
         else
             chunk_mfma<NQ>(bx, bw, wrow, xr, h, q0, acc);
@@ -337,14 +366,14 @@ linear_f32_kernel(Args a) {
         for (int r = 0; r < 16; ++r) acc[r] += park[r * 64 + lane];
     }
     // BM = 32: waves 4..7 stay (for the barriers below) but store nothing
-    const bool active = BM == 64 || sel == 0;
+    const bool active = BM != 32 || sel == 0;
 
     // acc[r] = Y[row m0 + mr][column n0 + 32 cb + 8 (r >> 2) + 4 h + (r & 3)]. LayerNorm row
     // statistics: the 4 column-block waves of a row group exchange partial sums through sRed.
+    // (a lambda: BM = 128 runs it for both accumulators; every wave calls it, so its barriers match)
     const int nb = n0 + 32 * cb + 4 * h;
-    const int mr = xr;
+    auto epilogue = [&](floatx16& y, const int mr) {
     const int m = m0 + mr;
-    floatx16& y = acc;
     if (a.flags & kBias) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -449,6 +478,9 @@ linear_f32_kernel(Args a) {
         if (res) o += *reinterpret_cast<const floatx4*>(res + nb + 8 * u);
         *reinterpret_cast<floatx4*>(dst + col0 + 8 * u) = o;
     }
+    };
+    epilogue(acc, xr);
+    if constexpr (BM == 128) epilogue(acc2, xr + 32);
 }
 
 }  // namespace linear
@@ -507,7 +539,14 @@ static int launch_linear(tsplat::linear::Args a, void* stream_) {
     // over the wave pairs (a 128-column GEMM of 8,192 rows: 256 workgroups)
     const bool tall = (long long)((M + 63) / 64) * (N / kBN) >= 256;
     const dim3 g64((M + 63) / 64, N / kBN), g32((M + 31) / 32, N / kBN);
-    if (flags & kBf16x3) {
+    // 128-row blocks (each W fragment feeds two accumulators: half the W staging and split work per
+    // row) where they still make >= 512 workgroups (C3's 65,536-row layers); TSPLAT_LIN128=0: off
+    static const bool lin128 = !getenv("TSPLAT_LIN128") || atoi(getenv("TSPLAT_LIN128")) != 0;
+    const bool tall128 = lin128 && (long long)((M + 127) / 128) * (N / kBN) >= 512;
+    if ((flags & kBf16x3) && tall128) {
+        hipLaunchKernelGGL((linear_f32_kernel<128, false, true>), dim3((M + 127) / 128, N / kBN), dim3(kThreads), 0,
+                           stream, a);
+    } else if (flags & kBf16x3) {
         if (tall)
             hipLaunchKernelGGL((linear_f32_kernel<64, false, true>), g64, dim3(kThreads), 0, stream, a);
         else

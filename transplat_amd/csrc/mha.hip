@@ -515,6 +515,195 @@ mha16_f32_kernel(const float* __restrict__ qkv, float* __restrict__ out, int N, 
     *reinterpret_cast<floatx4*>(dst) = (floatx4){acc[0], acc[1], acc[2], acc[3]};
 }
 
+// ---------------------------------------------------------------------------------------------
+// Split-bf16 ("bf16x3") form of mha16_f32_kernel for the dense-layer mode of the C2 step (the
+// reference's attention matmuls run under TF32, src/main.py:15). The projection output (+ its bias)
+// is split once per call by split_qkv_kernel into hi / lo bf16 images (x = hi + lo, |x - hi - lo| <=
+// 2^-16 |x|), and every product is hi*hi + hi*lo + lo*hi with fp32 accumulation:
+//   S^T = K Q^T: two k-steps of v_mfma_f32_16x16x32_bf16 (lane group g holds dims 16 g + 8 s .. + 7 of
+//     its key row / query row in k-step s) x 3 terms, instead of 16 v_mfma_f32_16x16x4_f32;
+//   O^T += V^T P^T: per 16-dim block dt, v_mfma_f32_16x16x16_bf16 (A = V[key 4 g + j][16 dt + c],
+//     B = the lane's own 4 probabilities, split) x 3 terms, instead of 16 fp32 MFMAs.
+// Same operand / output maps, softmax and merge as mha16_f32_kernel; the biases live in the split
+// image (q's scaled by scale * log2 e in registers after re-joining hi + lo exactly).
+__global__ void __launch_bounds__(256) split_qkv_kernel(const float4* __restrict__ x, const float* __restrict__ bias,
+                                                        int cols4, int64_t n4, uint2* __restrict__ hi,
+                                                        uint2* __restrict__ lo) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+        float4 v = x[i];
+        if (bias) {
+            const float4 b = reinterpret_cast<const float4*>(bias)[i % cols4];
+            v.x += b.x;
+            v.y += b.y;
+            v.z += b.z;
+            v.w += b.w;
+        }
+        const floatx4 f = {v.x, v.y, v.z, v.w};
+        const bf16x4 h = __builtin_convertvector(f, bf16x4);
+        const bf16x4 l = __builtin_convertvector(f - __builtin_convertvector(h, floatx4), bf16x4);
+        hi[i] = __builtin_bit_cast(uint2, h);
+        lo[i] = __builtin_bit_cast(uint2, l);
+    }
+}
+
+typedef __bf16 bf16x8m __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4m __attribute__((ext_vector_type(4)));
+typedef short shortx4m __attribute__((ext_vector_type(4)));
+
+template <int W>
+__global__ void __launch_bounds__(W * 64)
+mha16_x3_kernel(const __bf16* __restrict__ qh_img, const __bf16* __restrict__ ql_img, float* __restrict__ out, int N,
+                int H, float scale) {
+    __shared__ float sO[W][16][64];
+    __shared__ float sML[W][2][16];
+
+    const int nq = gridDim.x, total = nq * gridDim.y;
+    int lin = blockIdx.x + blockIdx.y * nq;
+    if ((total & 7) == 0) lin = (lin & 7) * (total >> 3) + (lin >> 3);
+    const int bh = lin / nq, qblk = lin - bh * nq;
+    const int b = bh / H, head = bh - b * H;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int c = lane & 15, g = lane >> 4;
+    const size_t tok = (size_t)3 * H * kD;
+    const size_t off0 = (size_t)b * N * tok + (size_t)head * kD;
+    const __bf16* kh_b = qh_img + off0 + (size_t)H * kD;
+    const __bf16* kl_b = ql_img + off0 + (size_t)H * kD;
+    const __bf16* vh_b = qh_img + off0 + (size_t)2 * H * kD;
+    const __bf16* vl_b = ql_img + off0 + (size_t)2 * H * kD;
+
+    const int nt = (N + 15) / 16;
+    const int t_lo = wid * nt / W, t_hi = (wid + 1) * nt / W;
+    const int q = qblk * 16 + c;
+
+    // this lane's query row, dims 16 g .. 16 g + 15: re-joined (exact), scaled, split again
+    bf16x8m qh[2], ql[2];
+    {
+        const float qs = scale * kLog2e;
+        const size_t qo = off0 + (size_t)min(q, N - 1) * tok + 16 * g;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8m h = *reinterpret_cast<const bf16x8m*>(qh_img + qo + 8 * s2);
+            const bf16x8m l = *reinterpret_cast<const bf16x8m*>(ql_img + qo + 8 * s2);
+            typedef float floatx8 __attribute__((ext_vector_type(8)));
+            const floatx8 f = (__builtin_convertvector(h, floatx8) + __builtin_convertvector(l, floatx8)) * qs;
+            qh[s2] = __builtin_convertvector(f, bf16x8m);
+            ql[s2] = __builtin_convertvector(f - __builtin_convertvector(qh[s2], floatx8), bf16x8m);
+        }
+    }
+    struct TileX3 {
+        bf16x8m kh[2], kl[2];      // K[key c][16 g + 8 s .. + 7]
+        __bf16 vh[16], vl[16];     // V[key 4 g + t][16 dt + c] at t * 4 + dt
+    };
+    auto load_tile = [&](int tile, TileX3& T) {
+        const int k0 = tile * 16;
+        const size_t ko = (size_t)min(k0 + c, N - 1) * tok + 16 * g;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            T.kh[s2] = *reinterpret_cast<const bf16x8m*>(kh_b + ko + 8 * s2);
+            T.kl[s2] = *reinterpret_cast<const bf16x8m*>(kl_b + ko + 8 * s2);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const size_t vo = (size_t)min(k0 + 4 * g + t, N - 1) * tok + c;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                T.vh[t * 4 + dt] = vh_b[vo + 16 * dt];
+                T.vl[t * 4 + dt] = vl_b[vo + 16 * dt];
+            }
+        }
+    };
+
+    floatx4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = (floatx4){0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.f;
+    TileX3 cur, nxt;
+    if (t_lo < t_hi) load_tile(t_lo, cur);
+    for (int tile = t_lo; tile < t_hi; ++tile) {
+        const bool has_next = tile + 1 < t_hi;
+        if (has_next) load_tile(tile + 1, nxt);
+        floatx4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.kl[s2], qh[s2], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.kh[s2], ql[s2], s, 0, 0, 0);
+            s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur.kh[s2], qh[s2], s, 0, 0, 0);
+        }
+        const int kg = tile * 16 + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (kg + i >= N) s[i] = -INFINITY;
+        float bmax = fmaxf(fmaxf(s[0], s[1]), fmaxf(s[2], s[3]));
+        bmax = halves_max(rows_max(bmax));
+        const float m_new = fmaxf(m_run, bmax);
+        if (__any(m_new > m_run)) {
+            const float corr = __builtin_amdgcn_exp2f(m_run - m_new);
+            l_run *= corr;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+            m_run = m_new;
+        }
+        float bsum = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            s[i] = __builtin_amdgcn_exp2f(s[i] - m_run);
+            bsum += s[i];
+        }
+        l_run += halves_sum(rows_sum(bsum));
+        const bf16x4m ph = __builtin_convertvector(s, bf16x4m);
+        const bf16x4m pl = __builtin_convertvector(s - __builtin_convertvector(ph, floatx4), bf16x4m);
+        const shortx4m phs = __builtin_bit_cast(shortx4m, ph), pls = __builtin_bit_cast(shortx4m, pl);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            const bf16x4m vh4 = {cur.vh[dt], cur.vh[4 + dt], cur.vh[8 + dt], cur.vh[12 + dt]};
+            const bf16x4m vl4 = {cur.vl[dt], cur.vl[4 + dt], cur.vl[8 + dt], cur.vl[12 + dt]};
+            const shortx4m vhs = __builtin_bit_cast(shortx4m, vh4), vls = __builtin_bit_cast(shortx4m, vl4);
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vls, phs, o[dt], 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vhs, pls, o[dt], 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(vhs, phs, o[dt], 0, 0, 0);
+        }
+        if (has_next) cur = nxt;
+    }
+
+    if (g == 0) {
+        sML[wid][0][c] = m_run;
+        sML[wid][1][c] = l_run;
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sO[wid][dt * 4 + i][lane] = o[dt][i];
+    __syncthreads();
+    if (tid >= 256) return;
+    const int qq = tid >> 4, j = tid & 15;
+    const int qo = qblk * 16 + qq;
+    if (qo >= N) return;
+    float mw[W], M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        mw[w] = sML[w][0][qq];
+        M = fmaxf(M, mw[w]);
+    }
+    float a[W], L = 0.f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        a[w] = mw[w] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw[w] - M);
+        L += a[w] * sML[w][1][qq];
+    }
+    const float inv = 1.0f / L;
+    float acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < W; ++w) t += a[w] * sO[w][(j >> 2) * 4 + i][(j & 3) * 16 + qq];
+        acc[i] = t * inv;
+    }
+    float* dst = out + (((size_t)b * N + qo) * H + head) * kD + 4 * j;
+    *reinterpret_cast<floatx4*>(dst) = (floatx4){acc[0], acc[1], acc[2], acc[3]};
+}
+
 }  // namespace mha
 }  // namespace tsplat
 
@@ -563,6 +752,34 @@ extern "C" int tsplat_qkv_attention_cf_fwd(const float* qkv, float* out, int32_t
     TSPLAT_PROF_BEGIN(tsplat::prof::kMha, stream);
     hipLaunchKernelGGL(mha_cf32_kernel, dim3((tokens + kQW - 1) / kQW, batch * heads), dim3(kCfWaves * 64), 0, stream,
                        qkv, out, batch, heads, tokens_per_view, tokens, scale);
+    TSPLAT_PROF_END(tsplat::prof::kMha, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" size_t tsplat_mha_x3_workspace_bytes(int32_t batch, int32_t tokens, int32_t heads, int32_t head_dim) {
+    if (batch <= 0 || tokens <= 0 || heads <= 0 || head_dim <= 0) return 0;
+    return (size_t)2 * batch * tokens * 3 * heads * head_dim * sizeof(__bf16);
+}
+
+extern "C" int tsplat_mha_x3_fwd(const float* qkv, const float* bias, float* out, void* workspace, int32_t batch,
+                                 int32_t tokens, int32_t heads, int32_t head_dim, float scale, void* stream_) {
+    using namespace tsplat::mha;
+    if (!qkv || !out || !workspace || batch <= 0 || tokens <= 0 || heads <= 0 || head_dim != kD) return TSPLAT_EINVAL;
+    if ((int64_t)batch * heads > 65535 || (reinterpret_cast<uintptr_t>(bias) & 15) ||
+        (reinterpret_cast<uintptr_t>(qkv) & 15) || (reinterpret_cast<uintptr_t>(workspace) & 15))
+        return TSPLAT_EINVAL;
+    hipStream_t stream = (hipStream_t)stream_;
+    const int64_t n = (int64_t)batch * tokens * 3 * heads * kD;
+    __bf16* hi = (__bf16*)workspace;
+    __bf16* lo = hi + n;
+    const int64_t n4 = n / 4;
+    const int blocks = (int)((n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096);
+    TSPLAT_PROF_BEGIN(tsplat::prof::kMha, stream);
+    hipLaunchKernelGGL(split_qkv_kernel, dim3(blocks), dim3(256), 0, stream, (const float4*)qkv, bias,
+                       3 * heads * kD / 4, n4, (uint2*)hi, (uint2*)lo);
+    hipLaunchKernelGGL(mha16_x3_kernel<4>, dim3((tokens + 15) / 16, batch * heads), dim3(256), 0, stream, hi, lo, out,
+                       tokens, heads, scale);
     TSPLAT_PROF_END(tsplat::prof::kMha, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;

@@ -850,6 +850,12 @@ static int pick_form(int n, int th, int tw, int co) {
     // 21.7 vs 24.6, 96 -> 128 at 72^2 18.4 vs 20.6, 128 -> 256 at 64^2 24.3 vs 27.5; at 128 or
     // fewer workgroups and at 324 or more it loses, and at b = 8 everywhere)
     const long wg6 = (tiles + 31) / 32 * ((co + 63) / 64);
+    // the persistent 32 x 32 form for 32-channel outputs over >= 2048 tile blocks (b = 8's 128^2 /
+    // 256^2 refine U-Net levels, profiles/r5/late/wino3_forms_p5.log: 32 -> 32 at 256^2 141.6 vs 164.7
+    // us, 64 -> 32 217.8 vs 250.0, 32 -> 32 at 128^2 39.0 vs 44.1; at b = 1's 1024 blocks it loses,
+    // 25.2 vs 23.8); the launcher falls back to form 1 where it does not apply
+    static const bool p5 = !getenv("TSPLAT_WINO3_P5") || atoi(getenv("TSPLAT_WINO3_P5")) != 0;  // A/B knob
+    if (p5 && co <= 32 && wg32 >= 2048) return 5;
     static const bool f6 = !getenv("TSPLAT_WINO3_F6") || atoi(getenv("TSPLAT_WINO3_F6")) != 0;  // A/B knob
     if (f6 && co % 64 == 0 && wg6 >= 150 && wg6 <= 320) return 6;
     if (co > 32 && wg64 > 128) return 4;

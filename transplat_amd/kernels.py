@@ -647,15 +647,33 @@ def depth_tail(fullres, head, near, far):
     return depth, dens
 
 
-def mha(qkv, heads: int, scale: float, bias=None):
+# DINOv2's attention in split-bf16 precision inside dense_precision("bf16x3") (tsplat_mha_x3_fwd) for
+# up to _MHA_X3_ROWS tokens per call: same-box C2 (2 x 325 tokens) 446.9 / 447.8 vs 445.6 / 445.5
+# views/s with the exact-fp32 kernel, but C3 (16 x 325) 900.1 / 899.8 vs 903.4 / 902.1 -- there the
+# split pass over the 48 MB qkv costs what the cheaper products save (profiles/r5/late/ab_mha_x3.txt).
+# TSPLAT_MHA_X3=0 keeps the exact-fp32 kernel in that mode (A/B knob)
+_MHA_X3 = os.environ.get("TSPLAT_MHA_X3", "1") == "1"
+_MHA_X3_ROWS = 2048
+
+
+def mha(qkv, heads: int, scale: float, bias=None, precision: str | None = None):
     """Multi-head self-attention from the qkv projection output [B, N, 3 * heads * 64] ->
     [B, N, heads * 64] (tsplat_mha_f32_fwd; no permute copies). bias: the projection's bias when
-    qkv was computed without it (tsplat_mha_bias_f32_fwd folds it in)."""
+    qkv was computed without it (tsplat_mha_bias_f32_fwd folds it in). precision "bf16x3" (default:
+    the dense mode's, see _MHA_X3) runs tsplat_mha_x3_fwd."""
     lib = _lib.load()
     b, n, c3 = qkv.shape
     d = c3 // (3 * heads)
     x = _f32(qkv)
     out = torch.empty((b, n, heads * d), dtype=torch.float32, device=qkv.device)
+    if precision is None:
+        precision = "bf16x3" if _MHA_X3 and _DENSE == "bf16x3" and b * n <= _MHA_X3_ROWS else "fp32"
+    if precision == "bf16x3":
+        ws = torch.empty(int(lib.tsplat_mha_x3_workspace_bytes(b, n, heads, d)), dtype=torch.uint8, device=x.device)
+        _lib.check(lib.tsplat_mha_x3_fwd(_lib.ptr(x), _lib.ptr(_f32(bias)) if bias is not None else None,
+                                         _lib.ptr(out), _lib.ptr(ws), b, n, heads, d, float(scale),
+                                         _lib.stream_ptr(qkv.device)), "tsplat_mha_x3_fwd")
+        return out
     if bias is not None:
         _lib.check(lib.tsplat_mha_bias_f32_fwd(_lib.ptr(x), _lib.ptr(_f32(bias)), _lib.ptr(out), b, n, heads, d,
                                                float(scale), _lib.stream_ptr(qkv.device)), "tsplat_mha_bias_f32_fwd")

@@ -189,7 +189,7 @@ class DepthPredictorTrans(nn.Module):
             img2world = match_img2world(intr_curr, extrinsics)
         pos_feature = self.cam_param_encoder(dino_feature, img2world)  # [(v b), C, h, w]
         # (b v)-ordered channel-last query positions: the reference's bev_pos after its permutes
-        bev_pos = rearrange(pos_feature, "(v b) c h w -> (b v) (h w) c", v=v, b=b)
+        bev_pos = rearrange(pos_feature, "(v b) c h w -> (b v) (h w) c", v=v, b=b).contiguous()  # read by 2 layers
         corr = self.fine_transformer([features], corr, w, h, bev_pos=bev_pos, cameras=cameras, channel_last=feat_cl)
         return rearrange(corr, "(b v) (h w) c -> (v b) c h w", b=b, v=v, h=h, w=w)
 
