@@ -82,7 +82,10 @@ GPU_TOL: dict = {
     ("depth_predictor_v2.depths", "bf16x3"): 2.0e-03,  # 2x would loosen the round-4 bound
     ("depth_predictor_v2.densities", "bf16x3"): 2.3e-05,
     ("depth_predictor_v2.raw", "bf16x3"): 3.9e-05,
-    ("depth_predictor_v3.depths", "bf16x3"): 2.0e-03,  # 2x would loosen the round-4 bound
+    # measured 1.60e-03, then 2.04e-03 once the 3-view 128 -> 128 64^2 maps took the 64 x 32 Winograd
+    # form (one k-group instead of two: another fp32 summation order; profiles/r5/late/): 2e-5 of
+    # the depth scale, still ~50x below the TF32 class
+    ("depth_predictor_v3.depths", "bf16x3"): 2.5e-03,
     ("depth_predictor_v3.densities", "bf16x3"): 2.3e-05,
     ("depth_predictor_v3.raw", "bf16x3"): 2.9e-05,
     ("depth_predictor_v4.depths", "bf16x3"): 2.0e-03,
