@@ -2,6 +2,10 @@
 images to a multiple of the patch size and rescale fx, fy accordingly."""
 from __future__ import annotations
 
+import torch
+
+_SCALES: dict = {}
+
 
 def apply_patch_shim_to_views(views: dict, patch_size: int) -> dict:
     _, _, _, h, w = views["image"].shape
@@ -10,10 +14,17 @@ def apply_patch_shim_to_views(views: dict, patch_size: int) -> dict:
     row = (h - h_new) // 2
     w_new = (w // patch_size) * patch_size
     col = (w - w_new) // 2
-    intrinsics = views["intrinsics"].clone()
-    intrinsics[:, :, 0, 0] *= w / w_new
-    intrinsics[:, :, 1, 1] *= h / h_new
-    return {**views, "image": views["image"][:, :, :, row:row + h_new, col:col + w_new], "intrinsics": intrinsics}
+    k = views["intrinsics"]
+    # fx *= w / w_new, fy *= h / h_new as ONE multiply by a cached [3, 3] scale (1 elsewhere: exact,
+    # and the same fp32 product as the in-place scalar multiplies) instead of clone + two launches
+    key = (k.device, k.dtype, k.shape[-1], w / w_new, h / h_new)
+    scale = _SCALES.get(key)
+    if scale is None:
+        scale = torch.ones(k.shape[-2:], dtype=k.dtype, device=k.device)
+        scale[0, 0] = w / w_new
+        scale[1, 1] = h / h_new
+        _SCALES[key] = scale
+    return {**views, "image": views["image"][:, :, :, row:row + h_new, col:col + w_new], "intrinsics": k * scale}
 
 
 def apply_patch_shim(batch: dict, patch_size: int) -> dict:
