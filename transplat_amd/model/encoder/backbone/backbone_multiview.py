@@ -8,7 +8,7 @@ import torch
 from einops import rearrange
 
 from ...utils.cam_param_encoder import cam_param_encoder
-from .multiview_transformer import MultiViewFeatureTransformer
+from .multiview_transformer import MultiViewFeatureTransformer, stacked_views
 from .unimatch import CNNEncoder, PositionEmbeddingSine, merge_splits, split_feature
 
 _IMAGENET_MEAN = (0.485, 0.456, 0.406)
@@ -102,5 +102,5 @@ class BackboneMultiview(torch.nn.Module):
             cur_features_list = feature_add_position_list(cur_features_list, attn_splits, self.feature_channels)
         with stage(None, "backbone_mvt"):
             cur_features_list = self.transformer(cur_features_list, attn_num_splits=attn_splits)
-        features = torch.stack(cur_features_list, dim=1)
+        features = stacked_views(cur_features_list)
         return [features, cnn_features]

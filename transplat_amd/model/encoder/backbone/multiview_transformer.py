@@ -7,6 +7,8 @@ AV, merge, roll back) is ONE gfx950 kernel call (transplat_amd.kernels.window_at
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -152,6 +154,21 @@ class TransformerBlock(nn.Module):
         return self.cross_attn_ffn._forward_fused(y, x, height, width, attn_num_splits, kv_shift=kv_shift)
 
 
+_ONE_COPY = os.environ.get("TSPLAT_MVT_ONE_COPY", "1") == "1"  # A/B knob for the single-copy output
+
+
+def stacked_views(features):
+    """torch.stack(features, dim=1), without a copy when the views already are the unbound views
+    of one contiguous [b, v, ...] tensor (MultiViewFeatureTransformer's two-view output)."""
+    base = features[0]._base
+    if (base is not None and base.is_contiguous() and base.dim() == features[0].dim() + 1
+            and base.shape[1] == len(features)
+            and all(f._base is base and f.data_ptr() == base[:, i].data_ptr() and f.shape == base[:, i].shape
+                    and f.stride() == base[:, i].stride() for i, f in enumerate(features))):
+        return base
+    return torch.stack(features, dim=1)
+
+
 def batch_features(features):
     """(reference :495-515) queries [N*B, ...] and the other N-1 views [N*B, N-1, ...]."""
     q, kv = [], []
@@ -194,7 +211,12 @@ class MultiViewFeatureTransformer(nn.Module):
             x = torch.cat(multi_view_features, dim=0).reshape(2 * b, c, -1).permute(0, 2, 1).contiguous()
             for layer in self.layers:
                 x = layer.forward_pair(x, h, w, attn_num_splits, kv_shift=b)
-            return [f.view(b, h, w, c).permute(0, 3, 1, 2).contiguous() for f in x.chunk(chunks=2, dim=0)]
+            # both views' NCHW maps in ONE permute copy, as views of a [b, v, c, h, w] tensor (the
+            # backbone stacks them without another copy, see stacked_views)
+            if not _ONE_COPY:
+                return [f.view(b, h, w, c).permute(0, 3, 1, 2).contiguous() for f in x.chunk(chunks=2, dim=0)]
+            stacked = x.view(2, b, h, w, c).permute(1, 0, 4, 2, 3).contiguous()
+            return list(stacked.unbind(1))
         concat0, concat1 = batch_features(multi_view_features)
         concat0 = concat0.reshape(num_views * b, c, -1).permute(0, 2, 1)  # [N*B, HW, C]
         concat1 = concat1.reshape(num_views * b, num_views - 1, c, -1).permute(0, 1, 3, 2)  # [N*B, N-1, HW, C]
