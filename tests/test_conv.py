@@ -346,7 +346,9 @@ def tf32_round(t: torch.Tensor) -> torch.Tensor:
 @pytest.mark.parametrize("n,ci,co,h,w,bias,act", WINO_CASES + [(1, 24, 48, 10, 96, True, "relu"),
                                                                (2, 40, 64, 22, 136, False, "none"),
                                                                (3, 32, 40, 36, 64, True, "gelu"),
-                                                               (2, 32, 32, 160, 160, True, "relu")])
+                                                               (2, 32, 32, 160, 160, True, "relu"),
+                                                               # 64-wide form + its 32 x 32 tail launch
+                                                               (2, 24, 84, 128, 128, True, "gelu")])
 def test_conv3x3_wino_bf16x3_kernel(device, monkeypatch, stage, form, n, ci, co, h, w, bias, act):
     """Winograd F(2x2, 3x3) in split-bf16 precision (tsplat_conv3x3_wino_bf16x3_fwd: hi*hi + hi*lo +
     lo*hi on bf16 MFMA, fp32 accumulation) against torch's conv2d in float64, with the launch's own

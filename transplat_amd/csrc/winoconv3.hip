@@ -863,8 +863,9 @@ static int pick_form(int n, int th, int tw, int co) {
 }
 
 template <int CB, int NB, int KS>
-static void launch(wino3::Args a, int blocks, bool staged, hipStream_t stream, hipEvent_t start, hipEvent_t stop) {
-    const int coblocks = (a.co + 32 * CB - 1) / (32 * CB);
+static void launch(wino3::Args a, int blocks, bool staged, hipStream_t stream, hipEvent_t start, hipEvent_t stop,
+                   int coblocks = -1) {
+    if (coblocks < 0) coblocks = (a.co - 32 * a.cob_base + 32 * CB - 1) / (32 * CB);
     if (staged)
         hipExtLaunchKernelGGL((wino3::conv_kernel<CB, NB, KS, true>), dim3(blocks, coblocks), dim3(256 * CB * KS), 0,
                               stream, start, stop, 0, a);
@@ -909,22 +910,24 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const
     a.res2 = residual2;
     a.cob_base = 0;
     int form = pick_form(n, a.th, a.tw, co);
-    const int ttiles = form == 3 || form == 4 ? 64 : 32;
-    // tile block: the widest of T x 1, T/2 x 2, T/4 x 4, T/8 x 8 with the fewest padded tiles
-    long best = -1;
-    for (int tbx = ttiles; tbx >= ttiles / 8; tbx /= 2) {
-        const int tby = ttiles / tbx;
-        const long padded = (long)((a.tw + tbx - 1) / tbx) * tbx * ((a.th + tby - 1) / tby) * tby;
-        if (best < 0 || padded < best) {
-            best = padded;
-            a.tbx = tbx;
+    // tile block: the widest of T x 1, T/2 x 2, T/4 x 4, T/8 x 8 with the fewest padded tiles; false
+    // where the staged region loads' R x C4 <= 72 (32-tile blocks) / 136 (64-tile blocks) fails
+    auto geometry = [&](int ttiles) {
+        long best = -1;
+        for (int tbx = ttiles; tbx >= ttiles / 8; tbx /= 2) {
+            const int tby = ttiles / tbx;
+            const long padded = (long)((a.tw + tbx - 1) / tbx) * tbx * ((a.th + tby - 1) / tby) * tby;
+            if (best < 0 || padded < best) {
+                best = padded;
+                a.tbx = tbx;
+            }
         }
-    }
-    a.tby = ttiles / a.tbx;
-    // the staged region loads assume R x C4 <= 72 (32-tile blocks) / 136 (64-tile blocks) float4 rows
-    if ((2 * a.tby + 2) * (a.tbx / 2 + 2) > (ttiles == 32 ? 72 : 136)) return TSPLAT_EINVAL;
-    a.bx = (a.tw + a.tbx - 1) / a.tbx;
-    a.by = (a.th + a.tby - 1) / a.tby;
+        a.tby = ttiles / a.tbx;
+        a.bx = (a.tw + a.tbx - 1) / a.tbx;
+        a.by = (a.th + a.tby - 1) / a.tby;
+        return (2 * a.tby + 2) * (a.tbx / 2 + 2) <= (ttiles == 32 ? 72 : 136);
+    };
+    if (!geometry(form == 3 || form == 4 ? 64 : 32)) return TSPLAT_EINVAL;
     const int blocks = n * a.bx * a.by;
     // staged input: float4 rows need a width that is a multiple of 4 and 16-B aligned sources
     bool staged = w % 4 == 0;
@@ -941,6 +944,18 @@ extern "C" int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const
         const int gx = std::max(1, std::min(blocks, (wgs + cob32 - 1) / cob32));
         hipExtLaunchKernelGGL(wino3::conv_persist_kernel, dim3(gx, cob32), dim3(256), 0, stream, ev.start, ev.stop, 0,
                               a, blocks);
+        TSPLAT_CHECK_LAUNCH();
+        return TSPLAT_OK;
+    }
+    // a 64-wide form over an output whose last 64-channel block is at most half used (the gaussian
+    // head's 168 -> 84: 44 of 128 columns padding): the full 64-channel blocks on it, the rest as
+    // 32 x 32 blocks (TSPLAT_WINO3_TAIL=0: off)
+    static const bool tail = !getenv("TSPLAT_WINO3_TAIL") || atoi(getenv("TSPLAT_WINO3_TAIL")) != 0;
+    if (form == 4 && tail && co > 64 && co % 64 != 0 && co % 64 <= 32) {
+        launch<2, 2, 1>(a, blocks, staged, stream, ev.start, nullptr, co / 64);
+        if (!geometry(32)) return TSPLAT_EINVAL;
+        a.cob_base = (co / 64) * 2;
+        launch<1, 1, 1>(a, n * a.bx * a.by, staged, stream, nullptr, ev.stop, 1);
         TSPLAT_CHECK_LAUNCH();
         return TSPLAT_OK;
     }
