@@ -161,7 +161,8 @@ def precision_label(dense_dtype: str, attn_dtype: str = "auto") -> str:
     corr = ("correlation table bf16x3 (split-bf16 GEMM), correlation gathers / norms / adapter / raster fp32"
             if dense_dtype == "bf16x3" else "correlation / norms / adapter / raster fp32")
     return (f"dense convs/GEMMs {dense}, window attention {attn}, {corr}"
-            + ("; DPT-head / stem / transposed convs on MIOpen exact fp32" if dense_dtype == "bf16x3" else ""))
+            + ("; DINOv2 attention bf16x3 up to 2048 tokens per call, exact fp32 above; DPT-head 3x3s on "
+               "MIOpen exact fp32, stem / transposed convs as exact fp32 GEMMs" if dense_dtype == "bf16x3" else ""))
 
 
 def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: str = "fp32", graph: bool = True,
