@@ -171,8 +171,10 @@ uv_coarse_kernel(Geo g, const float* __restrict__ feat, const float* __restrict_
 constexpr int kDedupWaves = 4;
 constexpr int kDedupMaxS = 4;  // D <= 256
 
-template <int S>
-__global__ void __launch_bounds__(kDedupWaves * 64)
+// WPE: waves per SIMD the register budget is sized for (5: 82 VGPRs, 1,280 of the production
+// launch's 2,048 workgroups resident; 6: 80 VGPRs with 2 spilled, 1,536 resident)
+template <int S, int WPE>
+__global__ void __launch_bounds__(kDedupWaves * 64, WPE)
 uv_coarse_dedup_kernel(Geo g, int nw, const float* __restrict__ feat, const float* __restrict__ cams,
                        const float* __restrict__ disp, float* __restrict__ out, int diag) {
     extern __shared__ unsigned smem[];
@@ -652,12 +654,26 @@ extern "C" int tsplat_uv_coarse_fwd(const float* feat, const float* cams, const 
     const char* env = getenv("TSPLAT_UV_COARSE_DIRECT");  // A/B switch: the sample-then-dot kernel
     if (S <= kDedupMaxS && lds <= 64 * 1024 && !(env && env[0] == '1')) {
         const dim3 grid(ceil_div(hw, kDedupWaves), 2 * batch), block(kDedupWaves * 64);
+        // 6 waves per SIMD (default; profiles/r5/late/corr_wpe.txt: b = 8 120.5 -> 111.4 us, b = 1 24.3 /
+        // 24.2 vs 24.2 / 24.6) or 5 (TSPLAT_CORR_WPE=5, the A/B knob)
+        const char* wenv = getenv("TSPLAT_CORR_WPE");
+        const bool w6 = !wenv || atoi(wenv) != 5;
+#define TSPLAT_UVC(SS)                                                                                           \
+    do {                                                                                                         \
+        if (w6)                                                                                                  \
+            hipLaunchKernelGGL((uv_coarse_dedup_kernel<SS, 6>), grid, block, lds, stream, g, nw, feat, cams, disp, \
+                               out, diag);                                                                       \
+        else                                                                                                     \
+            hipLaunchKernelGGL((uv_coarse_dedup_kernel<SS, 5>), grid, block, lds, stream, g, nw, feat, cams, disp, \
+                               out, diag);                                                                       \
+    } while (0)
         switch (S) {
-            case 1: hipLaunchKernelGGL(uv_coarse_dedup_kernel<1>, grid, block, lds, stream, g, nw, feat, cams, disp, out, diag); break;
-            case 2: hipLaunchKernelGGL(uv_coarse_dedup_kernel<2>, grid, block, lds, stream, g, nw, feat, cams, disp, out, diag); break;
-            case 3: hipLaunchKernelGGL(uv_coarse_dedup_kernel<3>, grid, block, lds, stream, g, nw, feat, cams, disp, out, diag); break;
-            default: hipLaunchKernelGGL(uv_coarse_dedup_kernel<4>, grid, block, lds, stream, g, nw, feat, cams, disp, out, diag); break;
+            case 1: TSPLAT_UVC(1); break;
+            case 2: TSPLAT_UVC(2); break;
+            case 3: TSPLAT_UVC(3); break;
+            default: TSPLAT_UVC(4); break;
         }
+#undef TSPLAT_UVC
     } else {
         hipLaunchKernelGGL(uv_coarse_kernel, dim3(hw, 2 * batch), dim3(kThreads), 0, stream, g, feat, cams, disp,
                            out);
