@@ -139,6 +139,37 @@ def test_mvt_gpu(device, dense, nv):
            f"mvt_v{nv} {dense}")
 
 
+def _mvt64(dev, nv, attn):
+    """The transformer at the encoder's 64 x 64 feature size (32 x 32 windows: the shapes where the
+    bf16x3 attention splits the keys and takes pre-split k / v from the projection)."""
+    from transplat_amd import kernels
+    from transplat_amd.model.encoder.backbone.multiview_transformer import MultiViewFeatureTransformer
+
+    t = canonical_init(MultiViewFeatureTransformer(num_layers=6, d_model=128, nhead=1, ffn_dim_expansion=4),
+                       seed=11).eval().to(dev)
+    feats = [seeded((1, 128, 64, 64), 210 + i).to(dev) for i in range(nv)]
+    with kernels.attention_precision(attn), torch.no_grad():
+        return torch.stack(t(feats, attn_num_splits=2), 1).cpu()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nv", [2, 3, 4])
+def test_mvt_attention_x3_views(device, nv):
+    """bf16x3 window attention inside the whole transformer for V = 2 (key-batch pairing), 3 and 4
+    (cross attention over V - 1 stacked key views, kv_views = V - 1) against the exact-fp32 attention
+    on the same weights and inputs, both in the bf16x3 dense mode. The bound is the x3 class (the
+    2-view 16 x 16 golden's 2.7e-4 whole-model error, x 4); attending to the wrong key views
+    (round 5's kv_views = 1 bug) gives O(1)."""
+    from transplat_amd import kernels
+
+    with kernels.dense_precision("bf16x3"):
+        with kernels.attention_precision("bf16x3"):
+            assert kernels.attention_x3_ready(nv, 64, 64, max(nv - 1, 1), 2)
+        ref = _mvt64(device, nv, "fp32")
+        out = _mvt64(device, nv, "bf16x3")
+    _close(out, ref, 1.1e-3, f"mvt64 v{nv} bf16x3 vs fp32 attention")
+
+
 # ------------------------------------------------------------------ backbone (CNN + cam + MVT)
 def _backbone(dev):
     from transplat_amd.model.encoder.backbone.backbone_multiview import BackboneMultiview

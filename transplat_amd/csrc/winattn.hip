@@ -44,12 +44,15 @@ constexpr float kMaskLog2 = -100.0f * kLog2e;  // the reference's -100 mask, log
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// v_max3_f32 as written: fmaxf() on MFMA results makes the compiler insert canonicalising
-// v_max_f32 x, x first (scores are finite products, no signalling NaNs to quieten)
+// max of three scores as ONE gfx950 v_maximum3_f32 (IEEE-2019 maximum: NaN-propagating, so no
+// canonicalising v_max_f32 x, x ahead of it as fmaxf's maxnum needs on MFMA results; the scores are
+// finite, so the two agree). Compiler-visible on purpose: the hazard recognizer then pads the
+// MFMA -> VALU read of the accumulators (s_nop 11 after a 32x32x16 chain). Round 5's inline-asm
+// v_max3_f32 was invisible to it and read the last MFMA's destination 0 wait states after issue
+// (a partial score, now and then: the bf16 v2 kernel's run-to-run drift). tests/test_isa_hazards.py
+// checks every built code object for such a read.
 __device__ __forceinline__ float max3_raw(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
 }
 
 // max / sum of lanes l and l ^ 32 (the two half-waves), in VALU via v_permlane32_swap instead of

@@ -482,7 +482,7 @@ def linear_kv_x3(x, weight, x3_from: int):
 
 
 def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, merge_weight, ln, residual=None,
-                    kv_shift: int = 0, kv_x3=None):
+                    kv_shift: int = 0, kv_x3=None, kv_views: int = 1):
     """norm(window_attention(q, k, v) merge_weight^T) [+ residual] for the fp32 transformer layer.
     Where the attention kernel splits the keys (b = 1 at 64x64), the combine of its partials runs
     in the merge kernel's operand staging (tsplat_win_attn_partials_fwd +
@@ -490,14 +490,17 @@ def attention_merge(q, k, v, h: int, w: int, num_splits: int, with_shift: bool, 
     otherwise window_attention + fused_linear. kv_shift: query batch i attends to the keys /
     values of batch (i + kv_shift) % B (the two-view cross pairing without a swapped copy). kv_x3:
     the bf16x3 kernel's pre-split [kh | kl | vh | vl] operand (linear_kv_x3) in place of k / v
-    (None), for shapes where attention_x3_ready() holds."""
+    (None), for shapes where attention_x3_ready() holds; kv_views = the key views per query batch it
+    holds ([4, B * kv_views * L * 128], i.e. k / v of shape [B, kv_views, L, 128])."""
     lib = _lib.load()
     b, l, c = q.shape
     if kv_x3 is not None:
-        if not attention_x3_ready(b, h, w, 1, num_splits):
+        if not attention_x3_ready(b, h, w, kv_views, num_splits):
             raise ValueError("kv_x3 given for a shape / precision that does not run the bf16x3 kernel")
+        if kv_x3.numel() != 4 * b * kv_views * l * c:
+            raise ValueError(f"kv_x3 holds {kv_x3.numel()} values, not 4 x {b} x {kv_views} key views x {l} x {c}")
         return _merge_partials(lib, q, None, None, h, w, num_splits, with_shift, merge_weight, ln, residual,
-                               kv_shift, 1, kv_x3)
+                               kv_shift, kv_views, kv_x3)
     m = 1 if k.dim() == 3 else k.shape[1]
     fp32 = q.dtype == k.dtype == v.dtype == torch.float32
     wl = (h // num_splits) * (w // num_splits)

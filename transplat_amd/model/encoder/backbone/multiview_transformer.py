@@ -61,9 +61,13 @@ class TransformerLayer(nn.Module):
         batch (i + kv_shift) % B (the swap is index arithmetic in the attention kernel)."""
         K = kernels
         kv_x3 = key = value = None
-        if source.dim() == 3 and K.attention_x3_ready(source.shape[0], height, width, 1, attn_num_splits):
+        # key views per query batch: 1 (self attention, the two-view pairing) or V - 1 (cross
+        # attention with the other views stacked, target [B, V-1, L, C])
+        kv_views = target.shape[1] if target.dim() == 4 else 1
+        if source.dim() == 3 and K.attention_x3_ready(source.shape[0], height, width, kv_views, attn_num_splits):
             # bf16x3 attention: the k / v column blocks leave the projection as the kernel's bf16 hi / lo
-            # operand (no fp32 k / v, no split pass)
+            # operand (no fp32 k / v, no split pass); for V - 1 key views the buffer holds
+            # [B, V-1, L, 128] per part, the layout the kernel indexes with key_views = V - 1
             if target is source:
                 (query,), kv_x3 = K.linear_kv_x3(source, self._cat_weights(("q_proj", "k_proj", "v_proj")), 1)
             else:
@@ -79,7 +83,7 @@ class TransformerLayer(nn.Module):
                 query = K.fused_linear(source, self.q_proj.weight, out_dtype=od)
                 key, value = K.fused_linear(target, self._cat_weights(("k_proj", "v_proj")), split=True, out_dtype=od)
         ln1 = (self.norm1.weight, self.norm1.bias, self.norm1.eps)
-        x3 = {"kv_x3": kv_x3} if kv_x3 is not None else {}
+        x3 = {"kv_x3": kv_x3, "kv_views": kv_views} if kv_x3 is not None else {}
         if self.no_ffn:
             return K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
                                      self.merge.weight, ln1, residual=source, kv_shift=kv_shift, **x3)
