@@ -98,6 +98,10 @@ def test_evaluate_cli_small_index(device):
         assert summary["scenes"] == 2 and summary["views"] == 6
         assert summary["psnr"] == summary["psnr"]  # finite
         assert summary["dense_dtype"] == "bf16x3" and summary["graph"] == (not extra)
+        assert "bf16x3" in summary["precision"]
+        # graph capture (warmup + capture) is reported apart from the steady per-scene time
+        assert summary["steady_scenes"] + summary["capture_scenes"] == 2
+        assert (summary["capture_scenes"] >= 1) == (not extra)
         runs[bool(extra)] = summary
     print(f"evaluate: graphed {runs[False]['psnr']:.4f} dB in {runs[False]['seconds']:.4f} s, "
           f"eager {runs[True]['psnr']:.4f} dB")

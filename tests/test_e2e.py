@@ -262,8 +262,12 @@ def test_tuned_gemms_keep_outputs(device):
     # is bounded by that size and by how many values move more than 1e-3 (1.5e-4 of them in round 5),
     # not tighter.
     d = (tuned[2] - ref[2]).abs()
+    n_big = int((d > 1e-2).sum().item())
+    print(f"  values moving > 1e-3: {(d > 1e-3).float().mean().item():.2e} of {d.numel()}; > 1e-2: {n_big}")
     assert rel(tuned[0], ref[0]) < 4e-4 and rel(tuned[1], ref[1]) < 3e-6
     assert d.max().item() < 3e-2 and (d > 1e-3).float().mean().item() < 1e-3
+    # a flipped blend decision moves single pixels; a systematic shift would move many past 1e-2
+    assert n_big <= 8
     assert d.mean().item() < 3e-6
 
 

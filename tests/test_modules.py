@@ -157,9 +157,9 @@ def _mvt64(dev, nv, attn):
 def test_mvt_attention_x3_views(device, nv):
     """bf16x3 window attention inside the whole transformer for V = 2 (key-batch pairing), 3 and 4
     (cross attention over V - 1 stacked key views, kv_views = V - 1) against the exact-fp32 attention
-    on the same weights and inputs, both in the bf16x3 dense mode. The bound is the x3 class (the
-    2-view 16 x 16 golden's 2.7e-4 whole-model error, x 4); attending to the wrong key views
-    (round 5's kv_views = 1 bug) gives O(1)."""
+    on the same weights and inputs, both in the bf16x3 dense mode. Bound: 2x the measured 2.0e-4
+    (profiles/r6/pytest_r6a.log); attending to the wrong key views (round 5's kv_views = 1 bug)
+    gives O(1)."""
     from transplat_amd import kernels
 
     with kernels.dense_precision("bf16x3"):
@@ -167,7 +167,7 @@ def test_mvt_attention_x3_views(device, nv):
             assert kernels.attention_x3_ready(nv, 64, 64, max(nv - 1, 1), 2)
         ref = _mvt64(device, nv, "fp32")
         out = _mvt64(device, nv, "bf16x3")
-    _close(out, ref, 1.1e-3, f"mvt64 v{nv} bf16x3 vs fp32 attention")
+    _close(out, ref, 4e-4, f"mvt64 v{nv} bf16x3 vs fp32 attention")
 
 
 # ------------------------------------------------------------------ backbone (CNN + cam + MVT)

@@ -387,6 +387,19 @@ def test_raster_graph_replay_with_new_inputs(device):
 
 
 @pytest.mark.gpu
+def test_raster_large_image_beyond_64k_scatter_lds(device):
+    """1280 x 1280 = 6,400 tiles: the scatter kernel's 3 T per-tile counters (75 KB) exceed the
+    default 64 KB dynamic-LDS limit, which the launch raises (up to gfx950's 160 KB). Round 5
+    returned EINVAL above 5,461 tiles."""
+    hw = (1280, 1280)
+    g = S.make_gaussians(1, image_shape=(64, 64))
+    cams = _target_cams(S.make_batch(1, num_target=1, image_shape=hw), hw)
+    color, radii, ref, counts = _run_both(g, cams, hw, 1, 3, device)
+    parity_report(color, radii, ref, tag=" (1280x1280, 6400 tiles)")
+    assert max(counts) > 0
+
+
+@pytest.mark.gpu
 def test_raster_dtu_stress_parity(device):
     """C5 stress: G = 3 x 512 x 384 = 589,824 Gaussians from three context views rendered at
     512x384 (32 x 24 tiles): long per-tile lists exercise the in-global sort path of the render

@@ -62,11 +62,13 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, const floatx16& acc
     __syncthreads();
     const int tile = blockIdx.x + gridDim.x * blockIdx.y;
     if (p.zsplit > 1) {
-        // this workgroup's partial tile -> workspace with write-through (sc1) stores, so no release
-        // fence; drained by every wave, then ONE lane takes an arrival ticket. The tile's last
-        // arriver: ONE agent-scope acquire (its L1 may hold stale lines of the other partials), then
-        // plain loads (cdna_hip_programming.md §5 "In-launch split-K reduction"; a __threadfence()
-        // in every thread instead made the C2 step 5 % slower)
+        // this workgroup's partial tile -> workspace with agent-scope (write-through) stores, drained
+        // by every wave; after the barrier ONE lane takes an arrival ticket with an agent-scope
+        // RELEASE (cumulative over the workgroup's stores through the barrier: the HIP memory model's
+        // publication, not only gfx9's write-through behaviour). The tile's last arriver: ONE
+        // agent-scope acquire (its L1 may hold stale lines of the other partials), then plain loads
+        // (cdna_hip_programming.md §5 "In-launch split-K reduction"; a __threadfence() in every
+        // thread instead made the C2 step 5 % slower)
         typedef __attribute__((address_space(1))) unsigned gu32;
         unsigned* mine = reinterpret_cast<unsigned*>(p.part + ((size_t)tile * p.zsplit + blockIdx.z) * 1024);
         for (int idx = threadIdx.x; idx < 1024; idx += blockDim.x) {
@@ -78,7 +80,7 @@ __device__ __forceinline__ void tile_epilogue(const Args& p, const floatx16& acc
         __syncthreads();
         int* flag = reinterpret_cast<int*>(sred + ksplit * 1024);  // one LDS word past the partials
         if (threadIdx.x == 0) {
-            const int t = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int t = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             const bool last = t == p.zsplit - 1;
             if (last) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");

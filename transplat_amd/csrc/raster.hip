@@ -43,6 +43,7 @@ constexpr int kTile = 16;                 // BLOCK_X = BLOCK_Y of the reference 
 constexpr int kTileThreads = kTile * kTile;
 constexpr int kSortCap = 4096;            // tile lists up to this length are sorted in LDS
 constexpr int kPreThreads = 256;
+constexpr size_t kMaxLdsBytes = 160 * 1024;  // gfx950 LDS per workgroup
 constexpr int kRecBytes = 64;             // per-(view, Gaussian) record (Workspace::rec)
 constexpr int kRecFields = 9;             // x, y, conic a b c, opacity, r g b
 
@@ -976,7 +977,16 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
         const int rows = (p.tiles_y + 1) / 3;
         p.view_rot = (r && !strcmp(r, "0")) ? 0 : rows * p.tiles_x;
     }
-    if ((size_t)p.T * 3 * sizeof(uint32_t) > 64 * 1024) return TSPLAT_EINVAL;  // scatter's LDS
+    // every argument check before the first launch (a rejected call queues nothing)
+    if (3 * p.M > kMaxShFloats || p.vps > 32) return TSPLAT_EINVAL;
+    // scatter keeps 3 T uint32 of per-tile counters in LDS: up to gfx950's 160 KB per workgroup
+    // (13,653 16x16 tiles, about 1860 x 1860 px); above 64 KB the kernel's dynamic-LDS limit is raised
+    const size_t scatter_lds = (size_t)p.T * 3 * sizeof(uint32_t);
+    if (scatter_lds > kMaxLdsBytes) return TSPLAT_EINVAL;
+    if (scatter_lds > 64 * 1024 &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(&scatter_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)scatter_lds) != hipSuccess)
+        return TSPLAT_EINVAL;
     Workspace ws = carve(workspace, p.G, p.V, p.T, p.capacity, nullptr);
 
     TSPLAT_PROF_BEGIN(prof::kRasterAll, stream);
@@ -987,7 +997,6 @@ extern "C" int tsplat_raster_fwd(const tsplat_raster_desc* d, const float* means
         hipLaunchKernelGGL(zero_kernel, dim3(blocks), dim3(256), 0, stream, (uint4*)ws.counts, n4);
         TSPLAT_CHECK_LAUNCH();
     }
-    if (3 * p.M > kMaxShFloats || p.vps > 32) return TSPLAT_EINVAL;
     const int scenes = p.V / p.vps;
     // a wave's SH block starts at 3 M (scene G + 64 k) floats: 16-byte aligned when the base is
     // and 3 M G is a multiple of 4 (or there is one scene)

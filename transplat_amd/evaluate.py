@@ -33,6 +33,7 @@ class SceneResult:
     psnr: float
     n_views: int
     seconds: float
+    capture: bool = False  # the step captured its hipGraph (warmup + capture inside `seconds`)
 
 
 def load_index(path: str | Path) -> list[tuple[str, dict]]:
@@ -48,9 +49,9 @@ def shard(items: list, rank: int, world: int) -> list[tuple[int, object]]:
 
 
 def gather_results(local: list[SceneResult], device: torch.device, world: int) -> list[SceneResult]:
-    """One all_gather of [n_local_max, 4] fp32 rows (padded with scene_idx = -1)."""
-    rows = torch.tensor([[r.scene_idx, r.psnr, r.n_views, r.seconds] for r in local], dtype=torch.float32,
-                        device=device).reshape(-1, 4)
+    """One all_gather of [n_local_max, 5] fp32 rows (padded with scene_idx = -1)."""
+    rows = torch.tensor([[r.scene_idx, r.psnr, r.n_views, r.seconds, float(r.capture)] for r in local],
+                        dtype=torch.float32, device=device).reshape(-1, 5)
     if world == 1:
         gathered = [rows]
     else:
@@ -58,7 +59,7 @@ def gather_results(local: list[SceneResult], device: torch.device, world: int) -
         counts = [torch.zeros_like(n) for _ in range(world)]
         dist.all_gather(counts, n)
         nmax = int(max(c.item() for c in counts))
-        pad = torch.full((nmax, 4), -1.0, device=device)
+        pad = torch.full((nmax, 5), -1.0, device=device)
         pad[: rows.shape[0]] = rows
         gathered = [torch.empty_like(pad) for _ in range(world)]
         dist.all_gather(gathered, pad)
@@ -66,7 +67,7 @@ def gather_results(local: list[SceneResult], device: torch.device, world: int) -
     for g in gathered:
         for row in g.cpu().tolist():
             if row[0] >= 0:
-                out.append(SceneResult(int(row[0]), row[1], int(row[2]), row[3]))
+                out.append(SceneResult(int(row[0]), row[1], int(row[2]), row[3], row[4] > 0.5))
     return sorted(out, key=lambda r: r.scene_idx)
 
 
@@ -86,6 +87,7 @@ class GraphedSteps:
 
     def __init__(self, model, max_graphs: int = 4):
         self.model, self.max_graphs, self.graphs = model, max_graphs, {}
+        self.last_captured = False  # the last call captured a graph (its time includes warmup + capture)
 
     @staticmethod
     def signature(batch) -> tuple:
@@ -103,6 +105,7 @@ class GraphedSteps:
 
         sig = self.signature(batch)
         g = self.graphs.get(sig)
+        self.last_captured = g is None
         if g is None:
             if len(self.graphs) >= self.max_graphs:
                 self.graphs.pop(next(iter(self.graphs)))
@@ -111,12 +114,16 @@ class GraphedSteps:
 
 
 class _Pending:
-    """Per-scene results held on the device until the shard's single synchronisation."""
+    """Per-scene results held on the device until the shard's single synchronisation. After each
+    scene a device-side copy of the rasterizer's sticky overflow flag is kept, so an overflow found
+    at the end names the first scene that raised it."""
 
     def __init__(self, device: torch.device):
         self.device, self.rows = device, []
 
     def run(self, idx: int, step, batch: dict) -> None:
+        from .model.decoder.hip_splatting import status_tensor
+
         gt = batch["target"]["image"][0]
         if self.device.type == "cuda":
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -124,21 +131,28 @@ class _Pending:
             color = step(batch)
             psnr = compute_psnr(gt.to(color.device), color[0]).mean()  # before a replay reuses color
             e1.record()
-            self.rows.append((idx, psnr, int(color.shape[1]), (e0, e1)))
+            st = status_tensor(self.device)
+            self.rows.append((idx, psnr, int(color.shape[1]), (e0, e1), getattr(step, "last_captured", False),
+                              st.clone() if st is not None else None))
         else:
             t0 = time.perf_counter()
             color = step(batch)
             psnr = compute_psnr(gt.to(color.device), color[0]).mean()
-            self.rows.append((idx, psnr, int(color.shape[1]), time.perf_counter() - t0))
+            self.rows.append((idx, psnr, int(color.shape[1]), time.perf_counter() - t0, False, None))
 
     def results(self) -> list[SceneResult]:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
-            _raster_status(self.device)  # a capacity overflow must not become a silent wrong-image PSNR
+            # a capacity overflow must not become a silent wrong-image PSNR: name the first scene
+            bad = [r[0] for r in self.rows if r[5] is not None and int(r[5].item()) != 0]
+            if bad:
+                _raster_status(self.device)  # clears the sticky flag and raises
+                raise RuntimeError(f"tsplat_raster_fwd: instance capacity exceeded (first at scene {bad[0]})")
+            _raster_status(self.device)
         out = []
-        for idx, psnr, nv, t in self.rows:
+        for idx, psnr, nv, t, cap, _ in self.rows:
             sec = t[0].elapsed_time(t[1]) / 1e3 if isinstance(t, tuple) else t
-            out.append(SceneResult(idx, float(psnr.item()), nv, sec))
+            out.append(SceneResult(idx, float(psnr.item()), nv, sec, bool(cap)))
         return out
 
 
@@ -169,12 +183,18 @@ def evaluate_stream(step: Callable[[dict], torch.Tensor], examples, device: torc
 
 
 def summarize(results: list[SceneResult]) -> dict:
+    """PSNR over every scene; `seconds` over the steady scenes only (a scene whose step captured a
+    hipGraph carries the warmup and the capture, reported apart as `capture_seconds`)."""
     n = len(results)
+    steady = [r for r in results if not r.capture]
     return {
         "scenes": n,
         "psnr": sum(r.psnr for r in results) / max(n, 1),
         "views": sum(r.n_views for r in results),
-        "seconds": sum(r.seconds for r in results),
+        "seconds": sum(r.seconds for r in steady),
+        "steady_scenes": len(steady),
+        "capture_scenes": n - len(steady),
+        "capture_seconds": sum(r.seconds for r in results if r.capture),
     }
 
 
@@ -201,7 +221,8 @@ def main(argv=None):
     ap.add_argument("--index", required=True)
     ap.add_argument("--checkpoint", default=None, help="reference Lightning checkpoint (loaded weights_only)")
     ap.add_argument("--dense-dtype", choices=["fp32", "bf16x3", "bf16"], default="bf16x3",
-                    help="dense-layer precision; bf16x3 = the bench's default (>= the reference's TF32)")
+                    help="dense-layer precision; bf16x3 = the bench's default (>= the reference's TF32); "
+                         "fp32 = the exact-fp32 parity path the module goldens pin")
     ap.add_argument("--no-graph", action="store_true", help="eager test_step per scene instead of the replayed hipGraph")
     ap.add_argument("--limit", type=int, default=None, help="first N scenes of the index")
     ap.add_argument("--data-root", action="append", default=None,
@@ -216,7 +237,7 @@ def main(argv=None):
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=device)
-    from .e2e import build_model
+    from .e2e import build_model, precision_label
 
     from .gemm_tuning import use_tuned_gemms
 
@@ -244,7 +265,8 @@ def main(argv=None):
     if rank == 0:
         summary = summarize(results)
         summary.update({"index": str(args.index), "world": world, "weights": args.checkpoint or "synthetic",
-                        "data": data, "dense_dtype": args.dense_dtype, "graph": not args.no_graph})
+                        "data": data, "dense_dtype": args.dense_dtype, "graph": not args.no_graph,
+                        "precision": precision_label(args.dense_dtype)})
         print(json.dumps(summary), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -721,6 +721,15 @@ _ZSPLIT_SLAB = 1 << 20
 
 
 def _zsplit_counters(device, tiles: int):
+    """A range of `tiles` zeroed arrival counters for one zsplit launch (its last arrivers reset them
+    to 0, so a range is clean again once its launch has finished). Ranges rotate through one slab per
+    device, in call order: two launches share counters only if 2^20 tiles of other launches were
+    handed out between them, i.e. hundreds of steps apart -- never two launches of one step, which
+    are the only ones that can run concurrently (the branches' streams join within the step; graph
+    replays are ordered on one stream). One slab per stream instead would have to be allocated inside
+    a capture (the capture stream is new), i.e. from the graph's private pool."""
+    if tiles > _ZSPLIT_SLAB // 16:
+        raise ValueError(f"zsplit launch of {tiles} tiles exceeds the counter slab's per-launch share")
     slab = _ZSPLIT_CNT.get(device)
     if slab is None:
         slab = [torch.zeros(_ZSPLIT_SLAB, dtype=torch.int32, device=device), 0]

@@ -225,6 +225,12 @@ def num_rendered(device) -> int:
     return int(ws[off:off + 4].view(torch.int32).item())
 
 
+def status_tensor(device):
+    """The device's sticky overflow flag (int32 [1]; None before the first rasterize) -- read
+    without a sync by copying it on the stream."""
+    return _STATE.status.get((device.type, device.index))
+
+
 def check_status(device) -> None:
     """Raise if any rasterizer call on `device` overflowed its instance capacity (syncs)."""
     st = _STATE.status.get((device.type, device.index))
