@@ -28,6 +28,7 @@
  * bit for bit on identical inputs. Compile with -O2 -ffp-contract=off (see oracle/Makefile).
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -569,6 +570,12 @@ long tsplat_ref_raster_view_literal(int G, int H, int W, int M, int deg, const f
 
     const size_t hwn = (size_t)H * W;
     const float a_min = 1.0f / 255.0f;
+    /* diagnostics: TSPLAT_REF_DEBUG_PIXEL=x,y prints that pixel's flagged-mode blend, entry by entry */
+    int dbx = -1, dby = -1;
+    {
+        const char* e = getenv("TSPLAT_REF_DEBUG_PIXEL");
+        if (e && sscanf(e, "%d,%d", &dbx, &dby) != 2) dbx = dby = -1;
+    }
 #pragma omp parallel for schedule(dynamic)
     for (int t = 0; t < T; ++t) {
         const int tx = t % tiles_x, ty = t / tiles_x;
@@ -619,6 +626,10 @@ long tsplat_ref_raster_view_literal(int G, int H, int W, int M, int deg, const f
                     const double ad = fmin(0.99, q->op * exp(pd));
                     const double ma = 4.0 * fabs((double)alpha - ad) + (double)alpha * (mp + 8.0 * kEps);
                     if (fabs((double)alpha - (double)a_min) <= ma) flag |= kFlagAlpha;
+                    if (pxi == dbx && pyi == dby)
+                        fprintf(stderr, "dbg k=%ld g=%u power=%.9g pd=%.9g mp=%.3g S=%.3g alpha=%.9g ad=%.9g ma=%.3g "
+                                "T=%.9g flag=%d\n", k - offs[t], (unsigned)(keys[k] & 0xffffffffu), power, pd, mp, S,
+                                alpha, ad, ma, Tr, flag);
                     if (alpha < a_min) continue;
                     const float test_T = Tr * (1 - alpha);
                     const double tTd = Td * (1.0 - ad);

@@ -392,7 +392,7 @@ def test_raster_large_image_beyond_64k_scatter_lds(device):
     default 64 KB dynamic-LDS limit, which the launch raises (up to gfx950's 160 KB). Round 5
     returned EINVAL above 5,461 tiles."""
     hw = (1280, 1280)
-    g = S.make_gaussians(1, image_shape=(64, 64))
+    g = S.make_gaussians(1, image_shape=(128, 128))  # 32,768 Gaussians (8,192 left 10 ambiguous radii: 1.2e-3)
     cams = _target_cams(S.make_batch(1, num_target=1, image_shape=hw), hw)
     color, radii, ref, counts = _run_both(g, cams, hw, 1, 3, device)
     parity_report(color, radii, ref, tag=" (1280x1280, 6400 tiles)")

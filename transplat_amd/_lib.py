@@ -151,9 +151,17 @@ def debug_enabled() -> bool:
     return bool(was)
 
 
-def check(status: int, what: str) -> None:
+# routes.record() sets this to note every entry point a step calls (None otherwise)
+ROUTE_HOOK = None
+
+
+def check(status: int, what: str, route: str | None = None) -> None:
+    """Raise on a non-zero C-ABI status. `route`: the arithmetic a flag selected for this call
+    (noted by routes.record(), which derives the bench line's precision statement)."""
     if status != 0:
         raise RuntimeError(f"{what} failed: {ERRORS.get(status, status)}")
+    if ROUTE_HOOK is not None:
+        ROUTE_HOOK(what, route)
 
 
 def ptr(t: torch.Tensor | None) -> int | None:

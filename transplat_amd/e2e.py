@@ -151,18 +151,25 @@ def _copy_batch(dst, src):
 
 
 def precision_label(dense_dtype: str, attn_dtype: str = "auto") -> str:
-    """What runs in which arithmetic, for the bench line's workload string."""
+    """The precision MODES a step runs under (what the model was asked for); route_label() states
+    what the step then actually launched."""
     from .kernels import auto_attention
 
     attn = attn_dtype if attn_dtype != "auto" else auto_attention(dense_dtype)
-    attn = {"bf16x3": "bf16x3 (split-bf16 products, fp32 softmax)"}.get(attn, attn)
     dense = {"fp32": "exact fp32", "bf16x3": "bf16x3 (split-bf16 products, fp32 accumulation; >= TF32)",
              "bf16": "bf16 (autocast)"}[dense_dtype]
-    corr = ("correlation table bf16x3 (split-bf16 GEMM), correlation gathers / norms / adapter / raster fp32"
-            if dense_dtype == "bf16x3" else "correlation / norms / adapter / raster fp32")
-    return (f"dense convs/GEMMs {dense}, window attention {attn}, {corr}"
-            + ("; DINOv2 attention bf16x3 up to 2048 tokens per call, exact fp32 above; DPT-head 3x3s on "
-               "MIOpen exact fp32, stem / transposed convs as exact fp32 GEMMs" if dense_dtype == "bf16x3" else ""))
+    return f"dense mode {dense}, window-attention mode {attn}"
+
+
+def route_label(model, data) -> str:
+    """Run one eager step under routes.record() and state what ran in which arithmetic (every HIP
+    entry point and every library GEMM / convolution the step reached, with launch counts)."""
+    from . import routes
+
+    with torch.no_grad(), routes.record() as r:
+        model.test_step(data)
+    torch.cuda.synchronize()
+    return r.label()
 
 
 def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: str = "fp32", graph: bool = True,
@@ -185,6 +192,6 @@ def build_e2e_workload(batch: int, device, scene_offset: int = 0, dense_dtype: s
         "eager_step": lambda: model.test_step(data),
         "views_per_step": batch * data["target"]["near"].shape[1],
         "workload": f"e2e TranSplat test_step: {batch} scene(s) x (2 ctx -> 3 tgt) 256x256; "
-                    + precision_label(dense_dtype, attn_dtype),
+                    + precision_label(dense_dtype, attn_dtype) + "; launched per step: " + route_label(model, data),
     }
     return step, info, model

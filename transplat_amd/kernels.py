@@ -370,6 +370,12 @@ def _lin_precision_flag() -> int:
     return _LIN_BF16X3 if _LINF3 and _DENSE == "bf16x3" else 0
 
 
+def _lin_route(flags: int) -> str:
+    """The arithmetic of a tsplat_linear_f32_* call with these flags (routes.record)."""
+    r = "bf16x3" if flags & _LIN_BF16X3 else "exact fp32"
+    return r + (", bf16 I/O" if flags & (_LIN_X_BF16 | _LIN_OUT_BF16) else "")
+
+
 def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, residual=None, split: bool = False,
                  gelu_in: bool = False, relu_in: bool = False, res_pre_ln: bool = False, out_dtype=torch.float32):
     """epilogue([x1 | x2] weight^T) in one exact-fp32 MFMA launch (tsplat_linear_f32_fwd; bf16x3
@@ -415,7 +421,7 @@ def fused_linear(x1, weight, x2=None, bias=None, gelu: bool = False, ln=None, re
     rc = lib.tsplat_linear_f32_fwd(_lib.ptr(a), k1, _lib.ptr(b), k2, _lib.ptr(_f32(weight)), _lib.ptr(bb),
                                    _lib.ptr(g), _lib.ptr(bt), eps, _lib.ptr(res), _lib.ptr(out), m * 128, m, n,
                                    flags, _lib.stream_ptr(x1.device))
-    _lib.check(rc, "tsplat_linear_f32_fwd")
+    _lib.check(rc, "tsplat_linear_f32_fwd", _lin_route(flags))
     if split:
         return [t.reshape(*lead, 128) for t in out.unbind(0)]
     return out.reshape(*lead, n)
@@ -476,7 +482,7 @@ def linear_kv_x3(x, weight, x3_from: int):
     kv = torch.empty((2 * (nb - x3_from), m * 128), dtype=torch.bfloat16, device=x.device)
     _lib.check(lib.tsplat_linear_f32_split_x3_fwd(_lib.ptr(a), k1, _lib.ptr(_f32(weight)), _lib.ptr(out), _lib.ptr(kv), m,
                                                   n, x3_from, _lin_precision_flag(), _lib.stream_ptr(x.device)),
-               "tsplat_linear_f32_split_x3_fwd")
+               "tsplat_linear_f32_split_x3_fwd", _lin_route(_lin_precision_flag()))
     blocks = [t.reshape(*lead, 128) for t in out.unbind(0)] if out is not None else []
     return blocks, kv
 
@@ -567,7 +573,7 @@ def _merge_partials(lib, q, k, v, h, w, num_splits, with_shift, merge_weight, ln
     rc = lib.tsplat_linear_f32_attn_merge_fwd(_lib.ptr(ws), b, h, w, m, num_splits, int(with_shift),
                                               _lib.ptr(_f32(merge_weight)), _lib.ptr(g), _lib.ptr(bt), eps,
                                               _lib.ptr(res), _lib.ptr(out), n, flags, _lib.stream_ptr(q.device))
-    _lib.check(rc, "tsplat_linear_f32_attn_merge_fwd")
+    _lib.check(rc, "tsplat_linear_f32_attn_merge_fwd", _lin_route(flags))
     return out
 
 
@@ -616,7 +622,7 @@ def layer_norm128(y, norm, residual=None, out_dtype=None):
                                       _lib.ptr(_f32(norm.weight)), _lib.ptr(_f32(norm.bias)), float(norm.eps),
                                       _lib.ptr(out), int(out_dtype == torch.bfloat16), yc.numel() // 128,
                                       _lib.stream_ptr(y.device))
-    _lib.check(rc, "tsplat_layer_norm128_fwd")
+    _lib.check(rc, "tsplat_layer_norm128_fwd", "bf16 I/O, fp32 statistics" if yc.dtype == torch.bfloat16 else "fp32")
     return out
 
 
@@ -771,9 +777,10 @@ def conv_pack_weight(weight):
     return packed
 
 
-def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsample: bool = False) -> bool:
+def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsample: bool = False,
+                     force: bool = False) -> bool:
     """True when tsplat_conv2d_f32_fwd takes this convolution and (mode "auto") it is a
-    latency-bound one where the direct kernel beats MIOpen."""
+    latency-bound one where the direct kernel beats MIOpen (force: whenever it takes it)."""
     if _CONV_MODE == "off" or not x.is_cuda or torch.is_autocast_enabled("cuda"):
         return False
     if x.dtype != torch.float32 or weight.dtype != torch.float32 or x.dim() != 4:
@@ -793,7 +800,7 @@ def conv2d_direct_ok(x, weight, stride: int = 1, padding=None, c2: int = 0, upsa
     c1 = x.shape[1]
     if pad != k // 2 or ci != c1 + c2 or c1 % 2 or c2 % 2:
         return False
-    if _CONV_MODE == "all":
+    if _CONV_MODE == "all" or force:
         return True
     h, w = x.shape[2] * (2 if upsample else 1), x.shape[3] * (2 if upsample else 1)
     npx = x.shape[0] * (h // stride) * (w // stride)
@@ -947,7 +954,8 @@ def wino_pack_weight(weight):
 WINO_MAX_CI_PAD = 1024  # winoconv.hip kMaxCiPad: input channels (padded to 16) of one launch
 
 
-def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=(), vs_miopen=False) -> bool:
+def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=(), vs_miopen=False,
+                    force=False) -> bool:
     """True when tsplat_conv3x3_wino_f32_fwd takes conv2d(x, weight) on the NCHW map x and (mode
     "auto") it is one of the 3x3s where it beats MIOpen's kernels (tools/bench_wino.py): above the
     direct kernel's FLOP range (unless `vs_miopen`: the caller's alternative is MIOpen, which the
@@ -970,7 +978,7 @@ def conv3x3_wino_ok(x, weight, stride=1, padding=1, dilation=1, groups=1, extra=
         return False
     if (ci + 15) // 16 * 16 > WINO_MAX_CI_PAD:  # the launch's LDS plane table (winoconv.hip kMaxCiPad)
         return False
-    if _WINO_MODE == "all":
+    if _WINO_MODE == "all" or force:
         return True
     n, _, h, w = x.shape
     co = weight.shape[0]
@@ -1000,6 +1008,16 @@ def conv2d_forward(mod, x):
         if (_ENC_DIRECT and st and x.is_contiguous() and x.dtype == torch.float32
                 and conv2d_direct_ok(x, mod.weight, st, mod.padding)):
             return conv2d_direct(x, mod.weight, mod.bias, st)
+        if _LIBFREE_X3 and split_mode() and st and x.is_contiguous() and x.dtype == torch.float32:
+            # bf16x3 mode, a shape the rules above leave to MIOpen (C3's b = 8 levels): the split-bf16
+            # Winograd for the 3x3 / stride-1 ones up to 256 input channels, the direct kernel for the
+            # rest -- per shape within ~1.4x of MIOpen either way, 1.26 vs 1.28 ms over C3's 18 calls
+            # (tools/c3_libconv.py, profiles/r6/c3_libconv.log), and no library convolution left
+            if mod.weight.shape[1] <= 256 and conv3x3_wino_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation,
+                                                               mod.groups, force=True):
+                return conv3x3_wino(x, mod.weight, mod.bias)
+            if conv2d_direct_ok(x, mod.weight, st, mod.padding, force=True):
+                return conv2d_direct(x, mod.weight, mod.bias, st)
         k = mod.kernel_size
         if (_LIBFREE and st and k[0] == k[1] and k[0] > 3 and mod.padding[0] == mod.padding[1] and x.is_cuda
                 and x.dtype == torch.float32 and mod.weight.dtype == torch.float32
@@ -1013,6 +1031,9 @@ def conv2d_forward(mod, x):
 # (cudnn.benchmark), so their bits could differ from process to process; these forms are exact fp32
 # and fixed. TSPLAT_CONV_LIBFREE=0 keeps them on MIOpen (A/B knob).
 _LIBFREE = os.environ.get("TSPLAT_CONV_LIBFREE", "1") == "1"
+# bf16x3 mode: every remaining Conv2d on the split-bf16 Winograd / direct kernels (TSPLAT_CONV_LIBFREE_X3=0:
+# the shapes above the latency-bound range stay on MIOpen, the A/B knob)
+_LIBFREE_X3 = os.environ.get("TSPLAT_CONV_LIBFREE_X3", "1") == "1"
 _DERIVED: dict = {}
 
 
