@@ -21,7 +21,7 @@ model = build_model(dev, dense, attn_dtype=attn)
 data = S.make_batch(batch, image_shape=(256, 256), device=dev)
 with torch.no_grad():
     model.test_step(data)
-    with routes.record() as r:
+    with routes.record() as r:  # run with TSPLAT_CONV_LIBFREE_X3=0 to list what reaches MIOpen without it
         model.test_step(data)
 torch.cuda.synchronize()
 convs = collections.Counter()

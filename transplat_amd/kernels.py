@@ -256,7 +256,7 @@ def conv_bias_act(conv, x, act: str = "none", residual=None, site: str = "", ext
     if extra:
         x = torch.cat([x, *extra], dim=1)
     if fused:
-        y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+        y = conv2d_fallback(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
         # the kernel indexes the residual with y's NCHW layout: a broadcastable residual ([C, 1, 1],
         # a batch-1 map) takes the module path, where `y + residual` broadcasts
         fused = ((y.shape[-1] * y.shape[-2]) % 4 == 0 and y.is_contiguous()
@@ -1008,16 +1008,9 @@ def conv2d_forward(mod, x):
         if (_ENC_DIRECT and st and x.is_contiguous() and x.dtype == torch.float32
                 and conv2d_direct_ok(x, mod.weight, st, mod.padding)):
             return conv2d_direct(x, mod.weight, mod.bias, st)
-        if _LIBFREE_X3 and split_mode() and st and x.is_contiguous() and x.dtype == torch.float32:
-            # bf16x3 mode, a shape the rules above leave to MIOpen (C3's b = 8 levels): the split-bf16
-            # Winograd for the 3x3 / stride-1 ones up to 256 input channels, the direct kernel for the
-            # rest -- per shape within ~1.4x of MIOpen either way, 1.26 vs 1.28 ms over C3's 18 calls
-            # (tools/c3_libconv.py, profiles/r6/c3_libconv.log), and no library convolution left
-            if mod.weight.shape[1] <= 256 and conv3x3_wino_ok(x, mod.weight, mod.stride, mod.padding, mod.dilation,
-                                                               mod.groups, force=True):
-                return conv3x3_wino(x, mod.weight, mod.bias)
-            if conv2d_direct_ok(x, mod.weight, st, mod.padding, force=True):
-                return conv2d_direct(x, mod.weight, mod.bias, st)
+        y = _conv2d_x3_libfree(x, mod.weight, mod.bias, mod.stride, mod.padding)
+        if y is not None:
+            return y
         k = mod.kernel_size
         if (_LIBFREE and st and k[0] == k[1] and k[0] > 3 and mod.padding[0] == mod.padding[1] and x.is_cuda
                 and x.dtype == torch.float32 and mod.weight.dtype == torch.float32
@@ -1093,6 +1086,35 @@ def conv_transpose_forward(mod, x):
             and not torch.is_autocast_enabled("cuda")):
         return conv_transpose_direct(x.contiguous(), mod.weight, mod.bias, st[0])
     return torch.nn.ConvTranspose2d.forward(mod, x)
+
+
+def _conv2d_x3_libfree(x, weight, bias, stride, padding):
+    """bf16x3 mode, a convolution the shape rules leave to MIOpen (C3's b = 8 levels): the split-bf16
+    Winograd for the 3x3 / stride-1 ones up to 256 input channels, the direct kernel for the rest --
+    per shape within ~1.4x of MIOpen either way, 1.26 vs 1.28 ms over C3's 18 such calls
+    (tools/c3_libconv.py, profiles/r6/c3_libconv.log), and no library convolution left. None when
+    the shape is not one of those (or TSPLAT_CONV_LIBFREE_X3=0, or another mode)."""
+    if not (_LIBFREE_X3 and split_mode() and x.is_cuda and x.dim() == 4 and x.is_contiguous()
+            and x.dtype == torch.float32 and weight.dim() == 4):
+        return None
+    st = stride if isinstance(stride, int) else (stride[0] if stride[0] == stride[1] else 0)
+    if not st:
+        return None
+    if weight.shape[1] <= 256 and conv3x3_wino_ok(x, weight, stride, padding, force=True):
+        return conv3x3_wino(x, weight, bias)
+    if conv2d_direct_ok(x, weight, st, padding, force=True):
+        return conv2d_direct(x, weight, bias, st)
+    return None
+
+
+def conv2d_fallback(x, weight, bias=None, stride=1, padding=0, dilation=1, groups=1):
+    """F.conv2d for the model code's last-resort branches: in the bf16x3 mode through
+    _conv2d_x3_libfree first, so no convolution of that mode reaches MIOpen."""
+    if groups == 1 and (dilation == 1 or tuple(dilation) == (1, 1)):
+        y = _conv2d_x3_libfree(x, weight, bias, stride, padding)
+        if y is not None:
+            return y
+    return torch.nn.functional.conv2d(x, weight, bias, stride, padding, dilation, groups)
 
 
 def install_conv2d_dispatch(module) -> int:

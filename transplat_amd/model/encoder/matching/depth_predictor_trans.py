@@ -32,7 +32,7 @@ def _conv_upsample_gelu(seq: nn.Sequential, x):
     if kernels.conv3x3_wino_ok(x, conv.weight, conv.stride, conv.padding, conv.dilation, conv.groups, vs_miopen=True):
         y = kernels.conv3x3_wino(x, conv.weight, None)  # (MIOpen 53 us at 256 -> 128 / 64^2; bf16x3 ~24 us)
     else:
-        y = F.conv2d(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
+        y = kernels.conv2d_fallback(x, conv.weight, None, conv.stride, conv.padding, conv.dilation, conv.groups)
     return kernels.upsample_bilinear_act(y, int(up.scale_factor), conv.bias, "gelu")
 
 

@@ -90,7 +90,7 @@ def conv(conv: nn.Module, x, x2=None, upsample: bool = False, bias: bool = True)
         y = torch.baddbmm(b.view(1, co, 1), wm, xm) if b is not None else torch.bmm(wm, xm)
         return y.view(n, co, h, w)
     if isinstance(conv, nn.Conv2d):
-        return F.conv2d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
+        return kernels.conv2d_fallback(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
     return F.conv1d(x, conv.weight, b, conv.stride, conv.padding, conv.dilation, conv.groups)
 
 
