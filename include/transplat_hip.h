@@ -523,6 +523,20 @@ int tsplat_conv3x3_wino_bf16x3_ex_fwd(const float* const* srcs, const int32_t* c
                                       const float* residual2, float* y, int32_t batch, int32_t height, int32_t width,
                                       int32_t c_out, int32_t act, int32_t relu_in, void* stream);
 
+/* The same 3x3 / stride-1 / pad-1 convolution (bf16x3 precision, identical arguments except the
+ * weight) as a direct implicit GEMM for FEW-channel, full-resolution maps -- the refine U-Net's
+ * 32-channel 256^2 / 128^2 levels and the depth heads (depth_predictor_trans.py:138-160, ldm_unet/
+ * unet.py at model_channels = 32), where the Winograd form's per-block prologue / epilogue dominate.
+ * w_packed = the direct kernels' split-bf16 A operand [ceil(c_out / 32)][9][ceil(c_in / 16)][hi, lo]
+ * [64 lanes][8] (as tsplat_conv2d_bf16x3_fwd). Requires width % 4 == 0, 16-B aligned sources,
+ * c_out <= 64, c_in <= 128 (else TSPLAT_EINVAL); tsplat_conv3x3_few_form() returns 0 for shapes it
+ * does not take and otherwise its launch form (10 * rows per block + 32-channel blocks per workgroup). */
+int32_t tsplat_conv3x3_few_form(int32_t batch, int32_t c_in, int32_t height, int32_t width, int32_t c_out);
+int tsplat_conv3x3_few_bf16x3_fwd(const float* const* srcs, const int32_t* chans, int32_t n_src,
+                                  const void* w_packed, const float* bias, const float* residual,
+                                  const float* residual2, float* y, int32_t batch, int32_t height, int32_t width,
+                                  int32_t c_out, int32_t act, int32_t relu_in, void* stream);
+
 /* Split-bf16 operands for ONE library bf16 GEMM that computes an fp32 linear layer in bf16x3
  * precision (the nn.Linear layers of the fp32 path -- DINOv2 qkv / proj / fc1 / fc2,
  * src/depth_anything_v2/dinov2_layers/{attention,mlp}.py, the transformer FFN's mlp[0],

@@ -15,6 +15,16 @@ from canonical import seeded  # noqa: E402
 
 from oracle import encoder_ops as E  # noqa: E402
 
+@pytest.fixture(autouse=True)
+def _winograd_tests_run_winograd(request, monkeypatch):
+    """The Winograd tests below pin the Winograd kernel; conv3x3_wino routes few-channel full-resolution
+    shapes to the direct kernel of csrc/convfew.hip instead (tested by the *few* tests)."""
+    if "wino" in request.node.name and "few" not in request.node.name:
+        from transplat_amd import kernels as K
+
+        monkeypatch.setattr(K, "_FEW", False)
+
+
 CASES = [
     # n, c1, c2, h, w, cout, k, stride, upsample, bias
     (2, 32, 0, 16, 16, 32, 3, 1, False, False),
@@ -757,3 +767,88 @@ def test_conv2d_direct_bf16x3_kernel(device, monkeypatch, n, c1, c2, h, w, cout,
     print(f"direct bf16x3 {(n, c1, c2, h, w, cout, k, stride, up)}: rel err {err:.2e} (TF32 operands {etf:.2e})")
     assert err < 2e-5 and err <= etf / 8, (err, etf)
     assert torch.equal(outs[0], outs[1])
+
+
+FEW_CASES = [
+    # n, source channels, co, h, w, act, relu_in, residuals
+    (2, (32,), 32, 256, 256, "none", False, 0),      # refine U-Net 256^2 ResBlock conv
+    (2, (64,), 32, 256, 256, "none", False, 0),      # its output block on cat([h, skip]) (one source here)
+    (2, (32, 32), 32, 256, 256, "none", False, 0),   # ... read as two sources in place
+    (2, (3, 1, 32, 1, 1), 32, 256, 256, "none", False, 0),  # the refine input cat (38 channels, 5 sources)
+    (2, (32,), 64, 256, 256, "gelu", False, 0),      # to_disparity conv 1 (+ GELU)
+    (2, (64,), 2, 256, 256, "none", False, 0),       # to_disparity conv 2 (2 of 32 columns used)
+    (2, (32,), 32, 128, 128, "none", False, 0),      # 128^2 level (4-row blocks)
+    (2, (64,), 64, 128, 128, "relu", True, 2),       # relu-on-load, both residuals
+    (1, (40,), 48, 36, 252, "none", False, 1),       # ragged: h % 8, w % 64 != 0, co % 32 != 0
+    (3, (96, 32), 16, 20, 68, "gelu", False, 0),     # 128 input channels (4 passes), tiny map (2-row form)
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,chans,co,h,w,act,relu_in,nres", FEW_CASES)
+def test_conv3x3_few_kernel(device, n, chans, co, h, w, act, relu_in, nres):
+    """tsplat_conv3x3_few_bf16x3_fwd (direct split-bf16 3x3 for few-channel full-resolution maps,
+    csrc/convfew.hip) against torch's conv2d in float64: the same bounds as the bf16x3 Winograd kernel
+    (2e-5 of max |y|, and <= 1/8 of the TF32-operand error). The launch is checked to take the direct
+    kernel (tsplat_conv3x3_few_form)."""
+    from transplat_amd import _lib
+    from transplat_amd import kernels as K
+
+    ci = sum(chans)
+    assert int(_lib.load().tsplat_conv3x3_few_form(n, ci, h, w, co)) != 0
+    parts = [seeded((n, c, h, w), 150 + 3 * i + c) for i, c in enumerate(chans)]
+    x = torch.cat(parts, 1)
+    wt = seeded((co, ci, 3, 3), 161) * (1.0 / (9 * ci) ** 0.5)
+    b = seeded((co,), 162)
+    res = [seeded((n, co, h, w), 163 + i) for i in range(nres)]
+    fn = {"none": lambda t: t, "relu": torch.relu, "gelu": torch.nn.functional.gelu}[act]
+    xin = torch.relu(x) if relu_in else x
+    ref = fn(torch.nn.functional.conv2d(xin.double(), wt.double(), b.double(), padding=1))
+    ref_tf32 = fn(torch.nn.functional.conv2d(tf32_round(xin).double(), tf32_round(wt).double(), b.double(),
+                                             padding=1))
+    for r in res:
+        ref, ref_tf32 = ref + r.double(), ref_tf32 + r.double()
+    lib = _lib.load()
+    import ctypes
+
+    srcs = [p.to(device).contiguous() for p in parts]
+    y = torch.empty((n, co, h, w), device=device)
+    ptrs = (ctypes.c_void_p * len(srcs))(*[t.data_ptr() for t in srcs])
+    cs = (ctypes.c_int32 * len(srcs))(*chans)
+    rd = [r.to(device) for r in res] + [None, None]
+    rc = lib.tsplat_conv3x3_few_bf16x3_fwd(ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(cs, ctypes.c_void_p),
+                                           len(srcs), K.conv_pack_weight_x3(wt.to(device)).data_ptr(),
+                                           b.to(device).data_ptr(), _lib.ptr(rd[0]), _lib.ptr(rd[1]), y.data_ptr(),
+                                           n, h, w, co, {"none": 0, "relu": 1, "gelu": 2}[act], int(relu_in),
+                                           _lib.stream_ptr(device))
+    assert rc == 0
+    out = y.cpu().double()
+    scale = ref.abs().max().item()
+    e3, etf = ((o - ref).abs().max().item() / scale for o in (out, ref_tf32))
+    print(f"few-channel conv {(n, chans, co, h, w, act, relu_in, nres)}: rel err {e3:.2e} (TF32 operands {etf:.2e})")
+    assert e3 < 2e-5, e3
+    assert e3 <= etf / 8, (e3, etf)
+
+
+@pytest.mark.gpu
+def test_conv3x3_few_route_matches_kernel(device):
+    """kernels.conv3x3_wino in the bf16x3 mode takes the direct few-channel kernel for a refine-U-Net
+    shape (same bits as the C-ABI call above would give), and the Winograd one with TSPLAT_CONV_FEW off;
+    both within the bf16x3 bound of float64."""
+    from transplat_amd import kernels as K
+
+    x = seeded((2, 32, 256, 256), 171).to(device)
+    wt = (seeded((32, 32, 3, 3), 172) / 17.0).to(device)
+    b = seeded((32,), 173).to(device)
+    with K.dense_precision("bf16x3"):
+        assert K._few_ok([x], 2, 256, 256, 32)
+        y_few = K.conv3x3_wino(x, wt, b)
+        K._FEW = False
+        try:
+            y_w = K.conv3x3_wino(x, wt, b)
+        finally:
+            K._FEW = True
+    ref = torch.nn.functional.conv2d(x.double(), wt.double(), b.double(), padding=1)
+    s = ref.abs().max().item()
+    assert (y_few.double() - ref).abs().max().item() / s < 2e-5
+    assert (y_w.double() - ref).abs().max().item() / s < 2e-5

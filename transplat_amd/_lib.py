@@ -105,6 +105,8 @@ SIGNATURES = {
     "tsplat_conv3x3_wino_bf16x3_fwd": (ctypes.c_int, [_P, _P, _P, _P] + [_I32] * 6 + [_P]),
     "tsplat_conv3x3_wino_bf16x3_cat_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P] + [_I32] * 5 + [_P]),
     "tsplat_conv3x3_wino_bf16x3_ex_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P] + [_I32] * 6 + [_P]),
+    "tsplat_conv3x3_few_form": (ctypes.c_int32, [_I32] * 5),
+    "tsplat_conv3x3_few_bf16x3_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P, _P] + [_I32] * 6 + [_P]),
     "tsplat_split_bf16x3": (ctypes.c_int, [_P, _P, ctypes.c_int64, _I32, _I32, _P]),
     "tsplat_conv2d_bf16_weight_bytes": (ctypes.c_size_t, [_I32, _I32, _I32]),
     "tsplat_conv2d_bf16_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, _P] + [_I32] * 7 + [_P]),

@@ -224,7 +224,7 @@ struct Region {
 };
 
 template <int CB, int NB, int KS, bool ST>
-__global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Args a) {
+__global__ void __launch_bounds__(256 * CB * KS, (NB == 1 && CB * KS <= 2) ? 2 : 1) conv_kernel(Args a) {
     constexpr int T = 32 * NB;                 // tiles per workgroup
     constexpr int GT = 256 * CB;               // threads per k-group
     constexpr int PHR = GT / (4 * T);          // pair halves (4 pairs each) covered per pass
@@ -240,8 +240,9 @@ __global__ void __launch_bounds__(256 * CB * KS, NB == 1 ? 2 : 1) conv_kernel(Ar
     // float4 region loads per thread and chunk: the largest R x C4 (72 for 32-tile blocks, 136 for
     // 64-tile ones) over the GT / 16 threads of a channel
     constexpr int NL = ((T == 32 ? 72 : 136) + GT / 16 - 1) / (GT / 16);
-    constexpr int SMEM = KS * (NSV * BUF + (ST ? 2 * RGN : 0));
-    static_assert(8 * CO * T * KS <= SMEM, "Z slabs fit");
+    // the pipeline's buffers, reused for the Z slabs after the last chunk (the larger of the two)
+    constexpr int SMEM_PIPE = KS * (NSV * BUF + (ST ? 2 * RGN : 0));
+    constexpr int SMEM = SMEM_PIPE > 8 * CO * T * KS ? SMEM_PIPE : 8 * CO * T * KS;
     __shared__ __attribute__((aligned(16))) uint32_t smem[SMEM];
     __shared__ const float* planes[kMaxCiPad];
 
@@ -827,7 +828,9 @@ extern "C" int tsplat_wino_weight_bf16x3(const float* weight, void* packed, int3
 // workgroup forms: 0 = auto, 1 = 32 co x 32 tiles (KS 1), 2 = 32 x 32 with two k-groups,
 // 3 = 32 co x 64 tiles, 4 = 64 co x 64 tiles, 5 = persistent 32 x 32 (staged maps only),
 // 6 = 64 co x 32 tiles (half the threads transform); staged input (Region) on top where the map
-// allows it
+// allows it. (Round 6, tried and removed: 96 co x 32 tiles, 12 waves, to amortise the input transform
+// over more outputs: the waves spilled at 170 registers, 472 vs 242 us for the gaussian head's
+// 163 -> 168 at 256^2, profiles/r6/wino3_forms_head.log)
 static int pick_form(int n, int th, int tw, int co) {
     if (const char* e = getenv("TSPLAT_WINO3_FORM")) {
         const int f = atoi(e);

@@ -1351,6 +1351,24 @@ def wino_pack_weight_bf16x3(weight):
     return packed
 
 
+# bf16x3 3x3s of few-channel full-resolution maps on the direct kernel tsplat_conv3x3_few_bf16x3_fwd
+# instead of the Winograd one (TSPLAT_CONV_FEW=0: Winograd everywhere, the A/B knob): <= 32 outputs from
+# <= 64 inputs over >= 2 x 256^2 pixels, where it measured faster (2 x 32 -> 32 at 256^2 20.9 vs 25.3 us,
+# 64 -> 32 32.1 vs 35.3, 38 -> 32 26.7 vs 29.6; at 64 outputs or 128^2 maps it only ties:
+# profiles/r6/few_sweep.log)
+_FEW = os.environ.get("TSPLAT_CONV_FEW", "1") != "0"
+FEW_MIN_PX = int(os.environ.get("TSPLAT_CONV_FEW_MIN_PX", str(2 * 256 * 256)))
+FEW_MAX_CI = int(os.environ.get("TSPLAT_CONV_FEW_MAX_CI", "64"))
+FEW_MAX_CO = int(os.environ.get("TSPLAT_CONV_FEW_MAX_CO", "32"))
+
+
+def _few_ok(srcs, n: int, h: int, w: int, co: int) -> bool:
+    ci = sum(t.shape[1] for t in srcs)
+    return (_FEW and co <= FEW_MAX_CO and ci <= FEW_MAX_CI and n * h * w >= FEW_MIN_PX and w % 4 == 0
+            and all(t.data_ptr() % 16 == 0 for t in srcs)
+            and int(_lib.load().tsplat_conv3x3_few_form(n, ci, h, w, co)) != 0)
+
+
 def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=(), precision: str | None = None, residual=None,
                  residual2=None, relu_in: bool = False):
     """act(conv2d(cat([x, *extra], 1), weight, bias, stride 1, padding 1)) (+ residual + residual2)
@@ -1384,6 +1402,14 @@ def conv3x3_wino(x, weight, bias=None, act: str = "none", extra=(), precision: s
         for r in res:
             if r is not None and tuple(r.shape) != tuple(y.shape):
                 raise ValueError(f"residual {tuple(r.shape)} != output {tuple(y.shape)}")
+        if _few_ok(srcs, n, h, w, co):
+            # few-channel full-resolution maps: the direct split-bf16 kernel (csrc/convfew.hip)
+            rc = lib.tsplat_conv3x3_few_bf16x3_fwd(
+                ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p), len(srcs),
+                _lib.ptr(conv_pack_weight_x3(weight)), _lib.ptr(pb), _lib.ptr(res[0]), _lib.ptr(res[1]),
+                _lib.ptr(y), n, h, w, co, _WINO_ACT[act], int(relu_in), _lib.stream_ptr(x.device))
+            _lib.check(rc, "tsplat_conv3x3_few_bf16x3_fwd")
+            return y
         rc = lib.tsplat_conv3x3_wino_bf16x3_ex_fwd(
             ctypes.cast(ptrs, ctypes.c_void_p), ctypes.cast(chans, ctypes.c_void_p), len(srcs),
             _lib.ptr(wino_pack_weight_bf16x3(weight)), _lib.ptr(pb), _lib.ptr(res[0]), _lib.ptr(res[1]), _lib.ptr(y),
