@@ -68,3 +68,19 @@ def test_c3_step_routes_library_conv_free(device):
     assert set(cats["window attention"]) == {"bf16 MFMA, fp32 softmax"}
     convs = [x for x in r.library if x[0] not in routes._GEMMS]
     assert not convs, convs
+
+
+def test_every_matmul_entry_point_is_censused():
+    """Every C-ABI convolution / attention / linear entry point the host code calls has a route
+    category, so a new kernel cannot silently drop out of the bench line's precision statement."""
+    import re
+    from pathlib import Path
+
+    pkg = Path(routes.__file__).parent
+    names = set()
+    for f in [pkg / "kernels.py", *pkg.glob("model/**/*.py")]:
+        names |= set(re.findall(r'check\(\s*\w+,\s*"(tsplat_\w+_fwd)"', f.read_text()))
+    hot = {n for n in names if re.search(r"conv|attn|attention|_linear_|mha|raster", n)}
+    assert hot, "no entry points found"
+    missing = sorted(n for n in hot if n not in routes._HIP)
+    assert not missing, missing

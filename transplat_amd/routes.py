@@ -35,6 +35,7 @@ _HIP = {
     "tsplat_conv3x3_wino_bf16x3_cat_fwd": ("3x3 convs (HIP Winograd)", "bf16x3"),
     "tsplat_conv3x3_wino_f32_fwd": ("3x3 convs (HIP Winograd)", "exact fp32"),
     "tsplat_conv3x3_wino_cat_f32_fwd": ("3x3 convs (HIP Winograd)", "exact fp32"),
+    "tsplat_conv3x3_few_bf16x3_fwd": ("direct convs (HIP)", "bf16x3"),
     "tsplat_conv2d_bf16x3_fwd": ("direct convs (HIP)", "bf16x3"),
     "tsplat_conv2d_f32_fwd": ("direct convs (HIP)", "exact fp32"),
     "tsplat_conv2d_f32_zsplit_fwd": ("direct convs (HIP)", "exact fp32"),
