@@ -102,19 +102,65 @@ def test_window_attention_kernel_large_logits(device):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("hw,b,variant", [(16, 1, "dedup"), (32, 2, "dedup"), (64, 1, "dedup"), (64, 2, "dedup"),
-                                          (16, 1, "direct"), (64, 1, "direct")])
+                                          (16, 1, "direct"), (64, 1, "direct"), (16, 1, "bitmap"),
+                                          (64, 2, "bitmap")])
 def test_uv_coarse_kernel(device, monkeypatch, hw, b, variant):
-    """Corner-deduplicated coarse correlation (default) and the sample-then-dot kernel
-    (TSPLAT_UV_COARSE_DIRECT=1), incl. the production 64 x 64 map at b = 1 and 2."""
+    """Run-deduplicated coarse correlation (default), the round-2 bitmap kernel
+    (TSPLAT_UV_COARSE_BITMAP=1) and the sample-then-dot kernel (TSPLAT_UV_COARSE_DIRECT=1), incl.
+    the production 64 x 64 map at b = 1 and 2."""
     from transplat_amd import kernels as K
 
     if variant == "direct":
         monkeypatch.setenv("TSPLAT_UV_COARSE_DIRECT", "1")
+    if variant == "bitmap":
+        monkeypatch.setenv("TSPLAT_UV_COARSE_BITMAP", "1")
     intr, pose, disp = _cams(b, hw)
     feat = seeded((b, 2, hw * hw, 128), 31)
     ref = E.uv_coarse(feat, intr, pose, disp, hw, hw)
     out = K.uv_coarse(feat.to(device), intr.to(device), pose.to(device), disp.to(device), hw, hw).cpu()
     assert (out - ref).abs().max().item() < 1e-4
+
+
+def _rotated_cams(b, hw, seed, depth_slice):
+    """_cams with the relative pose turned by a random rotation of up to ~0.35 rad and shifted, so
+    epipolar segments run diagonally, leave the image and re-enter the sampling window part-way,
+    and the depth count is changed (S = 1, 3 slices of 64 samples)."""
+    intr, pose, disp = _cams(b, hw)
+    g = torch.Generator().manual_seed(seed)
+    pose = pose.clone()
+    for i in range(pose.shape[0]):
+        w = (torch.rand(3, generator=g) - 0.5) * 0.7
+        th = w.norm()
+        kx = torch.tensor([[0.0, -w[2], w[1]], [w[2], 0.0, -w[0]], [-w[1], w[0], 0.0]]) / th
+        rot = torch.eye(3) + torch.sin(th) * kx + (1 - torch.cos(th)) * kx @ kx
+        pose[i, :3, :3] = rot @ pose[i, :3, :3]
+        pose[i, :3, 3] += (torch.rand(3, generator=g) - 0.5) * 0.6
+    return intr, pose, depth_slice(disp).contiguous()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,depths", [(1, 128), (2, 64), (3, 192)])
+def test_uv_coarse_run_matches_bitmap(device, monkeypatch, seed, depths):
+    """The run-deduplicated kernel equals the bitmap kernel BIT FOR BIT (same distinct-corner dots,
+    same per-sample sum order, sample positions from the same contraction-free sample_im) on
+    rotated cameras with D = 64 / 128 / 192, and holds the oracle's 1e-4."""
+    from transplat_amd import kernels as K
+
+    sl = {128: lambda d: d, 64: lambda d: d[:, ::2], 192: lambda d: torch.cat([d, d[:, ::2] * 1.003], 1)}[depths]
+    hw = 32
+    intr, pose, disp = _rotated_cams(2, hw, seed, sl)
+    assert disp.shape[1] == depths
+    feat = seeded((2, 2, hw * hw, 128), 40 + seed)
+    args = (feat.to(device), intr.to(device), pose.to(device), disp.to(device), hw, hw)
+    run = K.uv_coarse(*args).cpu()
+    monkeypatch.setenv("TSPLAT_UV_COARSE_BITMAP", "1")
+    bitmap = K.uv_coarse(*args).cpu()
+    ref = E.uv_coarse(feat, intr, pose, disp, hw, hw)
+    d_bitmap, d_ref = (run - bitmap).abs().max().item(), (run - ref).abs().max().item()
+    print(f"coarse run kernel seed={seed} D={depths}: vs bitmap kernel {d_bitmap:.2e} "
+          f"({(run != bitmap).float().mean().item():.2e} of outputs differ), vs oracle {d_ref:.2e}")
+    assert d_bitmap == 0 and d_ref < 1e-4
+    assert (ref != 0).float().mean().item() > 0.1  # the segments do cross the image
 
 
 @pytest.mark.gpu
@@ -439,6 +485,41 @@ def test_window_attention_x3_kernel(device, hw, m, shift, b, grow):
     err_tf = (ref_tf - ref).abs().max().item() / scale
     print(f"x3 attention hw={hw} m={m} shift={shift} b={b} grow={grow}: rel err {err:.2e}, TF32 operands {err_tf:.2e}")
     assert err < (2e-4 if grow else 3e-5) and err <= err_tf / 8, (err, err_tf)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant,ksplit,shift,grow", [("v1", 0, True, False), ("v1", 0, False, True),
+                                                        ("v2", 1, True, False), ("v2", 2, True, True),
+                                                        ("v2", 8, True, False), ("v2", 8, False, True)])
+def test_window_attention_x3_variants(device, monkeypatch, variant, ksplit, shift, grow):
+    """The round-5 4-wave x3 kernel (TSPLAT_WINATTN_X3=v1) and the two-group kernel (default) under
+    forced key splits (1: no partials, normalised output; 2 / 8: 8 / 2 key tiles per workgroup), same
+    bounds as test_window_attention_x3_kernel, and the two kernels within 2e-5 of each other (they
+    differ only in the running maxima the P split is taken against and the sum order)."""
+    from transplat_amd import kernels as K
+
+    hw, b = 64, 2
+    q = seeded((b, hw * hw, 128), 71) * (3.0 if grow else 1.0)
+    k = seeded((b, hw * hw, 128), 72)
+    if grow:
+        ys, xs = torch.meshgrid(torch.arange(hw), torch.arange(hw), indexing="ij")
+        t = ((ys % (hw // 2)) * (hw // 2) + xs % (hw // 2)).reshape(-1).float() / (hw * hw / 4)
+        k = k * (0.25 + 3.75 * t)[None, :, None]
+    v = seeded(k.shape, 73)
+    ref = E.window_attention(q.double(), k.double(), v.double(), hw, hw, 2, shift)
+    if ksplit:
+        monkeypatch.setenv("TSPLAT_WINATTN_KSPLIT", str(ksplit))
+    args = (q.to(device), k.to(device), v.to(device), hw, hw, 2, shift)
+    monkeypatch.setenv("TSPLAT_WINATTN_X3", variant)
+    out = K.window_attention_x3(*args).cpu().double()
+    monkeypatch.setenv("TSPLAT_WINATTN_X3", "v1" if variant == "v2" else "v2")
+    other = K.window_attention_x3(*args).cpu().double()
+    scale = max(1.0, ref.abs().max().item())
+    err = (out - ref).abs().max().item() / scale
+    diff = (out - other).abs().max().item() / scale
+    print(f"x3 {variant} ksplit={ksplit} shift={shift} grow={grow}: rel err {err:.2e}, vs the other form {diff:.2e}")
+    assert err < (2e-4 if grow else 3e-5), err
+    assert diff < (2e-4 if grow else 2e-5), diff
 
 
 @pytest.mark.gpu

@@ -30,9 +30,17 @@ if args.dtype == "x3":  # bf16x3: K / V split once (as the merge path does per l
     ws = torch.empty(max(int(_lib.load().tsplat_win_attn_workspace_bytes(b, hw, hw, 1, 2)), 4), dtype=torch.uint8,
                      device=dev)
 
+    split = int(_lib.load().tsplat_win_attn_split(b, hw, hw, 1, 2))
+    out = torch.empty_like(q)
+
     def attn():
-        _lib.check(_lib.load().tsplat_win_attn_x3_partials_fwd(_lib.ptr(q), _lib.ptr(kv), _lib.ptr(ws), b, hw, hw, 128,
-                                                               1, 2, int(args.shift), 0, _lib.stream_ptr(dev)), "x3")
+        if split > 1:  # main kernel only (the merge projection folds the combine)
+            _lib.check(_lib.load().tsplat_win_attn_x3_partials_fwd(_lib.ptr(q), _lib.ptr(kv), _lib.ptr(ws), b, hw, hw,
+                                                                   128, 1, 2, int(args.shift), 0,
+                                                                   _lib.stream_ptr(dev)), "x3")
+        else:  # no key split: the kernel writes the normalised output
+            _lib.check(_lib.load().tsplat_win_attn_x3_fwd(_lib.ptr(q), _lib.ptr(kv), _lib.ptr(out), _lib.ptr(ws), b, hw,
+                                                          hw, 128, 1, 2, int(args.shift), _lib.stream_ptr(dev)), "x3")
 else:
     def attn():
         kernels.window_attention(q, k, v, hw, hw, 2, bool(args.shift))

@@ -45,6 +45,7 @@ __device__ __forceinline__ const float* cam_ptr(const float* cams, const Geo& g,
 
 // ray of integer pixel (x, y) in the own camera, rotated into the other: R K^-1 [x, y, 1]
 __device__ __forceinline__ void pixel_ray(const float* c, float x, float y, float ray[3]) {
+#pragma clang fp contract(off)
     const float* ki = c;
     const float* R = c + 18;
     const float p0 = ki[0] * x + ki[1] * y + ki[2];
@@ -58,6 +59,7 @@ __device__ __forceinline__ void pixel_ray(const float* c, float x, float y, floa
 // ref_3d of the ray at depth 1/disp: normalised grid coordinate / 2 + 0.5, in [0, 1] on-image
 __device__ __forceinline__ void sample_ref(const float* c, const Geo& g, const float ray[3],
                                            float disp, float& rx, float& ry) {
+#pragma clang fp contract(off)
     const float* K = c + 9;
     const float* t = c + 27;
     const float depth = 1.0f / disp;
@@ -71,6 +73,18 @@ __device__ __forceinline__ void sample_ref(const float* c, const Geo& g, const f
     const float gy = 2.0f * (v / w) / (float)(g.H - 1) - 1.0f;
     rx = gx / 2.0f + 0.5f;
     ry = gy / 2.0f + 0.5f;
+}
+
+// sampling position of depth sample `disp` in the other view's pixel grid (mmcv: loc * size - 0.5),
+// with no fma contraction, so every kernel that places samples this way places them identically
+// (the dedup kernels compare bit for bit; near w = 1e-3 the division amplifies a contraction's ulp)
+__device__ __forceinline__ void sample_im(const float* c, const Geo& g, const float ray[3], float disp, float& xim,
+                                          float& yim) {
+#pragma clang fp contract(off)
+    float rx, ry;
+    sample_ref(c, g, ray, disp, rx, ry);
+    xim = rx * (float)g.W - 0.5f;
+    yim = ry * (float)g.H - 0.5f;
 }
 
 // bilinear sample (zero padding, mmcv ms_deform_attn_im2col_bilinear) of 8 channels [c0, c0+8)
@@ -225,9 +239,8 @@ uv_coarse_dedup_kernel(Geo g, int nw, const float* __restrict__ feat, const floa
         }
         int y0 = 0, x0 = 0, cell = -1;
         if (active && d < g.D) {
-            float rx, ry;
-            sample_ref(c, g, ray, dv[s], rx, ry);
-            const float xim = rx * fw - 0.5f, yim = ry * fh - 0.5f;
+            float xim, yim;
+            sample_im(c, g, ray, dv[s], xim, yim);
             if (yim > -1.0f && xim > -1.0f && yim < fh && xim < fw) {
                 const float fy = floorf(yim), fx = floorf(xim);
                 y0 = (int)fy;
@@ -343,6 +356,209 @@ uv_coarse_dedup_kernel(Geo g, int nw, const float* __restrict__ feat, const floa
             const unsigned wd = bm[ci >> 5];
             const int rank = (int)pre[ci >> 5] + __popc(wd & ((1u << (ci & 31)) - 1u));
             val += cw[s][k] * dots[rank];
+        }
+        o[d] = val * inv_sqrt_c;
+    }
+}
+
+// ---- coarse, run-deduplicated (round 6; default): the corner dedup above without the bitmap.
+// A pixel's D samples walk its epipolar segment in depth order, so their bilinear cells
+// (y0, x0) come in runs, and along a straight path (x and y each monotone) a corner shared by two
+// distinct cells is shared by every cell between them: a corner is new exactly when the PREVIOUS
+// distinct cell does not hold it. So, per wave (one query pixel), with no LDS bitmap, no ds_or
+// atomics, no popcount scan over H*W / 32 words and no workgroup barrier:
+//   1. each lane places its samples; a sample whose cell differs from the previous sample's is a
+//      run head; a head's new corners (in bounds, outside the previous cell's 2 x 2) get ranks by a
+//      ballot prefix sum and are listed; its other corners point at the previous cell's entry;
+//   2. those pointers are resolved in place (chains of <= 3 cells on a monotone path; the loop
+//      runs until none is left, so a non-monotone rounding step only costs an extra dot);
+//   3. one dot per listed corner (the 8-lane row dot above, same sum order);
+//   4. each sample reads its run's 4 corner ranks (one ds_read_b128) and combines as above.
+// The result is the bitmap kernel's bit for bit (same dots, same per-sample sum order).
+constexpr int kRunWaves = 4;
+
+// LDS words per wave: src [D cells][4] ranks, list [4 D] corner pixels, dots [4 D]
+__host__ __device__ inline int run_lds_words(int depths) { return 12 * depths; }
+
+// LDS hand-off between the lanes of ONE wave (its LDS operations execute in order)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int S>
+__global__ void __launch_bounds__(kRunWaves * 64)
+uv_coarse_run_kernel(Geo g, const float* __restrict__ feat, const float* __restrict__ cams,
+                     const float* __restrict__ disp, float* __restrict__ out) {
+    extern __shared__ int rsmem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = blockIdx.y;
+    const int HW = g.H * g.W;
+    const int p = blockIdx.x * kRunWaves + wave;
+    if (p >= HW) return;  // wave-uniform; nothing below synchronises the workgroup
+    int* src = rsmem + (size_t)wave * run_lds_words(g.D);
+    int* list = src + 4 * g.D;
+    float* dots = reinterpret_cast<float*>(list + 4 * g.D);
+
+    // own feature (dot operand, 8 lanes per corner) and this lane's disparities first
+    const int sub = lane & 7;
+    float4 key[4];
+    {
+        const float4* own = reinterpret_cast<const float4*>(feat + ((size_t)n * HW + p) * kC) + sub;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) key[i] = own[8 * i];
+    }
+    const float* c = cam_ptr(cams, g, n);
+    const int b = n >> 1, v = n & 1;
+    const float* dsp = disp + (size_t)(v * g.B + b) * g.D;
+    float dv[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) dv[s] = dsp[min(lane + 64 * s, g.D - 1)];
+
+    // 1. samples -> cells, run heads, new corners
+    const unsigned long long lt = (1ull << lane) - 1ull, le = lt | (1ull << lane);
+    const float fw = (float)g.W, fh = (float)g.H;
+    float ray[3];
+    pixel_ray(c, (float)(p % g.W), (float)(p / g.W), ray);
+    int cell_of[S];    // the sample's run (distinct-cell) index, -1 = outside the sampling window
+    float cw[S][4];
+    int cells = 0, total = 0, prev_cell = -1;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int d = lane + 64 * s;
+        int y0 = 0, x0 = 0, cell = -1, inb = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cw[s][k] = 0.f;
+        if (d < g.D) {
+            float xim, yim;
+            sample_im(c, g, ray, dv[s], xim, yim);
+            if (yim > -1.0f && xim > -1.0f && yim < fh && xim < fw) {
+                const float fy = floorf(yim), fx = floorf(xim);
+                y0 = (int)fy;
+                x0 = (int)fx;
+                const int y1 = y0 + 1, x1 = x0 + 1;
+                const float ly = yim - fy, lx = xim - fx, hy = 1.0f - ly, hx = 1.0f - lx;
+                if (y0 >= 0 && x0 >= 0) { inb |= 1; cw[s][0] = hy * hx; }
+                if (y0 >= 0 && x1 <= g.W - 1) { inb |= 2; cw[s][1] = hy * lx; }
+                if (y1 <= g.H - 1 && x0 >= 0) { inb |= 4; cw[s][2] = ly * hx; }
+                if (y1 <= g.H - 1 && x1 <= g.W - 1) { inb |= 8; cw[s][3] = ly * lx; }
+                cell = (y0 + 1) * (g.W + 2) + (x0 + 1);  // y0, x0 >= -1
+            }
+        }
+        // the previous depth sample's cell: lane - 1 of this slice, lane 63 of the previous one
+        int pcell = __shfl_up(cell, 1, 64);
+        const int last = __shfl(cell, 63, 64);
+        if (lane == 0) pcell = prev_cell;
+        prev_cell = last;
+        const bool head = cell >= 0 && cell != pcell;
+        const int py0 = pcell >= 0 ? pcell / (g.W + 2) - 1 : -100, px0 = pcell >= 0 ? pcell % (g.W + 2) - 1 : -100;
+        int code[4], nnew = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int dy = y0 + (k >> 1) - py0, dx = x0 + (k & 1) - px0;
+            if (!((inb >> k) & 1)) code[k] = -1;                                   // zero padding
+            else if (dy >= 0 && dy <= 1 && dx >= 0 && dx <= 1) code[k] = -2 - (2 * dy + dx);  // previous cell's
+            else code[k] = nnew++;                                               // new: local index
+        }
+        if (!head) nnew = 0;
+        const unsigned long long hb = __ballot(head);
+        const unsigned long long n0 = __ballot(nnew & 1), n1 = __ballot(nnew & 2), n2 = __ballot(nnew & 4);
+        const int rbase = total + __popcll(n0 & lt) + 2 * __popcll(n1 & lt) + 4 * __popcll(n2 & lt);
+        const int ci = cells + __popcll(hb & le) - 1;
+        if (head) {
+            int e[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                e[k] = code[k] >= 0 ? rbase + code[k] : code[k];
+                if (code[k] >= 0) list[rbase + code[k]] = (y0 + (k >> 1)) * g.W + x0 + (k & 1);
+            }
+            *reinterpret_cast<int4*>(src + 4 * ci) = make_int4(e[0], e[1], e[2], e[3]);
+        }
+        cell_of[s] = cell >= 0 ? ci : -1;
+        cells += __popcll(hb);
+        total += __popcll(n0) + 2 * __popcll(n1) + 4 * __popcll(n2);
+    }
+    wave_lds_sync();
+
+    // 2. a corner held by the previous cell takes that cell's entry (resolved in place; progress
+    //    is guaranteed because cell 0 has no predecessor)
+    for (;;) {
+        bool pending = false;
+        for (int c0 = 0; c0 < cells; c0 += 64) {
+            const int ce = c0 + lane;
+            if (ce < cells) {
+                int4 e = *reinterpret_cast<const int4*>(src + 4 * ce);
+                int ev[4] = {e.x, e.y, e.z, e.w};
+                bool changed = false;
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (ev[k] <= -2) {
+                        const int r = src[4 * (ce - 1) + (-2 - ev[k])];
+                        if (r > -2) {
+                            ev[k] = r;
+                            changed = true;
+                        } else {
+                            pending = true;
+                        }
+                    }
+                if (changed) *reinterpret_cast<int4*>(src + 4 * ce) = make_int4(ev[0], ev[1], ev[2], ev[3]);
+            }
+        }
+        wave_lds_sync();
+        if (!__any(pending)) break;
+    }
+
+    // 3. one dot per listed corner: 8 lanes per corner, 8 corners per pass, the next pass in flight
+    {
+        const float4* other = reinterpret_cast<const float4*>(feat + (size_t)(n ^ 1) * HW * kC) + sub;
+        const int jend = (total + 7) & ~7;
+        auto load = [&](int jj, float4* x) {
+            const float4* row = other + (size_t)(jj < total ? list[jj] : 0) * (kC / 4);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = row[8 * i];
+        };
+        auto dot = [&](int jj, const float4* x) {
+            float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                a0 += x[i].x * key[i].x;
+                a1 += x[i].y * key[i].y;
+                a0 += x[i].z * key[i].z;
+                a1 += x[i].w * key[i].w;
+            }
+            float acc = a0 + a1;
+            acc += __shfl_xor(acc, 1, 8);
+            acc += __shfl_xor(acc, 2, 8);
+            acc += __shfl_xor(acc, 4, 8);
+            if (jj < total && sub == 0) dots[jj] = acc;
+        };
+        float4 xa[4], xb[4];
+        int j = lane >> 3;
+        if (j < jend) load(j, xa);
+        for (; j < jend; j += 16) {
+            if (j + 8 < jend) load(j + 8, xb);
+            dot(j, xa);
+            if (j + 16 < jend) load(j + 16, xa);
+            if (j + 8 < jend) dot(j + 8, xb);
+        }
+    }
+    wave_lds_sync();
+
+    // 4. each sample = its run's corners' weighted dots
+    const float inv_sqrt_c = 1.0f / sqrtf((float)kC);
+    float* o = out + ((size_t)n * HW + p) * g.D;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int d = lane + 64 * s;
+        if (d >= g.D) continue;
+        float val = 0.f;
+        if (cell_of[s] >= 0) {
+            const int4 e = *reinterpret_cast<const int4*>(src + 4 * cell_of[s]);
+            const int ev[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ev[k] >= 0) val += cw[s][k] * dots[ev[k]];
         }
         o[d] = val * inv_sqrt_c;
     }
@@ -652,7 +868,17 @@ extern "C" int tsplat_uv_coarse_fwd(const float* feat, const float* cams, const 
     const char* denv = getenv("TSPLAT_CORR_DIAG");  // diagnostic builds: stop after phase 1 / 2 / 3
     const int diag = denv ? atoi(denv) : 0;
     const char* env = getenv("TSPLAT_UV_COARSE_DIRECT");  // A/B switch: the sample-then-dot kernel
-    if (S <= kDedupMaxS && lds <= 64 * 1024 && !(env && env[0] == '1')) {
+    const char* benv = getenv("TSPLAT_UV_COARSE_BITMAP");  // A/B switch: the round-2 bitmap dedup kernel
+    const size_t run_lds = (size_t)kRunWaves * run_lds_words(depths) * sizeof(int);
+    if (S <= kDedupMaxS && run_lds <= 64 * 1024 && !(env && env[0] == '1') && !(benv && benv[0] == '1') && !diag) {
+        const dim3 grid(ceil_div(hw, kRunWaves), 2 * batch), block(kRunWaves * 64);
+        switch (S) {
+            case 1: hipLaunchKernelGGL(uv_coarse_run_kernel<1>, grid, block, run_lds, stream, g, feat, cams, disp, out); break;
+            case 2: hipLaunchKernelGGL(uv_coarse_run_kernel<2>, grid, block, run_lds, stream, g, feat, cams, disp, out); break;
+            case 3: hipLaunchKernelGGL(uv_coarse_run_kernel<3>, grid, block, run_lds, stream, g, feat, cams, disp, out); break;
+            default: hipLaunchKernelGGL(uv_coarse_run_kernel<4>, grid, block, run_lds, stream, g, feat, cams, disp, out); break;
+        }
+    } else if (S <= kDedupMaxS && lds <= 64 * 1024 && !(env && env[0] == '1')) {
         const dim3 grid(ceil_div(hw, kDedupWaves), 2 * batch), block(kDedupWaves * 64);
         // 6 waves per SIMD (default; profiles/r5/late/corr_wpe.txt: b = 8 120.5 -> 111.4 us, b = 1 24.3 /
         // 24.2 vs 24.2 / 24.6) or 5 (TSPLAT_CORR_WPE=5, the A/B knob)

@@ -1005,7 +1005,10 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
     }
 
     // staging: a group moves its half of a tile: thread (key row grow, part gp) holds 16-B chunks
-    // 8 grp + 2 gp + {0, 1} of the row's K and V (and, for gp == 0, the row's mask fragment grp)
+    // 8 grp + 2 gp + {0, 1} of the row's K and V (and, for gp == 0, the row's mask fragment grp).
+    // (Round 6, measured slower and removed: whole 256-B rows per wave instruction -- K by two waves,
+    // V by two, row offsets and mask regions shuffled -- 61.8 vs 51.1 us at B = 16 shifted, 51.5 vs
+    // 49.0 unshifted; profiles/r6/wa_v3_rows.log)
     const int t8 = tid & 255, grow = t8 & 63, gp = t8 >> 6;
     const int ntiles = p.L * p.m / kBK;
     bf16x8 kv[2], vv[2];
@@ -1401,6 +1404,311 @@ win_attn_x3_kernel(Params p, const float* __restrict__ q, const __bf16* __restri
     WA_STAMP(13, wall_clock64());
 }
 
+// ============================================================================================
+// bf16x3 v2 (round 6, default): 8 waves = two 4-wave groups on the SAME 128 queries; group g owns
+// keys 32 g .. 32 g + 31 of every 64-key tile, i.e. its own half tiles (K hi / lo, V hi / lo: 32 KB,
+// double-buffered per group, 128 KB in all), and keeps its own running (m, l, O); the two are
+// combined through LDS at the end. The groups run win_attn_bf16_v3_kernel's one-phase stagger, so
+// each SIMD pairs one group's MFMA phase (PV of the previous tile, QK of this one: 49 MFMAs) with
+// the other group's VALU phase (softmax, P split, staging) instead of one wave doing both in turn
+// (win_attn_x3_kernel: 6.4k cycles per tile for 3.1k of MFMAs):
+//   group-local step s (group 0: s = i, group 1: s = i - 1 at global interval i, one barrier each)
+//     s = 2t     (MFMA): O += V(t-1)^T P(t-1)^T (t >= 1), then S(t) = K(t) Q^T (+ mask step)
+//     s = 2t + 1 (VALU): stage half tile t + 1 from registers into buffer (t + 1) % 2 (last read by
+//                        PV(t - 1) in step 2t), request half tile t + 2, softmax of S(t) -> P(t).
+// Q is loaded once per workgroup (512 threads, coalesced), split, and handed to both groups through
+// LDS (the buffers-1 region, free until step 1). The mask A fragment is formed in registers from
+// the key index. Operand maps, log2-domain softmax with deferred rescale, the mask step and the
+// partials layout are those of win_attn_x3_kernel.
+// ============================================================================================
+constexpr int kHalfK = 32;                 // keys per group per tile
+constexpr int kHImgB = kHalfK * kC * 2;    // one bf16 image of a half tile (8 KB)
+constexpr int kX3BufB = 4 * kHImgB;        // Kh, Kl, Vh, Vl (32 KB)
+constexpr int kX3GrpB = 2 * kX3BufB;       // two buffers per group (64 KB)
+constexpr int kX3Lds = 2 * kX3GrpB;        // 128 KB
+
+template <bool PRIO>
+__global__ void __launch_bounds__(kThreads8, 1)
+win_attn_x3_v2_kernel(Params p, const float* __restrict__ q, const __bf16* __restrict__ khg,
+                      const __bf16* __restrict__ klg, const __bf16* __restrict__ vhg, const __bf16* __restrict__ vlg,
+                      float* __restrict__ out, Partials part) {
+    __shared__ __attribute__((aligned(16))) unsigned char smem[kX3Lds];
+
+    WA_STAMP(0, wall_clock64());
+    WA_STAMP(1, WA_HWID());
+    WA_STAMP(2, WA_CLOCK());
+    int qblk, wi, bz;
+    xcd_block_coords(qblk, wi, bz);
+    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wid >> 2, wq = wid & 3;
+    const int c = lane & 31, h = lane >> 5;
+    const size_t HW = (size_t)p.H * p.W;
+    const int kvb = (b + p.kv_shift) % p.nbatch;
+    const size_t kvoff = (size_t)kvb * p.m * HW * kC;
+    const float cl2 = p.scale * kLog2e;
+    const int kbeg = ks * p.keys_per_split;
+    const int nt = p.keys_per_split / kBK;
+
+    const int tq = qblk * kBQ3 + wq * kQW + c;
+    const int qpix = win_pixel(p, wi, tq);
+    bf16x8 qmask;
+    {
+        const int qreg = p.shift ? win_region(p, wi, tq) : 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qmask[j] = (__bf16)(qreg == 8 * h + j ? 1.0f : 0.0f);
+    }
+
+    // gather: wave wq of a group moves image wq (Kh, Kl, Vh, Vl) of its half tile, one 1-KB wave
+    // instruction = 4 whole 256-B rows (16 lanes per row, lane = 16-B chunk: 8 cache lines per
+    // instruction; a lane-per-row map touches 64 lines per instruction and ran the chip at ~9 B per
+    // CU cycle). Lane c computes row c's offset (in rows); the 8 loads take theirs by shuffle.
+    unsigned char* const gsm = smem + grp * kX3GrpB;
+    const __bf16* const garr = (wq == 0 ? khg : wq == 1 ? klg : wq == 2 ? vhg : vlg) + kvoff;
+    const int gch = lane & 15, gr = lane >> 4;  // chunk, row within a 4-row instruction
+    bf16x8 gv[8];
+    auto gather = [&](int t) {
+        const int j = kbeg + t * kBK + kHalfK * grp + c;
+        int tk = j, vi = 0;
+        if (p.m != 1) {
+            tk = j / p.m;
+            vi = j - tk * p.m;
+        }
+        const int rowoff = vi * (int)HW + win_pixel(p, wi, tk);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int ro = __shfl(rowoff, 4 * i + gr, 64);
+            gv[i] = *(reinterpret_cast<const bf16x8*>(garr + (size_t)ro * kC) + gch);
+        }
+    };
+    auto stage = [&](int buf) {
+        unsigned char* img = gsm + buf * kX3BufB + wq * kHImgB;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int r = 4 * i + gr;
+            const int off = wq < 2 ? r * 256 + ((gch ^ (r & 15)) * 16) : vimg_off(r, gch);
+            *reinterpret_cast<bf16x8*>(img + off) = gv[i];
+        }
+    };
+
+    // prologue: half tile 0 staged, half tile 1 requested; Q (128 queries x 128 fp32) loaded by all
+    // 512 threads (wave w, instruction i: rows 16 i + 2 w + {0, 1}, 32 lanes x 16 B per 512-B row),
+    // split, and written as hi / lo images (row = query, 16-B chunk XOR-swizzled) into the
+    // buffers-1 region of group 0 (hi) and group 1 (lo)
+    gather(0);
+    float4 qraw[8];
+    const int c4 = lane & 31;  // float4 of the query row: channels 4 c4 .. 4 c4 + 3
+    {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int qp = win_pixel(p, wi, qblk * kBQ3 + 16 * i + 2 * wid + h);
+            qraw[i] = reinterpret_cast<const float4*>(q + ((size_t)b * HW + qp) * kC)[c4];
+        }
+    }
+    stage(0);
+    if (nt > 1) gather(1);  // in flight while Q is split
+    {
+        unsigned char* qh_img = smem + kX3BufB;            // group 0, buffer 1
+        unsigned char* ql_img = smem + kX3GrpB + kX3BufB;  // group 1, buffer 1
+        typedef __bf16 bf16x4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int row = 16 * i + 2 * wid + h;
+            const float x[4] = {qraw[i].x, qraw[i].y, qraw[i].z, qraw[i].w};
+            bf16x4v hi, lo;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                hi[e] = (__bf16)x[e];
+                lo[e] = (__bf16)(x[e] - (float)hi[e]);
+            }
+            const int off = row * 256 + (((c4 >> 1) ^ (row & 15)) * 16) + 8 * (c4 & 1);
+            *reinterpret_cast<bf16x4v*>(qh_img + off) = hi;
+            *reinterpret_cast<bf16x4v*>(ql_img + off) = lo;
+        }
+    }
+    lds_barrier();
+    WA_STAMP(3, WA_CLOCK());
+    bf16x8 qh[8], ql[8];
+    {
+        const unsigned char* qh_img = smem + kX3BufB;
+        const unsigned char* ql_img = smem + kX3GrpB + kX3BufB;
+        const int row = wq * kQW + c;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int off = row * 256 + (((2 * i + h) ^ (row & 15)) * 16);
+            qh[i] = *reinterpret_cast<const bf16x8*>(qh_img + off);
+            ql[i] = *reinterpret_cast<const bf16x8*>(ql_img + off);
+        }
+    }
+    // group 1 runs one interval behind group 0 (its Q reads above finish before this barrier, i.e.
+    // before group 0 stages half tile 1 over the Q images in its step 1)
+    if (grp == 1) lds_barrier();
+    // static priority for the second-dispatched half (MI355X_MICROARCH.md "Two waves per SIMD" 4)
+    if (PRIO && grp == 1) __builtin_amdgcn_s_setprio(1);
+
+    floatx16 o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+    float m_run = -INFINITY, l_run = 0.f;
+    bf16x8 ph[2], pl[2];
+    floatx16 sacc;
+
+    // PV tr16 read addresses within a V image (keys 16 ksx + 4h + qq and + 8, d block dt)
+    const int gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+    auto iter = [&](int t, auto bufc) -> bool {
+        constexpr int BUF = decltype(bufc)::value;
+        // ======== MFMA interval
+        if (t >= 1) {
+            const unsigned char* vh = gsm + (BUF ^ 1) * kX3BufB + 2 * kHImgB;
+            const unsigned char* vl = vh + kHImgB;
+#pragma unroll
+            for (int ksx = 0; ksx < 2; ++ksx) {
+                const int r0 = 16 * ksx + 4 * h + qq;
+#pragma unroll
+                for (int dt = 0; dt < 4; ++dt) {
+                    const int c0 = 4 * dt + 2 * ((lane >> 4) & 1) + (pp >> 1);
+                    const int a0 = vimg_off(r0, c0) + 8 * (pp & 1), a1 = vimg_off(r0 + 8, c0) + 8 * (pp & 1);
+                    typedef __attribute__((address_space(3))) shortx4 lds4;
+                    const shortx4 h0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(vh + a0));
+                    const shortx4 h1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(vh + a1));
+                    const shortx4 l0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(vl + a0));
+                    const shortx4 l1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds4*)(vl + a1));
+                    typedef short shortx8 __attribute__((ext_vector_type(8)));
+                    const shortx8 vh8 = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+                    const shortx8 vl8 = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vl8), ph[ksx], o[dt], 0, 0, 0);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vh8), pl[ksx], o[dt], 0, 0, 0);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vh8), ph[ksx], o[dt], 0, 0, 0);
+                }
+            }
+        }
+        if (t < nt) {
+            const unsigned char* kh = gsm + BUF * kX3BufB;
+            const unsigned char* kl = kh + kHImgB;
+            const floatx16 zero = {};
+            sacc = zero;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int off = c * 256 + (((2 * i + h) ^ (c & 15)) * 16);
+                const bf16x8 kh8 = *reinterpret_cast<const bf16x8*>(kh + off);
+                const bf16x8 kl8 = *reinterpret_cast<const bf16x8*>(kl + off);
+                sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kl8, qh[i], sacc, 0, 0, 0);
+                sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh8, ql[i], sacc, 0, 0, 0);
+                sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kh8, qh[i], sacc, 0, 0, 0);
+            }
+            if (p.shift) {
+                // one-hot key-region A fragment of key row c (slots 8h .. 8h + 7)
+                const int j = kbeg + t * kBK + kHalfK * grp + c;
+                const int kreg = win_region(p, wi, p.m == 1 ? j : j % p.L);
+                bf16x8 ma;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) ma[e] = (__bf16)(kreg == 8 * h + e ? kMaskBonus : 0.0f);
+                sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma, qmask, sacc, 0, 0, 0);
+            }
+        }
+        lds_barrier();
+        if (t < 8) WA_STAMP(4 + t, WA_CLOCK());
+        if (t == nt) return true;
+        // ======== VALU interval: staging, then the online softmax of S(t) -> P(t)
+        if (t + 1 < nt) {
+            stage(BUF ^ 1);
+            if (t + 2 < nt) gather(t + 2);
+        }
+        float bmax = max3_raw(sacc[0], sacc[1], sacc[2]);
+#pragma unroll
+        for (int r = 3; r < 15; r += 2) bmax = max3_raw(bmax, sacc[r], sacc[r + 1]);
+        bmax = fmaxf(bmax, sacc[15]);
+        const float bm2 = halves_max(bmax) * cl2;
+        if (__any(bm2 > m_run + kThr)) {
+            const float m_new = fmaxf(m_run, bm2);
+            const float corr = fast_exp2(m_run - m_new);
+            l_run *= corr;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= corr;
+            m_run = m_new;
+        }
+        float bsum = 0.f;
+#pragma unroll
+        for (int ksx = 0; ksx < 2; ++ksx) {
+            float pv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                pv[e] = fast_exp2(fmaf(sacc[8 * ksx + e], cl2, -m_run));
+                bsum += pv[e];
+            }
+            split8(pv, ph[ksx], pl[ksx]);
+        }
+        l_run += halves_sum(bsum);
+        lds_barrier();
+        return false;
+    };
+    for (int t = 0;; t += 2) {
+        if (iter(t, IC<0>{})) break;
+        if (iter(t + 1, IC<1>{})) break;
+    }
+    if (grp == 0) lds_barrier();
+
+    // combine the two key halves: group 1 parks (O, m, l) in LDS, group 0 merges and writes
+    float4* const park = reinterpret_cast<float4*>(smem) + (size_t)wq * 16 * 64 + lane;
+    float* const park_ml = reinterpret_cast<float*>(smem + 4 * 16 * 64 * 16) + (wq * 64 + lane) * 2;
+    if (grp == 1) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                park[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
+        park_ml[0] = m_run;
+        park_ml[1] = l_run;
+    }
+    lds_barrier();
+    if (grp == 1) return;
+    {
+        const float m1 = park_ml[0], l1 = park_ml[1];
+        const float mm = fmaxf(m_run, m1);
+        const float f0 = fast_exp2(m_run - mm), f1 = fast_exp2(m1 - mm);
+        l_run = l_run * f0 + l1 * f1;
+        m_run = mm;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const float4 x = park[(dt * 4 + u) * 64];
+                o[dt][4 * u] = o[dt][4 * u] * f0 + x.x * f1;
+                o[dt][4 * u + 1] = o[dt][4 * u + 1] * f0 + x.y * f1;
+                o[dt][4 * u + 2] = o[dt][4 * u + 2] * f0 + x.z * f1;
+                o[dt][4 * u + 3] = o[dt][4 * u + 3] * f0 + x.w * f1;
+            }
+    }
+    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
+    if (p.ksplit == 1) {
+        const float inv = 1.0f / l_run;
+        float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                store4(dst + 32 * dt + 8 * u, make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv,
+                                                          o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
+    } else {
+        const size_t row = pidx(p, b, wi, ks, tq);
+        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, wq)) + lane;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
+        if (h == 0) {
+            part.m[row] = m_run * kLn2;
+            part.l[row] = l_run;
+        }
+    }
+    WA_STAMP(12, WA_CLOCK());
+    WA_STAMP(13, wall_clock64());
+}
+
 // K and V (fp32, n elements each) -> [kh | kl | vh | vl] bf16, x = xh + xl (see win_attn_x3_kernel)
 __global__ void __launch_bounds__(256) split_kv_kernel(const float4* __restrict__ k, const float4* __restrict__ v,
                                                        __bf16* __restrict__ out, size_t n4) {
@@ -1717,6 +2025,24 @@ static int x3_params(tsplat::winattn::Params& p, int32_t batch, int32_t height, 
     return TSPLAT_OK;
 }
 
+// the bf16x3 main kernel: the 8-wave two-group form (default) or the round-5 4-wave form
+// (TSPLAT_WINATTN_X3=v1, the A/B knob); same grid, partials and output either way
+static void launch_x3(const tsplat::winattn::Params& p, int splits, int batch, const float* q, const __bf16* kv,
+                      size_t nkv, float* out, tsplat::winattn::Partials part, const tsplat::prof::ExtEvents& ev,
+                      hipStream_t stream) {
+    using namespace tsplat::winattn;
+    const dim3 grid(p.L / kBQ3, splits * splits, batch * p.ksplit);
+    if (env_is("TSPLAT_WINATTN_X3", "v1"))
+        hipExtLaunchKernelGGL(win_attn_x3_kernel, grid, dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p, q, kv,
+                              kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
+    else if (env_is("TSPLAT_WINATTN_X3_PRIO", "0"))  // A/B knob: no static priority
+        hipExtLaunchKernelGGL(win_attn_x3_v2_kernel<false>, grid, dim3(kThreads8), 0, stream, ev.start, ev.stop, 0, p,
+                              q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
+    else
+        hipExtLaunchKernelGGL(win_attn_x3_v2_kernel<true>, grid, dim3(kThreads8), 0, stream, ev.start, ev.stop, 0, p,
+                              q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
+}
+
 // bf16x3 window attention, main kernel only (partials for the merge projection); kv_x3 =
 // tsplat_split_kv_bf16x3(k, v) ([kh | kl | vh | vl], k / v [batch, key_views, H*W, 128]). Same
 // shapes, key split and workspace as tsplat_win_attn_partials_fwd.
@@ -1738,9 +2064,7 @@ extern "C" int tsplat_win_attn_x3_partials_fwd(const float* q, const void* kv_x3
     const __bf16* kv = (const __bf16*)kv_x3;
     hipStream_t stream = (hipStream_t)stream_;
     const prof::ExtEvents ev = prof::ext_events(prof::kWinAttn);
-    hipExtLaunchKernelGGL(win_attn_x3_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit), dim3(kThreads), 0,
-                          stream, ev.start, ev.stop, 0, p, q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv,
-                          (float*)nullptr, part);
+    launch_x3(p, splits, batch, q, kv, nkv, (float*)nullptr, part, ev, stream);
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
@@ -1767,8 +2091,7 @@ extern "C" int tsplat_win_attn_x3_fwd(const float* q, const void* kv_x3, float* 
     const __bf16* kv = (const __bf16*)kv_x3;
     hipStream_t stream = (hipStream_t)stream_;
     const prof::ExtEvents ev = prof::ext_events(prof::kWinAttn);
-    hipExtLaunchKernelGGL(win_attn_x3_kernel, dim3(p.L / kBQ3, splits * splits, batch * p.ksplit), dim3(kThreads), 0,
-                          stream, ev.start, ev.stop, 0, p, q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
+    launch_x3(p, splits, batch, q, kv, nkv, out, part, ev, stream);
     if (p.ksplit > 1)
         hipLaunchKernelGGL(win_attn_combine_x32_kernel<float>, dim3(p.L / kBQ3 * 16, splits * splits, batch),
                            dim3(kThreads), 0, stream, p, part, out);
