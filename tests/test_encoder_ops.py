@@ -103,17 +103,19 @@ def test_window_attention_kernel_large_logits(device):
 @pytest.mark.gpu
 @pytest.mark.parametrize("hw,b,variant", [(16, 1, "dedup"), (32, 2, "dedup"), (64, 1, "dedup"), (64, 2, "dedup"),
                                           (16, 1, "direct"), (64, 1, "direct"), (16, 1, "bitmap"),
-                                          (64, 2, "bitmap")])
+                                          (64, 2, "bitmap"), (64, 2, "run6")])
 def test_uv_coarse_kernel(device, monkeypatch, hw, b, variant):
-    """Run-deduplicated coarse correlation (default), the round-2 bitmap kernel
-    (TSPLAT_UV_COARSE_BITMAP=1) and the sample-then-dot kernel (TSPLAT_UV_COARSE_DIRECT=1), incl.
-    the production 64 x 64 map at b = 1 and 2."""
+    """Run-deduplicated coarse correlation (default; run6: its 6-wave form, TSPLAT_CORR_RUN_WPE=6),
+    the round-2 bitmap kernel (TSPLAT_UV_COARSE_BITMAP=1) and the sample-then-dot kernel
+    (TSPLAT_UV_COARSE_DIRECT=1), incl. the production 64 x 64 map at b = 1 and 2."""
     from transplat_amd import kernels as K
 
     if variant == "direct":
         monkeypatch.setenv("TSPLAT_UV_COARSE_DIRECT", "1")
     if variant == "bitmap":
         monkeypatch.setenv("TSPLAT_UV_COARSE_BITMAP", "1")
+    if variant == "run6":  # the run kernel at the 6-wave register budget (two dot passes in flight)
+        monkeypatch.setenv("TSPLAT_CORR_RUN_WPE", "6")
     intr, pose, disp = _cams(b, hw)
     feat = seeded((b, 2, hw * hw, 128), 31)
     ref = E.uv_coarse(feat, intr, pose, disp, hw, hw)
@@ -490,10 +492,12 @@ def test_window_attention_x3_kernel(device, hw, m, shift, b, grow):
 @pytest.mark.gpu
 @pytest.mark.parametrize("variant,ksplit,shift,grow", [("v1", 0, True, False), ("v1", 0, False, True),
                                                         ("v2", 1, True, False), ("v2", 2, True, True),
-                                                        ("v2", 8, True, False), ("v2", 8, False, True)])
+                                                        ("v2", 8, True, False), ("v2", 8, False, True),
+                                                        ("v2s", 0, True, False), ("v2s", 2, False, True)])
 def test_window_attention_x3_variants(device, monkeypatch, variant, ksplit, shift, grow):
-    """The round-5 4-wave x3 kernel (TSPLAT_WINATTN_X3=v1) and the two-group kernel (default) under
-    forced key splits (1: no partials, normalised output; 2 / 8: 8 / 2 key tiles per workgroup), same
+    """The round-5 4-wave x3 kernel (TSPLAT_WINATTN_X3=v1) and the two-group kernel (default, in
+    window-major XCD order; v2s: key-split-major order, TSPLAT_WINATTN_X3_XCD=split) under forced
+    key splits (1: no partials, normalised output; 2 / 8: 8 / 2 key tiles per workgroup), same
     bounds as test_window_attention_x3_kernel, and the two kernels within 2e-5 of each other (they
     differ only in the running maxima the P split is taken against and the sum order)."""
     from transplat_amd import kernels as K
@@ -510,6 +514,9 @@ def test_window_attention_x3_variants(device, monkeypatch, variant, ksplit, shif
     if ksplit:
         monkeypatch.setenv("TSPLAT_WINATTN_KSPLIT", str(ksplit))
     args = (q.to(device), k.to(device), v.to(device), hw, hw, 2, shift)
+    if variant == "v2s":  # the two-group kernel in key-split-major XCD order
+        monkeypatch.setenv("TSPLAT_WINATTN_X3_XCD", "split")
+        variant = "v2"
     monkeypatch.setenv("TSPLAT_WINATTN_X3", variant)
     out = K.window_attention_x3(*args).cpu().double()
     monkeypatch.setenv("TSPLAT_WINATTN_X3", "v1" if variant == "v2" else "v2")

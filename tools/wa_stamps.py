@@ -3,7 +3,8 @@ tools/_bin/wastamp.so, tools/build_stamp_wa.sh; run with TSPLAT_LIB pointing at 
 For each shape: workgroups per CU (HW_ID / XCC_ID), the spread of start times, the shader clock
 rate, and the median / p90 of each phase in shader cycles: prologue (Q + first K/V tile, first
 barrier), each key tile, epilogue (partial or output store).
-usage: TSPLAT_LIB=tools/_bin/wastamp.so python tools/wa_stamps.py [--x3]  (--x3: the bf16x3 kernel)"""
+usage: TSPLAT_LIB=tools/_bin/wastamp.so python tools/wa_stamps.py [--x3 | --bf16]  (--x3: the bf16x3 kernel,
+--bf16: bf16 operands, i.e. the v3 kernel at b = 16 -- there "tile t" is the MFMA interval of tile t)"""
 import collections
 import ctypes
 import sys
@@ -28,12 +29,15 @@ def q(t, f):
 
 
 X3 = "--x3" in sys.argv
+BF16 = "--bf16" in sys.argv  # the bf16 v3 kernel (B >= 8 windows x 4 query blocks: b = 16 here)
 attn = kernels.window_attention_x3 if X3 else kernels.window_attention
 g = torch.Generator(device=dev).manual_seed(0)
 with torch.no_grad():
     for b, shift in ((2, 0), (2, 1), (16, 1)):
         hw = 64
         qq, k, v = (torch.randn((b, hw * hw, 128), device=dev, generator=g) for _ in range(3))
+        if BF16:
+            qq, k, v = qq.bfloat16(), k.bfloat16(), v.bfloat16()
         for _ in range(3):
             attn(qq, k, v, hw, hw, 2, bool(shift))
         torch.cuda.synchronize()

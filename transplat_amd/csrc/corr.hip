@@ -377,8 +377,9 @@ uv_coarse_dedup_kernel(Geo g, int nw, const float* __restrict__ feat, const floa
 // The result is the bitmap kernel's bit for bit (same dots, same per-sample sum order).
 constexpr int kRunWaves = 4;
 
-// LDS words per wave: src [D cells][4] ranks, list [4 D] corner pixels, dots [4 D]
-__host__ __device__ inline int run_lds_words(int depths) { return 12 * depths; }
+// LDS words per wave: src [D cells][4] ranks, then [4 D] corner pixels that the dot phase overwrites
+// with the corners' dots (entry j is read by its 8 lanes before its dot is stored there)
+__host__ __device__ inline int run_lds_words(int depths) { return 8 * depths; }
 
 // LDS hand-off between the lanes of ONE wave (its LDS operations execute in order)
 __device__ __forceinline__ void wave_lds_sync() {
@@ -387,8 +388,11 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int S>
-__global__ void __launch_bounds__(kRunWaves * 64)
+// WPE: waves per SIMD the register budget is sized for -- 8 (default for D <= 128: 60 VGPRs, one dot
+// pass in flight per wave, all 2,048 workgroups of the production launch resident at once) or 6
+// (73 VGPRs, two passes in flight; TSPLAT_CORR_RUN_WPE=6, and D > 128)
+template <int S, int WPE>
+__global__ void __launch_bounds__(kRunWaves * 64, WPE)
 uv_coarse_run_kernel(Geo g, const float* __restrict__ feat, const float* __restrict__ cams,
                      const float* __restrict__ disp, float* __restrict__ out) {
     extern __shared__ int rsmem[];
@@ -399,7 +403,7 @@ uv_coarse_run_kernel(Geo g, const float* __restrict__ feat, const float* __restr
     if (p >= HW) return;  // wave-uniform; nothing below synchronises the workgroup
     int* src = rsmem + (size_t)wave * run_lds_words(g.D);
     int* list = src + 4 * g.D;
-    float* dots = reinterpret_cast<float*>(list + 4 * g.D);
+    float* dots = reinterpret_cast<float*>(list);
 
     // own feature (dot operand, 8 lanes per corner) and this lane's disparities first
     const int sub = lane & 7;
@@ -533,14 +537,23 @@ uv_coarse_run_kernel(Geo g, const float* __restrict__ feat, const float* __restr
             acc += __shfl_xor(acc, 4, 8);
             if (jj < total && sub == 0) dots[jj] = acc;
         };
-        float4 xa[4], xb[4];
-        int j = lane >> 3;
-        if (j < jend) load(j, xa);
-        for (; j < jend; j += 16) {
-            if (j + 8 < jend) load(j + 8, xb);
-            dot(j, xa);
-            if (j + 16 < jend) load(j + 16, xa);
-            if (j + 8 < jend) dot(j + 8, xb);
+        if constexpr (WPE >= 8) {
+            // one pass in flight per wave: at 8 waves per SIMD the other waves cover the latency
+            for (int j = lane >> 3; j < jend; j += 8) {
+                float4 xa[4];
+                load(j, xa);
+                dot(j, xa);
+            }
+        } else {
+            float4 xa[4], xb[4];
+            int j = lane >> 3;
+            if (j < jend) load(j, xa);
+            for (; j < jend; j += 16) {
+                if (j + 8 < jend) load(j + 8, xb);
+                dot(j, xa);
+                if (j + 16 < jend) load(j + 16, xa);
+                if (j + 8 < jend) dot(j + 8, xb);
+            }
         }
     }
     wave_lds_sync();
@@ -872,12 +885,22 @@ extern "C" int tsplat_uv_coarse_fwd(const float* feat, const float* cams, const 
     const size_t run_lds = (size_t)kRunWaves * run_lds_words(depths) * sizeof(int);
     if (S <= kDedupMaxS && run_lds <= 64 * 1024 && !(env && env[0] == '1') && !(benv && benv[0] == '1') && !diag) {
         const dim3 grid(ceil_div(hw, kRunWaves), 2 * batch), block(kRunWaves * 64);
-        switch (S) {
-            case 1: hipLaunchKernelGGL(uv_coarse_run_kernel<1>, grid, block, run_lds, stream, g, feat, cams, disp, out); break;
-            case 2: hipLaunchKernelGGL(uv_coarse_run_kernel<2>, grid, block, run_lds, stream, g, feat, cams, disp, out); break;
-            case 3: hipLaunchKernelGGL(uv_coarse_run_kernel<3>, grid, block, run_lds, stream, g, feat, cams, disp, out); break;
-            default: hipLaunchKernelGGL(uv_coarse_run_kernel<4>, grid, block, run_lds, stream, g, feat, cams, disp, out); break;
+        const char* renv = getenv("TSPLAT_CORR_RUN_WPE");
+        const bool w8 = !renv || atoi(renv) != 6;
+#define TSPLAT_UVR(SS)                                                                                           \
+    do {                                                                                                         \
+        if (w8)                                                                                                  \
+            hipLaunchKernelGGL((uv_coarse_run_kernel<SS, 8>), grid, block, run_lds, stream, g, feat, cams, disp, out); \
+        else                                                                                                     \
+            hipLaunchKernelGGL((uv_coarse_run_kernel<SS, 6>), grid, block, run_lds, stream, g, feat, cams, disp, out); \
+    } while (0)
+        switch (S) {  // (S >= 3 spills at the 8-wave budget: 6)
+            case 1: TSPLAT_UVR(1); break;
+            case 2: TSPLAT_UVR(2); break;
+            case 3: hipLaunchKernelGGL((uv_coarse_run_kernel<3, 6>), grid, block, run_lds, stream, g, feat, cams, disp, out); break;
+            default: hipLaunchKernelGGL((uv_coarse_run_kernel<4, 6>), grid, block, run_lds, stream, g, feat, cams, disp, out); break;
         }
+#undef TSPLAT_UVR
     } else if (S <= kDedupMaxS && lds <= 64 * 1024 && !(env && env[0] == '1')) {
         const dim3 grid(ceil_div(hw, kDedupWaves), 2 * batch), block(kDedupWaves * 64);
         // 6 waves per SIMD (default; profiles/r5/late/corr_wpe.txt: b = 8 120.5 -> 111.4 us, b = 1 24.3 /

@@ -955,6 +955,9 @@ __global__ void __launch_bounds__(kThreads8, 1)
 win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __restrict__ k,
                         const __bf16* __restrict__ v, __bf16* __restrict__ out) {
     __shared__ __attribute__((aligned(16))) unsigned char smem[kLds3];
+    WA_STAMP(0, wall_clock64());
+    WA_STAMP(1, WA_HWID());
+    WA_STAMP(2, WA_CLOCK());
 
     int qblk, wi, b;
     xcd_block_coords(qblk, wi, b);
@@ -1054,6 +1057,7 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
     }
     if (grp == 0 ? ntiles > 1 : ntiles > 2) gather(grp == 0 ? 1 : 2);
     lds_barrier();
+    WA_STAMP(3, WA_CLOCK());
     // group B runs one interval behind A: one barrier before its loop (A: one after), so every
     // wave passes 2 (ntiles + 1) + 1 barriers
     if (grp == 1) lds_barrier();
@@ -1100,6 +1104,7 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
             }
         }
         lds_barrier();
+        if (t < 8) WA_STAMP(4 + t, WA_CLOCK());
         if (t == ntiles) return true;
         // ======== VALU interval: staging, then the online softmax of S(t) -> P(t)
         // A writes tile t + 1 into buffer (t + 1) % 3, whose previous tile t - 2 was last read by
@@ -1158,6 +1163,8 @@ win_attn_bf16_v3_kernel(Params p, const __bf16* __restrict__ q, const __bf16* __
         for (int u = 0; u < 4; ++u)
             store4(dst + 32 * dt + 8 * u, make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv,
                                                       o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
+    WA_STAMP(12, WA_CLOCK());
+    WA_STAMP(13, wall_clock64());
 }
 
 // ============================================================================================
@@ -1427,7 +1434,7 @@ constexpr int kX3BufB = 4 * kHImgB;        // Kh, Kl, Vh, Vl (32 KB)
 constexpr int kX3GrpB = 2 * kX3BufB;       // two buffers per group (64 KB)
 constexpr int kX3Lds = 2 * kX3GrpB;        // 128 KB
 
-template <bool PRIO>
+template <bool PRIO, bool WXCD>
 __global__ void __launch_bounds__(kThreads8, 1)
 win_attn_x3_v2_kernel(Params p, const float* __restrict__ q, const __bf16* __restrict__ khg,
                       const __bf16* __restrict__ klg, const __bf16* __restrict__ vhg, const __bf16* __restrict__ vlg,
@@ -1437,9 +1444,26 @@ win_attn_x3_v2_kernel(Params p, const float* __restrict__ q, const __bf16* __res
     WA_STAMP(0, wall_clock64());
     WA_STAMP(1, WA_HWID());
     WA_STAMP(2, WA_CLOCK());
-    int qblk, wi, bz;
-    xcd_block_coords(qblk, wi, bz);
-    const int b = bz / p.ksplit, ks = bz - b * p.ksplit;
+    int qblk, wi, b, ks;
+    if (WXCD) {
+        // window-major XCD order: the remapped id walks query block, then key split, then window,
+        // so the 8 x ksplit workgroups of one (batch, window) share an XCD (and its L2): Q is
+        // fetched there once instead of once per key split's XCD
+        const int X = gridDim.x, nwin = gridDim.y;
+        const int n = blockIdx.x + X * (blockIdx.y + nwin * blockIdx.z);
+        int m = xcd_remap(n, X * nwin * gridDim.z);
+        qblk = m % X;
+        m /= X;
+        ks = m % p.ksplit;
+        m /= p.ksplit;
+        wi = m % nwin;
+        b = m / nwin;
+    } else {
+        int bz;
+        xcd_block_coords(qblk, wi, bz);
+        b = bz / p.ksplit;
+        ks = bz - b * p.ksplit;
+    }
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int grp = wid >> 2, wq = wid & 3;
@@ -1452,13 +1476,8 @@ win_attn_x3_v2_kernel(Params p, const float* __restrict__ q, const __bf16* __res
     const int nt = p.keys_per_split / kBK;
 
     const int tq = qblk * kBQ3 + wq * kQW + c;
-    const int qpix = win_pixel(p, wi, tq);
-    bf16x8 qmask;
-    {
-        const int qreg = p.shift ? win_region(p, wi, tq) : 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qmask[j] = (__bf16)(qreg == 8 * h + j ? 1.0f : 0.0f);
-    }
+    // the query's region slot in the mask step's B operand (formed per tile: 4 registers fewer)
+    const int qslot = (p.shift ? win_region(p, wi, tq) : 0) - 8 * h;
 
     // gather: wave wq of a group moves image wq (Kh, Kl, Vh, Vl) of its half tile, one 1-KB wave
     // instruction = 4 whole 256-B rows (16 lanes per row, lane = 16-B chunk: 8 cache lines per
@@ -1606,6 +1625,9 @@ win_attn_x3_v2_kernel(Params p, const float* __restrict__ q, const __bf16* __res
                 bf16x8 ma;
 #pragma unroll
                 for (int e = 0; e < 8; ++e) ma[e] = (__bf16)(kreg == 8 * h + e ? kMaskBonus : 0.0f);
+                bf16x8 qmask;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) qmask[e] = (__bf16)(qslot == e ? 1.0f : 0.0f);
                 sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ma, qmask, sacc, 0, 0, 0);
             }
         }
@@ -1651,60 +1673,70 @@ win_attn_x3_v2_kernel(Params p, const float* __restrict__ q, const __bf16* __res
     }
     if (grp == 0) lds_barrier();
 
-    // combine the two key halves: group 1 parks (O, m, l) in LDS, group 0 merges and writes
-    float4* const park = reinterpret_cast<float4*>(smem) + (size_t)wq * 16 * 64 + lane;
-    float* const park_ml = reinterpret_cast<float*>(smem + 4 * 16 * 64 * 16) + (wq * 64 + lane) * 2;
-    if (grp == 1) {
+    // combine the two key halves, split by d: group g finishes O^T rows d in [64 g, 64 g + 64)
+    // (accumulators dt = 2 g, 2 g + 1) and parks the other half, plus its (m, l), for the other group
+    float4* const park = reinterpret_cast<float4*>(smem);
+    float2* const park_ml = reinterpret_cast<float2*>(smem + 2 * 4 * 8 * 64 * 16);
+    auto finish = [&](auto gc) {
+        constexpr int G = decltype(gc)::value;  // this group (static accumulator indices)
+        float4* const mine = park + (size_t)(G * 4 + wq) * 8 * 64 + lane;
+        const float4* const theirs = park + (size_t)((G ^ 1) * 4 + wq) * 8 * 64 + lane;
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                park[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
-        park_ml[0] = m_run;
-        park_ml[1] = l_run;
-    }
-    lds_barrier();
-    if (grp == 1) return;
-    {
-        const float m1 = park_ml[0], l1 = park_ml[1];
-        const float mm = fmaxf(m_run, m1);
-        const float f0 = fast_exp2(m_run - mm), f1 = fast_exp2(m1 - mm);
-        l_run = l_run * f0 + l1 * f1;
-        m_run = mm;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const float4 x = park[(dt * 4 + u) * 64];
-                o[dt][4 * u] = o[dt][4 * u] * f0 + x.x * f1;
-                o[dt][4 * u + 1] = o[dt][4 * u + 1] * f0 + x.y * f1;
-                o[dt][4 * u + 2] = o[dt][4 * u + 2] * f0 + x.z * f1;
-                o[dt][4 * u + 3] = o[dt][4 * u + 3] * f0 + x.w * f1;
+                constexpr int D0 = 2 * (G ^ 1);
+                mine[(j * 4 + u) * 64] =
+                    make_float4(o[D0 + j][4 * u], o[D0 + j][4 * u + 1], o[D0 + j][4 * u + 2], o[D0 + j][4 * u + 3]);
             }
-    }
-    // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
-    if (p.ksplit == 1) {
-        const float inv = 1.0f / l_run;
-        float* dst = out + ((size_t)b * HW + qpix) * kC + 4 * h;
+        park_ml[(G * 4 + wq) * 64 + lane] = make_float2(m_run, l_run);
+        lds_barrier();
+        const float2 ml1 = park_ml[((G ^ 1) * 4 + wq) * 64 + lane];
+        const float mm = fmaxf(m_run, ml1.x);
+        const float f0 = fast_exp2(m_run - mm), f1 = fast_exp2(ml1.x - mm);
+        l_run = l_run * f0 + ml1.y * f1;
+        m_run = mm;
+        constexpr int D = 2 * G;
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
+        for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                store4(dst + 32 * dt + 8 * u, make_float4(o[dt][4 * u] * inv, o[dt][4 * u + 1] * inv,
-                                                          o[dt][4 * u + 2] * inv, o[dt][4 * u + 3] * inv));
-    } else {
-        const size_t row = pidx(p, b, wi, ks, tq);
-        float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, wq)) + lane;
+            for (int u = 0; u < 4; ++u) {
+                const float4 x = theirs[(j * 4 + u) * 64];
+                o[D + j][4 * u] = o[D + j][4 * u] * f0 + x.x * f1;
+                o[D + j][4 * u + 1] = o[D + j][4 * u + 1] * f0 + x.y * f1;
+                o[D + j][4 * u + 2] = o[D + j][4 * u + 2] * f0 + x.z * f1;
+                o[D + j][4 * u + 3] = o[D + j][4 * u + 3] * f0 + x.w * f1;
+            }
+        // O^T[d = 32 dt + 8u + 4h + j][q = c] in o[dt][4u + j]
+        if (p.ksplit == 1) {
+            const float inv = 1.0f / l_run;
+            float* dst = out + ((size_t)b * HW + win_pixel(p, wi, tq)) * kC + 4 * h;
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
+            for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                dst[(dt * 4 + u) * 64] = make_float4(o[dt][4 * u], o[dt][4 * u + 1], o[dt][4 * u + 2], o[dt][4 * u + 3]);
-        if (h == 0) {
-            part.m[row] = m_run * kLn2;
-            part.l[row] = l_run;
+                for (int u = 0; u < 4; ++u)
+                    store4(dst + 32 * (D + j) + 8 * u,
+                           make_float4(o[D + j][4 * u] * inv, o[D + j][4 * u + 1] * inv, o[D + j][4 * u + 2] * inv,
+                                       o[D + j][4 * u + 3] * inv));
+        } else {
+            float4* dst = reinterpret_cast<float4*>(part.o + lane_tile_base(p, b, wi, ks, qblk, wq)) + lane;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    dst[((D + j) * 4 + u) * 64] =
+                        make_float4(o[D + j][4 * u], o[D + j][4 * u + 1], o[D + j][4 * u + 2], o[D + j][4 * u + 3]);
+            if (G == 0 && h == 0) {
+                const size_t row = pidx(p, b, wi, ks, tq);
+                part.m[row] = m_run * kLn2;
+                part.l[row] = l_run;
+            }
         }
-    }
+    };
+    if (grp == 0)
+        finish(IC<0>{});
+    else
+        finish(IC<1>{});
     WA_STAMP(12, WA_CLOCK());
     WA_STAMP(13, wall_clock64());
 }
@@ -2036,11 +2068,14 @@ static void launch_x3(const tsplat::winattn::Params& p, int splits, int batch, c
         hipExtLaunchKernelGGL(win_attn_x3_kernel, grid, dim3(kThreads), 0, stream, ev.start, ev.stop, 0, p, q, kv,
                               kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
     else if (env_is("TSPLAT_WINATTN_X3_PRIO", "0"))  // A/B knob: no static priority
-        hipExtLaunchKernelGGL(win_attn_x3_v2_kernel<false>, grid, dim3(kThreads8), 0, stream, ev.start, ev.stop, 0, p,
-                              q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
-    else
-        hipExtLaunchKernelGGL(win_attn_x3_v2_kernel<true>, grid, dim3(kThreads8), 0, stream, ev.start, ev.stop, 0, p,
-                              q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
+        hipExtLaunchKernelGGL((win_attn_x3_v2_kernel<false, true>), grid, dim3(kThreads8), 0, stream, ev.start,
+                              ev.stop, 0, p, q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
+    else if (env_is("TSPLAT_WINATTN_X3_XCD", "split"))  // A/B knob: key-split-major XCD order
+        hipExtLaunchKernelGGL((win_attn_x3_v2_kernel<true, false>), grid, dim3(kThreads8), 0, stream, ev.start,
+                              ev.stop, 0, p, q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
+    else  // window-major XCD order (profiles/r6/traffic_win_attn_x3_xcd.txt: fetch 17.4 vs 30.0 MB)
+        hipExtLaunchKernelGGL((win_attn_x3_v2_kernel<true, true>), grid, dim3(kThreads8), 0, stream, ev.start,
+                              ev.stop, 0, p, q, kv, kv + nkv, kv + 2 * nkv, kv + 3 * nkv, out, part);
 }
 
 // bf16x3 window attention, main kernel only (partials for the merge projection); kv_x3 =
