@@ -1,0 +1,6 @@
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export PYTHONPATH=$(pwd)
+r() { echo "== $1"; env $2 timeout -k 10 200 python -u tools/graph_vs_eager.py 2>&1 | grep -v amdgpu.ids | tail -5; }
+r linx0 TSPLAT_LINX=0 && r linx0b TSPLAT_LINX=0 && r side0 TSPLAT_LINX_SIDE=0 && r side0b TSPLAT_LINX_SIDE=0 && r side0c TSPLAT_LINX_SIDE=0

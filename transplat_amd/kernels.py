@@ -1268,8 +1268,14 @@ def linear_bf16x3(x, weight, bias=None, act: str = "none", cache: bool = True):
 # faster where N >= 1024 or M >= 4096 (tools/bench_xf32.py, profiles/r4/g12/xf32_tf32.log: DINOv2
 # qkv 20.7 vs 29.6 us, fc1 25.7 vs 30.5, MVT fc1 22.8 vs 39.2; proj / fc2 at N = 768 slower: they stay
 # exact fp32). The bias (+ exact GELU) then runs as one pass (tsplat_bias_act_nhwc_fwd on [rows, N]).
-# TSPLAT_LINX=0 keeps every linear on exact fp32 F.linear in bf16x3 mode.
-_LINX = os.environ.get("TSPLAT_LINX", "1") == "1"
+# OFF by default since round 6: with these emulated-xf32 library GEMMs in the step (DINOv2's on the
+# current stream beside the backbone branch's library GEMMs on the side stream), hipGraph replays of
+# the C2 step were NOT the eager step: 1-3 of 4 replays moved 0.6-4 % of the pixels by up to 4e-2
+# (tools/graph_vs_eager.py, profiles/r6/graph_vs_eager.log), with every library GEMM exact fp32 8 of
+# 8 replays were bit-identical to eager. TSPLAT_LINX=1 restores the route (A/B only);
+# TSPLAT_LINX_SIDE=0 with it keeps it off the side streams (measured: still racing).
+_LINX = os.environ.get("TSPLAT_LINX", "0") == "1"
+_LINX_SIDE = os.environ.get("TSPLAT_LINX_SIDE", "1") == "1"
 
 
 def linear_xf32_ok(x, weight) -> bool:
@@ -1279,6 +1285,11 @@ def linear_xf32_ok(x, weight) -> bool:
         return False
     n, k = weight.shape
     m = x.numel() // max(k, 1)
+    if not _LINX_SIDE:
+        from . import streams
+
+        if streams._is_side(torch.cuda.current_stream(x.device)):
+            return False
     return n % 4 == 0 and ((n >= 1024 and m >= 512) or (m >= 4096 and n >= 512))
 
 
