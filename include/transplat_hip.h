@@ -596,6 +596,26 @@ int tsplat_resize_bilinear_nhwc_fwd(const float* x, float* y, int32_t n, int32_t
 int tsplat_resize_bilinear_nchw_fwd(const float* x, float* y, int32_t planes, int32_t height, int32_t width,
                                     int32_t out_height, int32_t out_width, void* stream);
 
+/* Split-bf16 ("bf16x3") GEMM for the bf16x3 dense mode's fp32 linears (DINOv2-B/14 qkv / proj /
+ * fc1 + GELU / fc2 at M = 650: src/depth_anything_v2/dinov2_layers/attention.py:70-75, mlp.py:33-40;
+ * the reference's nn.Linear in TF32, src/main.py:15), replacing the hipBLASLt calls of F.linear.
+ * tsplat_gemm_x3_pack splits W [n, k] fp32 (nn.Linear weight) once into its hi / lo bf16 MFMA
+ * fragments (tsplat_gemm_x3_pack_bytes(n, k) bytes, 16-B aligned). tsplat_gemm_x3_fwd:
+ * out[s, m, n] = sum over split s's share of k of x[m, k] W[n, k] (+ bias[n] in slab 0; act 1 =
+ * exact-erf GELU, only with ksplit 1), x [m, k] fp32 rows contiguous, k % 4 == 0, n % 4 == 0, x /
+ * bias / out 16-B aligned, 1 <= ksplit <= ceil(k / 64) with every split non-empty; out holds ksplit
+ * slabs [m, n] whose sum is the product (tsplat_residual_ln_slabs_fwd adds them in order). */
+size_t tsplat_gemm_x3_pack_bytes(int32_t n, int32_t k);
+int tsplat_gemm_x3_pack(const float* w, void* wp, int32_t n, int32_t k, void* stream);
+int tsplat_gemm_x3_fwd(const float* x, const void* wp, const float* bias, float* out, int32_t m, int32_t n, int32_t k,
+                       int32_t ksplit, int32_t act, void* stream);
+
+/* tsplat_residual_ln_fwd with the sub-layer output y given as nslab partial slabs [nslab, rows, dim]
+ * (split-K GEMM output, tsplat_gemm_x3_fwd) summed in slab order before the LayerScale multiply. */
+int tsplat_residual_ln_slabs_fwd(const float* x, const float* y, int32_t nslab, const float* ls, const float* ln_w,
+                                 const float* ln_b, float ln_eps, float* x_out, float* n_out, int32_t rows,
+                                 int32_t dim, void* stream);
+
 /* Diagnostics: write the 100-MHz device wall clock into ((uint64_t*)buf)[slot] when this launch
  * runs on `stream` (stage marks of a captured / replayed step, tools/graph_stages.py). */
 int tsplat_timestamp(void* buf, int32_t slot, void* stream);

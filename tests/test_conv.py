@@ -855,3 +855,55 @@ def test_conv3x3_few_route_matches_kernel(device):
     s = ref.abs().max().item()
     assert (y_few.double() - ref).abs().max().item() / s < 2e-5
     assert (y_w.double() - ref).abs().max().item() / s < 2e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k,n,bias,act,ksplit", [
+    (650, 768, 2304, True, "none", 1), (650, 768, 3072, True, "gelu", 1), (650, 3072, 768, True, "none", 4),
+    (650, 768, 768, True, "none", 0), (650, 3072, 768, False, "none", 48), (33, 72, 100, True, "gelu", 1),
+    (1, 4, 4, False, "none", 1), (8192, 256, 1024, True, "none", 1), (130, 200, 260, True, "none", 2)])
+def test_gemm_x3_kernel(device, m, k, n, bias, act, ksplit):
+    """tsplat_gemm_x3_fwd (the bf16x3 mode's DINOv2 linears) against float64: the sum of its split-K
+    slabs within 2e-5 of max |y| and at most 1/8 of the TF32-operand error (the bar of the other
+    split kernels); ragged m / n / k (tile, chunk and split edges), every split a partial product
+    with the bias only in slab 0, the exact-GELU epilogue; two launches bit-identical."""
+    from transplat_amd import kernels as K
+
+    x = seeded((m, k), 191)
+    w = seeded((n, k), 192) / k ** 0.5
+    b = seeded((n,), 193) if bias else None
+    fn = torch.nn.functional.gelu if act == "gelu" else (lambda t: t)
+    ref = fn(torch.nn.functional.linear(x.double(), w.double(), b.double() if bias else None))
+    ref_tf = fn(torch.nn.functional.linear(tf32_round(x).double(), tf32_round(w).double(), b.double() if bias else None))
+    xd, wd = x.to(device), w.to(device)
+    with K.dense_precision("bf16x3"):
+        assert K.gemm_x3_ok(xd, wd)
+        y = K.gemm_x3(xd, wd, b.to(device) if bias else None, act=act, ksplit=ksplit)
+        y2 = K.gemm_x3(xd, wd, b.to(device) if bias else None, act=act, ksplit=ksplit)
+    s = ksplit if ksplit else K.gemm_ksplit(m, n, k)
+    assert y.shape == ((m, n) if s == 1 else (s, m, n))
+    assert torch.equal(y, y2)
+    out = (y.double().sum(0) if s > 1 else y.double()).cpu()
+    scale = ref.abs().max().item()
+    e3, etf = (out - ref).abs().max().item() / scale, (ref_tf - ref).abs().max().item() / scale
+    print(f"gemm x3 {(m, k, n)} {act} ksplit {s}: rel err {e3:.2e}, TF32 operands {etf:.2e}")
+    assert e3 < 2e-5 and e3 <= etf / 8, (e3, etf)
+
+
+@pytest.mark.gpu
+def test_residual_ln_slabs(device):
+    """tsplat_residual_ln_slabs_fwd == tsplat_residual_ln_fwd on the slabs' sum (summed in slab order,
+    bit for bit against the same order in fp32)."""
+    from transplat_amd import kernels as K
+
+    x = seeded((2, 325, 768), 201).to(device)
+    y = seeded((4, 2, 325, 768), 202).to(device)
+    ls = seeded((768,), 203).to(device)
+    norm = torch.nn.LayerNorm(768, eps=1e-6).to(device)
+    with torch.no_grad():
+        norm.weight.copy_(seeded((768,), 204))
+        norm.bias.copy_(seeded((768,), 205))
+    xs, ns = K.residual_ln(x, y, ls, norm)
+    ysum = ((y[0] + y[1]) + y[2]) + y[3]
+    xr, nr = K.residual_ln(x, ysum, ls, norm)
+    assert torch.equal(xs, xr) and torch.equal(ns, nr)

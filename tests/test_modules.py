@@ -94,7 +94,9 @@ GPU_TOL: dict = {
     ("depth_anything.depth", "fp32"): 4.6e-06,
     ("depth_anything.feat", "fp32"): 2.0e-06,
     ("depth_anything.depth", "bf16x3"): 4.2e-05,
-    ("depth_anything.feat", "bf16x3"): 1.5e-05,
+    # round 6: DINOv2's proj / fc2 moved from exact-fp32 hipBLASLt to the bf16x3 GEMM too (all four
+    # linears split-bf16 now): 1.43e-5 measured (1.13e-5 before), bound 2x
+    ("depth_anything.feat", "bf16x3"): 2.9e-05,
 }
 _GPU_TOL_DEFAULT = {"mvt_v2": 1e-3, "mvt_v3": 1e-3, "backbone.cnn": 1e-3, "backbone.trans": 1e-3, "uv.coarse": 1e-4,
                     "uv.fine": 1e-3, "unet_cv": 1e-4, "unet_depth": 1e-4, "depth_anything.depth": 1e-3,

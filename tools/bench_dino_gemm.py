@@ -1,6 +1,8 @@
 """DINOv2 ViT-B linears at M = 650 rows (2 images x 325 tokens): F.linear exact fp32 vs the
 emulated-xf32 library path vs split-K forms (K sliced over a batched GEMM, partials summed + bias),
 graph-timed, each with its max error / max |y| against float64. usage: bench_dino_gemm.py"""
+import sys
+
 import torch
 import torch.nn.functional as F
 
@@ -46,6 +48,15 @@ for name, (K, N) in SHAPES.items():
     ref = F.linear(x.double(), w.double(), b.double())
     scale = ref.abs().max().item()
     forms = {"fp32": lambda: F.linear(x, w, b), "xf32": xf32(lambda: torch.matmul(x, w.t()) + b)}
+    from transplat_amd import kernels as KK  # the hand-written split-bf16 GEMM (slabs summed for the error)
+    KK._DENSE = "bf16x3"
+    for s_ in (1, 2, 3, 4, 6, 8, 12):
+        if s_ == 1 or (s_ <= K // 128):
+            forms[f"gemm_x3_s{s_}"] = (lambda s_=s_: (lambda y: y if y.dim() == 2 else y.sum(0))(
+                KK.gemm_x3(x, w, b, ksplit=s_)))
+    forms["gemm_x3_auto"] = lambda: (lambda y: y if y.dim() == 2 else y.sum(0))(KK.gemm_x3(x, w, b, ksplit=0))
+    if "--only-x3" in sys.argv:
+        forms = {k_: v_ for k_, v_ in forms.items() if k_.startswith("gemm") or k_ == "fp32"}
     for s in (2, 4, 8):
         if K % s:
             continue

@@ -84,6 +84,10 @@ SIGNATURES = {
     "tsplat_upsample_bilinear_act_fwd": (ctypes.c_int, [_P, _P, _P] + [_I32] * 6 + [_P]),
     "tsplat_conv2d_f32_nhwc_fwd": (ctypes.c_int, [_P, _I32, _P, _P, _P, _P] + [_I32] * 7 + [_P]),
     "tsplat_residual_ln_fwd": (ctypes.c_int, [_P] * 5 + [ctypes.c_float, _P, _P, _I32, _I32, _P]),
+    "tsplat_residual_ln_slabs_fwd": (ctypes.c_int, [_P, _P, _I32, _P, _P, _P, ctypes.c_float, _P, _P, _I32, _I32, _P]),
+    "tsplat_gemm_x3_pack_bytes": (ctypes.c_size_t, [_I32, _I32]),
+    "tsplat_gemm_x3_pack": (ctypes.c_int, [_P, _P, _I32, _I32, _P]),
+    "tsplat_gemm_x3_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _P]),
     "tsplat_residual_ln_bf16_fwd": (ctypes.c_int, [_P] * 5 + [ctypes.c_float, _P, _P, _I32, _I32, _P]),
     "tsplat_bias_act_fwd": (ctypes.c_int, [_P] * 4 + [_I32, _I32, ctypes.c_int64, _I32, _P]),
     "tsplat_bias_act_nhwc_fwd": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_int64, _I32, _I32, _P]),
@@ -180,7 +184,8 @@ def stream_ptr(device: torch.device | None = None) -> int:
 
 PROF_IDS = {"raster_preprocess": 1, "raster_scan": 2, "raster_scatter": 3, "raster_render": 4,
             "uv_coarse": 5, "uv_cross": 6, "msda": 7, "win_attn": 8, "raster": 9,
-            "group_norm": 10, "uv_cross_table": 11, "linear": 12, "mha": 13, "conv": 14, "wino_conv": 15}
+            "group_norm": 10, "uv_cross_table": 11, "linear": 12, "mha": 13, "conv": 14, "wino_conv": 15,
+            "gemm_x3": 16}
 
 
 def prof_enable(name: str | None) -> None:

@@ -1,0 +1,310 @@
+// Split-bf16 ("bf16x3") GEMM with fused bias / exact-GELU epilogue and split-K partial slabs, for the
+// fp32 linears of the C2 step's bf16x3 dense mode that ran on hipBLASLt: DINOv2-B/14's qkv / proj /
+// fc1 / fc2 at M = 650 rows (reference src/depth_anything_v2/dinov2_layers/attention.py:70-75,
+// mlp.py:33-40; the reference runs them in TF32, src/main.py:15).
+//
+//   out[s][m][n] = sum over k in split s of x[m][k] w[n][k]   (+ bias[n] in slab 0, GELU if 1 split)
+//
+// Products as in the other bf16x3 kernels: x = xh + xl, w = wh + wl (hi = bf16(v), lo = bf16(v - hi)),
+// x w ~ xh wh + xh wl + xl wh on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (<= 3 * 2^-18
+// relative per product; TF32 rounds each operand to 2^-11).
+//
+// Why a hand-written kernel: hipBLASLt's emulated-xf32 GEMMs raced inside the graphed two-stream
+// step, and its exact-fp32 ones take 19-30 us per DINOv2 linear at M = 650
+// (11 row blocks: the launch is operand-delivery-bound, not MFMA-bound). Here:
+//   * W is split and packed once per weight version (tsplat_gemm_x3_pack) in MFMA A-fragment order
+//     [n-tile 32][k-step 16][hi / lo][64 lanes][8 bf16], so a wave's fragment load is one contiguous
+//     1-KB read (no LDS, each wave owns its 32 columns);
+//   * x is read as fp32 with coalesced float4 rows, split in registers and written to LDS as B
+//     fragments [hi / lo][k-step][m-tile][64 lanes][8 bf16] (lane slot XOR-swizzled by the k-step and
+//     half so the 16-lane store groups hit 32 distinct banks; the fragment reads stay one
+//     conflict-free ds_read_b128);
+//   * workgroup = 64 rows x 128 columns, 4 waves (wave w: columns 32 w .. 32 w + 31, both 32-row
+//     m-tiles: 6 MFMAs per 16-deep k-step on 4 LDS fragment reads and 2 fragment loads); K in
+//     64-deep chunks, x double-buffered in LDS with one barrier per chunk, the chunk after next in
+//     flight (x rows in registers, W fragments in a second register set);
+//   * split-K: the K chunks are divided over `ksplit` workgroups per tile, each writing its own fp32
+//     slab; the consumer (tsplat_residual_ln_slabs_fwd) sums the slabs in order, so the result is
+//     deterministic and no atomics are needed;
+//   * XCD-aware order: the workgroups of one column block (same W slice) are dealt to one XCD;
+//   * the output tile goes through LDS and is stored as whole 512-B rows.
+#include "common.h"
+#include "prof.h"
+
+namespace tsplat {
+namespace gemm3 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) f4v* gptr;  // global loads (not flat)
+
+constexpr int kBM = 64;       // rows per workgroup (2 m-tiles)
+constexpr int kBN = 128;      // columns per workgroup (4 waves x 32)
+constexpr int kBK = 64;       // K per chunk
+constexpr int kSteps = kBK / 16;
+constexpr int kThreads = 256;
+constexpr int kBufDw = 2 * kSteps * 2 * 64 * 4;  // dwords per x buffer: [hl][step][mt][lane][4 dw] = 4096
+constexpr int kOutStride = kBN + 4;             // floats per row of the output tile in LDS
+constexpr int kSmemDw = kBM * kOutStride > 2 * kBufDw ? kBM * kOutStride : 2 * kBufDw;
+
+__device__ float4 g_zero16 = {0.f, 0.f, 0.f, 0.f};
+
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector((floatx2){a, b}, bf16x2));
+}
+
+// hi / lo bf16 halves of (a, b), each pair packed into one dword (a in the low half)
+__device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint32_t& lo) {
+    hi = pack_bf16(a, b);
+    const float ah = __builtin_bit_cast(float, hi << 16), bh = __builtin_bit_cast(float, hi & 0xffff0000u);
+    lo = pack_bf16(a - ah, b - bh);
+}
+
+__device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }
+
+// W [n][k] fp32 -> [ntp][kcp][hl][64 lanes][8 bf16]: lane (n & 31) + 32 ((k >> 3) & 1), element k & 7;
+// rows n >= N and columns k >= K are zeros. One thread per (row, 8 consecutive k).
+__global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, uint4* __restrict__ wp, int n_rows,
+                                                   int k_cols, int ntp, int kcp) {
+    const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+    const long long groups = 2LL * kcp;  // 8-wide k groups per row
+    if (idx >= (long long)ntp * 32 * groups) return;
+    const int n = (int)(idx / groups), g = (int)(idx % groups);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int k = 8 * g + j;
+        v[j] = (n < n_rows && k < k_cols) ? w[(size_t)n * k_cols + k] : 0.0f;
+    }
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) split_pair(v[2 * j], v[2 * j + 1], hi[j], lo[j]);
+    const int kc = g >> 1, lane = (n & 31) + 32 * (g & 1);
+    const size_t base = ((size_t)(n >> 5) * kcp + kc) * 128 + lane;
+    wp[base] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
+    wp[base + 64] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
+}
+
+struct Args {
+    const float* x;    // [m][k] fp32, rows contiguous
+    const uint4* w;    // packed W
+    const float* bias; // [n] or null
+    float* out;        // [ksplit][m][n]
+    int m, n, k;
+    int kcp;           // packed k-steps (a multiple of kSteps)
+    int nchunk;        // K chunks = kcp / kSteps
+    int cps;           // chunks per split
+    int ksplit, act;
+    int mb, nb;        // row / column blocks
+};
+
+__global__ void __launch_bounds__(kThreads, 2) gemm_x3_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) uint32_t smem[kSmemDw];
+    // XCD-aware order: logical = (column block, split, row block) with the row block fastest; each XCD
+    // takes a contiguous logical range, so the workgroups sharing one W slice share one L2
+    const int logical = xcd_remap(blockIdx.x, gridDim.x);
+    const int mbk = logical % a.mb;
+    const int rest = logical / a.mb;
+    const int ks = rest % a.ksplit, nbk = rest / a.ksplit;
+    const int c0 = ks * a.cps, c1 = min(c0 + a.cps, a.nchunk), nc = c1 - c0;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint4* wb = a.w + (size_t)(nbk * 4 + w) * a.kcp * 128 + lane;
+
+    // x staging: thread = (row r0 + 16 i, float4 column c4), i = 0..3
+    const int c4 = tid & 15, r0 = tid >> 4;
+    const int st = c4 >> 2, sh = (c4 >> 1) & 1, jh = c4 & 1;
+    int xoff[4];  // dword offset of this thread's hi pair in a buffer (lo at + 2 * kSteps * 2 * 64 * 4 / 2)
+    const float* xrow[4];
+    bool rok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int r = r0 + 16 * i, gm = mbk * kBM + r;
+        rok[i] = gm < a.m;
+        xrow[i] = a.x + (size_t)(rok[i] ? gm : 0) * a.k + 4 * c4;
+        const int slot = ((r & 31) + 32 * sh) ^ (2 * st + sh);
+        xoff[i] = ((st * 2 + (r >> 5)) * 64 + slot) * 4 + 2 * jh;
+    }
+    constexpr int kLoDw = kSteps * 2 * 64 * 4;  // hl stride in dwords (2048)
+
+    float4 xr[4];
+    uint4 wr[2][kSteps][2];
+    floatx16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[t][e] = 0.0f;
+
+    // unconditional loads (rows past M and columns past K read 16 zero bytes instead): a branch
+    // around them would make the waits before the next store vmcnt(0), draining the W prefetch too
+    auto gload_x = [&](int c) {
+        const bool kok = c * kBK + 4 * c4 < a.k;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const float* p = rok[i] && kok ? xrow[i] + c * kBK : reinterpret_cast<const float*>(&g_zero16);
+            const f4v v = *(gptr)p;
+            xr[i] = make_float4(v.x, v.y, v.z, v.w);
+        }
+    };
+    auto gload_w = [&](int c, auto S) {
+#pragma unroll
+        for (int s = 0; s < kSteps; ++s)
+#pragma unroll
+            for (int hl = 0; hl < 2; ++hl) wr[decltype(S)::value][s][hl] = wb[((size_t)c * kSteps + s) * 128 + hl * 64];
+    };
+    auto store_x = [&](int buf) {
+        uint32_t* b = smem + buf * kBufDw;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t h0, l0, h1, l1;
+            split_pair(xr[i].x, xr[i].y, h0, l0);
+            split_pair(xr[i].z, xr[i].w, h1, l1);
+            *reinterpret_cast<uint2*>(b + xoff[i]) = make_uint2(h0, h1);
+            *reinterpret_cast<uint2*>(b + kLoDw + xoff[i]) = make_uint2(l0, l1);
+        }
+    };
+    auto mma = [&](int buf, auto S) {
+        const uint32_t* b = smem + buf * kBufDw;
+#pragma unroll
+        for (int s = 0; s < kSteps; ++s) {
+            const bf16x8 wh = __builtin_bit_cast(bf16x8, wr[decltype(S)::value][s][0]);
+            const bf16x8 wl = __builtin_bit_cast(bf16x8, wr[decltype(S)::value][s][1]);
+            const int slot = lane ^ (2 * s + (lane >> 5));
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const uint32_t* p = b + ((s * 2 + t) * 64 + slot) * 4;
+                const bf16x8 xh = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p));
+                const bf16x8 xl = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p + kLoDw));
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl, acc[t], 0, 0, 0);
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh, acc[t], 0, 0, 0);
+            }
+        }
+    };
+
+    const std::integral_constant<int, 0> I0;
+    const std::integral_constant<int, 1> I1;
+    if (nc > 0) {
+        gload_x(c0);
+        gload_w(c0, I0);
+        store_x(0);
+        if (nc > 1) {
+            gload_x(c0 + 1);
+            gload_w(c0 + 1, I1);
+        }
+        __syncthreads();
+        // step it: MFMAs on x buffer it & 1 with W set S = it & 1; x(it + 1) to the other buffer;
+        // loads of chunk it + 2 (x rows first: the next store waits only for them)
+        auto step = [&](int it, auto S) {
+            mma(it & 1, S);
+            if (it + 1 < nc) store_x((it + 1) & 1);
+            if (it + 2 < nc) {
+                gload_x(c0 + it + 2);
+                gload_w(c0 + it + 2, S);
+            }
+            __syncthreads();
+        };
+        for (int it = 0; it < nc; it += 2) {
+            step(it, I0);
+            if (it + 1 < nc) step(it + 1, I1);
+        }
+    }
+
+    // epilogue: accumulators -> LDS tile [64 rows][128 + 4] -> whole rows (+ bias, GELU) to the slab.
+    // acc[t][e]: column (n) 32 w + (e & 3) + 8 (e >> 2) + 4 (lane >> 5), row (m) 32 t + (lane & 31)
+    float* so = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int mrow = 32 * t + (lane & 31), ncol = 32 * w + 8 * q + 4 * (lane >> 5);
+            *reinterpret_cast<float4*>(so + mrow * kOutStride + ncol) =
+                make_float4(acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]);
+        }
+    __syncthreads();
+    float* slab = a.out + (size_t)ks * a.m * a.n;
+    const bool add_bias = a.bias && ks == 0;
+#pragma unroll
+    for (int i = 0; i < kBM * kBN / 4 / kThreads; ++i) {
+        const int idx = tid + kThreads * i;
+        const int mrow = idx >> 5, n4 = idx & 31;
+        const int gm = mbk * kBM + mrow, gn = nbk * kBN + 4 * n4;
+        if (gm >= a.m || gn >= a.n) continue;
+        float4 v = *reinterpret_cast<const float4*>(so + mrow * kOutStride + 4 * n4);
+        if (add_bias) {
+            const float4 bb = *reinterpret_cast<const float4*>(a.bias + gn);
+            v.x += bb.x;
+            v.y += bb.y;
+            v.z += bb.z;
+            v.w += bb.w;
+        }
+        if (a.act == 1) v = make_float4(gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w));
+        *reinterpret_cast<float4*>(slab + (size_t)gm * a.n + gn) = v;
+    }
+}
+
+}  // namespace gemm3
+}  // namespace tsplat
+
+using namespace tsplat::gemm3;
+
+static void packed_dims(int n, int k, int& ntp, int& kcp) {
+    ntp = tsplat::ceil_div(n, kBN) * (kBN / 32);
+    kcp = tsplat::ceil_div(k, kBK) * kSteps;
+}
+
+extern "C" size_t tsplat_gemm_x3_pack_bytes(int32_t n, int32_t k) {
+    if (n <= 0 || k <= 0) return 0;
+    int ntp, kcp;
+    packed_dims(n, k, ntp, kcp);
+    return (size_t)ntp * kcp * 128 * sizeof(uint4);
+}
+
+extern "C" int tsplat_gemm_x3_pack(const float* w, void* wp, int32_t n, int32_t k, void* stream_) {
+    if (!w || !wp || n <= 0 || k <= 0) return TSPLAT_EINVAL;
+    int ntp, kcp;
+    packed_dims(n, k, ntp, kcp);
+    const long long threads = (long long)ntp * 32 * 2 * kcp;
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream_, w,
+                       (uint4*)wp, n, k, ntp, kcp);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}
+
+extern "C" int tsplat_gemm_x3_fwd(const float* x, const void* wp, const float* bias, float* out, int32_t m, int32_t n,
+                                  int32_t k, int32_t ksplit, int32_t act, void* stream_) {
+    if (!x || !wp || !out || m <= 0 || n <= 0 || k <= 0 || ksplit <= 0) return TSPLAT_EINVAL;
+    // float4 rows: k and n multiples of 4, x / bias / out 16-B aligned
+    if (k % 4 || n % 4 || ((uintptr_t)x & 15) || ((uintptr_t)out & 15) || (bias && ((uintptr_t)bias & 15)))
+        return TSPLAT_EINVAL;
+    if (act != 0 && act != 1) return TSPLAT_EINVAL;
+    if (act && ksplit > 1) return TSPLAT_EINVAL;  // the activation needs the whole sum
+    Args a{};
+    a.x = x;
+    a.w = (const uint4*)wp;
+    a.bias = bias;
+    a.out = out;
+    a.m = m;
+    a.n = n;
+    a.k = k;
+    int ntp;
+    packed_dims(n, k, ntp, a.kcp);
+    a.nchunk = a.kcp / kSteps;
+    if (ksplit > a.nchunk) return TSPLAT_EINVAL;
+    a.cps = tsplat::ceil_div(a.nchunk, ksplit);
+    if ((ksplit - 1) * a.cps >= a.nchunk) return TSPLAT_EINVAL;  // every split gets >= 1 chunk
+    a.ksplit = ksplit;
+    a.act = act;
+    a.mb = tsplat::ceil_div(m, kBM);
+    a.nb = tsplat::ceil_div(n, kBN);
+    const long long grid = (long long)a.mb * a.nb * ksplit;
+    if (grid > 0x7fffffff) return TSPLAT_EINVAL;
+    TSPLAT_PROF_BEGIN(tsplat::prof::kGemmX3, (hipStream_t)stream_);
+    hipLaunchKernelGGL(gemm_x3_kernel, dim3((unsigned)grid), dim3(kThreads), 0, (hipStream_t)stream_, a);
+    TSPLAT_PROF_END(tsplat::prof::kGemmX3, (hipStream_t)stream_);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

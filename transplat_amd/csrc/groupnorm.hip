@@ -539,7 +539,7 @@ template <int V4, typename TY, typename TN>  // float4s per lane (dim = 256 V4)
 __global__ void __launch_bounds__(kThreads)
 residual_ln_kernel(const float* __restrict__ x, const TY* __restrict__ y, const float* __restrict__ ls,
                    const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ x_out,
-                   TN* __restrict__ n_out, int rows, float eps) {
+                   TN* __restrict__ n_out, int rows, float eps, int nslab) {
     const int row = blockIdx.x * (kThreads / kWave) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= rows) return;
@@ -552,7 +552,15 @@ residual_ln_kernel(const float* __restrict__ x, const TY* __restrict__ y, const 
         const int c = 4 * (lane + 64 * k);
         v[k] = *reinterpret_cast<const float4*>(x + off + c);
         if (y) {
-            const float4 t = ld4(y + off + c);
+            float4 t = ld4(y + off + c);
+            // split-K slabs, summed in slab order (deterministic)
+            for (int sl = 1; sl < nslab; ++sl) {
+                const float4 u = ld4(y + (size_t)sl * rows * D + off + c);
+                t.x += u.x;
+                t.y += u.y;
+                t.z += u.z;
+                t.w += u.w;
+            }
             float4 g = make_float4(1.f, 1.f, 1.f, 1.f);
             if (ls) g = *reinterpret_cast<const float4*>(ls + c);
             v[k].x += g.x * t.x;
@@ -589,15 +597,16 @@ residual_ln_kernel(const float* __restrict__ x, const TY* __restrict__ y, const 
 
 template <typename TY, typename TN>
 static int residual_ln_launch(const float* x, const TY* y, const float* ls, const float* ln_w, const float* ln_b,
-                              float ln_eps, float* x_out, TN* n_out, int32_t rows, int32_t dim, void* stream_) {
+                              float ln_eps, float* x_out, TN* n_out, int32_t rows, int32_t dim, void* stream_,
+                              int32_t nslab = 1) {
     using namespace tsplat::gn;
-    if (!x || !ln_w || !ln_b || !n_out || rows <= 0 || (ls && !y)) return TSPLAT_EINVAL;
+    if (!x || !ln_w || !ln_b || !n_out || rows <= 0 || (ls && !y) || nslab < 1) return TSPLAT_EINVAL;
     if (y && !x_out) return TSPLAT_EINVAL;
     hipStream_t stream = (hipStream_t)stream_;
     const dim3 grid((rows + kThreads / kWave - 1) / (kThreads / kWave));
 #define TSPLAT_RLN(V)                                                                                   \
     hipLaunchKernelGGL((residual_ln_kernel<V, TY, TN>), grid, dim3(kThreads), 0, stream, x, y, ls, ln_w, ln_b, \
-                       x_out, n_out, rows, ln_eps)
+                       x_out, n_out, rows, ln_eps, nslab)
     switch (dim) {
         case 256: TSPLAT_RLN(1); break;
         case 512: TSPLAT_RLN(2); break;
@@ -614,6 +623,13 @@ extern "C" int tsplat_residual_ln_fwd(const float* x, const float* y, const floa
                                       const float* ln_b, float ln_eps, float* x_out, float* n_out, int32_t rows,
                                       int32_t dim, void* stream_) {
     return residual_ln_launch<float, float>(x, y, ls, ln_w, ln_b, ln_eps, x_out, n_out, rows, dim, stream_);
+}
+
+extern "C" int tsplat_residual_ln_slabs_fwd(const float* x, const float* y, int32_t nslab, const float* ls,
+                                            const float* ln_w, const float* ln_b, float ln_eps, float* x_out,
+                                            float* n_out, int32_t rows, int32_t dim, void* stream_) {
+    if (!y) return TSPLAT_EINVAL;
+    return residual_ln_launch<float, float>(x, y, ls, ln_w, ln_b, ln_eps, x_out, n_out, rows, dim, stream_, nslab);
 }
 
 extern "C" int tsplat_residual_ln_bf16_fwd(const float* x, const void* y, const float* ls, const float* ln_w,

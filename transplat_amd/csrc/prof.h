@@ -26,7 +26,8 @@ enum KernelId : int {
     kMha = 13,        // tsplat_mha_f32_fwd
     kConv = 14,       // tsplat_conv2d_f32_fwd
     kWinoConv = 15,   // tsplat_conv3x3_wino_f32_fwd
-    kNumKernels = 16,
+    kGemmX3 = 16,     // tsplat_gemm_x3_fwd
+    kNumKernels = 17,
 };
 
 int active();                 // kernel id being timed (0 = off)

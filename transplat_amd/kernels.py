@@ -580,11 +580,24 @@ def _merge_partials(lib, q, k, v, h, w, num_splits, with_shift, merge_weight, ln
 def residual_ln(x, y, ls, norm, bf16_out: bool = False):
     """(x + ls * y, LayerNorm(x + ls * y)) in one pass (tsplat_residual_ln_fwd); y None: (x, LN(x)).
     norm: an nn.LayerNorm (weight, bias, eps); ls: LayerScale gamma or None. A bf16 y, or
-    bf16_out, selects the bf16 form (y read and LN written in bf16; x fp32 either way)."""
+    bf16_out, selects the bf16 form (y read and LN written in bf16; x fp32 either way). y with one
+    leading dimension more than x is the split-K slabs of gemm_x3 (summed in order,
+    tsplat_residual_ln_slabs_fwd)."""
     lib = _lib.load()
     d = x.shape[-1]
     xf = _f32(x)
     rows = xf.numel() // d
+    if y is not None and y.dim() == x.dim() + 1:
+        if y.dtype != torch.float32 or bf16_out or tuple(y.shape[1:]) != tuple(x.shape):
+            raise ValueError(f"residual_ln: slabs {tuple(y.shape)} for x {tuple(x.shape)}")
+        yf = y.contiguous()
+        x_out, n_out = torch.empty_like(xf), torch.empty_like(xf)
+        rc = lib.tsplat_residual_ln_slabs_fwd(_lib.ptr(xf), _lib.ptr(yf), y.shape[0],
+                                              _lib.ptr(_f32(ls)) if ls is not None else None,
+                                              _lib.ptr(_f32(norm.weight)), _lib.ptr(_f32(norm.bias)), float(norm.eps),
+                                              _lib.ptr(x_out), _lib.ptr(n_out), rows, d, _lib.stream_ptr(x.device))
+        _lib.check(rc, "tsplat_residual_ln_slabs_fwd")
+        return x_out, n_out
     if _BF16_NORMS and (bf16_out or (y is not None and y.dtype == torch.bfloat16)):
         yb = y.to(torch.bfloat16).contiguous() if y is not None else None
         x_out = torch.empty_like(xf) if y is not None else xf
@@ -1311,6 +1324,75 @@ def linear_xf32(x, weight, bias=None, act: str = "none"):
                                       y.shape[-1], _ACTS[act], _lib.stream_ptr(y.device))
     _lib.check(rc, "tsplat_bias_act_nhwc_fwd")
     return y
+
+
+# Hand-written split-bf16 GEMM (tsplat_gemm_x3_fwd) for the bf16x3 mode's DINOv2 linears (round 6):
+# replaces hipBLASLt's exact-fp32 / emulated-xf32 GEMMs there. TSPLAT_GEMM_X3=0: the library path.
+_GEMM_X3 = os.environ.get("TSPLAT_GEMM_X3", "1") == "1"
+_GEMM_KSPLIT = int(os.environ.get("TSPLAT_GEMM_KSPLIT", "0"))  # 0: auto
+_GEMM_W: dict = {}
+GEMM_LOG = None  # list: (m, n, k, ksplit) per launch when set (bench.py's roofline)
+
+
+def gemm_x3_ok(x, weight) -> bool:
+    """True when gemm_x3 takes F.linear(x, weight) in the current mode: bf16x3 dense mode, fp32 on
+    the GPU, k and n multiples of 4."""
+    if not (_GEMM_X3 and _DENSE == "bf16x3" and x.is_cuda and x.dtype == torch.float32
+            and weight.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")):
+        return False
+    n, k = weight.shape
+    return k % 4 == 0 and n % 4 == 0 and x.shape[-1] == k
+
+
+def _gemm_pack(weight):
+    """W [n, k] -> its packed hi / lo MFMA fragments, cached per weight tensor version."""
+    hit = _GEMM_W.get(id(weight))
+    if hit is not None and hit[0]() is weight and hit[1] == weight._version:
+        return hit[2]
+    lib = _lib.load()
+    n, k = weight.shape
+    wf = _f32(weight.detach())
+    wp = torch.empty(int(lib.tsplat_gemm_x3_pack_bytes(n, k)), dtype=torch.uint8, device=weight.device)
+    _lib.check(lib.tsplat_gemm_x3_pack(_lib.ptr(wf), _lib.ptr(wp), n, k, _lib.stream_ptr(weight.device)),
+               "tsplat_gemm_x3_pack")
+    if len(_GEMM_W) > 512:
+        for key in [key for key, v in _GEMM_W.items() if v[0]() is None]:
+            del _GEMM_W[key]
+    _GEMM_W[id(weight)] = (weakref.ref(weight), weight._version, wp)
+    return wp
+
+
+def gemm_ksplit(m: int, n: int, k: int) -> int:
+    """Split-K factor: the tile grid (64-row x 128-column blocks) filled towards one workgroup per
+    CU, every split at least two 64-deep chunks."""
+    if _GEMM_KSPLIT > 0:
+        return _GEMM_KSPLIT
+    tiles = -(-m // 64) * -(-n // 128)
+    nchunk = -(-k // 64)
+    s = max(1, min(nchunk // 2, 264 // tiles))
+    while s > 1 and (s - 1) * -(-nchunk // s) >= nchunk:
+        s -= 1
+    return s
+
+
+def gemm_x3(x, weight, bias=None, act: str = "none", ksplit: int = 1):
+    """act(x W^T + bias) on the split-bf16 GEMM (tsplat_gemm_x3_fwd); ksplit > 1 returns the [ksplit,
+    *x.shape[:-1], n] partial slabs (bias in slab 0) for residual_ln to sum; ksplit 0: gemm_ksplit's
+    choice (1 with an activation)."""
+    lib = _lib.load()
+    n, k = weight.shape
+    xf = _f32(x)
+    m = xf.numel() // k
+    if ksplit == 0:
+        ksplit = 1 if act != "none" else gemm_ksplit(m, n, k)
+    shape = (*x.shape[:-1], n) if ksplit == 1 else (ksplit, *x.shape[:-1], n)
+    out = torch.empty(shape, dtype=torch.float32, device=x.device)
+    if GEMM_LOG is not None:
+        GEMM_LOG.append((m, n, k, ksplit))
+    rc = lib.tsplat_gemm_x3_fwd(_lib.ptr(xf), _lib.ptr(_gemm_pack(weight)), _lib.ptr(_f32(bias)) if bias is not None else None,
+                                _lib.ptr(out), m, n, k, ksplit, {"none": 0, "gelu": 1}[act], _lib.stream_ptr(x.device))
+    _lib.check(rc, "tsplat_gemm_x3_fwd", "bf16x3")
+    return out
 
 
 def linear_forward(mod, x):

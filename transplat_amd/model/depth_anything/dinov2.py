@@ -52,7 +52,14 @@ class Mlp(nn.Module):
         self.act = act_layer()
         self.fc2 = nn.Linear(hidden_features, out_features, bias=bias)
 
-    def forward(self, x):
+    def forward(self, x, slabs: bool = False):
+        """slabs=True (the fused block chain, whose residual step sums them): fc2 may return its
+        split-K partial slabs [s, *x.shape] (kernels.gemm_x3)."""
+        if (slabs and type(self.act) is nn.GELU and self.act.approximate == "none" and self.fc1.bias is not None
+                and kernels.gemm_x3_ok(x, self.fc1.weight)):
+            # bf16x3 dense mode: fc1 + bias + exact GELU and fc2 on the split-bf16 GEMM
+            h = kernels.gemm_x3(x, self.fc1.weight, self.fc1.bias, act="gelu")
+            return kernels.gemm_x3(h, self.fc2.weight, self.fc2.bias, ksplit=0)
         if type(self.act) is nn.GELU and self.act.approximate == "none":
             # bf16x3 dense mode: fc1 on hipBLASLt's emulated-xf32 GEMM + bias + exact GELU in one pass
             # (kernels.linear_xf32)
@@ -78,8 +85,16 @@ class Attention(nn.Module):
         self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
         self.proj = nn.Linear(dim, dim, bias=proj_bias)
 
-    def forward(self, x):
+    def forward(self, x, slabs: bool = False):
+        """slabs=True: proj may return split-K partial slabs (see Mlp.forward)."""
         b, n, c = x.shape
+        if (slabs and c // self.num_heads == 64 and self.qkv.bias is not None and self.proj.bias is not None
+                and kernels.gemm_x3_ok(x, self.qkv.weight)):
+            # bf16x3 dense mode: both projections on the split-bf16 GEMM (bias in its epilogue), the
+            # attention on the bf16x3 MFMA kernel straight from the [b, n, 3c] layout
+            qkv = kernels.gemm_x3(x, self.qkv.weight, self.qkv.bias)
+            return kernels.gemm_x3(kernels.mha(qkv, self.num_heads, self.scale), self.proj.weight, self.proj.bias,
+                                   ksplit=0)
         if x.dtype == torch.float32 and c // self.num_heads == 64 and not torch.is_autocast_enabled(x.device.type):
             # exact-fp32 MFMA attention straight from the qkv projection's layout; in bf16x3 mode the
             # projection runs without its bias (hipBLASLt's emulated-xf32 GEMM) and the attention
@@ -195,9 +210,9 @@ class DinoVisionTransformer(nn.Module):
         _, h = kernels.residual_ln(x, None, None, blocks[0].norm1, bf16_out=bf)
         outputs = []
         for i, blk in enumerate(blocks):
-            x, h2 = kernels.residual_ln(x, blk.attn(h), gamma(blk.ls1), blk.norm2, bf16_out=bf)
+            x, h2 = kernels.residual_ln(x, blk.attn(h, slabs=True), gamma(blk.ls1), blk.norm2, bf16_out=bf)
             last = i + 1 == len(blocks)
-            x, h = kernels.residual_ln(x, blk.mlp(h2), gamma(blk.ls2), self.norm if last else blocks[i + 1].norm1,
+            x, h = kernels.residual_ln(x, blk.mlp(h2, slabs=True), gamma(blk.ls2), self.norm if last else blocks[i + 1].norm1,
                                        bf16_out=bf)
             if i in take:
                 if not norm:

@@ -44,6 +44,7 @@ _HIP = {
     "tsplat_linear_f32_fwd": ("transformer linears (HIP)", None),
     "tsplat_linear_f32_split_x3_fwd": ("transformer linears (HIP)", None),
     "tsplat_linear_f32_attn_merge_fwd": ("transformer linears (HIP)", None),
+    "tsplat_gemm_x3_fwd": ("GEMMs (HIP)", "bf16x3"),
     "tsplat_mha_x3_fwd": ("DINOv2 attention (HIP)", "bf16x3"),
     "tsplat_mha_f32_fwd": ("DINOv2 attention (HIP)", "exact fp32"),
     "tsplat_mha_bias_f32_fwd": ("DINOv2 attention (HIP)", "exact fp32"),
@@ -59,12 +60,13 @@ _HIP = {
     "tsplat_group_norm_bf16_fwd": ("norms (HIP)", "bf16 I/O, fp32 statistics"),
     "tsplat_layer_norm128_fwd": ("norms (HIP)", None),
     "tsplat_residual_ln_fwd": ("norms (HIP)", "fp32"),
+    "tsplat_residual_ln_slabs_fwd": ("norms (HIP)", "fp32"),
     "tsplat_residual_ln_bf16_fwd": ("norms (HIP)", "bf16 I/O, fp32 statistics"),
     "tsplat_gaussian_adapter_fwd": ("gaussian adapter (HIP)", "fp32"),
     "tsplat_sh_rotation_fwd": ("gaussian adapter (HIP)", "fp32"),
     "tsplat_raster_fwd": ("rasterizer (HIP)", "fp32"),
 }
-_ORDER = ("window attention", "transformer linears (HIP)", "3x3 convs (HIP Winograd)", "direct convs (HIP)",
+_ORDER = ("window attention", "transformer linears (HIP)", "GEMMs (HIP)", "3x3 convs (HIP Winograd)", "direct convs (HIP)",
           "DINOv2 attention (HIP)", "U-Net attention (HIP)", "library GEMMs (hipBLASLt)", "library convs (MIOpen)",
           "correlation (HIP)", "norms (HIP)", "gaussian adapter (HIP)", "rasterizer (HIP)")
 _GEMMS = {"mm", "addmm", "bmm", "baddbmm", "addbmm", "_scaled_mm"}
