@@ -1,0 +1,7 @@
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export PYTHONPATH=$(pwd)
+timeout -k 10 300 python -u -m pytest tests/test_conv.py -m gpu -q --timeout 200 --timeout-method thread -s -k "gemm_x3" 2>&1 | grep -E "rel err|passed|failed|Error" | tail -12
+TSPLAT_LIB=tools/var/gemm_stamp.so timeout -k 10 120 python tools/gemm_stamps.py 2>&1 | grep -v amdgpu.ids || exit 1
+for v in "" tools/var/gemm_kg1.so; do echo "== ${v:-kg2}"; TSPLAT_LIB=$v timeout -k 10 120 python -u tools/bench_gemm_x3.py 2>&1 | grep -v amdgpu.ids; done

@@ -41,16 +41,41 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) f4v* gptr;  // global loads (not flat)
 
+#ifndef TSPLAT_GEMM_SB
+#define TSPLAT_GEMM_SB 0
+#endif
+
 constexpr int kBM = 64;       // rows per workgroup (2 m-tiles)
 constexpr int kBN = 128;      // columns per workgroup (4 waves x 32)
 constexpr int kBK = 64;       // K per chunk
 constexpr int kSteps = kBK / 16;
-constexpr int kThreads = 256;
+#ifndef TSPLAT_GEMM_KG
+#define TSPLAT_GEMM_KG 2
+#endif
+// k-groups: KG sets of 4 waves share each chunk's k-steps (2: two waves per SIMD, each with half the
+// chunk's MFMAs, so one wave's LDS / barrier waits overlap the other's MFMAs); summed through LDS
+constexpr int KG = TSPLAT_GEMM_KG;
+constexpr int kThreads = 256 * KG;
+constexpr int kSpw = 4 / KG;      // k-steps per wave and chunk
+constexpr int kXr = 4 / KG;       // x float4 per thread and chunk
 constexpr int kBufDw = 2 * kSteps * 2 * 64 * 4;  // dwords per x buffer: [hl][step][mt][lane][4 dw] = 4096
 constexpr int kOutStride = kBN + 4;             // floats per row of the output tile in LDS
 constexpr int kSmemDw = kBM * kOutStride > 2 * kBufDw ? kBM * kOutStride : 2 * kBufDw;
 
 __device__ float4 g_zero16 = {0.f, 0.f, 0.f, 0.f};
+
+#ifndef TSPLAT_GEMM_STAMP
+#define TSPLAT_GEMM_STAMP 0  // diagnostic builds only: per-workgroup phase clocks (tools/gemm_stamps.py)
+#endif
+#if TSPLAT_GEMM_STAMP
+__device__ unsigned long long* g_gemm_stamps = nullptr;
+#define G_STAMP(slot)                                                                             \
+    do {                                                                                          \
+        if (threadIdx.x == 0 && g_gemm_stamps) g_gemm_stamps[(size_t)blockIdx.x * 8 + (slot)] = wall_clock64(); \
+    } while (0)
+#else
+#define G_STAMP(slot) do {} while (0)
+#endif
 
 __device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((floatx2){a, b}, bf16x2));
@@ -63,7 +88,20 @@ __device__ __forceinline__ void split_pair(float a, float b, uint32_t& hi, uint3
     lo = pack_bf16(a - ah, b - bh);
 }
 
-__device__ __forceinline__ float gelu_erf(float v) { return 0.5f * v * (1.0f + erff(v * 0.70710678118654752f)); }
+// GELU with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 absolute, branch-free: one
+// reciprocal, one exp2, five FMAs): the device library's erff (ranges, branches) made fc1's epilogue
+// 4.8 of its 23.5 us (tools/gemm_stamps.py). The difference to the exact erf is below the bf16x3
+// products' own rounding (~4e-6 relative).
+__device__ __forceinline__ float gelu_erf(float v) {
+    const float z = fabsf(v) * 0.70710678118654752f;
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+    float p = fmaf(1.061405429f, t, -1.453152027f);
+    p = fmaf(p, t, 1.421413741f);
+    p = fmaf(p, t, -0.284496736f);
+    p = fmaf(p, t, 0.254829592f);
+    const float e = 1.0f - p * t * __builtin_amdgcn_exp2f(-z * z * 1.44269504088896341f);
+    return 0.5f * v * (1.0f + copysignf(e, v));
+}
 
 // W [n][k] fp32 -> [ntp][kcp][hl][64 lanes][8 bf16]: lane (n & 31) + 32 ((k >> 3) & 1), element k & 7;
 // rows n >= N and columns k >= K are zeros. One thread per (row, 8 consecutive k).
@@ -101,28 +139,29 @@ struct Args {
     int mb, nb;        // row / column blocks
 };
 
-__global__ void __launch_bounds__(kThreads, 2) gemm_x3_kernel(Args a) {
+__global__ void __launch_bounds__(kThreads, 2 / KG) gemm_x3_kernel(Args a) {
     __shared__ __attribute__((aligned(16))) uint32_t smem[kSmemDw];
     // XCD-aware order: logical = (column block, split, row block) with the row block fastest; each XCD
     // takes a contiguous logical range, so the workgroups sharing one W slice share one L2
+    G_STAMP(0);
     const int logical = xcd_remap(blockIdx.x, gridDim.x);
     const int mbk = logical % a.mb;
     const int rest = logical / a.mb;
     const int ks = rest % a.ksplit, nbk = rest / a.ksplit;
     const int c0 = ks * a.cps, c1 = min(c0 + a.cps, a.nchunk), nc = c1 - c0;
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, g = tid >> 8;
     const uint4* wb = a.w + (size_t)(nbk * 4 + w) * a.kcp * 128 + lane;
 
-    // x staging: thread = (row r0 + 16 i, float4 column c4), i = 0..3
+    // x staging: thread = (row r0 + 16 KG i, float4 column c4), i < 4 / KG
     const int c4 = tid & 15, r0 = tid >> 4;
     const int st = c4 >> 2, sh = (c4 >> 1) & 1, jh = c4 & 1;
-    int xoff[4];  // dword offset of this thread's hi pair in a buffer (lo at + 2 * kSteps * 2 * 64 * 4 / 2)
-    const float* xrow[4];
-    bool rok[4];
+    int xoff[kXr];  // dword offset of this thread's hi pair in a buffer (lo at + kLoDw)
+    const float* xrow[kXr];
+    bool rok[kXr];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = r0 + 16 * i, gm = mbk * kBM + r;
+    for (int i = 0; i < kXr; ++i) {
+        const int r = r0 + 16 * KG * i, gm = mbk * kBM + r;
         rok[i] = gm < a.m;
         xrow[i] = a.x + (size_t)(rok[i] ? gm : 0) * a.k + 4 * c4;
         const int slot = ((r & 31) + 32 * sh) ^ (2 * st + sh);
@@ -130,8 +169,10 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_x3_kernel(Args a) {
     }
     constexpr int kLoDw = kSteps * 2 * 64 * 4;  // hl stride in dwords (2048)
 
-    float4 xr[4];
-    uint4 wr[2][kSteps][2];
+    const std::integral_constant<int, 0> I0;
+    const std::integral_constant<int, 1> I1;
+    float4 xr[2][kXr];  // x rows of two chunks in flight: chunk c in set (c - c0) & 1
+    uint4 wr[2][kSpw][2];  // this wave's k-steps g kSpw .. of a chunk
     floatx16 acc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -140,44 +181,64 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_x3_kernel(Args a) {
 
     // unconditional loads (rows past M and columns past K read 16 zero bytes instead): a branch
     // around them would make the waits before the next store vmcnt(0), draining the W prefetch too
-    auto gload_x = [&](int c) {
+    auto gload_x = [&](int c, auto X) {
         const bool kok = c * kBK + 4 * c4 < a.k;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < kXr; ++i) {
             const float* p = rok[i] && kok ? xrow[i] + c * kBK : reinterpret_cast<const float*>(&g_zero16);
             const f4v v = *(gptr)p;
-            xr[i] = make_float4(v.x, v.y, v.z, v.w);
+            xr[decltype(X)::value][i] = make_float4(v.x, v.y, v.z, v.w);
         }
     };
     auto gload_w = [&](int c, auto S) {
 #pragma unroll
-        for (int s = 0; s < kSteps; ++s)
+        for (int ss = 0; ss < kSpw; ++ss)
 #pragma unroll
-            for (int hl = 0; hl < 2; ++hl) wr[decltype(S)::value][s][hl] = wb[((size_t)c * kSteps + s) * 128 + hl * 64];
+            for (int hl = 0; hl < 2; ++hl)
+                wr[decltype(S)::value][ss][hl] = wb[((size_t)c * kSteps + g * kSpw + ss) * 128 + hl * 64];
     };
-    auto store_x = [&](int buf) {
+    auto store_x = [&](int buf, auto X) {
         uint32_t* b = smem + buf * kBufDw;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < kXr; ++i) {
+            const float4 v = xr[decltype(X)::value][i];
             uint32_t h0, l0, h1, l1;
-            split_pair(xr[i].x, xr[i].y, h0, l0);
-            split_pair(xr[i].z, xr[i].w, h1, l1);
+            split_pair(v.x, v.y, h0, l0);
+            split_pair(v.z, v.w, h1, l1);
             *reinterpret_cast<uint2*>(b + xoff[i]) = make_uint2(h0, h1);
             *reinterpret_cast<uint2*>(b + kLoDw + xoff[i]) = make_uint2(l0, l1);
         }
     };
+    // fragment reads of k-step s into register set F (the next step's reads are issued before the
+    // current step's MFMAs, so only the first read of a chunk waits on LDS latency)
+    bf16x8 xf[2][2][2];  // [set][m-tile][hi / lo]
+    auto read_frags = [&](const uint32_t* b, int s, auto F) {
+        const int slot = lane ^ (2 * s + (lane >> 5));
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const uint32_t* p = b + ((s * 2 + t) * 64 + slot) * 4;
+            xf[decltype(F)::value][t][0] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p));
+            xf[decltype(F)::value][t][1] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p + kLoDw));
+        }
+    };
     auto mma = [&](int buf, auto S) {
         const uint32_t* b = smem + buf * kBufDw;
+        read_frags(b, g * kSpw, I0);
 #pragma unroll
-        for (int s = 0; s < kSteps; ++s) {
-            const bf16x8 wh = __builtin_bit_cast(bf16x8, wr[decltype(S)::value][s][0]);
-            const bf16x8 wl = __builtin_bit_cast(bf16x8, wr[decltype(S)::value][s][1]);
-            const int slot = lane ^ (2 * s + (lane >> 5));
+        for (int ss = 0; ss < kSpw; ++ss) {
+            if (ss + 1 < kSpw) {
+                if (ss & 1) read_frags(b, g * kSpw + ss + 1, I0);
+                else read_frags(b, g * kSpw + ss + 1, I1);
+            }
+#if TSPLAT_GEMM_SB
+            __builtin_amdgcn_sched_barrier(0);  // keep the next step's reads ahead of these MFMAs
+#endif
+            const bf16x8 wh = __builtin_bit_cast(bf16x8, wr[decltype(S)::value][ss][0]);
+            const bf16x8 wl = __builtin_bit_cast(bf16x8, wr[decltype(S)::value][ss][1]);
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
-                const uint32_t* p = b + ((s * 2 + t) * 64 + slot) * 4;
-                const bf16x8 xh = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p));
-                const bf16x8 xl = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(p + kLoDw));
+                const bf16x8 xh = (ss & 1) ? xf[1][t][0] : xf[0][t][0];
+                const bf16x8 xl = (ss & 1) ? xf[1][t][1] : xf[0][t][1];
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wl, xh, acc[t], 0, 0, 0);
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xl, acc[t], 0, 0, 0);
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wh, xh, acc[t], 0, 0, 0);
@@ -185,37 +246,72 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_x3_kernel(Args a) {
         }
     };
 
-    const std::integral_constant<int, 0> I0;
-    const std::integral_constant<int, 1> I1;
     if (nc > 0) {
-        gload_x(c0);
+        // every load is unconditional (chunks past the split's last re-read the last one; their
+        // registers are never consumed): a skipped load on one path would turn the waits of the
+        // merged paths into vmcnt(0), draining the prefetch before the MFMAs
+        const auto cl = [&](int c) { return min(c, c1 - 1); };
+        gload_x(c0, I0);
         gload_w(c0, I0);
-        store_x(0);
-        if (nc > 1) {
-            gload_x(c0 + 1);
-            gload_w(c0 + 1, I1);
-        }
+        gload_x(cl(c0 + 1), I1);
+        gload_w(cl(c0 + 1), I1);
+        store_x(0, I0);
+        gload_x(cl(c0 + 2), I0);
         __syncthreads();
-        // step it: MFMAs on x buffer it & 1 with W set S = it & 1; x(it + 1) to the other buffer;
-        // loads of chunk it + 2 (x rows first: the next store waits only for them)
+        G_STAMP(1);
+        // step it (S = it & 1): MFMAs on x buffer S with W set S; x(it + 1) (loaded two steps ago, set
+        // !S) to the other buffer (past the last chunk: a copy nobody reads); then the loads of x(it + 3)
+        // into set !S and W(it + 2) into set S. x rows go first so that a store waits only for its own
+        // rows and the W of its step.
         auto step = [&](int it, auto S) {
-            mma(it & 1, S);
-            if (it + 1 < nc) store_x((it + 1) & 1);
-            if (it + 2 < nc) {
-                gload_x(c0 + it + 2);
-                gload_w(c0 + it + 2, S);
-            }
+            constexpr int s_ = decltype(S)::value;
+            const std::integral_constant<int, 1 - s_> NS;
+            mma(s_, S);
+            store_x(1 - s_, NS);
+            gload_x(cl(c0 + it + 3), NS);
+            gload_w(cl(c0 + it + 2), S);
             __syncthreads();
+            if (it < 4) G_STAMP(2 + it);
         };
-        for (int it = 0; it < nc; it += 2) {
+        int it = 0;
+        for (; it + 1 < nc; it += 2) {
             step(it, I0);
-            if (it + 1 < nc) step(it + 1, I1);
+            step(it + 1, I1);
         }
+        if (it < nc) step(it, I0);
     }
+    G_STAMP(6);
 
     // epilogue: accumulators -> LDS tile [64 rows][128 + 4] -> whole rows (+ bias, GELU) to the slab.
     // acc[t][e]: column (n) 32 w + (e & 3) + 8 (e >> 2) + 4 (lane >> 5), row (m) 32 t + (lane & 31)
     float* so = reinterpret_cast<float*>(smem);
+    if constexpr (KG == 2) {
+        // k-group 1's partial sums -> LDS [w][t][q][lane][4] -> added by k-group 0
+        float4* ex = reinterpret_cast<float4*>(smem);
+        if (g == 1) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    ex[((w * 2 + t) * 4 + q) * 64 + lane] =
+                        make_float4(acc[t][4 * q], acc[t][4 * q + 1], acc[t][4 * q + 2], acc[t][4 * q + 3]);
+        }
+        __syncthreads();
+        if (g == 0) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 o = ex[((w * 2 + t) * 4 + q) * 64 + lane];
+                    acc[t][4 * q] += o.x;
+                    acc[t][4 * q + 1] += o.y;
+                    acc[t][4 * q + 2] += o.z;
+                    acc[t][4 * q + 3] += o.w;
+                }
+        }
+        __syncthreads();
+    }
+    if (g == 0)
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -244,12 +340,19 @@ __global__ void __launch_bounds__(kThreads, 2) gemm_x3_kernel(Args a) {
         if (a.act == 1) v = make_float4(gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w));
         *reinterpret_cast<float4*>(slab + (size_t)gm * a.n + gn) = v;
     }
+    G_STAMP(7);
 }
 
 }  // namespace gemm3
 }  // namespace tsplat
 
 using namespace tsplat::gemm3;
+
+#if TSPLAT_GEMM_STAMP
+extern "C" int tsplat_gemm_stamps(void* buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_stamps), &buf, sizeof(buf)) == hipSuccess ? TSPLAT_OK : TSPLAT_EINVAL;
+}
+#endif
 
 static void packed_dims(int n, int k, int& ntp, int& kcp) {
     ntp = tsplat::ceil_div(n, kBN) * (kBN / 32);
