@@ -41,6 +41,9 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef float f4v __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) f4v* gptr;  // global loads (not flat)
 
+#ifndef TSPLAT_GEMM_WKMAJOR
+#define TSPLAT_GEMM_WKMAJOR 1  // packed W k-step-major: a k-step's n-tiles adjacent
+#endif
 #ifndef TSPLAT_GEMM_SB
 #define TSPLAT_GEMM_SB 0
 #endif
@@ -103,7 +106,7 @@ __device__ __forceinline__ float gelu_erf(float v) {
     return 0.5f * v * (1.0f + copysignf(e, v));
 }
 
-// W [n][k] fp32 -> [ntp][kcp][hl][64 lanes][8 bf16]: lane (n & 31) + 32 ((k >> 3) & 1), element k & 7;
+// W [n][k] fp32 -> [kcp][ntp][hl][64 lanes][8 bf16] (TSPLAT_GEMM_WKMAJOR; 0: [ntp][kcp][...]): lane (n & 31) + 32 ((k >> 3) & 1), element k & 7;
 // rows n >= N and columns k >= K are zeros. One thread per (row, 8 consecutive k).
 __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, uint4* __restrict__ wp, int n_rows,
                                                    int k_cols, int ntp, int kcp) {
@@ -121,7 +124,11 @@ __global__ void __launch_bounds__(256) pack_kernel(const float* __restrict__ w, 
 #pragma unroll
     for (int j = 0; j < 4; ++j) split_pair(v[2 * j], v[2 * j + 1], hi[j], lo[j]);
     const int kc = g >> 1, lane = (n & 31) + 32 * (g & 1);
+#if TSPLAT_GEMM_WKMAJOR
+    const size_t base = ((size_t)kc * ntp + (n >> 5)) * 128 + lane;
+#else
     const size_t base = ((size_t)(n >> 5) * kcp + kc) * 128 + lane;
+#endif
     wp[base] = make_uint4(hi[0], hi[1], hi[2], hi[3]);
     wp[base + 64] = make_uint4(lo[0], lo[1], lo[2], lo[3]);
 }
@@ -133,6 +140,7 @@ struct Args {
     float* out;        // [ksplit][m][n]
     int m, n, k;
     int kcp;           // packed k-steps (a multiple of kSteps)
+    int ntp;           // packed 32-row n-tiles
     int nchunk;        // K chunks = kcp / kSteps
     int cps;           // chunks per split
     int ksplit, act;
@@ -151,7 +159,13 @@ __global__ void __launch_bounds__(kThreads, 2 / KG) gemm_x3_kernel(Args a) {
     const int c0 = ks * a.cps, c1 = min(c0 + a.cps, a.nchunk), nc = c1 - c0;
 
     const int tid = threadIdx.x, lane = tid & 63, w = (tid >> 6) & 3, g = tid >> 8;
+#if TSPLAT_GEMM_WKMAJOR
+    const uint4* wb = a.w + (size_t)(nbk * 4 + w) * 128 + lane;
+    const size_t wstep = (size_t)a.ntp * 128;  // uint4 per k-step
+#else
     const uint4* wb = a.w + (size_t)(nbk * 4 + w) * a.kcp * 128 + lane;
+    const size_t wstep = 128;
+#endif
 
     // x staging: thread = (row r0 + 16 KG i, float4 column c4), i < 4 / KG
     const int c4 = tid & 15, r0 = tid >> 4;
@@ -195,7 +209,7 @@ __global__ void __launch_bounds__(kThreads, 2 / KG) gemm_x3_kernel(Args a) {
         for (int ss = 0; ss < kSpw; ++ss)
 #pragma unroll
             for (int hl = 0; hl < 2; ++hl)
-                wr[decltype(S)::value][ss][hl] = wb[((size_t)c * kSteps + g * kSpw + ss) * 128 + hl * 64];
+                wr[decltype(S)::value][ss][hl] = wb[((size_t)c * kSteps + g * kSpw + ss) * wstep + hl * 64];
     };
     auto store_x = [&](int buf, auto X) {
         uint32_t* b = smem + buf * kBufDw;
@@ -393,8 +407,7 @@ extern "C" int tsplat_gemm_x3_fwd(const float* x, const void* wp, const float* b
     a.m = m;
     a.n = n;
     a.k = k;
-    int ntp;
-    packed_dims(n, k, ntp, a.kcp);
+    packed_dims(n, k, a.ntp, a.kcp);
     a.nchunk = a.kcp / kSteps;
     if (ksplit > a.nchunk) return TSPLAT_EINVAL;
     a.cps = tsplat::ceil_div(a.nchunk, ksplit);
