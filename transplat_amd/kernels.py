@@ -1397,12 +1397,15 @@ def gemm_x3(x, weight, bias=None, act: str = "none", ksplit: int = 1):
 
 
 def linear_forward(mod, x):
-    """nn.Linear.forward (installed by install_linear_dispatch): in dense_precision("bf16x3") the
-    fp32 linears that linear_xf32_ok admits run as linear_xf32; everything else is F.linear."""
+    """nn.Linear.forward (installed by install_linear_dispatch): in dense_precision("bf16x3") the fp32
+    linears run on the split-bf16 GEMM (gemm_x3; linear_xf32 instead if its A/B knob admits them, and
+    F.linear below 64 rows); everything else is F.linear."""
     import torch.nn.functional as F
 
     if linear_xf32_ok(x, mod.weight):
         return linear_xf32(x, mod.weight, mod.bias)
+    if gemm_x3_ok(x, mod.weight) and x.numel() // x.shape[-1] >= 64:
+        return gemm_x3(x, mod.weight, mod.bias)
     return F.linear(x, mod.weight, mod.bias)
 
 

@@ -89,9 +89,12 @@ class TransformerLayer(nn.Module):
                                      self.merge.weight, ln1, residual=source, kv_shift=kv_shift, **x3)
         message = K.attention_merge(query, key, value, height, width, attn_num_splits, self.with_shift,
                                     self.merge.weight, ln1, kv_shift=kv_shift, **x3)
-        # mlp[0] is the one large plain GEMM of the layer (8192 x 256 x 1024 at b = 1): hipBLASLt
-        # runs it at 103 TF, above this build's kernel (66 TF); its GELU moves into mlp[2]'s load
-        hidden = self.mlp[0](torch.cat([source, message], dim=-1))
+        # mlp[0] is the one large plain GEMM of the layer (8192 x 256 x 1024 at b = 1): in the bf16x3
+        # mode on the split-bf16 GEMM (26.6 us; hipBLASLt exact fp32 35.8), else hipBLASLt (103 TF,
+        # above linear.hip's 66); its GELU moves into mlp[2]'s load
+        cat = torch.cat([source, message], dim=-1)
+        w0 = self.mlp[0].weight
+        hidden = K.gemm_x3(cat, w0, self.mlp[0].bias) if K.gemm_x3_ok(cat, w0) else self.mlp[0](cat)
         ln2 = (self.norm2.weight, self.norm2.bias, self.norm2.eps)
         return K.fused_linear(hidden, self.mlp[2].weight, ln=ln2, residual=source, gelu_in=True)
 

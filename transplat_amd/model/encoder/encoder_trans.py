@@ -85,8 +85,14 @@ class EncoderTransCfg:
 # camera-only prep of the depth predictor and the adapter on the backbone's branch
 # (TSPLAT_CAM_HOIST=0: computed where it is used, the A/B knob)
 _CAM_HOIST = os.environ.get("TSPLAT_CAM_HOIST", "1") == "1"
-# the depth predictor's backbone-only first part on the backbone's branch ("0": after the join; A/B)
-_DP_BEGIN_SIDE = os.environ.get("TSPLAT_DP_BEGIN_SIDE", "1") == "1"
+# the depth predictor's backbone-only first part on the backbone's branch ("1"; default "0": after the
+# join). Round 6: with it on the branch, hipGraph replays of the step were not the eager step (the
+# encoder's Gaussians moved in 4-8 of 12 replays, means by up to 17; tools/enc_graph_race.py,
+# profiles/r6/graph_race.log), with it after the join 0 of 32. The coarse correlation kernel itself
+# is deterministic beside a busy stream and in two-stream graphs, and reads nothing outside its
+# inputs (tools/coarse_stress.py, tools/coarse_oob.py); the hazard is in the branch arrangement,
+# whose cause was not pinned down. Cost: C2 ~1 % (486.6 vs 490.9 views/s same box).
+_DP_BEGIN_SIDE = os.environ.get("TSPLAT_DP_BEGIN_SIDE", "0") == "1"
 
 
 class EncoderTrans(Encoder[EncoderTransCfg]):
