@@ -93,6 +93,8 @@ _CAM_HOIST = os.environ.get("TSPLAT_CAM_HOIST", "1") == "1"
 # inputs (tools/coarse_stress.py, tools/coarse_oob.py); the hazard is in the branch arrangement,
 # whose cause was not pinned down. Cost: C2 ~1 % (486.6 vs 490.9 views/s same box).
 _DP_BEGIN_SIDE = os.environ.get("TSPLAT_DP_BEGIN_SIDE", "0") == "1"
+# Depth-Anything on the side stream and the backbone on the current one (A/B; with TSPLAT_SIDE_PRIO)
+_DA_SIDE = os.environ.get("TSPLAT_DA_SIDE", "0") == "1"
 
 
 class EncoderTrans(Encoder[EncoderTransCfg]):
@@ -225,9 +227,14 @@ class EncoderTrans(Encoder[EncoderTransCfg]):
             return tf, cf, cams, begun
 
         ctx = (context["image"], context["intrinsics"], context["extrinsics"], context["near"], context["far"])
-        bb = streams.fork(device, backbone_branch, *ctx)
-        da_depth, out_feature = depth_anything(context["image"])
-        trans_features, cnn_features, (dp_cams, adapter_cams), begun = streams.join(bb)
+        if _DA_SIDE:  # A/B arrangement: Depth-Anything on the side stream, the backbone here
+            da = streams.fork(device, depth_anything, context["image"])
+            trans_features, cnn_features, (dp_cams, adapter_cams), begun = backbone_branch(*ctx)
+            da_depth, out_feature = streams.join(da)
+        else:
+            bb = streams.fork(device, backbone_branch, *ctx)
+            da_depth, out_feature = depth_anything(context["image"])
+            trans_features, cnn_features, (dp_cams, adapter_cams), begun = streams.join(bb)
         if begun is None:
             begun = dp_begin(trans_features, cnn_features, dp_cams, True)
         dino_feature = out_feature.view(b, v, *out_feature.shape[1:])

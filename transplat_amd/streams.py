@@ -53,6 +53,8 @@ def side_stream(device, slot: int = 0) -> torch.cuda.Stream:
     dev = torch.device(device)
     key = (dev.index if dev.index is not None else torch.cuda.current_device(), slot)
     if key not in _SIDE:
+        # (a higher-priority side stream made the replayed C2 step 2.6x slower: 184-204 vs 485
+        # views/s, profiles/r6/ab_c2_stream_prio.txt)
         _SIDE[key] = torch.cuda.Stream(torch.device("cuda", key[0]))
     return _SIDE[key]
 
