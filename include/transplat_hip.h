@@ -427,6 +427,10 @@ int tsplat_mha_bias_f32_fwd(const float* qkv, const float* bias, float* out, int
  * into hi / lo bf16 images in workspace (tsplat_mha_x3_workspace_bytes), and QK^T / PV run as
  * hi*hi + hi*lo + lo*hi on v_mfma_f32_16x16x32_bf16 / 16x16x16_bf16 with fp32 accumulation and the
  * fp32 online softmax of tsplat_mha_f32_fwd. qkv, bias and workspace 16-B aligned. */
+/* tsplat_mha_x3_fwd on qkv already split into hi / lo bf16 images (bias included), lo = hi + batch
+ * tokens 3 heads head_dim elements (tsplat_gemm_x3_fwd act 2 writes them so). */
+int tsplat_mha_x3_presplit_fwd(const void* qkv_hi, const void* qkv_lo, float* out, int32_t batch, int32_t tokens,
+                               int32_t heads, int32_t head_dim, float scale, void* stream);
 size_t tsplat_mha_x3_workspace_bytes(int32_t batch, int32_t tokens, int32_t heads, int32_t head_dim);
 int tsplat_mha_x3_fwd(const float* qkv, const float* bias, float* out, void* workspace, int32_t batch,
                       int32_t tokens, int32_t heads, int32_t head_dim, float scale, void* stream);
@@ -602,7 +606,9 @@ int tsplat_resize_bilinear_nchw_fwd(const float* x, float* y, int32_t planes, in
  * tsplat_gemm_x3_pack splits W [n, k] fp32 (nn.Linear weight) once into its hi / lo bf16 MFMA
  * fragments (tsplat_gemm_x3_pack_bytes(n, k) bytes, 16-B aligned). tsplat_gemm_x3_fwd:
  * out[s, m, n] = sum over split s's share of k of x[m, k] W[n, k] (+ bias[n] in slab 0; act 1 =
- * exact-erf GELU, only with ksplit 1), x [m, k] fp32 rows contiguous, k % 4 == 0, n % 4 == 0, x /
+ * exact-erf GELU, only with ksplit 1; act 2 = no activation, the output written as hi / lo bf16
+ * images [m, n] at out and out + m n bf16 elements, x = hi + lo, only with ksplit 1), x [m, k] fp32 rows
+ * contiguous, k % 4 == 0, n % 4 == 0, x /
  * bias / out 16-B aligned, 1 <= ksplit <= ceil(k / 64) with every split non-empty; out holds ksplit
  * slabs [m, n] whose sum is the product (tsplat_residual_ln_slabs_fwd adds them in order). */
 size_t tsplat_gemm_x3_pack_bytes(int32_t n, int32_t k);

@@ -907,3 +907,24 @@ def test_residual_ln_slabs(device):
     ysum = ((y[0] + y[1]) + y[2]) + y[3]
     xr, nr = K.residual_ln(x, ysum, ls, norm)
     assert torch.equal(xs, xr) and torch.equal(ns, nr)
+
+
+@pytest.mark.gpu
+def test_gemm_x3_split_output_feeds_mha(device):
+    """gemm_x3(act="split") writes x W^T + bias as hi / lo bf16 images equal (bit for bit) to splitting
+    the fp32 output; tsplat_mha_x3_presplit_fwd on them == tsplat_mha_x3_fwd on the fp32 qkv (DINOv2's
+    qkv -> attention hand-off, 2 x 325 tokens, 12 heads)."""
+    from transplat_amd import kernels as K
+
+    x = seeded((2, 325, 768), 211).to(device)
+    w = (seeded((2304, 768), 212) / 768 ** 0.5).to(device)
+    b = seeded((2304,), 213).to(device)
+    with K.dense_precision("bf16x3"):
+        y = K.gemm_x3(x, w, b)
+        sp = K.gemm_x3(x, w, b, act="split")
+        hi = y.to(torch.bfloat16)
+        lo = (y - hi.float()).to(torch.bfloat16)
+        assert torch.equal(sp[0], hi) and torch.equal(sp[1], lo)
+        o_ref = K.mha(y, 12, 0.125)
+        o = K.mha_presplit(sp, 12, 0.125)
+    assert torch.equal(o, o_ref)

@@ -75,6 +75,7 @@ SIGNATURES = {
     "tsplat_mha_bias_f32_fwd": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, ctypes.c_float, _P]),
     "tsplat_mha_x3_workspace_bytes": (ctypes.c_size_t, [_I32] * 4),
     "tsplat_mha_x3_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I32, _I32, _I32, _I32, ctypes.c_float, _P]),
+    "tsplat_mha_x3_presplit_fwd": (ctypes.c_int, [_P, _P, _P, _I32, _I32, _I32, _I32, ctypes.c_float, _P]),
     "tsplat_qkv_attention_cf_fwd": (ctypes.c_int, [_P, _P] + [_I32] * 5 + [ctypes.c_float, _P]),
     "tsplat_conv2d_f32_fwd": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _P, _P] + [_I32] * 8 + [_P]),
     "tsplat_conv2d_f32_zsplit_fwd": (ctypes.c_int, [_P, _I32, _P, _I32, _P, _P, _P] + [_I32] * 9 + [_P, _P, _P]),

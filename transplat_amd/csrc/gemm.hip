@@ -352,6 +352,16 @@ __global__ void __launch_bounds__(kThreads, 2 / KG) gemm_x3_kernel(Args a) {
             v.w += bb.w;
         }
         if (a.act == 1) v = make_float4(gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w));
+        if (a.act == 2) {  // hi / lo bf16 images [m][n] at out and out + m n bf16 (the x3 MHA's operands)
+            uint32_t h0, l0, h1, l1;
+            split_pair(v.x, v.y, h0, l0);
+            split_pair(v.z, v.w, h1, l1);
+            uint2* ob = reinterpret_cast<uint2*>(a.out);
+            const size_t e4 = ((size_t)gm * a.n + gn) / 4;
+            ob[e4] = make_uint2(h0, h1);
+            ob[e4 + (size_t)a.m * a.n / 4] = make_uint2(l0, l1);
+            continue;
+        }
         *reinterpret_cast<float4*>(slab + (size_t)gm * a.n + gn) = v;
     }
     G_STAMP(7);
@@ -397,7 +407,7 @@ extern "C" int tsplat_gemm_x3_fwd(const float* x, const void* wp, const float* b
     // float4 rows: k and n multiples of 4, x / bias / out 16-B aligned
     if (k % 4 || n % 4 || ((uintptr_t)x & 15) || ((uintptr_t)out & 15) || (bias && ((uintptr_t)bias & 15)))
         return TSPLAT_EINVAL;
-    if (act != 0 && act != 1) return TSPLAT_EINVAL;
+    if (act < 0 || act > 2) return TSPLAT_EINVAL;
     if (act && ksplit > 1) return TSPLAT_EINVAL;  // the activation needs the whole sum
     Args a{};
     a.x = x;

@@ -784,3 +784,24 @@ extern "C" int tsplat_mha_x3_fwd(const float* qkv, const float* bias, float* out
     TSPLAT_CHECK_LAUNCH();
     return TSPLAT_OK;
 }
+
+// The same attention on q / k / v already split into hi / lo bf16 images ([batch, tokens, 3 heads
+// kD] each, the qkv projection's bias included): written by the projection GEMM's epilogue
+// (tsplat_gemm_x3_fwd act 2), so the split pass and the fp32 qkv round trip are gone.
+extern "C" int tsplat_mha_x3_presplit_fwd(const void* qkv_hi, const void* qkv_lo, float* out, int32_t batch,
+                                          int32_t tokens, int32_t heads, int32_t head_dim, float scale,
+                                          void* stream_) {
+    using namespace tsplat::mha;
+    if (!qkv_hi || !qkv_lo || !out || batch <= 0 || tokens <= 0 || heads <= 0 || head_dim != kD) return TSPLAT_EINVAL;
+    if ((int64_t)batch * heads > 65535 || (reinterpret_cast<uintptr_t>(qkv_hi) & 15) ||
+        (reinterpret_cast<uintptr_t>(qkv_lo) & 15) ||
+        (const char*)qkv_lo - (const char*)qkv_hi != (int64_t)batch * tokens * 3 * heads * kD * 2)
+        return TSPLAT_EINVAL;  // the kernel takes lo at hi + n (one workspace-shaped image)
+    hipStream_t stream = (hipStream_t)stream_;
+    TSPLAT_PROF_BEGIN(tsplat::prof::kMha, stream);
+    hipLaunchKernelGGL(mha16_x3_kernel<4>, dim3((tokens + 15) / 16, batch * heads), dim3(256), 0, stream,
+                       (const __bf16*)qkv_hi, (const __bf16*)qkv_lo, out, tokens, heads, scale);
+    TSPLAT_PROF_END(tsplat::prof::kMha, stream);
+    TSPLAT_CHECK_LAUNCH();
+    return TSPLAT_OK;
+}

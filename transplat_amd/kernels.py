@@ -678,6 +678,28 @@ _MHA_X3 = os.environ.get("TSPLAT_MHA_X3", "1") == "1"
 _MHA_X3_ROWS = 2048
 
 
+_MHA_PRESPLIT = os.environ.get("TSPLAT_MHA_PRESPLIT", "1") == "1"  # A/B knob (DINOv2 qkv -> split output)
+
+
+def mha_x3_ok(rows: int) -> bool:
+    """True when DINOv2's qkv GEMM hands the bf16x3 attention pre-split operands (mha's default
+    precision in the current mode is bf16x3 for `rows` = B * N tokens)."""
+    return _MHA_PRESPLIT and _MHA_X3 and _DENSE == "bf16x3" and rows <= _MHA_X3_ROWS
+
+
+def mha_presplit(qkv_split, heads: int, scale: float):
+    """mha in bf16x3 on q / k / v already split: qkv_split [2, B, N, 3 * heads * 64] bf16 (hi, lo;
+    gemm_x3(..., act="split")) -> [B, N, heads * 64] fp32 (tsplat_mha_x3_presplit_fwd)."""
+    lib = _lib.load()
+    _, b, n, c3 = qkv_split.shape
+    d = c3 // (3 * heads)
+    x = qkv_split.contiguous()
+    out = torch.empty((b, n, heads * d), dtype=torch.float32, device=x.device)
+    _lib.check(lib.tsplat_mha_x3_presplit_fwd(_lib.ptr(x[0]), _lib.ptr(x[1]), _lib.ptr(out), b, n, heads, d, float(scale),
+                                              _lib.stream_ptr(x.device)), "tsplat_mha_x3_presplit_fwd")
+    return out
+
+
 def mha(qkv, heads: int, scale: float, bias=None, precision: str | None = None):
     """Multi-head self-attention from the qkv projection output [B, N, 3 * heads * 64] ->
     [B, N, heads * 64] (tsplat_mha_f32_fwd; no permute copies). bias: the projection's bias when
@@ -1386,12 +1408,18 @@ def gemm_x3(x, weight, bias=None, act: str = "none", ksplit: int = 1):
     m = xf.numel() // k
     if ksplit == 0:
         ksplit = 1 if act != "none" else gemm_ksplit(m, n, k)
-    shape = (*x.shape[:-1], n) if ksplit == 1 else (ksplit, *x.shape[:-1], n)
-    out = torch.empty(shape, dtype=torch.float32, device=x.device)
+    if act == "split":  # [2, *x.shape[:-1], n] bf16: hi and lo images (x W^T + bias = hi + lo)
+        if ksplit != 1:
+            raise ValueError("gemm_x3: the split output needs ksplit 1")
+        out = torch.empty((2, *x.shape[:-1], n), dtype=torch.bfloat16, device=x.device)
+    else:
+        shape = (*x.shape[:-1], n) if ksplit == 1 else (ksplit, *x.shape[:-1], n)
+        out = torch.empty(shape, dtype=torch.float32, device=x.device)
     if GEMM_LOG is not None:
         GEMM_LOG.append((m, n, k, ksplit))
     rc = lib.tsplat_gemm_x3_fwd(_lib.ptr(xf), _lib.ptr(_gemm_pack(weight)), _lib.ptr(_f32(bias)) if bias is not None else None,
-                                _lib.ptr(out), m, n, k, ksplit, {"none": 0, "gelu": 1}[act], _lib.stream_ptr(x.device))
+                                _lib.ptr(out), m, n, k, ksplit, {"none": 0, "gelu": 1, "split": 2}[act],
+                                _lib.stream_ptr(x.device))
     _lib.check(rc, "tsplat_gemm_x3_fwd", "bf16x3")
     return out
 

@@ -92,9 +92,12 @@ class Attention(nn.Module):
                 and kernels.gemm_x3_ok(x, self.qkv.weight)):
             # bf16x3 dense mode: both projections on the split-bf16 GEMM (bias in its epilogue), the
             # attention on the bf16x3 MFMA kernel straight from the [b, n, 3c] layout
-            qkv = kernels.gemm_x3(x, self.qkv.weight, self.qkv.bias)
-            return kernels.gemm_x3(kernels.mha(qkv, self.num_heads, self.scale), self.proj.weight, self.proj.bias,
-                                   ksplit=0)
+            if kernels.mha_x3_ok(b * n):  # the projection writes the attention's hi / lo operands
+                o = kernels.mha_presplit(kernels.gemm_x3(x, self.qkv.weight, self.qkv.bias, act="split"),
+                                         self.num_heads, self.scale)
+            else:
+                o = kernels.mha(kernels.gemm_x3(x, self.qkv.weight, self.qkv.bias), self.num_heads, self.scale)
+            return kernels.gemm_x3(o, self.proj.weight, self.proj.bias, ksplit=0)
         if x.dtype == torch.float32 and c // self.num_heads == 64 and not torch.is_autocast_enabled(x.device.type):
             # exact-fp32 MFMA attention straight from the qkv projection's layout; in bf16x3 mode the
             # projection runs without its bias (hipBLASLt's emulated-xf32 GEMM) and the attention

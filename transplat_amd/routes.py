@@ -46,6 +46,7 @@ _HIP = {
     "tsplat_linear_f32_attn_merge_fwd": ("transformer linears (HIP)", None),
     "tsplat_gemm_x3_fwd": ("GEMMs (HIP)", "bf16x3"),
     "tsplat_mha_x3_fwd": ("DINOv2 attention (HIP)", "bf16x3"),
+    "tsplat_mha_x3_presplit_fwd": ("DINOv2 attention (HIP)", "bf16x3"),
     "tsplat_mha_f32_fwd": ("DINOv2 attention (HIP)", "exact fp32"),
     "tsplat_mha_bias_f32_fwd": ("DINOv2 attention (HIP)", "exact fp32"),
     "tsplat_qkv_attention_cf_fwd": ("U-Net attention (HIP)", "exact fp32"),
