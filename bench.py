@@ -519,6 +519,29 @@ def main():
                 "ms_per_step": cms / n_prof, "share_of_step": cms / n_prof / (elapsed / args.steps * 1e3),
             }
 
+    # the split-bf16 GEMM launches of one step (DINOv2 / MVT linears, csrc/gemm.hip), timed the same way
+    gemm_roofline = None
+    if args.workload == "e2e" and args.dense_dtype == "bf16x3":
+        from transplat_amd import kernels as K
+
+        K.GEMM_LOG = []
+        _lib.prof_enable("gemm_x3")
+        for _ in range(n_prof):
+            prof_step()
+        gms, glaunches = _lib.prof_read()
+        _lib.prof_enable(None)
+        glog, K.GEMM_LOG = K.GEMM_LOG, None
+        if glaunches and gms > 0 and len(glog) == glaunches:
+            flops = sum(3 * 2 * m * n * k for m, n, k, _ in glog)
+            g_achieved = flops / (gms * 1e-3) / 1e12
+            gemm_roofline = {
+                "kernel": "gemm_x3", "bound": "mfma", "achieved": g_achieved, "peak": BF16_MFMA_PEAK_TFS,
+                "unit": "TFLOP/s", "frac": g_achieved / BF16_MFMA_PEAK_TFS,
+                "flops": "bf16 MFMA products 3 * 2*m*n*k per launch (hi*hi + hi*lo + lo*hi)",
+                "launches_per_step": glaunches / n_prof, "ms_per_step": gms / n_prof,
+                "share_of_step": gms / n_prof / (elapsed / args.steps * 1e3),
+            }
+
     render_valu = render_valu_roofline(step, n_prof) if args.workload == "raster" else None
     serial.__exit__(None, None, None)
     views = world * info["views_per_step"] * args.steps
@@ -561,6 +584,8 @@ def main():
         result["roofline"]["fp32_equivalent_achieved"] = info["fp32_equivalent_flops_per_launch"] / (avg_ms * 1e-3) / 1e12
     if conv_roofline is not None:
         result["roofline_step_dominant"] = conv_roofline
+    if gemm_roofline is not None:
+        result["roofline_gemm"] = gemm_roofline
     if render_valu is not None:
         result["roofline_render_valu"] = render_valu
     if rank == 0 and not args.no_cpu_baseline and cpu_inputs is not None:
