@@ -30,7 +30,8 @@ _DPT_EPI = os.environ.get("TSPLAT_DPT_EPI", "1") != "0"
 # Opt-in "1": the reassemble branches of ViT layers 1-3 forked onto a side stream while the later
 # blocks run (needs streams.enabled). Measured SLOWER end to end (profiles/r3/ab_r3c: C2 332 vs
 # 356 views/s, C3 849 vs 887): the branches' MIOpen convolutions take CUs from the critical path
-# (DINOv2 blocks and the backbone beside them) rather than filling idle ones.
+# (DINOv2 blocks and the backbone beside them) rather than filling idle ones. Round 6 (hand-written
+# DINOv2 GEMMs): still slower, 444.7 vs 487.6 views/s same box (profiles/r6/ab_c2_dpt_hoist.txt).
 _DPT_HOIST = os.environ.get("TSPLAT_DPT_HOIST", "0") == "1"
 # bf16x3 dense mode (kernels.dense_precision): the head runs on NCHW maps instead, so its 3x3
 # convolutions take the bf16x3 Winograd kernel with the ResidualConvUnit glue fused (ReLU on load,
