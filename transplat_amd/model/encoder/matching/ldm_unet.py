@@ -34,6 +34,11 @@ def gn_act(norm: nn.GroupNorm, x, act: str = "none", residual=None, pre_bias=Non
     return y.type(x.dtype)
 
 
+# the output blocks' skip concatenation read in place by both ResBlock convolutions in the bf16x3
+# mode (round 6; TSPLAT_UNET_CAT_FREE=0: materialised once, the A/B knob)
+_CAT_FREE = os.environ.get("TSPLAT_UNET_CAT_FREE", "1") == "1"
+
+
 def _direct(conv: nn.Module, x, x2=None, upsample: bool = False) -> bool:
     """Whether conv(cat([x, x2])) runs as the direct kernel (kernels.conv2d_direct_ok)."""
     if not (isinstance(conv, nn.Conv2d) and conv.dilation == (1, 1) and conv.groups == 1
@@ -160,15 +165,32 @@ class ResBlock(nn.Module):
         self.skip_connection = (nn.Identity() if self.out_channels == channels
                                 else nn.Conv2d(channels, self.out_channels, 1))
 
+    def _concat_free(self, x, x2) -> bool:
+        """bf16x3 mode, a Winograd / few-channel in_layers conv: both convolutions read cat([x, x2])
+        in place (the 3x3 as a two-source launch, a 1x1 skip on the two-source direct kernel)."""
+        c, sk = self.in_layers[0], self.skip_connection
+        if not (_CAT_FREE and kernels.split_mode() and isinstance(c, nn.Conv2d)
+                and kernels.conv3x3_wino_ok(x, c.weight, c.stride, c.padding, c.dilation, c.groups, (x2,))):
+            return False
+        return isinstance(sk, nn.Identity) or (
+            isinstance(sk, nn.Conv2d) and sk.kernel_size == (1, 1) and sk.stride == (1, 1) and sk.groups == 1
+            and kernels.conv2d_direct_ok(x, sk.weight, 1, sk.padding, c2=x2.shape[1], force=True))
+
     def forward(self, x, x2=None):
         # skip + SiLU(GN(conv(SiLU(GN(conv(x)))))): both GN + SiLU pairs and the residual fused;
         # x2: the output blocks' skip input, x = cat([x, x2], 1) without materialising the concat
         # where the convolutions read it in place
+        cat_free = False
         if x2 is not None and not _direct(self.in_layers[0], x, x2):
-            x, x2 = torch.cat([x, x2], dim=1), None  # materialised once for both convolutions
+            cat_free = self._concat_free(x, x2)
+            if not cat_free:
+                x, x2 = torch.cat([x, x2], dim=1), None  # materialised once for both convolutions
         h = conv_gn_act(self.in_layers[0], self.in_layers[1], x, "silu", x2=x2)
         if isinstance(self.skip_connection, nn.Identity):
             skip = x if x2 is None else (x, x2)  # the concat read in place by the norm's residual add
+        elif cat_free and not _direct(self.skip_connection, x, x2):
+            sk = self.skip_connection
+            skip = kernels.conv2d_direct(x, sk.weight, sk.bias, 1, x2=x2)
         else:
             skip = conv(self.skip_connection, x, x2)
         return conv_gn_act(self.out_layers[0], self.out_layers[1], h, "silu", residual=skip)
